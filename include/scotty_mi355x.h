@@ -1,0 +1,126 @@
+/*
+ * scotty_mi355x.h -- C-ABI of the MI355X-native general-stream-slicing operator.
+ *
+ * Drop-in boundary for the reference's operator interface
+ *   core/src/main/java/de/tub/dima/scotty/core/WindowOperator.java:9-40
+ *   slicing/src/main/java/de/tub/dima/scotty/slicing/SlicingWindowOperator.java:21-69
+ * A JVM shim (Panama FFM / JNI) binds exactly these symbols:
+ * processElement() calls are buffered off-heap and handed over once per
+ * micro-batch; processWatermark() returns the emitted windows.
+ *
+ * Conventions: plain pointers and sizes, no exceptions across the boundary,
+ * int status (0 = OK, <0 = error, >0 = warning) plus scotty_last_error().
+ * One op is single-threaded (like the reference: one operator per task thread).
+ */
+#ifndef SCOTTY_MI355X_H
+#define SCOTTY_MI355X_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes */
+#define SCOTTY_OK 0
+#define SCOTTY_WARN_LATE_DROPPED 1     /* tuples older than the oldest slice were dropped (the reference
+                                          throws IndexOutOfBoundsException, S/SliceManager.java:75-76) */
+#define SCOTTY_ERR_ARG (-1)            /* bad argument / unknown kind */
+#define SCOTTY_ERR_UNSUPPORTED (-2)    /* configuration not implemented on the MI355X path */
+#define SCOTTY_ERR_HIP (-3)            /* HIP runtime error / no device */
+#define SCOTTY_ERR_STATE (-4)          /* call sequence error */
+#define SCOTTY_ERR_INDEX (-5)          /* IndexOutOfBoundsException of the reference */
+#define SCOTTY_ERR_NOMEM (-6)
+
+/* ---- window kinds (core/windowType) */
+#define SCOTTY_WIN_TUMBLING 0   /* TumblingWindow(measure, size)            C/windowType/TumblingWindow.java */
+#define SCOTTY_WIN_SLIDING 1    /* SlidingWindow(measure, size, slide)      C/windowType/SlidingWindow.java */
+#define SCOTTY_WIN_SESSION 2    /* SessionWindow(measure, gap)              C/windowType/SessionWindow.java */
+#define SCOTTY_WIN_FIXED_BAND 3 /* FixedBandWindow(measure, start, size)    C/windowType/FixedBandWindow.java */
+#define SCOTTY_MEASURE_TIME 0   /* C/windowType/WindowMeasure.java */
+#define SCOTTY_MEASURE_COUNT 1
+
+/* ---- value column type of an op (the reference's InputType) */
+#define SCOTTY_VALUE_I32 0
+#define SCOTTY_VALUE_I64 1
+#define SCOTTY_VALUE_F64 2
+
+/* ---- aggregate kinds: the GPU recognises these AggregateFunction classes
+ * (C/windowFunction/ReduceAggregateFunction.java, InvertibleReduceAggregateFunction.java) */
+#define SCOTTY_AGG_SUM_I32 0 /* Integer sum, int32 wrap (B/flinkBenchmark/aggregations/SumAggregation.java:16-18) */
+#define SCOTTY_AGG_COUNT 1   /* lift=1, combine=+ (D/storm-demo/.../windowFunctions/Count.java) */
+#define SCOTTY_AGG_MIN_I32 2 /* Math.min (D/flink-demo/.../MinWindowFunction.java:12) */
+#define SCOTTY_AGG_MAX_I32 3 /* Math.max (D/flink-demo/.../MaxWindowFunction.java:12) */
+#define SCOTTY_AGG_SUM_I64 4
+#define SCOTTY_AGG_MIN_I64 5
+#define SCOTTY_AGG_MAX_I64 6
+#define SCOTTY_AGG_SUM_F64 7 /* within 1e-6 relative of the reference's arrival-order fold */
+#define SCOTTY_AGG_MIN_F64 8
+#define SCOTTY_AGG_MAX_F64 9
+#define SCOTTY_MAX_AGGS 8
+
+/* ---- create flags */
+#define SCOTTY_FLAG_KEYED 0x1u /* reserved: keyed operator (one logical operator per key) */
+
+typedef struct scotty_op scotty_op;
+
+/* Result of one processWatermark: SoA columns owned by the library, valid until the next call on
+ * the op.  Row i is the i-th AggregateWindow of the reference's List (S/WindowManager.java:41-80),
+ * in the reference's emission order.  values[a][i] is the lowered value of aggregation a
+ * (registration order), stored as int64 (integer kinds, already wrapped to the kind's width) or as
+ * the bits of a double (F64 kinds).  has_value[i]==0 <=> AggregateWindow.hasValue()==false, in which
+ * case getAggValues() is the empty list. */
+typedef struct {
+  size_t n_windows;
+  int32_t n_aggs;
+  const int64_t* start;
+  const int64_t* end;
+  const int32_t* measure;
+  const uint8_t* has_value;
+  const int64_t* values[SCOTTY_MAX_AGGS];
+} scotty_windows;
+
+/* new SlicingWindowOperator(stateFactory)  (S/SlicingWindowOperator.java:30-37) */
+int scotty_create(scotty_op** op, int device, int value_type, uint32_t flags);
+void scotty_destroy(scotty_op* op);
+const char* scotty_last_error(scotty_op* op);
+
+/* WindowOperator.addWindowAssigner(Window)  (C/WindowOperator.java:24; S/WindowManager.java:121-147)
+ * a,b = size,0 | size,slide | gap,0 | start,size */
+int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b);
+/* WindowOperator.addAggregation / SlicingWindowOperator.addWindowFunction (C/WindowOperator.java:30,
+ * S/SlicingWindowOperator.java:57-63).  Returns the aggregation index (>=0) or an error. */
+int scotty_add_aggregation(scotty_op* op, int agg_kind);
+/* WindowOperator.setMaxLateness (C/WindowOperator.java:37; default 1000, S/WindowManager.java:24) */
+int scotty_set_max_lateness(scotty_op* op, int64_t max_lateness);
+
+/* A micro-batch of WindowOperator.processElement(element, ts) calls (C/WindowOperator.java:14) in
+ * arrival order.  Host memory, caller-owned, consumed (copied) before return.  val points to n
+ * values of the op's value type. */
+int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, size_t n);
+/* Same, with device pointers already resident in HBM (device `device` of the op).  The buffers must
+ * stay valid and unmodified until the next scotty_process_watermark() returns. */
+int scotty_process_elements_device(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n);
+
+/* WindowOperator.processWatermark(wm) (C/WindowOperator.java:19).  Blocks until results are ready. */
+int scotty_process_watermark(scotty_op* op, int64_t watermark_ts, scotty_windows* out);
+
+/* Counters: tuples dropped as too late since creation; tuples processed. */
+uint64_t scotty_dropped_count(scotty_op* op);
+uint64_t scotty_processed_count(scotty_op* op);
+/* Number of retained slices (LazyAggregateStore.size(), S/aggregationstore/LazyAggregateStore.java:54). */
+int64_t scotty_slice_count(scotty_op* op);
+
+/* Optional HIP-event timing of the dominant (ingest) kernel on the op's stream.  When enabled, each
+ * push records events around the ingest kernel; scotty_ingest_timing() returns the summed device
+ * milliseconds and launch count since the last reset. */
+int scotty_enable_timing(scotty_op* op, int on);
+int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, uint64_t* tuples);
+
+/* Wait for all work enqueued on the op's stream. */
+int scotty_sync(scotty_op* op);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,319 @@
+"""Python host mirror of the reference operator API over the MI355X C-ABI (include/scotty_mi355x.h).
+
+Same names, argument meaning and error behaviour as the reference
+(core/src/main/java/de/tub/dima/scotty/core/WindowOperator.java:9-40 and
+slicing/src/main/java/de/tub/dima/scotty/slicing/SlicingWindowOperator.java:21-69):
+
+    op = SlicingWindowOperator()
+    op.addWindowFunction(SumAggregateFunction())          # or the integer kind SCOTTY_AGG_SUM_I32
+    op.addWindowAssigner(TumblingWindow(WindowMeasure.Time, 10))
+    op.processElement(1, 1)
+    for w in op.processWatermark(22): w.getStart(), w.getEnd(), w.getAggValues(), w.hasValue()
+
+processElement() calls are buffered host-side (as the JVM shim buffers them off-heap) and handed to the
+GPU as one micro-batch; processElements()/processElementsDevice() hand over whole batches.  There is no
+CPU fallback: if libscotty_mi355x.so cannot be loaded or no GPU is present, construction raises.
+"""
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libscotty_mi355x.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "scotty_mi355x.h")
+
+SCOTTY_OK, SCOTTY_WARN_LATE_DROPPED = 0, 1
+ERRORS = {-1: "SCOTTY_ERR_ARG", -2: "SCOTTY_ERR_UNSUPPORTED", -3: "SCOTTY_ERR_HIP", -4: "SCOTTY_ERR_STATE",
+          -5: "SCOTTY_ERR_INDEX", -6: "SCOTTY_ERR_NOMEM"}
+VALUE_I32, VALUE_I64, VALUE_F64 = 0, 1, 2
+AGG_SUM_I32, AGG_COUNT, AGG_MIN_I32, AGG_MAX_I32 = 0, 1, 2, 3
+AGG_SUM_I64, AGG_MIN_I64, AGG_MAX_I64 = 4, 5, 6
+AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64 = 7, 8, 9
+F64_AGGS = (AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64)
+MAX_AGGS = 8
+
+
+class ScottyError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (ERRORS.get(code, code), msg))
+        self.code = code
+
+
+class UnsupportedError(ScottyError):
+    pass
+
+
+class WindowMeasure:  # C/windowType/WindowMeasure.java
+    Time = 0
+    Count = 1
+
+
+class _Window:
+    kind = -1
+
+    def __init__(self, measure, a, b=0):
+        self.measure, self.a, self.b = measure, a, b
+
+
+class TumblingWindow(_Window):  # C/windowType/TumblingWindow.java
+    kind = 0
+
+    def __init__(self, measure, size):
+        super().__init__(measure, size)
+
+
+class SlidingWindow(_Window):  # C/windowType/SlidingWindow.java
+    kind = 1
+
+    def __init__(self, measure, size, slide):
+        super().__init__(measure, size, slide)
+
+
+class SessionWindow(_Window):  # C/windowType/SessionWindow.java
+    kind = 2
+
+    def __init__(self, measure, gap):
+        super().__init__(measure, gap)
+
+
+class FixedBandWindow(_Window):  # C/windowType/FixedBandWindow.java
+    kind = 3
+
+    def __init__(self, measure, start, size):
+        super().__init__(measure, start, size)
+
+
+class _Agg:  # known AggregateFunction classes the GPU path recognises (C/windowFunction/)
+    kind = -1
+
+
+def _agg(kind_, name):
+    return type(name, (_Agg,), {"kind": kind_})
+
+
+SumAggregateFunction = _agg(AGG_SUM_I32, "SumAggregateFunction")
+CountAggregateFunction = _agg(AGG_COUNT, "CountAggregateFunction")
+MinAggregateFunction = _agg(AGG_MIN_I32, "MinAggregateFunction")
+MaxAggregateFunction = _agg(AGG_MAX_I32, "MaxAggregateFunction")
+LongSumAggregateFunction = _agg(AGG_SUM_I64, "LongSumAggregateFunction")
+DoubleSumAggregateFunction = _agg(AGG_SUM_F64, "DoubleSumAggregateFunction")
+
+
+class scotty_windows(ctypes.Structure):
+    _fields_ = [("n_windows", ctypes.c_size_t), ("n_aggs", ctypes.c_int32),
+                ("start", ctypes.POINTER(ctypes.c_int64)), ("end", ctypes.POINTER(ctypes.c_int64)),
+                ("measure", ctypes.POINTER(ctypes.c_int32)), ("has_value", ctypes.POINTER(ctypes.c_uint8)),
+                ("values", ctypes.POINTER(ctypes.c_int64) * MAX_AGGS)]
+
+
+_lib = None
+
+
+def header_functions():
+    """Function names declared by include/scotty_mi355x.h."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|uint64_t|int64_t)\s+(scotty_\w+)\(", txt, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libscotty_mi355x.so not built (run __graft_entry__.build()): " + LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        P, i64, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64
+        sig = {
+            "scotty_create": (ctypes.c_int, [ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, ctypes.c_uint32]),
+            "scotty_destroy": (None, [P]),
+            "scotty_last_error": (ctypes.c_char_p, [P]),
+            "scotty_add_window": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, i64, i64]),
+            "scotty_add_aggregation": (ctypes.c_int, [P, ctypes.c_int]),
+            "scotty_set_max_lateness": (ctypes.c_int, [P, i64]),
+            "scotty_process_elements": (ctypes.c_int, [P, P, P, ctypes.c_size_t]),
+            "scotty_process_elements_device": (ctypes.c_int, [P, P, P, ctypes.c_size_t]),
+            "scotty_process_watermark": (ctypes.c_int, [P, i64, ctypes.POINTER(scotty_windows)]),
+            "scotty_dropped_count": (u64, [P]),
+            "scotty_processed_count": (u64, [P]),
+            "scotty_slice_count": (i64, [P]),
+            "scotty_enable_timing": (ctypes.c_int, [P, ctypes.c_int]),
+            "scotty_ingest_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
+                                                    ctypes.POINTER(u64)]),
+            "scotty_sync": (ctypes.c_int, [P]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+class AggregateWindow:  # C/AggregateWindow.java:8-21
+    __slots__ = ("start", "end", "measure", "_has", "_values")
+
+    def __init__(self, start, end, measure, has, values):
+        self.start, self.end, self.measure, self._has, self._values = start, end, measure, has, values
+
+    def getStart(self):
+        return self.start
+
+    def getEnd(self):
+        return self.end
+
+    def getMeasure(self):
+        return self.measure
+
+    def hasValue(self):
+        return self._has
+
+    def getAggValues(self):
+        return list(self._values)
+
+    def key(self):
+        return (self.start, self.end, self.measure, self._has, tuple(self._values))
+
+    def __repr__(self):
+        return "AggregateWindow(%d,%d,m=%d,%s)" % (self.start, self.end, self.measure, self._values)
+
+
+def _kind_of(fn):
+    if isinstance(fn, int):
+        return fn
+    if isinstance(fn, type) and issubclass(fn, _Agg):
+        return fn.kind
+    if isinstance(fn, _Agg):
+        return fn.kind
+    raise UnsupportedError(-2, "AggregateFunction %r has no GPU kind (user lambdas cannot run on the GPU)" % (fn,))
+
+
+class SlicingWindowOperator:
+    """de.tub.dima.scotty.slicing.SlicingWindowOperator backed by libscotty_mi355x.so."""
+
+    def __init__(self, device=0, value_type=VALUE_I32):
+        self._l = lib()
+        self._h = ctypes.c_void_p()
+        rc = self._l.scotty_create(ctypes.byref(self._h), device, value_type, 0)
+        if rc != 0:
+            raise ScottyError(rc, "scotty_create failed (no MI355X / HIP device?)")
+        self.value_type = value_type
+        self._aggs = []
+        self._buf_ts, self._buf_v = [], []
+        self.last_status = 0
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._l.scotty_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc < 0:
+            msg = self._l.scotty_last_error(self._h).decode()
+            raise (UnsupportedError if rc == -2 else ScottyError)(rc, msg)
+        return rc
+
+    # ---- WindowOperator API
+    def addWindowAssigner(self, window):
+        self._flush()
+        self._check(self._l.scotty_add_window(self._h, window.kind, window.measure, window.a, window.b))
+
+    def addAggregation(self, fn):
+        self._flush()
+        kind = _kind_of(fn)
+        idx = self._check(self._l.scotty_add_aggregation(self._h, kind))
+        self._aggs.append(kind)
+        return idx
+
+    addWindowFunction = addAggregation
+
+    def setMaxLateness(self, max_lateness):
+        self._flush()
+        self._check(self._l.scotty_set_max_lateness(self._h, max_lateness))
+
+    def processElement(self, element, ts):
+        self._buf_ts.append(ts)
+        self._buf_v.append(element)
+
+    def processElements(self, ts, values):
+        """A micro-batch of processElement calls in arrival order (host arrays)."""
+        self._flush()
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        dt = {VALUE_I32: np.int32, VALUE_I64: np.int64, VALUE_F64: np.float64}[self.value_type]
+        v = np.ascontiguousarray(values, dtype=dt)
+        assert len(ts) == len(v)
+        if len(ts):
+            self._check(self._l.scotty_process_elements(self._h, ts.ctypes.data, v.ctypes.data, len(ts)))
+
+    def processElementsDevice(self, ts_ptr, val_ptr, n):
+        """A micro-batch already resident in HBM (e.g. torch tensors' data_ptr()); buffers must stay valid
+        until the next processWatermark returns."""
+        self._flush()
+        self._check(self._l.scotty_process_elements_device(self._h, ts_ptr, val_ptr, n))
+
+    def _flush(self):
+        if self._buf_ts:
+            ts, v = self._buf_ts, self._buf_v
+            self._buf_ts, self._buf_v = [], []
+            self.processElements(ts, v)
+
+    def processWatermark(self, watermark_ts):
+        self._flush()
+        out = scotty_windows()
+        self.last_status = self._check(self._l.scotty_process_watermark(self._h, watermark_ts, ctypes.byref(out)))
+        return self._windows(out)
+
+    def _windows(self, out):
+        n = out.n_windows
+        res = []
+        if n == 0:
+            return res
+        start = np.ctypeslib.as_array(out.start, shape=(n,)).copy()
+        end = np.ctypeslib.as_array(out.end, shape=(n,)).copy()
+        meas = np.ctypeslib.as_array(out.measure, shape=(n,)).copy()
+        has = np.ctypeslib.as_array(out.has_value, shape=(n,)).copy()
+        cols = []
+        for k, kind in enumerate(self._aggs):
+            col = np.ctypeslib.as_array(out.values[k], shape=(n,)).copy()
+            cols.append(col.view(np.float64) if kind in F64_AGGS else col)
+        for i in range(n):
+            vals = [c[i].item() for c in cols] if has[i] else []
+            res.append(AggregateWindow(int(start[i]), int(end[i]), int(meas[i]), bool(has[i]), vals))
+        return res
+
+    def processWatermarkRaw(self, watermark_ts):
+        """processWatermark without building Python objects: returns (n_windows, status)."""
+        self._flush()
+        out = scotty_windows()
+        st = self._check(self._l.scotty_process_watermark(self._h, watermark_ts, ctypes.byref(out)))
+        return out.n_windows, st
+
+    # ---- extras
+    def droppedCount(self):
+        return self._l.scotty_dropped_count(self._h)
+
+    def processedCount(self):
+        return self._l.scotty_processed_count(self._h)
+
+    def sliceCount(self):
+        return self._l.scotty_slice_count(self._h)
+
+    def enableTiming(self, on=True):
+        self._check(self._l.scotty_enable_timing(self._h, 1 if on else 0))
+
+    def ingestTiming(self):
+        ms, launches, tuples = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._l.scotty_ingest_timing(self._h, ctypes.byref(ms), ctypes.byref(launches),
+                                                 ctypes.byref(tuples)))
+        return ms.value, launches.value, tuples.value
+
+    def sync(self):
+        self._check(self._l.scotty_sync(self._h))
+
+from . import workloads  # noqa: E402,F401

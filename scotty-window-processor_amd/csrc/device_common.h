@@ -1,0 +1,97 @@
+// device_common.h -- data layout shared by the host engine and the gfx950 kernels.
+//
+// HBM layout of one operator (all SoA, 64-bit words):
+//   slices   [SCAP]  t_start, t_last, cnt(u64), part[3] (sum | min | max)   -- LazyAggregateStore's SliceList
+//   grid     [GCAP]  sorted union edge grid of the context-free time windows  -- StreamSlicer's edge function
+//   cells    [CCAP]  per-micro-batch partials: old slices ++ grid cells        -- refined slices of one batch
+//   tilemax  [TCAP]  max ts of each 4096-tuple arrival tile                    -- edge first-crossing lookups
+//   meta             DevMeta (device-resident slicer / store scalars)
+#pragma once
+#include <stdint.h>
+
+namespace scotty {
+
+constexpr int TILE = 4096;        // tuples per arrival-order tile (tilemax granularity)
+constexpr int WCAP = 1024;        // cells in a workgroup's LDS window
+constexpr int NPART = 3;          // partial slots per slice/cell: 0 sum, 1 min, 2 max
+
+enum : int { VT_I32 = 0, VT_I64 = 1, VT_F64 = 2 };
+enum : int { NEED_SUM = 1, NEED_MIN = 2, NEED_MAX = 4 };
+
+// Device-resident scalars.  The StreamSlicer state (maxEventTime, min_next_edge_ts) lives here so
+// consecutive micro-batches need no host round trip (S/StreamSlicer.java:10-14).
+struct DevMeta {
+  int64_t head, tail;        // retained slices are [head, tail) of the slice arrays
+  int64_t prev_max;          // StreamSlicer.maxEventTime
+  int64_t j0;                // grid index of min_next_edge_ts (the pending edge N)
+  int64_t gcount;            // valid grid entries
+  int64_t batch_max;         // scratch: max ts of the last push (valid also on overflow)
+  int64_t n_emitted;         // edges appended by the last push
+  int64_t overflow;          // != 0: a push exceeded the grid horizon / slice capacity; nothing committed
+  int64_t failed_push;       // push sequence number that overflowed
+  int64_t push_seq;          // pushes committed or attempted since creation
+  int64_t oldest_start;      // t_start[head] after the last GC (host mirror)
+  uint64_t late_push, overflow_push;   // per-push counters (reset by the commit kernel)
+  uint64_t late_total, processed_total;
+  int64_t pad[1];
+};
+
+struct IngestArgs {
+  const int64_t* ts;
+  const void* val;
+  int64_t n;
+  // slices (read-only here)
+  const int64_t* s_tstart;
+  // grid
+  const int64_t* grid;
+  // cells (atomically accumulated)
+  unsigned long long* c_cnt;
+  long long* c_tmax;
+  unsigned long long* c_part[NPART];
+  // tile maxima
+  long long* tilemax;
+  DevMeta* meta;
+  int64_t per_wave;          // tuples per wave (multiple of TILE)
+};
+
+struct CommitArgs {
+  const int64_t* ts;
+  int64_t n;
+  int64_t max_lateness;
+  int64_t scap;              // slice capacity
+  const int64_t* grid;
+  long long* tilemax;
+  long long* pmax;           // scratch [TCAP]
+  int32_t* rank;             // scratch [GCAP]
+  int32_t* flag;             // scratch [GCAP]
+  int64_t* s_tstart;
+  int64_t* s_tlast;
+  unsigned long long* s_cnt;
+  unsigned long long* s_part[NPART];
+  unsigned long long* c_cnt;
+  long long* c_tmax;
+  unsigned long long* c_part[NPART];
+  DevMeta* meta;
+  int need;
+  int vt;
+  int64_t push_seq;
+};
+
+struct WindowArgs {
+  const int64_t* w_start;
+  const int64_t* w_end;
+  int64_t n_windows;
+  const int64_t* s_tstart;
+  const int64_t* s_tlast;
+  const unsigned long long* s_cnt;
+  const unsigned long long* s_part[NPART];
+  DevMeta* meta;
+  // outputs
+  uint8_t* has_value;
+  unsigned long long* o_cnt;
+  unsigned long long* o_part[NPART];
+  int need;
+  int vt;
+};
+
+}  // namespace scotty

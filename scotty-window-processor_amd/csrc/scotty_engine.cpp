@@ -1,0 +1,833 @@
+// scotty_engine.cpp -- host side of the MI355X operator: control state, edge grid, window triggering,
+// and the C-ABI of include/scotty_mi355x.h.
+//
+// Per-tuple work never runs here: every tuple is read, assigned and aggregated by the gfx950 kernels
+// (slicing_kernels.hip).  The host keeps what the reference keeps in scalars of the WindowManager /
+// StreamSlicer (S/WindowManager.java:18-33, S/StreamSlicer.java:10-14), generates the triggered window
+// list (pure arithmetic of C/windowType/*Window.triggerWindows) and the union edge grid of the
+// context-free windows (their assignNextWindowStart), and sequences launches on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include "../../include/scotty_mi355x.h"
+#include "device_common.h"
+
+namespace scotty {
+hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st);
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
+hipError_t launch_windows(const WindowArgs& a, hipStream_t st);
+hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st);
+hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
+hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st);
+}  // namespace scotty
+
+using namespace scotty;
+
+namespace {
+
+constexpr int64_t JMAX = INT64_MAX, JMIN = INT64_MIN;
+inline int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+inline int64_t jsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+inline int64_t jmod(int64_t a, int64_t b) { return b == -1 ? 0 : a % b; }
+
+struct CFWin {  // context-free window (C/windowType/ContextFreeWindow.java)
+  int kind;
+  int64_t a, b;
+  // assignNextWindowStart: TumblingWindow.java:29-31, SlidingWindow.java:41-43, FixedBandWindow.java:37-48
+  int64_t next_start(int64_t t) const {
+    if (kind == SCOTTY_WIN_TUMBLING) return jsub(jadd(t, a), jmod(t, a));
+    if (kind == SCOTTY_WIN_SLIDING) return jsub(jadd(t, b), jmod(t, b));
+    if (t == JMAX || t < a) return a;
+    if (t >= a && t < jadd(a, b)) return jadd(a, b);
+    return JMAX;
+  }
+  int64_t clear_delay() const { return kind == SCOTTY_WIN_FIXED_BAND ? b : a; }
+};
+
+struct TrigWin {
+  int64_t start, end;
+  int32_t measure;
+};
+
+}  // namespace
+
+struct scotty_op {
+  int device = 0;
+  int vt = VT_I32;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool failed = false;
+
+  // ---- WindowManager / StreamSlicer scalars
+  std::vector<CFWin> windows;
+  std::vector<int> aggs;
+  int need = 0;
+  int64_t max_lateness = 1000;
+  int64_t max_fixed_window_size = 0;
+  bool has_fixed = false;
+  bool started = false;            // store non-empty (at least one tuple processed)
+  bool walk_pending = false;       // first context-free window added after tuples were processed
+  int64_t last_watermark = -1;
+  int64_t h_oldest = 0;            // t_start of the oldest retained slice (mirror)
+  int64_t h_prev_max = JMIN;       // mirror of DevMeta.prev_max after the last sync
+  int64_t last_span = 1000;        // event-time span of the last watermark interval (grid horizon sizing)
+
+  // ---- union edge grid (host copy of d_grid)
+  std::vector<int64_t> grid;
+  bool grid_complete = false;
+
+  // ---- device buffers
+  int64_t scap = 0, gcap = 0, ccap = 0, tcap = 0, wcap = 0;
+  DevMeta* d_meta = nullptr;
+  DevMeta* d_snap = nullptr;
+  DevMeta* h_snap = nullptr;  // pinned
+  int64_t* d_tstart = nullptr;
+  int64_t* d_tlast = nullptr;
+  unsigned long long* d_scnt = nullptr;
+  unsigned long long* d_spart[NPART] = {};
+  int64_t* d_grid = nullptr;
+  unsigned long long* d_ccnt = nullptr;
+  long long* d_ctmax = nullptr;
+  unsigned long long* d_cpart[NPART] = {};
+  long long* d_tilemax = nullptr;
+  long long* d_pmax = nullptr;
+  int32_t* d_rank = nullptr;
+  int32_t* d_flag = nullptr;
+  unsigned long long* d_scratch = nullptr;
+  // windows
+  int64_t* d_wstart = nullptr;
+  int64_t* d_wend = nullptr;
+  uint8_t* d_has = nullptr;
+  unsigned long long* d_ocnt = nullptr;
+  unsigned long long* d_opart[NPART] = {};
+  int64_t* h_wbuf = nullptr;        // pinned [2*wcap]
+  unsigned char* h_obuf = nullptr;  // pinned results
+
+  // ---- pushes of the current watermark interval (replayed after a horizon overflow)
+  struct Push {
+    const int64_t* ts;
+    const void* val;
+    int64_t n;
+    int64_t seq;
+  };
+  std::vector<Push> pending;
+  std::vector<void*> owned;  // staging copies of host pushes
+  int64_t push_seq = 0;
+  uint64_t dropped = 0, processed = 0;
+
+  // ---- timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;
+  double t_ms = 0.0;
+  uint64_t t_launches = 0, t_tuples = 0;
+
+  // ---- results
+  std::vector<TrigWin> trig;
+  std::vector<int64_t> r_start, r_end;
+  std::vector<int32_t> r_measure;
+  std::vector<uint8_t> r_has;
+  std::vector<std::vector<int64_t>> r_vals;
+};
+
+namespace {
+
+int fail(scotty_op* op, int code, const std::string& m) {
+  op->err = m;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      op->failed = true;                                                              \
+      return fail(op, SCOTTY_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+    }                                                                                 \
+  } while (0)
+
+int agg_value_type(int kind) {
+  switch (kind) {
+    case SCOTTY_AGG_SUM_I32: case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MAX_I32: return VT_I32;
+    case SCOTTY_AGG_SUM_I64: case SCOTTY_AGG_MIN_I64: case SCOTTY_AGG_MAX_I64: return VT_I64;
+    case SCOTTY_AGG_SUM_F64: case SCOTTY_AGG_MIN_F64: case SCOTTY_AGG_MAX_F64: return VT_F64;
+    case SCOTTY_AGG_COUNT: return -1;
+    default: return -2;
+  }
+}
+int agg_need(int kind) {
+  switch (kind) {
+    case SCOTTY_AGG_SUM_I32: case SCOTTY_AGG_SUM_I64: case SCOTTY_AGG_SUM_F64: return NEED_SUM;
+    case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MIN_I64: case SCOTTY_AGG_MIN_F64: return NEED_MIN;
+    case SCOTTY_AGG_MAX_I32: case SCOTTY_AGG_MAX_I64: case SCOTTY_AGG_MAX_F64: return NEED_MAX;
+    default: return 0;
+  }
+}
+
+double key_to_f64(int64_t k) {  // inverse of f64_key (slicing_kernels.hip)
+  int64_t b = k ^ ((k >> 63) & 0x7FFFFFFFFFFFFFFFLL);
+  double d;
+  std::memcpy(&d, &b, 8);
+  return d;
+}
+
+// lowered value of aggregation kind from (cnt, sum word, min word, max word)
+int64_t lower_value(int kind, uint64_t cnt, uint64_t sw, int64_t mn, int64_t mx) {
+  switch (kind) {
+    case SCOTTY_AGG_SUM_I32: return (int64_t)(int32_t)(uint32_t)sw;
+    case SCOTTY_AGG_COUNT: return (int64_t)(int32_t)(uint32_t)cnt;
+    case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MIN_I64: return mn;
+    case SCOTTY_AGG_MAX_I32: case SCOTTY_AGG_MAX_I64: return mx;
+    case SCOTTY_AGG_SUM_I64: return (int64_t)sw;
+    case SCOTTY_AGG_SUM_F64: return (int64_t)sw;  // already double bits
+    case SCOTTY_AGG_MIN_F64: {
+      double d = mn == INT64_MIN ? __builtin_nan("") : key_to_f64(mn);
+      int64_t b;
+      std::memcpy(&b, &d, 8);
+      return b;
+    }
+    case SCOTTY_AGG_MAX_F64: {
+      double d = mx == INT64_MAX ? __builtin_nan("") : key_to_f64(mx);
+      int64_t b;
+      std::memcpy(&b, &d, 8);
+      return b;
+    }
+  }
+  return 0;
+}
+
+// min over context-free time windows of assignNextWindowStart (StreamSlicer.calculateNextFixedEdge's loop,
+// S/StreamSlicer.java:108-114)
+int64_t next_edge(const scotty_op* op, int64_t t) {
+  int64_t e = JMAX;
+  for (const CFWin& w : op->windows) e = std::min(e, w.next_start(t));
+  return e;
+}
+
+// Union edge grid: first entry is the pending edge N, then every point of the union of the windows'
+// grids above N up to the horizon.  A finite grid (fixed-band windows only) ends with a JMAX sentinel.
+void build_grid(scotty_op* op, int64_t n_pending, int64_t horizon_end) {
+  op->grid.clear();
+  op->grid_complete = false;
+  if (n_pending == JMAX) {
+    op->grid.push_back(JMAX);
+    op->grid_complete = true;
+    return;
+  }
+  op->grid.push_back(n_pending);
+  // k-way merge of arithmetic progressions / fixed points
+  using Item = std::pair<int64_t, size_t>;
+  std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+  std::vector<int64_t> fixed_pts;
+  bool infinite = false;
+  for (size_t i = 0; i < op->windows.size(); i++) {
+    const CFWin& w = op->windows[i];
+    if (w.kind == SCOTTY_WIN_FIXED_BAND) {
+      fixed_pts.push_back(w.a);
+      fixed_pts.push_back(jadd(w.a, w.b));
+    } else {
+      infinite = true;
+      pq.push({w.next_start(n_pending), i});
+    }
+  }
+  for (int64_t p : fixed_pts)
+    if (p > n_pending) pq.push({p, (size_t)-1});
+  const int64_t cap = op->gcap - 1;
+  while (!pq.empty() && (int64_t)op->grid.size() < cap) {
+    Item it = pq.top();
+    pq.pop();
+    if (it.first <= op->grid.back()) {
+      if (it.second != (size_t)-1) {
+        const int64_t nx = op->windows[it.second].next_start(it.first);
+        if (nx > it.first) pq.push({nx, it.second});  // a progression that wraps past Long.MAX_VALUE ends
+      }
+      continue;
+    }
+    if (it.first > horizon_end && infinite) break;
+    op->grid.push_back(it.first);
+    if (it.second != (size_t)-1) pq.push({op->windows[it.second].next_start(it.first), it.second});
+  }
+  if (!infinite && pq.empty()) {
+    op->grid.push_back(JMAX);
+    op->grid_complete = true;
+  }
+}
+
+int upload_grid(scotty_op* op) {
+  HIPCHK(hipMemcpyAsync(op->d_grid, op->grid.data(), op->grid.size() * 8, hipMemcpyHostToDevice, op->stream));
+  // DevMeta.j0 = 0, gcount = grid.size()  (offsets of DevMeta fields)
+  int64_t v[2] = {0, (int64_t)op->grid.size()};
+  HIPCHK(hipMemcpyAsync(&op->d_meta->j0, v, 16, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  return SCOTTY_OK;
+}
+
+int alloc_all(scotty_op* op) {
+  op->scap = 1 << 20;
+  op->gcap = 1 << 20;
+  op->ccap = op->scap + op->gcap;
+  op->tcap = 0;
+  op->wcap = 0;
+  HIPCHK(hipSetDevice(op->device));
+  HIPCHK(hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking));
+  HIPCHK(hipMalloc(&op->d_meta, sizeof(DevMeta)));
+  HIPCHK(hipMalloc(&op->d_snap, sizeof(DevMeta)));
+  HIPCHK(hipHostMalloc(&op->h_snap, sizeof(DevMeta), hipHostMallocDefault));
+  HIPCHK(hipMemset(op->d_meta, 0, sizeof(DevMeta)));
+  HIPCHK(hipMalloc(&op->d_tstart, op->scap * 8));
+  HIPCHK(hipMalloc(&op->d_tlast, op->scap * 8));
+  HIPCHK(hipMalloc(&op->d_scnt, op->scap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_spart[k], op->scap * 8));
+  HIPCHK(hipMalloc(&op->d_grid, op->gcap * 8));
+  HIPCHK(hipMalloc(&op->d_ccnt, op->ccap * 8));
+  HIPCHK(hipMalloc(&op->d_ctmax, op->ccap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_cpart[k], op->ccap * 8));
+  HIPCHK(hipMalloc(&op->d_rank, op->gcap * 4));
+  HIPCHK(hipMalloc(&op->d_flag, op->gcap * 4));
+  HIPCHK(hipMalloc(&op->d_scratch, 64));
+  HIPCHK(launch_fill_u64(op->d_ccnt, op->ccap, 0, op->stream));
+  HIPCHK(launch_fill_u64((unsigned long long*)op->d_ctmax, op->ccap, (unsigned long long)INT64_MIN, op->stream));
+  HIPCHK(launch_fill_u64(op->d_cpart[0], op->ccap, 0, op->stream));
+  HIPCHK(launch_fill_u64(op->d_cpart[1], op->ccap, (unsigned long long)INT64_MAX, op->stream));
+  HIPCHK(launch_fill_u64(op->d_cpart[2], op->ccap, (unsigned long long)INT64_MIN, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  return SCOTTY_OK;
+}
+
+int ensure_tiles(scotty_op* op, int64_t n) {
+  int64_t nt = (n + TILE - 1) / TILE + 1;
+  if (nt <= op->tcap) return SCOTTY_OK;
+  HIPCHK(hipStreamSynchronize(op->stream));
+  if (op->d_tilemax) HIPCHK(hipFree(op->d_tilemax));
+  if (op->d_pmax) HIPCHK(hipFree(op->d_pmax));
+  op->tcap = std::max(nt, (int64_t)1024);
+  HIPCHK(hipMalloc(&op->d_tilemax, op->tcap * 8));
+  HIPCHK(hipMalloc(&op->d_pmax, op->tcap * 8));
+  return SCOTTY_OK;
+}
+
+int ensure_windows(scotty_op* op, int64_t nw) {
+  if (nw <= op->wcap) return SCOTTY_OK;
+  HIPCHK(hipStreamSynchronize(op->stream));
+  auto F = [&](void* p) { if (p) (void)hipFree(p); };
+  F(op->d_wstart); F(op->d_wend); F(op->d_has); F(op->d_ocnt);
+  for (int k = 0; k < NPART; k++) F(op->d_opart[k]);
+  if (op->h_wbuf) (void)hipHostFree(op->h_wbuf);
+  if (op->h_obuf) (void)hipHostFree(op->h_obuf);
+  op->wcap = ((std::max(nw, (int64_t)1024) + 63) / 64) * 64;
+  HIPCHK(hipMalloc(&op->d_wstart, op->wcap * 8));
+  HIPCHK(hipMalloc(&op->d_wend, op->wcap * 8));
+  HIPCHK(hipMalloc(&op->d_has, op->wcap));
+  HIPCHK(hipMalloc(&op->d_ocnt, op->wcap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_opart[k], op->wcap * 8));
+  HIPCHK(hipHostMalloc(&op->h_wbuf, op->wcap * 16, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc(&op->h_obuf, op->wcap * (1 + 8 * (1 + NPART)), hipHostMallocDefault));
+  return SCOTTY_OK;
+}
+
+// The first in-order tuple after the first context-free window exists runs StreamSlicer.determineSlices
+// with min_next_edge_ts == Long.MIN_VALUE (S/StreamSlicer.java:52-84): calculateNextFixedEdge starts from
+// Long.MAX_VALUE, whose assignNextWindowStart wraps negative, and the loop then walks up from te-maxLateness.
+// Returns the edges appended (in order) and the resulting pending edge.
+void first_walk(const scotty_op* op, int64_t te, std::vector<int64_t>& edges, int64_t& n_out) {
+  auto calc = [&](int64_t cur_next, int64_t t) {  // calculateNextFixedEdge
+    int64_t cur = cur_next == JMIN ? JMAX : cur_next;
+    int64_t tc = std::max(jsub(t, op->max_lateness), cur);
+    return next_edge(op, tc);
+  };
+  int64_t n = calc(JMIN, te);
+  while (te > n) {
+    if (n >= 0) edges.push_back(n);
+    n = calc(n, te);
+  }
+  if (n == te) {
+    edges.push_back(n);
+    n = calc(n, te);
+  }
+  n_out = n;
+}
+
+int compact_if_needed(scotty_op* op) {
+  DevMeta& m = *op->h_snap;
+  if (m.tail < op->scap / 2 || m.head == 0) return SCOTTY_OK;
+  const int64_t live = m.tail - m.head;
+  int64_t* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, std::max<int64_t>(live, 1) * 8));
+  int64_t* arrs[3 + NPART] = {op->d_tstart, op->d_tlast, (int64_t*)op->d_scnt, (int64_t*)op->d_spart[0],
+                             (int64_t*)op->d_spart[1], (int64_t*)op->d_spart[2]};
+  for (int64_t* a : arrs) {
+    HIPCHK(hipMemcpyAsync(tmp, a + m.head, live * 8, hipMemcpyDeviceToDevice, op->stream));
+    HIPCHK(hipMemcpyAsync(a, tmp, live * 8, hipMemcpyDeviceToDevice, op->stream));
+  }
+  int64_t ht[2] = {0, live};
+  HIPCHK(hipMemcpyAsync(&op->d_meta->head, ht, 16, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  HIPCHK(hipFree(tmp));
+  m.head = 0;
+  m.tail = live;
+  return SCOTTY_OK;
+}
+
+int sync_snapshot(scotty_op* op) {
+  HIPCHK(hipMemcpyAsync(op->h_snap, op->d_meta, sizeof(DevMeta), hipMemcpyDeviceToHost, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  return SCOTTY_OK;
+}
+
+// Runs the ingest + commit launches of one micro-batch (no host synchronisation).
+int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t seq) {
+  int rc = ensure_tiles(op, n);
+  if (rc) return rc;
+  IngestArgs ia{};
+  ia.ts = d_ts;
+  ia.val = d_val;
+  ia.n = n;
+  ia.s_tstart = op->d_tstart;
+  ia.grid = op->d_grid;
+  ia.c_cnt = op->d_ccnt;
+  ia.c_tmax = op->d_ctmax;
+  for (int k = 0; k < NPART; k++) ia.c_part[k] = op->d_cpart[k];
+  ia.tilemax = op->d_tilemax;
+  ia.meta = op->d_meta;
+  // ~4 workgroups per CU on 256 CUs; each wave streams a TILE-aligned contiguous range
+  const int64_t target_blocks = 1024;
+  int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
+  per_wave = ((per_wave + TILE - 1) / TILE) * TILE;
+  if (per_wave < TILE) per_wave = TILE;
+  ia.per_wave = per_wave;
+  const int64_t nblocks = (n + per_wave * 4 - 1) / (per_wave * 4);
+  std::pair<hipEvent_t, hipEvent_t> ev{};
+  if (op->timing) {
+    if (!op->ev_pool.empty()) {
+      ev = op->ev_pool.back();
+      op->ev_pool.pop_back();
+    } else {
+      HIPCHK(hipEventCreate(&ev.first));
+      HIPCHK(hipEventCreate(&ev.second));
+    }
+    HIPCHK(hipEventRecord(ev.first, op->stream));
+  }
+  HIPCHK(launch_ingest(ia, op->vt, op->need, nblocks, op->stream));
+  if (op->timing) {
+    HIPCHK(hipEventRecord(ev.second, op->stream));
+    op->ev_pending.push_back(ev);
+    op->t_tuples += n;
+  }
+  CommitArgs ca{};
+  ca.ts = d_ts;
+  ca.n = n;
+  ca.max_lateness = op->max_lateness;
+  ca.scap = op->scap;
+  ca.grid = op->d_grid;
+  ca.tilemax = op->d_tilemax;
+  ca.pmax = op->d_pmax;
+  ca.rank = op->d_rank;
+  ca.flag = op->d_flag;
+  ca.s_tstart = op->d_tstart;
+  ca.s_tlast = op->d_tlast;
+  ca.s_cnt = op->d_scnt;
+  for (int k = 0; k < NPART; k++) ca.s_part[k] = op->d_spart[k];
+  ca.c_cnt = op->d_ccnt;
+  ca.c_tmax = op->d_ctmax;
+  for (int k = 0; k < NPART; k++) ca.c_part[k] = op->d_cpart[k];
+  ca.meta = op->d_meta;
+  ca.need = op->need;
+  ca.vt = op->vt;
+  ca.push_seq = seq;
+  HIPCHK(launch_commit(ca, op->stream));
+  return SCOTTY_OK;
+}
+
+// First tuple of the operator's life: StreamSlicer + SliceManager for tuple 0 (the store is empty).
+int start_stream(scotty_op* op, int64_t ts0) {
+  std::vector<int64_t> edges;
+  int64_t n_pending = JMIN;
+  if (op->has_fixed) first_walk(op, ts0, edges, n_pending);
+  // SliceManager.processElement: an empty store first gets the slice [0, MAX) (S/SliceManager.java:49-51)
+  if (edges.empty()) edges.push_back(0);
+  const int64_t s0 = (int64_t)edges.size();
+  std::vector<int64_t> zeros(s0, 0), idmin(s0, INT64_MAX), idmax(s0, INT64_MIN);
+  HIPCHK(hipMemcpyAsync(op->d_tstart, edges.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(op->d_tlast, edges.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(op->d_scnt, zeros.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(op->d_spart[0], zeros.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(op->d_spart[1], idmin.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(op->d_spart[2], idmax.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  DevMeta m{};
+  m.head = 0;
+  m.tail = s0;
+  m.prev_max = ts0;  // maxEventTime after the first tuple
+  m.oldest_start = edges[0];
+  if (op->has_fixed) {
+    build_grid(op, n_pending, std::max(ts0, (int64_t)0) + std::max<int64_t>(64 * op->last_span, 600000));
+  } else {
+    op->grid.clear();
+  }
+  m.j0 = 0;
+  m.gcount = (int64_t)op->grid.size();
+  if (!op->grid.empty())
+    HIPCHK(hipMemcpyAsync(op->d_grid, op->grid.data(), op->grid.size() * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(op->d_meta, &m, sizeof(DevMeta), hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  *op->h_snap = m;
+  op->h_oldest = edges[0];
+  op->h_prev_max = ts0;
+  op->started = true;
+  return SCOTTY_OK;
+}
+
+// Re-extend the grid horizon from the current pending edge (only at synchronisation points).
+int maybe_extend_grid(scotty_op* op, bool force) {
+  if (!op->has_fixed || op->grid_complete) return SCOTTY_OK;
+  const DevMeta& m = *op->h_snap;
+  const int64_t j0 = m.j0;
+  const int64_t remaining = (int64_t)op->grid.size() - j0;
+  const int64_t last = op->grid.back();
+  const int64_t margin = std::max<int64_t>(16 * op->last_span, 60000);
+  if (!force && remaining > op->gcap / 4 && jsub(last, m.prev_max) > margin) return SCOTTY_OK;
+  const int64_t n_pending = op->grid[j0];
+  const int64_t need_to = std::max(m.batch_max, m.prev_max);
+  build_grid(op, n_pending, jadd(need_to, std::max<int64_t>(64 * op->last_span, 600000)));
+  if ((int64_t)op->grid.size() >= op->gcap - 1 && op->grid.back() <= need_to)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "micro-batch spans more edge-grid points than the grid capacity");
+  return upload_grid(op);
+}
+
+int replay_after_overflow(scotty_op* op) {
+  for (int attempt = 0; attempt < 4; attempt++) {
+    DevMeta& m = *op->h_snap;
+    if (!m.overflow) return SCOTTY_OK;
+    if (m.overflow == 2) return fail(op, SCOTTY_ERR_NOMEM, "slice capacity exceeded");
+    const int64_t failed = m.failed_push;
+    int64_t zero = 0;
+    HIPCHK(hipMemcpyAsync(&op->d_meta->overflow, &zero, 8, hipMemcpyHostToDevice, op->stream));
+    m.overflow = 0;
+    int rc = maybe_extend_grid(op, true);
+    if (rc) return rc;
+    for (auto& p : op->pending)
+      if (p.seq >= failed) {
+        rc = enqueue_push(op, p.ts, p.val, p.n, p.seq);
+        if (rc) return rc;
+      }
+    rc = sync_snapshot(op);
+    if (rc) return rc;
+  }
+  return fail(op, SCOTTY_ERR_UNSUPPORTED, "edge-grid horizon overflow could not be resolved");
+}
+
+void trigger_windows(scotty_op* op, int64_t last_wm, int64_t wm) {
+  // WindowManager.assignContextFreeWindows (S/WindowManager.java:104-118) in registration order
+  op->trig.clear();
+  for (const CFWin& w : op->windows) {
+    if (w.kind == SCOTTY_WIN_TUMBLING) {  // TumblingWindow.triggerWindows :34-39
+      const int64_t size = w.a;
+      const int64_t last_start = jsub(last_wm, jmod(jadd(last_wm, size), size));
+      for (int64_t ws = last_start; jadd(ws, size) <= wm; ws = jadd(ws, size))
+        op->trig.push_back({ws, jadd(ws, size), SCOTTY_MEASURE_TIME});
+    } else if (w.kind == SCOTTY_WIN_SLIDING) {  // SlidingWindow.triggerWindows :50-57
+      const int64_t size = w.a, slide = w.b;
+      const int64_t last_start = jsub(wm, jmod(jadd(wm, slide), slide));
+      for (int64_t ws = last_start; jadd(ws, size) > last_wm; ws = jsub(ws, slide))
+        if (ws >= 0 && jadd(ws, size) <= jadd(wm, 1)) op->trig.push_back({ws, jadd(ws, size), SCOTTY_MEASURE_TIME});
+    } else {  // FixedBandWindow.triggerWindows :51-57
+      const int64_t e = jadd(w.a, w.b);
+      if (last_wm <= e && e <= wm) op->trig.push_back({w.a, e, SCOTTY_MEASURE_TIME});
+    }
+  }
+}
+
+}  // namespace
+
+// ====================================================================== C-ABI
+extern "C" {
+
+int scotty_create(scotty_op** out, int device, int value_type, uint32_t flags) {
+  if (!out) return SCOTTY_ERR_ARG;
+  *out = nullptr;
+  if (value_type < VT_I32 || value_type > VT_F64) return SCOTTY_ERR_ARG;
+  if (flags & SCOTTY_FLAG_KEYED) return SCOTTY_ERR_UNSUPPORTED;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SCOTTY_ERR_HIP;
+  if (device < 0 || device >= ndev) return SCOTTY_ERR_ARG;
+  scotty_op* op = new scotty_op();
+  op->device = device;
+  op->vt = value_type;
+  int rc = alloc_all(op);
+  if (rc) {
+    scotty_destroy(op);
+    return rc;
+  }
+  *out = op;
+  return SCOTTY_OK;
+}
+
+void scotty_destroy(scotty_op* op) {
+  if (!op) return;
+  (void)hipSetDevice(op->device);
+  if (op->stream) (void)hipStreamSynchronize(op->stream);
+  auto F = [](void* p) { if (p) (void)hipFree(p); };
+  F(op->d_meta); F(op->d_snap); F(op->d_tstart); F(op->d_tlast); F(op->d_scnt); F(op->d_grid);
+  F(op->d_ccnt); F(op->d_ctmax); F(op->d_tilemax); F(op->d_pmax); F(op->d_rank); F(op->d_flag);
+  F(op->d_scratch); F(op->d_wstart); F(op->d_wend); F(op->d_has); F(op->d_ocnt);
+  for (int k = 0; k < NPART; k++) { F(op->d_spart[k]); F(op->d_cpart[k]); F(op->d_opart[k]); }
+  for (void* p : op->owned) F(p);
+  if (op->h_snap) (void)hipHostFree(op->h_snap);
+  if (op->h_wbuf) (void)hipHostFree(op->h_wbuf);
+  if (op->h_obuf) (void)hipHostFree(op->h_obuf);
+  for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  if (op->stream) (void)hipStreamDestroy(op->stream);
+  delete op;
+}
+
+const char* scotty_last_error(scotty_op* op) { return op ? op->err.c_str() : "null op"; }
+
+int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b) {
+  if (!op) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (kind < SCOTTY_WIN_TUMBLING || kind > SCOTTY_WIN_FIXED_BAND || (measure != SCOTTY_MEASURE_TIME &&
+                                                                     measure != SCOTTY_MEASURE_COUNT))
+    return fail(op, SCOTTY_ERR_ARG, "unknown window kind / measure");
+  if ((kind == SCOTTY_WIN_TUMBLING && a <= 0) || (kind == SCOTTY_WIN_SLIDING && (a <= 0 || b <= 0)))
+    return fail(op, SCOTTY_ERR_ARG, "window size / slide must be positive");
+  if (kind == SCOTTY_WIN_SESSION)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "SessionWindow is not implemented on the MI355X path yet");
+  if (measure == SCOTTY_MEASURE_COUNT)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "count-measure windows are not implemented on the MI355X path yet");
+  CFWin w{kind, a, b};
+  const bool had_fixed = op->has_fixed;
+  if (op->started && !had_fixed)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED,
+                "first context-free window added after elements were processed (edge walk would append "
+                "slices out of order)");
+  op->windows.push_back(w);
+  op->max_fixed_window_size = std::max(op->max_fixed_window_size, w.clear_delay());  // S/WindowManager.java:124
+  op->has_fixed = true;
+  if (op->started) {
+    // mid-stream addition: the pending edge N keeps its value (computed with the old grid); later edges
+    // follow the new union grid (StreamSlicer.calculateNextFixedEdge only runs at the next crossing).
+    int rc = sync_snapshot(op);
+    if (rc) return rc;
+    const int64_t n_pending = op->h_snap->gcount > 0 ? op->grid[op->h_snap->j0] : JMAX;
+    build_grid(op, n_pending, jadd(op->h_snap->prev_max, std::max<int64_t>(64 * op->last_span, 600000)));
+    rc = upload_grid(op);
+    if (rc) return rc;
+    rc = sync_snapshot(op);
+    if (rc) return rc;
+  }
+  return SCOTTY_OK;
+}
+
+int scotty_add_aggregation(scotty_op* op, int kind) {
+  if (!op) return SCOTTY_ERR_ARG;
+  const int vt = agg_value_type(kind);
+  if (vt == -2) return fail(op, SCOTTY_ERR_ARG, "unknown aggregation kind");
+  if (vt >= 0 && vt != op->vt) return fail(op, SCOTTY_ERR_ARG, "aggregation kind does not match the value type");
+  if ((int)op->aggs.size() >= SCOTTY_MAX_AGGS) return fail(op, SCOTTY_ERR_ARG, "too many aggregations");
+  if (op->started && (agg_need(kind) & ~op->need))
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "aggregation needing a new partial added after elements were processed");
+  op->aggs.push_back(kind);
+  op->need |= agg_need(kind);
+  return (int)op->aggs.size() - 1;
+}
+
+int scotty_set_max_lateness(scotty_op* op, int64_t l) {
+  if (!op) return SCOTTY_ERR_ARG;
+  op->max_lateness = l;
+  return SCOTTY_OK;
+}
+
+static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, const int64_t* h_ts0) {
+  if (n <= 0) return SCOTTY_OK;
+  int rc;
+  if (!op->started) {
+    int64_t ts0;
+    if (h_ts0) ts0 = *h_ts0;
+    else HIPCHK(hipMemcpy(&ts0, d_ts, 8, hipMemcpyDeviceToHost));
+    rc = start_stream(op, ts0);
+    if (rc) return rc;
+  }
+  const int64_t seq = op->push_seq++;
+  op->pending.push_back({d_ts, d_val, n, seq});
+  return enqueue_push(op, d_ts, d_val, n, seq);
+}
+
+int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, size_t n) {
+  if (!op || (n && (!ts || !val))) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (n == 0) return SCOTTY_OK;
+  const size_t vb = op->vt == VT_I32 ? 4 : 8;
+  void* d = nullptr;
+  HIPCHK(hipMalloc(&d, n * 8 + n * vb + 16));
+  int64_t* d_ts = (int64_t*)d;
+  void* d_val = (unsigned char*)d + ((n * 8 + 15) / 16) * 16;
+  op->owned.push_back(d);
+  HIPCHK(hipMemcpyAsync(d_ts, ts, n * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync(d_val, val, n * vb, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));  // host memory is consumed before return
+  return push_impl(op, d_ts, d_val, (int64_t)n, ts);
+}
+
+int scotty_process_elements_device(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n) {
+  if (!op || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (((uintptr_t)d_ts & 15) || ((uintptr_t)d_val & 15))
+    return fail(op, SCOTTY_ERR_ARG, "device buffers must be 16-byte aligned");
+  return push_impl(op, d_ts, d_val, (int64_t)n, nullptr);
+}
+
+int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
+  if (!op) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  int rc;
+  const uint64_t dropped_before = op->dropped;
+  // WindowManager.processWatermark (S/WindowManager.java:41-80)
+  if (op->last_watermark == -1) op->last_watermark = std::max((int64_t)0, jsub(wm, op->max_lateness));
+  op->r_start.clear(); op->r_end.clear(); op->r_measure.clear(); op->r_has.clear();
+  op->r_vals.assign(op->aggs.size(), {});
+  if (!op->started) {
+    op->last_watermark = wm;
+  } else {
+    int64_t last_wm = op->last_watermark;
+    if (last_wm < op->h_oldest) last_wm = op->h_oldest;
+    trigger_windows(op, last_wm, wm);
+    const int64_t nw = (int64_t)op->trig.size();
+    rc = ensure_windows(op, nw);
+    if (rc) return rc;
+    const int64_t remove_from = jsub(jsub(wm, op->max_lateness), op->max_fixed_window_size);
+    for (int attempt = 0; attempt < 2; attempt++) {
+      if (nw > 0) {
+        for (int64_t i = 0; i < nw; i++) {
+          op->h_wbuf[i] = op->trig[i].start;
+          op->h_wbuf[op->wcap + i] = op->trig[i].end;
+        }
+        HIPCHK(hipMemcpyAsync(op->d_wstart, op->h_wbuf, nw * 8, hipMemcpyHostToDevice, op->stream));
+        HIPCHK(hipMemcpyAsync(op->d_wend, op->h_wbuf + op->wcap, nw * 8, hipMemcpyHostToDevice, op->stream));
+        WindowArgs wa{};
+        wa.w_start = op->d_wstart;
+        wa.w_end = op->d_wend;
+        wa.n_windows = nw;
+        wa.s_tstart = op->d_tstart;
+        wa.s_tlast = op->d_tlast;
+        wa.s_cnt = op->d_scnt;
+        for (int k = 0; k < NPART; k++) wa.s_part[k] = op->d_spart[k];
+        wa.meta = op->d_meta;
+        wa.has_value = op->d_has;
+        wa.o_cnt = op->d_ocnt;
+        for (int k = 0; k < NPART; k++) wa.o_part[k] = op->d_opart[k];
+        wa.need = op->need;
+        wa.vt = op->vt;
+        HIPCHK(launch_windows(wa, op->stream));
+        unsigned char* hb = op->h_obuf;
+        HIPCHK(hipMemcpyAsync(hb, op->d_has, nw, hipMemcpyDeviceToHost, op->stream));
+        HIPCHK(hipMemcpyAsync(hb + op->wcap, op->d_ocnt, nw * 8, hipMemcpyDeviceToHost, op->stream));
+        for (int k = 0; k < NPART; k++)
+          HIPCHK(hipMemcpyAsync(hb + op->wcap * (1 + 8 * (1 + k)), op->d_opart[k], nw * 8, hipMemcpyDeviceToHost,
+                                op->stream));
+      }
+      HIPCHK(launch_gc(op->d_meta, op->d_tstart, remove_from, op->d_snap, op->stream));
+      HIPCHK(hipMemcpyAsync(op->h_snap, op->d_snap, sizeof(DevMeta), hipMemcpyDeviceToHost, op->stream));
+      HIPCHK(hipStreamSynchronize(op->stream));
+      if (!op->h_snap->overflow) break;
+      rc = replay_after_overflow(op);
+      if (rc) {
+        op->failed = true;
+        return rc;
+      }
+    }
+    if (op->h_snap->overflow) {
+      op->failed = true;
+      return fail(op, SCOTTY_ERR_UNSUPPORTED, "edge-grid horizon overflow");
+    }
+    // results (AggregateWindowState.getAggValues / hasValue, S/state/AggregateWindowState.java:41-49)
+    const unsigned char* hb = op->h_obuf;
+    const uint64_t* ocnt = (const uint64_t*)(hb + op->wcap);
+    const uint64_t* op0 = (const uint64_t*)(hb + op->wcap * (1 + 8));
+    const int64_t* op1 = (const int64_t*)(hb + op->wcap * (1 + 16));
+    const int64_t* op2 = (const int64_t*)(hb + op->wcap * (1 + 24));
+    for (int64_t i = 0; i < nw; i++) {
+      op->r_start.push_back(op->trig[i].start);
+      op->r_end.push_back(op->trig[i].end);
+      op->r_measure.push_back(op->trig[i].measure);
+      op->r_has.push_back(hb[i]);
+      for (size_t k = 0; k < op->aggs.size(); k++)
+        op->r_vals[k].push_back(hb[i] ? lower_value(op->aggs[k], ocnt[i], op0[i], op1[i], op2[i]) : 0);
+    }
+    op->last_watermark = wm;
+    // bookkeeping at the synchronisation point
+    const DevMeta& m = *op->h_snap;
+    op->last_span = std::max<int64_t>(1, jsub(m.prev_max, op->h_prev_max));
+    op->h_prev_max = m.prev_max;
+    op->h_oldest = m.oldest_start;
+    op->dropped = m.late_total;
+    op->processed = m.processed_total;
+    rc = maybe_extend_grid(op, false);
+    if (rc) return rc;
+    rc = compact_if_needed(op);
+    if (rc) return rc;
+  }
+  // timing of the ingest launches of this interval
+  for (auto& e : op->ev_pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) op->t_ms += ms;
+    op->t_launches++;
+    op->ev_pool.push_back(e);
+  }
+  op->ev_pending.clear();
+  for (void* p : op->owned) (void)hipFree(p);
+  op->owned.clear();
+  op->pending.clear();
+  if (out) {
+    std::memset(out, 0, sizeof(*out));
+    out->n_windows = op->r_start.size();
+    out->n_aggs = (int32_t)op->aggs.size();
+    out->start = op->r_start.data();
+    out->end = op->r_end.data();
+    out->measure = op->r_measure.data();
+    out->has_value = op->r_has.data();
+    for (size_t k = 0; k < op->aggs.size(); k++) out->values[k] = op->r_vals[k].data();
+  }
+  if (op->dropped > dropped_before) {
+    op->err = "tuples older than the oldest retained slice were dropped (reference: IndexOutOfBoundsException)";
+    return SCOTTY_WARN_LATE_DROPPED;
+  }
+  return SCOTTY_OK;
+}
+
+uint64_t scotty_dropped_count(scotty_op* op) { return op ? op->dropped : 0; }
+uint64_t scotty_processed_count(scotty_op* op) { return op ? op->processed : 0; }
+int64_t scotty_slice_count(scotty_op* op) {
+  if (!op || !op->started) return 0;
+  if (sync_snapshot(op)) return -1;
+  return op->h_snap->tail - op->h_snap->head;
+}
+
+int scotty_enable_timing(scotty_op* op, int on) {
+  if (!op) return SCOTTY_ERR_ARG;
+  op->timing = on != 0;
+  op->t_ms = 0.0;
+  op->t_launches = 0;
+  op->t_tuples = 0;
+  return SCOTTY_OK;
+}
+
+int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, uint64_t* tuples) {
+  if (!op) return SCOTTY_ERR_ARG;
+  if (total_ms) *total_ms = op->t_ms;
+  if (launches) *launches = op->t_launches;
+  if (tuples) *tuples = op->t_tuples;
+  return SCOTTY_OK;
+}
+
+int scotty_sync(scotty_op* op) {
+  if (!op) return SCOTTY_ERR_ARG;
+  HIPCHK(hipStreamSynchronize(op->stream));
+  return SCOTTY_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,758 @@
+// slicing_kernels.hip -- gfx950 kernels of the general-stream-slicing hot path.
+//
+// One micro-batch (all processElement calls between two processWatermark calls, in arrival order)
+// is handled by three launches on the op's stream:
+//   1. ingest_kernel   (the hot, HBM-bound pass; replaces SliceManager.processElement ->
+//                       AggregationStore.insertValueToSlice / findSliceIndexByTimestamp, S/SliceManager.java:47-87,
+//                       S/aggregationstore/LazyAggregateStore.java:29-37, and EagerSlice.addElement ->
+//                       AggregateValueState.addElement, S/slice/EagerSlice.java:23-26,
+//                       S/state/AggregateValueState.java:23-31).
+//      Every tuple is lifted and combined into a "cell": cells are the retained slices of the store plus
+//      every grid point of the union edge grid above the running max.  Slices of the reference are
+//      unions of consecutive cells, so partials per cell are exact refinements.  Reads ts (8 B) + value
+//      once, coalesced 16 B / lane; per-wave register accumulators for the cell most tuples of an
+//      arrival-ordered wave fall into; LDS-window atomics for the rest (out-of-order tuples);
+//      max ts per 4096-tuple arrival tile.
+//   2. commit_kernel   (one workgroup; replaces StreamSlicer.determineSlices / calculateNextFixedEdge,
+//                       S/StreamSlicer.java:36-116, and SliceManager.appendSlice, S/SliceManager.java:27-38):
+//      decides which grid points become slice edges with the reference's rule, evaluated for every
+//      candidate in parallel from first-crossing lookups (prefix max over tile maxima + an exact
+//      in-tile scan for the rare ambiguous case), appends the new slices and folds cells into slices.
+//   3. window_kernel + gc_kernel at a watermark (replace LazyAggregateStore.aggregate,
+//      S/aggregationstore/LazyAggregateStore.java:83-111, AggregateWindowState.containsSlice/addState,
+//      S/state/AggregateWindowState.java:25-53, and WindowManager.clearAfterWatermark /
+//      LazyAggregateStore.removeSlices, S/WindowManager.java:82-95, LazyAggregateStore.java:138-146).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "device_common.h"
+
+namespace scotty {
+
+// ---------------------------------------------------------------- small helpers
+__device__ __forceinline__ int64_t rl64(int64_t v, int lane) {
+  uint32_t lo = __builtin_amdgcn_readlane((uint32_t)(uint64_t)v, lane);
+  uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t uni64(int64_t v) {  // make a wave-uniform value scalar
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t wmax64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, o));
+  return v;
+}
+__device__ __forceinline__ int64_t wmin64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, o));
+  return v;
+}
+__device__ __forceinline__ uint64_t wsum64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o);
+  return v;
+}
+__device__ __forceinline__ double wsumf(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t wsum32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  return v;
+}
+
+// Ordered int64 keys for Java Math.min/Math.max on double: NaN dominates, -0.0 < +0.0.
+__device__ __forceinline__ int64_t f64_key(double d) {
+  int64_t b = __double_as_longlong(d);
+  return b ^ ((b >> 63) & 0x7FFFFFFFFFFFFFFFLL);
+}
+__device__ __forceinline__ int64_t f64_min_key(double d) { return d != d ? INT64_MIN : f64_key(d); }
+__device__ __forceinline__ int64_t f64_max_key(double d) { return d != d ? INT64_MAX : f64_key(d); }
+
+constexpr int64_t PART_ID_MIN = INT64_MAX;
+constexpr int64_t PART_ID_MAX = INT64_MIN;
+
+// virtual cell-start table: cells [0, c_old) are retained slices, cells c_old + k are grid cells
+struct CellView {
+  const int64_t* tstart;  // + head
+  const int64_t* grid;    // + j0
+  int64_t c_old, kc, h_end;
+  __device__ __forceinline__ int64_t start(int64_t c) const {
+    return c < c_old ? tstart[c] : (c - c_old < kc ? grid[c - c_old] : h_end);
+  }
+  // largest c with start(c) <= t; requires start(0) <= t < h_end
+  __device__ int64_t find(int64_t t) const {
+    if (kc > 0 && t >= grid[0]) {
+      int64_t lo = 0, hi = kc;  // find last k in [0,kc) with grid[k] <= t
+      while (hi - lo > 1) {
+        int64_t mid = (lo + hi) >> 1;
+        if (grid[mid] <= t) lo = mid; else hi = mid;
+      }
+      return c_old + lo;
+    }
+    int64_t lo = 0, hi = c_old;
+    while (hi - lo > 1) {
+      int64_t mid = (lo + hi) >> 1;
+      if (tstart[mid] <= t) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
+};
+
+template <int VT>
+struct ValT;
+template <> struct ValT<VT_I32> { using T = int32_t; };
+template <> struct ValT<VT_I64> { using T = int64_t; };
+template <> struct ValT<VT_F64> { using T = double; };
+
+// per-lane accumulator of one cell
+template <int VT, int NEED>
+struct Acc {
+  uint32_t cnt;
+  int64_t tmax;
+  typename std::conditional<VT == VT_F64, double, typename std::conditional<VT == VT_I32, uint32_t, uint64_t>::type>::type sum;
+  int64_t mn, mx;
+  __device__ __forceinline__ void reset() {
+    cnt = 0; tmax = INT64_MIN; sum = 0; mn = PART_ID_MIN; mx = PART_ID_MAX;
+  }
+  __device__ __forceinline__ void add(int64_t t, typename ValT<VT>::T v) {
+    cnt += 1;
+    tmax = max(tmax, t);
+    if constexpr ((NEED & NEED_SUM) != 0) {
+      if constexpr (VT == VT_I32) sum += (uint32_t)v;
+      else if constexpr (VT == VT_I64) sum += (uint64_t)v;
+      else sum += v;
+    }
+    if constexpr ((NEED & NEED_MIN) != 0) {
+      if constexpr (VT == VT_F64) mn = min(mn, f64_min_key(v));
+      else mn = min(mn, (int64_t)v);
+    }
+    if constexpr ((NEED & NEED_MAX) != 0) {
+      if constexpr (VT == VT_F64) mx = max(mx, f64_max_key(v));
+      else mx = max(mx, (int64_t)v);
+    }
+  }
+  // sum word as stored in cells / slices (u64 for integers, double bits for f64)
+  __device__ __forceinline__ uint64_t sum_word() const {
+    if constexpr (VT == VT_F64) return 0;
+    else return (uint64_t)sum;
+  }
+  __device__ __forceinline__ double sum_f() const {
+    if constexpr (VT == VT_F64) return sum;
+    else return 0.0;
+  }
+};
+
+
+// LDS cell window of a workgroup
+struct LdsWin {
+  int64_t* tw;                // [WCAP+1] cell starts
+  uint32_t* cnt;              // [WCAP]
+  long long* tmax;            // [WCAP]
+  unsigned long long* part[NPART];
+};
+
+template <int VT, int NEED>
+__device__ __forceinline__ void lds_add(const LdsWin& w, int64_t i, uint32_t cnt, int64_t tmax, uint64_t sumw,
+                                        double sumf, int64_t mn, int64_t mx) {
+  atomicAdd(&w.cnt[i], cnt);
+  atomicMax(&w.tmax[i], (long long)tmax);
+  if constexpr ((NEED & NEED_SUM) != 0) {
+    if constexpr (VT == VT_F64) atomicAdd((double*)&w.part[0][i], sumf);
+    else atomicAdd(&w.part[0][i], (unsigned long long)sumw);
+  }
+  if constexpr ((NEED & NEED_MIN) != 0) atomicMin((long long*)&w.part[1][i], (long long)mn);
+  if constexpr ((NEED & NEED_MAX) != 0) atomicMax((long long*)&w.part[2][i], (long long)mx);
+}
+
+template <int VT, int NEED>
+__device__ __forceinline__ void glb_add(const IngestArgs& a, int64_t c, uint64_t cnt, int64_t tmax, uint64_t sumw,
+                                        double sumf, int64_t mn, int64_t mx) {
+  atomicAdd(&a.c_cnt[c], (unsigned long long)cnt);
+  atomicMax(&a.c_tmax[c], (long long)tmax);
+  if constexpr ((NEED & NEED_SUM) != 0) {
+    if constexpr (VT == VT_F64) atomicAdd((double*)&a.c_part[0][c], sumf);
+    else atomicAdd(&a.c_part[0][c], (unsigned long long)sumw);
+  }
+  if constexpr ((NEED & NEED_MIN) != 0) atomicMin((long long*)&a.c_part[1][c], (long long)mn);
+  if constexpr ((NEED & NEED_MAX) != 0) atomicMax((long long*)&a.c_part[2][c], (long long)mx);
+}
+
+// ================================================================ 1. ingest
+template <int VT, int NEED>
+__global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
+  using V = typename ValT<VT>::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int64_t* sc = (int64_t*)smem;  // block scalars [16]
+  LdsWin w;
+  w.tw = (int64_t*)(smem + 128);
+  w.cnt = (uint32_t*)(smem + 128 + 8 * (WCAP + 2));
+  w.tmax = (long long*)((unsigned char*)w.cnt + 4 * WCAP);
+  unsigned char* p = (unsigned char*)(w.tmax + WCAP);
+#pragma unroll
+  for (int k = 0; k < NPART; k++) {
+    if (NEED & (1 << k)) {
+      w.part[k] = (unsigned long long*)p;
+      p += 8 * WCAP;
+    } else {
+      w.part[k] = nullptr;
+    }
+  }
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int64_t per_block = a.per_wave * 4;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = min(a.n, b0 + per_block);
+
+  if (tid == 0) {
+    const DevMeta& m = *a.meta;
+    int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
+    int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+    if (kc < 0) kc = 0;
+    int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
+    CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+    int64_t ctot = cv.c_old + kc;
+    int64_t first_start = cv.start(0);
+    int64_t x = max(a.ts[b0], a.ts[b1 - 1]);
+    int64_t chi;
+    if (x < first_start) chi = 0;
+    else if (x >= h_end) chi = ctot - 1;
+    else chi = cv.find(x);
+    int64_t wbase = max((int64_t)0, chi + 16 - WCAP);
+    int64_t wn = min((int64_t)WCAP, ctot - wbase);
+    sc[0] = m.overflow;
+    sc[1] = head; sc[2] = tail; sc[3] = j0; sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
+    sc[7] = wbase; sc[8] = wn;
+  }
+  __syncthreads();
+  if (sc[0] != 0) return;  // an earlier push of this interval overflowed: nothing is committed until replay
+  const int64_t head = sc[1], tail = sc[2], j0 = sc[3], kc = sc[4], h_end = sc[5], first_start = sc[6];
+  const int64_t wbase = sc[7], wn = sc[8];
+  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+  for (int64_t i = tid; i <= wn; i += 256) w.tw[i] = cv.start(wbase + i);
+  for (int64_t i = tid; i < wn; i += 256) {
+    w.cnt[i] = 0;
+    w.tmax[i] = INT64_MIN;
+    if (NEED & NEED_SUM) w.part[0][i] = 0;
+    if (NEED & NEED_MIN) w.part[1][i] = (unsigned long long)PART_ID_MIN;
+    if (NEED & NEED_MAX) w.part[2][i] = (unsigned long long)PART_ID_MAX;
+  }
+  __syncthreads();
+  const int64_t tw0 = w.tw[0], twn = w.tw[wn];
+
+  const int64_t w0 = b0 + (int64_t)wid * a.per_wave;
+  const int64_t w1 = min(b1, w0 + a.per_wave);
+
+  Acc<VT, NEED> acc;
+  acc.reset();
+  int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
+  uint32_t n_late = 0, n_ovf = 0;
+  int64_t tile_max = INT64_MIN;
+
+  auto flush = [&]() {
+    uint32_t c = wsum32(acc.cnt);
+    if (c != 0) {
+      int64_t tm = wmax64(acc.tmax);
+      uint64_t sw = 0;
+      double sf = 0.0;
+      if constexpr ((NEED & NEED_SUM) != 0) {
+        if constexpr (VT == VT_F64) sf = wsumf(acc.sum_f());
+        else sw = wsum64(acc.sum_word());
+      }
+      int64_t mn = (NEED & NEED_MIN) ? wmin64(acc.mn) : 0;
+      int64_t mx = (NEED & NEED_MAX) ? wmax64(acc.mx) : 0;
+      if (lane == 0) {
+        if (cstar >= wbase && cstar < wbase + wn) lds_add<VT, NEED>(w, cstar - wbase, c, tm, sw, sf, mn, mx);
+        else glb_add<VT, NEED>(a, cstar, c, tm, sw, sf, mn, mx);
+      }
+    }
+    acc.reset();
+  };
+
+  auto slow = [&](int64_t t, V v) {
+    if (t < first_start) {
+      n_late++;
+    } else if (t >= h_end && h_end != INT64_MAX) {
+      n_ovf++;
+    } else if (t >= tw0 && t < twn) {
+      int64_t l = 0, h = wn;
+      while (h - l > 1) {
+        int64_t mid = (l + h) >> 1;
+        if (w.tw[mid] <= t) l = mid; else h = mid;
+      }
+      Acc<VT, NEED> one;
+      one.reset();
+      one.add(t, v);
+      const uint64_t sw = one.sum_word();
+      const double sf = one.sum_f();
+      lds_add<VT, NEED>(w, l, 1u, t, sw, sf, one.mn, one.mx);
+    } else {
+      int64_t c = cv.find(t);
+      Acc<VT, NEED> one;
+      one.reset();
+      one.add(t, v);
+      const uint64_t sw = one.sum_word();
+      const double sf = one.sum_f();
+      glb_add<VT, NEED>(a, c, 1u, t, sw, sf, one.mn, one.mx);
+    }
+  };
+
+  for (int64_t s = w0; s < w1; s += 256) {
+    const bool full = s + 256 <= w1;
+    int64_t t[4];
+    V v[4];
+    const int64_t i0 = s + 2 * lane, i1 = s + 128 + 2 * lane;
+    if (full) {
+      const longlong2 ta = *reinterpret_cast<const longlong2*>(a.ts + i0);
+      const longlong2 tb = *reinterpret_cast<const longlong2*>(a.ts + i1);
+      t[0] = ta.x; t[1] = ta.y; t[2] = tb.x; t[3] = tb.y;
+      const V* vp = (const V*)a.val;
+      if (VT == VT_I32) {
+        const int2 va = *reinterpret_cast<const int2*>(vp + i0);
+        const int2 vb = *reinterpret_cast<const int2*>(vp + i1);
+        v[0] = (V)va.x; v[1] = (V)va.y; v[2] = (V)vb.x; v[3] = (V)vb.y;
+      } else {
+        const longlong2 va = *reinterpret_cast<const longlong2*>(vp + i0);
+        const longlong2 vb = *reinterpret_cast<const longlong2*>(vp + i1);
+        if (VT == VT_I64) {
+          v[0] = (V)va.x; v[1] = (V)va.y; v[2] = (V)vb.x; v[3] = (V)vb.y;
+        } else {
+          v[0] = (V)__longlong_as_double(va.x); v[1] = (V)__longlong_as_double(va.y);
+          v[2] = (V)__longlong_as_double(vb.x); v[3] = (V)__longlong_as_double(vb.y);
+        }
+      }
+      // move the wave's current cell forward when the stream has advanced past it
+      const int64_t x = rl64(t[3], 63);
+      if (x >= hi && x >= first_start && (x < h_end || h_end == INT64_MAX)) {
+        flush();
+        int64_t c;
+        if (x >= tw0 && x < twn) {
+          int64_t l = 0, h = wn;
+          while (h - l > 1) {
+            int64_t mid = (l + h) >> 1;
+            if (w.tw[mid] <= x) l = mid; else h = mid;
+          }
+          c = wbase + l;
+          lo = w.tw[l];
+          hi = w.tw[l + 1];
+        } else {
+          c = cv.find(x);
+          lo = cv.start(c);
+          hi = cv.start(c + 1);
+        }
+        cstar = uni64(c);
+        lo = uni64(lo);
+        hi = uni64(hi);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        tile_max = max(tile_max, t[j]);
+        if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
+        else slow(t[j], v[j]);
+      }
+    } else {
+      const V* vp = (const V*)a.val;
+      const int64_t idx[4] = {i0, i0 + 1, i1, i1 + 1};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (idx[j] < w1) {
+          int64_t tj = a.ts[idx[j]];
+          V vj = vp[idx[j]];
+          tile_max = max(tile_max, tj);
+          if (tj >= lo && tj < hi) acc.add(tj, vj);
+          else slow(tj, vj);
+        }
+      }
+    }
+    const int64_t done = s + 256;
+    if (((done - w0) % TILE) == 0 || done >= w1) {
+      int64_t tm = wmax64(tile_max);
+      if (lane == 0) a.tilemax[s / TILE] = tm;
+      tile_max = INT64_MIN;
+    }
+  }
+  flush();
+  {
+    uint32_t nl = wsum32(n_late), no = wsum32(n_ovf);
+    if (lane == 0 && (nl | no)) {
+      if (nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
+      if (no) atomicAdd((unsigned long long*)&a.meta->overflow_push, (unsigned long long)no);
+    }
+  }
+  __syncthreads();
+  for (int64_t i = tid; i < wn; i += 256) {
+    uint32_t c = w.cnt[i];
+    if (c) {
+      uint64_t sw = (NEED & NEED_SUM) ? w.part[0][i] : 0;
+      double sf = (NEED & NEED_SUM) ? __longlong_as_double((long long)sw) : 0.0;
+      glb_add<VT, NEED>(a, wbase + i, c, w.tmax[i], sw, sf, (NEED & NEED_MIN) ? (int64_t)w.part[1][i] : 0,
+                        (NEED & NEED_MAX) ? (int64_t)w.part[2][i] : 0);
+    }
+  }
+}
+
+// ================================================================ 2. commit (single workgroup)
+__device__ __forceinline__ int64_t lower_bound_i64(const long long* a, int64_t n, int64_t x) {  // first a[i] >= x
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
+  __shared__ long long s_red[1024];
+  __shared__ int64_t sc[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    const DevMeta& m = *a.meta;
+    sc[0] = m.overflow; sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount; sc[5] = m.prev_max;
+  }
+  __syncthreads();
+  if (sc[0] != 0) return;
+  const int64_t head = sc[1], tail = sc[2], j0 = sc[3], gcount = sc[4], prev_max = sc[5];
+  const int64_t c_old = tail - head;
+  int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+  if (kc < 0) kc = 0;
+  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
+  const int64_t* g = a.grid + j0;
+  const int64_t L = a.max_lateness;
+
+  // ---- (a) prefix max over tile maxima (arrival order)
+  const int64_t nT = (a.n + TILE - 1) / TILE;
+  const int64_t ch = (nT + 1023) / 1024;
+  const int64_t t0 = tid * ch, t1 = min(nT, t0 + ch);
+  long long lm = INT64_MIN;
+  for (int64_t t = t0; t < t1; t++) lm = max(lm, a.tilemax[t]);
+  s_red[tid] = lm;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive max scan (Hillis-Steele)
+    long long v = tid >= o ? s_red[tid - o] : INT64_MIN;
+    __syncthreads();
+    s_red[tid] = max(s_red[tid], v);
+    __syncthreads();
+  }
+  long long run = tid > 0 ? s_red[tid - 1] : INT64_MIN;
+  for (int64_t t = t0; t < t1; t++) {
+    run = max(run, a.tilemax[t]);
+    a.pmax[t] = run;
+  }
+  const int64_t batch_max = max(prev_max, (int64_t)s_red[1023]);
+  __syncthreads();
+
+  // ---- (b) candidates: grid points g[k] <= batch_max (k < kc)
+  if (tid == 0) {
+    int64_t lo = 0, hi = kc;  // count of g[k] <= batch_max
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (g[mid] <= batch_max) lo = mid + 1; else hi = mid;
+    }
+    sc[8] = lo;
+    sc[9] = (h_end != INT64_MAX && batch_max >= h_end) ? 1 : 0;
+  }
+  __syncthreads();
+  const int64_t ncand = sc[8];
+  int ovf = (int)sc[9];
+
+  // ---- (c) edge decision, StreamSlicer.determineSlices (S/StreamSlicer.java:55-84) per candidate.
+  // For a grid point g with pending edge N (g in the effective grid above N's predecessor) the
+  // in-order tuple e(g) that first reaches g appends {N} U {g' : max(N, e - maxLateness) < g' <= e};
+  // hence g becomes an edge iff g == nextGrid(m(g)) or e(g) - g < maxLateness, where m(g) is the
+  // running max before e(g).  e(g), m(g) come from the tile prefix maxima; ambiguous cases scan the tile.
+  if (!ovf) {
+    for (int64_t k = tid; k < ncand; k += 1024) {
+      const int64_t gk = g[k];
+      const int64_t ts_ = lower_bound_i64(a.pmax, nT, gk);
+      const int64_t pprev = ts_ > 0 ? max(prev_max, (int64_t)a.pmax[ts_ - 1]) : prev_max;
+      const int64_t tm = a.tilemax[ts_];
+      int f;
+      if (k == 0 || g[k - 1] <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < L) f = 1;
+      else f = 2;
+      a.flag[k] = f;
+    }
+  }
+  __syncthreads();
+  if (!ovf) {
+    for (int64_t k = wid; k < ncand; k += 16) {
+      if (a.flag[k] != 2) continue;
+      const int64_t gk = g[k];
+      const int64_t ts_ = lower_bound_i64(a.pmax, nT, gk);
+      int64_t r = ts_ > 0 ? max(prev_max, (int64_t)a.pmax[ts_ - 1]) : prev_max;
+      const int64_t e0 = ts_ * TILE, e1 = min(a.n, e0 + TILE);
+      int64_t e = INT64_MIN, m = INT64_MIN;
+      for (int64_t base = e0; base < e1; base += 64) {
+        const int64_t i = base + lane;
+        const int64_t v = i < e1 ? a.ts[i] : INT64_MIN;
+        // inclusive prefix max within the wave
+        int64_t incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          int64_t u = (int64_t)__shfl_up((long long)incl, o);
+          if (lane >= o) incl = max(incl, u);
+        }
+        int64_t excl = (int64_t)__shfl_up((long long)incl, 1);
+        if (lane == 0) excl = INT64_MIN;
+        excl = max(excl, r);
+        const unsigned long long hit = __ballot(v >= gk);
+        if (hit) {
+          const int f = __ffsll((long long)hit) - 1;
+          e = rl64(v, f);
+          m = rl64(excl, f);
+          break;
+        }
+        r = max(r, rl64(incl, 63));
+      }
+      if (lane == 0) {
+        const bool emit = (int64_t)((uint64_t)e - (uint64_t)gk) < L || g[k - 1] <= m;
+        a.flag[k] = emit ? 1 : 0;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- (d) rank = inclusive prefix count of emitted edges
+  int64_t n_emit = 0;
+  if (!ovf) {
+    long long carry = 0;
+    for (int64_t base = 0; base < ncand; base += 1024) {
+      const int64_t k = base + tid;
+      const int f = (k < ncand && a.flag[k] == 1) ? 1 : 0;
+      s_red[tid] = f;
+      __syncthreads();
+      for (int o = 1; o < 1024; o <<= 1) {
+        long long v = tid >= o ? s_red[tid - o] : 0;
+        __syncthreads();
+        s_red[tid] += v;
+        __syncthreads();
+      }
+      if (k < ncand) a.rank[k] = (int32_t)(carry + s_red[tid]);
+      carry += s_red[1023];
+      __syncthreads();
+    }
+    n_emit = carry;
+    if (tail + n_emit > a.scap) ovf = 2;
+  }
+
+  if (!ovf) {
+    // ---- (e) append new slices (SliceManager.appendSlice: tStart = edge, tLast = tStart, empty partial)
+    for (int64_t k = tid; k < ncand; k += 1024) {
+      if (a.flag[k] == 1) {
+        const int64_t s = tail + a.rank[k] - 1;
+        a.s_tstart[s] = g[k];
+        a.s_tlast[s] = g[k];
+        a.s_cnt[s] = 0;
+        a.s_part[0][s] = 0;
+        a.s_part[1][s] = (unsigned long long)PART_ID_MIN;
+        a.s_part[2][s] = (unsigned long long)PART_ID_MAX;
+      }
+    }
+    __syncthreads();
+    // ---- (f) fold cells into slices (AbstractSlice.addElement + AggregateState.merge semantics)
+    const int64_t ncell = c_old + ncand;
+    for (int64_t c = tid; c < ncell; c += 1024) {
+      const unsigned long long cnt = a.c_cnt[c];
+      if (cnt == 0) continue;
+      int64_t s;
+      if (c < c_old) {
+        s = head + c;
+      } else {
+        const int32_t r = a.rank[c - c_old];
+        s = r > 0 ? tail + r - 1 : tail - 1;
+      }
+      atomicAdd(&a.s_cnt[s], cnt);
+      atomicMax((long long*)&a.s_tlast[s], a.c_tmax[c]);
+      if (a.need & NEED_SUM) {
+        if (a.vt == VT_F64) atomicAdd((double*)&a.s_part[0][s], __longlong_as_double((long long)a.c_part[0][c]));
+        else atomicAdd(&a.s_part[0][s], a.c_part[0][c]);
+      }
+      if (a.need & NEED_MIN) atomicMin((long long*)&a.s_part[1][s], (long long)a.c_part[1][c]);
+      if (a.need & NEED_MAX) atomicMax((long long*)&a.s_part[2][s], (long long)a.c_part[2][c]);
+      a.c_cnt[c] = 0;
+      a.c_tmax[c] = INT64_MIN;
+      a.c_part[0][c] = 0;
+      a.c_part[1][c] = (unsigned long long)PART_ID_MIN;
+      a.c_part[2][c] = (unsigned long long)PART_ID_MAX;
+    }
+  } else {
+    // nothing committed: return every touched cell to identity (the push is replayed by the host)
+    const int64_t ncell = c_old + kc;
+    for (int64_t c = tid; c < ncell; c += 1024) {
+      if (a.c_cnt[c] == 0) continue;
+      a.c_cnt[c] = 0;
+      a.c_tmax[c] = INT64_MIN;
+      a.c_part[0][c] = 0;
+      a.c_part[1][c] = (unsigned long long)PART_ID_MIN;
+      a.c_part[2][c] = (unsigned long long)PART_ID_MAX;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    DevMeta& m = *a.meta;
+    m.batch_max = batch_max;
+    if (!ovf) {
+      m.tail = tail + n_emit;
+      m.j0 = j0 + ncand;
+      m.prev_max = batch_max;
+      m.n_emitted = n_emit;
+      m.late_total += m.late_push;
+      m.processed_total += (uint64_t)a.n - m.late_push;
+    } else {
+      m.overflow = ovf;
+      m.failed_push = a.push_seq;
+    }
+    m.late_push = 0;
+    m.overflow_push = 0;
+  }
+}
+
+// ================================================================ 3. windows + GC
+// One wave per window: contained slices are the contiguous range [first tStart >= start, first tLast >= end)
+// (AggregateWindowState.containsSlice: start <= tStart && end > tLast, S/state/AggregateWindowState.java:25-31).
+__global__ __launch_bounds__(256) void window_kernel(WindowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wi >= a.n_windows) return;
+  if (a.meta->overflow) return;
+  const int64_t head = a.meta->head, tail = a.meta->tail;
+  const int64_t ws = a.w_start[wi], we = a.w_end[wi];
+  int64_t lo = head, hi = tail;
+  while (lo < hi) {  // first tStart >= ws
+    int64_t mid = (lo + hi) >> 1;
+    if (a.s_tstart[mid] < ws) lo = mid + 1; else hi = mid;
+  }
+  const int64_t sa = lo;
+  lo = head; hi = tail;
+  while (lo < hi) {  // first tLast >= we
+    int64_t mid = (lo + hi) >> 1;
+    if (a.s_tlast[mid] < we) lo = mid + 1; else hi = mid;
+  }
+  const int64_t sb = lo;
+  uint64_t cnt = 0, sw = 0;
+  double sf = 0.0;
+  int64_t mn = PART_ID_MIN, mx = PART_ID_MAX;
+  for (int64_t s = sa + lane; s < sb; s += 64) {
+    const uint64_t c = a.s_cnt[s];
+    if (c == 0) continue;
+    cnt += c;
+    if (a.need & NEED_SUM) {
+      if (a.vt == VT_F64) sf += __longlong_as_double((long long)a.s_part[0][s]);
+      else sw += a.s_part[0][s];
+    }
+    if (a.need & NEED_MIN) mn = min(mn, (int64_t)a.s_part[1][s]);
+    if (a.need & NEED_MAX) mx = max(mx, (int64_t)a.s_part[2][s]);
+  }
+  cnt = wsum64(cnt);
+  if (a.need & NEED_SUM) {
+    if (a.vt == VT_F64) sf = wsumf(sf);
+    else sw = wsum64(sw);
+  }
+  if (a.need & NEED_MIN) mn = wmin64(mn);
+  if (a.need & NEED_MAX) mx = wmax64(mx);
+  if (lane == 0) {
+    a.has_value[wi] = cnt ? 1 : 0;
+    a.o_cnt[wi] = cnt;
+    a.o_part[0][wi] = a.vt == VT_F64 ? (unsigned long long)__double_as_longlong(sf) : sw;
+    a.o_part[1][wi] = (unsigned long long)mn;
+    a.o_part[2][wi] = (unsigned long long)mx;
+  }
+}
+
+// WindowManager.clearAfterWatermark -> LazyAggregateStore.removeSlices(t): drop [0, idx) with idx the
+// last slice whose tStart <= t (S/aggregationstore/LazyAggregateStore.java:138-146).
+__global__ void gc_kernel(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DevMeta& m = *meta;
+  if (!m.overflow && m.tail > m.head) {
+    int64_t lo = m.head, hi = m.tail;  // count of tStart <= t -> idx = that - 1
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (s_tstart[mid] <= remove_from) lo = mid + 1; else hi = mid;
+    }
+    const int64_t idx = lo - 1;
+    if (idx > m.head) m.head = idx;
+    m.oldest_start = s_tstart[m.head];
+  }
+  *snapshot = m;
+}
+
+__global__ void fill_u64_kernel(unsigned long long* p, int64_t n, unsigned long long v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// Locate the first tuple (arrival order) with ts >= x: used once when the first context-free window is
+// in place and the operator needs the in-order tuple that starts the edge walk.
+__global__ void first_ge_kernel(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (ts[i] >= x) atomicMin(out_idx, (unsigned long long)i);
+}
+
+// ---------------------------------------------------------------- host-side launch wrappers
+template <int VT, int NEED>
+static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStream_t st) {
+  size_t lds = 128 + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP;
+  for (int k = 0; k < NPART; k++)
+    if (NEED & (1 << k)) lds += 8 * WCAP;
+  hipLaunchKernelGGL((ingest_kernel<VT, NEED>), dim3((unsigned)nblocks), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int VT>
+static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
+  switch (need) {
+    case 0: return launch_ingest_t<VT, 0>(a, nblocks, st);
+    case 1: return launch_ingest_t<VT, 1>(a, nblocks, st);
+    case 2: return launch_ingest_t<VT, 2>(a, nblocks, st);
+    case 3: return launch_ingest_t<VT, 3>(a, nblocks, st);
+    case 4: return launch_ingest_t<VT, 4>(a, nblocks, st);
+    case 5: return launch_ingest_t<VT, 5>(a, nblocks, st);
+    case 6: return launch_ingest_t<VT, 6>(a, nblocks, st);
+    default: return launch_ingest_t<VT, 7>(a, nblocks, st);
+  }
+}
+
+hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st) {
+  if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);
+  if (vt == VT_I64) return launch_ingest_vt<VT_I64>(a, need, nblocks, st);
+  return launch_ingest_vt<VT_F64>(a, need, nblocks, st);
+}
+
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(1024), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_windows(const WindowArgs& a, hipStream_t st) {
+  if (a.n_windows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(window_kernel, dim3((unsigned)((a.n_windows + 3) / 4)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st) {
+  hipLaunchKernelGGL(gc_kernel, dim3(1), dim3(64), 0, st, meta, s_tstart, remove_from, snapshot);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = min((int64_t)2048, (n + 255) / 256);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st) {
+  int64_t blocks = min((int64_t)2048, (n + 255) / 256);
+  hipLaunchKernelGGL(first_ge_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ts, n, x, out_idx);
+  return hipGetLastError();
+}
+
+}  // namespace scotty

@@ -1,0 +1,99 @@
+"""Shared helpers for the parity tests (oracle = CPU checker, product = MI355X C-ABI)."""
+import importlib
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def product():
+    return importlib.import_module("scotty-window-processor_amd")
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def same_windows(a, b, f64_cols=(), rel=1e-6):
+    """Window lists equal position by position: start, end, measure, hasValue bit-exact; values bit-exact
+    except the columns in f64_cols, compared within ``rel`` relative tolerance (SUM_F64, north_star)."""
+    assert len(a) == len(b), ("window count", len(a), len(b))
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert (x.getStart(), x.getEnd(), x.getMeasure(), x.hasValue()) == \
+               (y.getStart(), y.getEnd(), y.getMeasure(), y.hasValue()), (i, x, y)
+        xv, yv = x.getAggValues(), y.getAggValues()
+        assert len(xv) == len(yv), (i, x, y)
+        for j, (p, q) in enumerate(zip(xv, yv)):
+            if j in f64_cols:
+                if isinstance(p, float) and math.isnan(p):
+                    assert isinstance(q, float) and math.isnan(q), (i, j, p, q)
+                else:
+                    assert abs(p - q) <= rel * max(1.0, abs(q)), (i, j, p, q)
+            else:
+                assert p == q, (i, j, p, q, x, y)
+
+
+def build_ops(cfg, value_type="i32", device=0):
+    """Create (product, oracle) operators with the same windows / functions / lateness.
+    cfg: dict(windows=[spec...], aggs=[kind...], lateness=int|None)."""
+    from oracle.oracle import OracleOperator
+    pkg = product()
+    vt = {"i32": pkg.VALUE_I32, "i64": pkg.VALUE_I64, "f64": pkg.VALUE_F64}[value_type]
+    gpu = pkg.SlicingWindowOperator(device=device, value_type=vt)
+    ora = OracleOperator()
+    for op in (gpu, ora):
+        for a in cfg["aggs"]:
+            op.addWindowFunction(a)
+        if cfg.get("lateness") is not None:
+            op.setMaxLateness(cfg["lateness"])
+        for w in cfg["windows"]:
+            op.addWindowAssigner(w)
+    return gpu, ora
+
+
+def run_schedule(gpu, ora, ts, vals, schedule, value_type="i32", f64_cols=()):
+    """schedule: list of ("push", lo, hi) / ("wm", watermark).  Compares every watermark's windows and the
+    number of too-late tuples (product drops + counts them; the reference throws per tuple)."""
+    import numpy as np
+    n_windows = 0
+    fails = 0
+    for step in schedule:
+        if step[0] == "push":
+            lo, hi = step[1], step[2]
+            if hi <= lo:
+                continue
+            gpu.processElements(ts[lo:hi], vals[lo:hi])
+            if value_type == "f64":
+                fails += ora.processElements(ts[lo:hi], np.zeros(hi - lo, dtype=np.int64), vals[lo:hi])
+            else:
+                fails += ora.processElements(ts[lo:hi], vals[lo:hi])
+        else:
+            a = gpu.processWatermark(step[1])
+            b = ora.processWatermark(step[1])
+            same_windows(a, b, f64_cols=f64_cols)
+            n_windows += len(a)
+            assert gpu.droppedCount() == fails, ("dropped", gpu.droppedCount(), fails)
+    return n_windows
+
+
+def interval_schedule(ts, n_intervals, lag, pushes_per_interval=1):
+    """Cut the arrival sequence into n_intervals equal intervals; after each, a watermark max_ts - lag."""
+    import numpy as np
+    n = len(ts)
+    sched = []
+    bounds = np.linspace(0, n, n_intervals + 1).astype(np.int64)
+    for i in range(n_intervals):
+        lo, hi = int(bounds[i]), int(bounds[i + 1])
+        sub = np.linspace(lo, hi, pushes_per_interval + 1).astype(np.int64)
+        for j in range(pushes_per_interval):
+            sched.append(("push", int(sub[j]), int(sub[j + 1])))
+        if hi > 0:
+            sched.append(("wm", int(ts[:hi].max()) - lag))
+    return sched
