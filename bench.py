@@ -1,0 +1,178 @@
+"""Headline benchmark: tuples/s of the MI355X slicing operator on BASELINE.json's config (configs[1]).
+
+Workload (N=1): 1000 concurrent tumbling windows with sizes from BenchmarkRunner.randomTumbling(1000,1,20)
+(java.util.Random(10)), SUM_I32 + COUNT, in-order synthetic stream, maxLateness 1 (Flink connector default).
+One step = one watermark interval: a micro-batch of --batch tuples covering 1 s of event time, resident in
+HBM before the timed region, pushed through the C-ABI (ingest + edge commit kernels) followed by
+processWatermark (window assembly + GC + results to host).  N>1: one process per GPU, each rank runs an
+independent operator on its own key-hash shard (weak scaling, no collective on the data path); value is
+the aggregate over ranks divided by the max-over-ranks time.
+
+Prints ONE JSON line (rank 0).  cpu_baseline = the CPU restatement of SlicingWindowOperator (oracle/),
+single thread, on a bounded sample of the same workload.
+"""
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+METRIC = "tuples/sec (1/2/4/8 GPU) at 1000 concurrent windows; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_TUPLE = 12   # int64 ts + int32 value, read once
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sizes, rate_per_ms, budget_s=12.0):
+    """Oracle (C++ restatement of the reference operator, 1 thread) on a bounded prefix of the same stream."""
+    from oracle.oracle import OracleOperator
+    op = OracleOperator()
+    op.addWindowFunction(0)  # SUM_I32
+    op.addWindowFunction(1)  # COUNT
+    op.setMaxLateness(1)
+    for s in sizes:
+        op.addWindowAssigner(0, 0, s, 0)
+    chunk = 1 << 21
+    rng = np.random.default_rng(11)
+    done, t_proc, ms_per_chunk = 0, 0.0, chunk / rate_per_ms
+    t_start = time.time()
+    k = 0
+    while time.time() - t_start < budget_s:
+        idx = np.arange(done, done + chunk, dtype=np.int64)
+        ts = (idx // rate_per_ms).astype(np.int64)
+        vals = rng.integers(-2**31, 2**31, size=chunk, dtype=np.int64).astype(np.int32).astype(np.int64)
+        t0 = time.perf_counter()
+        op.processElements(ts, vals)
+        op.processWatermark(int(ts[-1]))
+        t_proc += time.perf_counter() - t0
+        done += chunk
+        k += 1
+    return {"value": done / t_proc, "unit": "tuples/s", "cores": 1, "kind": "port",
+            "sample": "%d tuples (%.0f ms of event time at %d tuples/ms, %d watermarks) of the same C2 stream, "
+                      "oracle/ C++ restatement of SlicingWindowOperator, 1 thread" % (done, done / rate_per_ms,
+                                                                                    rate_per_ms, k)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    pkg = importlib.import_module("scotty-window-processor_amd")
+
+    sizes = pkg.workloads.random_tumbling_sizes(1000, 1, 20, seed=10)
+    B = args.batch
+    rate = max(1, B // 1000)  # tuples per ms of event time
+    nsteps = args.steps + args.warmup
+
+    # ---- inputs resident in HBM before the timed region (one batch per step)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    batches = []
+    base = torch.arange(B, device=dev, dtype=torch.int64) // rate
+    for s in range(nsteps):
+        ts = base + s * 1000
+        vals = torch.randint(-2**31, 2**31, (B,), device=dev, dtype=torch.int32, generator=gen)
+        batches.append((ts, vals, int(s * 1000 + (B - 1) // rate)))
+    torch.cuda.synchronize(dev)
+
+    op = pkg.SlicingWindowOperator(device=local)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.addWindowFunction(pkg.AGG_COUNT)
+    op.setMaxLateness(1)
+    for s in sizes:
+        op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Time, s))
+    n_windows = 0
+
+    def step(i):
+        ts, vals, wm = batches[i]
+        op.processElementsDevice(ts.data_ptr(), vals.data_ptr(), B)
+        nw, _ = op.processWatermarkRaw(wm)
+        return nw
+
+    for i in range(args.warmup):
+        step(i)
+    op.enableTiming(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, nsteps):
+        n_windows += step(i)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    ingest_ms, launches, tuples = op.ingestTiming()
+    assert op.processedCount() >= B * nsteps - 1, op.processedCount()
+
+    if rank == 0:
+        total = B * args.steps * world
+        avg_ms = ingest_ms / max(1, launches)
+        achieved = (B * BYTES_PER_TUPLE) / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "ingest_traffic.json")
+        if os.path.exists(tfile):
+            try:
+                tj = json.load(open(tfile))
+                if tj.get("batch") == B:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": METRIC,
+            "value": total / elapsed,
+            "unit": "tuples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32 values / int64 timestamps",
+            "data": "synthetic (in-HBM, seeded): ts = step*1000 + i//%d ms, int32 uniform values" % rate,
+            "config": {"workload": "C2: 1000 concurrent tumbling windows, sizes randomTumbling(1000,1,20) "
+                                   "java.util.Random(10), SUM_I32+COUNT, in-order, maxLateness=1",
+                       "tuples_per_step": B, "event_ms_per_step": 1000, "windows_emitted": n_windows,
+                       "parallelism": "key-shard x%d (one operator per GPU)" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "ingest_kernel<VT_I32,NEED_SUM>", "algorithmic_bytes_per_launch":
+                             B * BYTES_PER_TUPLE, "avg_launch_ms": avg_ms, "launches": launches},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(sizes, rate)
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

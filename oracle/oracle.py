@@ -26,7 +26,9 @@ STATE_MEMORY, STATE_MOCK = 0, 1
 F64_AGGS = (AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64)
 
 ERR_NAMES = {-1: "IndexOutOfBoundsException", -2: "NullPointerException",
-             -3: "NoSuchElementException", -4: "ArithmeticException", -5: "IllegalArgument"}
+             -3: "NoSuchElementException", -4: "ArithmeticException", -5: "IllegalArgument",
+             -6: "ReferenceWouldHang"}
+ERR_HANG = -6
 
 
 class JavaError(Exception):

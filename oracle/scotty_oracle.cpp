@@ -767,6 +767,12 @@ struct Op {
         while (hasFixedWindows && te > min_next_edge_ts) {
           if (min_next_edge_ts >= 0) appendSlice(min_next_edge_ts, SliceType::Fixed());
           min_next_edge_ts = calculateNextFixedEdge(te);
+          // If the minimum assignNextWindowStart is exactly Long.MIN_VALUE (a power-of-two tumbling size or
+          // sliding slide wraps Long.MAX_VALUE + 1 on the first call), calculateNextFixedEdge treats the edge
+          // as "unset" again and the reference spins in this loop forever.  Report instead of hanging.
+          if (min_next_edge_ts == JMIN)
+            throw JavaException{ORC_ERR_HANG, "reference StreamSlicer loops forever: calculateNextFixedEdge "
+                                              "returned Long.MIN_VALUE (power-of-two window size/slide)"};
         }
         if (min_next_edge_ts == te) {
           if (flex > 0) appendSlice(te, SliceType::Fixed());

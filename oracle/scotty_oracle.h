@@ -55,6 +55,7 @@ extern "C" {
 #define ORC_ERR_NOELEM -3   /* NoSuchElementException */
 #define ORC_ERR_ARITH -4    /* ArithmeticException (/ by zero) */
 #define ORC_ERR_ARG -5      /* bad argument to the oracle API itself */
+#define ORC_ERR_HANG -6     /* the reference would loop forever (StreamSlicer, see oracle.cpp) */
 
 typedef struct orc_op orc_op;
 

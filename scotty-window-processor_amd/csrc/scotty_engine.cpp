@@ -334,7 +334,8 @@ int ensure_windows(scotty_op* op, int64_t nw) {
 // with min_next_edge_ts == Long.MIN_VALUE (S/StreamSlicer.java:52-84): calculateNextFixedEdge starts from
 // Long.MAX_VALUE, whose assignNextWindowStart wraps negative, and the loop then walks up from te-maxLateness.
 // Returns the edges appended (in order) and the resulting pending edge.
-void first_walk(const scotty_op* op, int64_t te, std::vector<int64_t>& edges, int64_t& n_out) {
+// Returns false when the reference would never leave this loop (see oracle: ORC_ERR_HANG).
+bool first_walk(const scotty_op* op, int64_t te, std::vector<int64_t>& edges, int64_t& n_out) {
   auto calc = [&](int64_t cur_next, int64_t t) {  // calculateNextFixedEdge
     int64_t cur = cur_next == JMIN ? JMAX : cur_next;
     int64_t tc = std::max(jsub(t, op->max_lateness), cur);
@@ -344,12 +345,14 @@ void first_walk(const scotty_op* op, int64_t te, std::vector<int64_t>& edges, in
   while (te > n) {
     if (n >= 0) edges.push_back(n);
     n = calc(n, te);
+    if (n == JMIN) return false;
   }
   if (n == te) {
     edges.push_back(n);
     n = calc(n, te);
   }
   n_out = n;
+  return true;
 }
 
 int compact_if_needed(scotty_op* op) {
@@ -447,7 +450,10 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
 int start_stream(scotty_op* op, int64_t ts0) {
   std::vector<int64_t> edges;
   int64_t n_pending = JMIN;
-  if (op->has_fixed) first_walk(op, ts0, edges, n_pending);
+  if (op->has_fixed && !first_walk(op, ts0, edges, n_pending))
+    return fail(op, SCOTTY_ERR_UNSUPPORTED,
+                "the reference StreamSlicer loops forever on this configuration (calculateNextFixedEdge returns "
+                "Long.MIN_VALUE for a power-of-two time window size/slide, S/StreamSlicer.java:103-116)");
   // SliceManager.processElement: an empty store first gets the slice [0, MAX) (S/SliceManager.java:49-51)
   if (edges.empty()) edges.push_back(0);
   const int64_t s0 = (int64_t)edges.size();

@@ -29,21 +29,26 @@ def test_junit_golden_values_on_gpu(pkg, case):
 
 @pytest.mark.parametrize("case", junit_cases.SESSION + junit_cases.TUMBLING_COUNT, ids=lambda c: c.__name__)
 def test_junit_session_and_count_not_yet_on_gpu(pkg, case):
-    """Sessions / count windows fail loudly (no CPU fallback) until the replay engine lands."""
-    with pytest.raises(pkg.UnsupportedError):
+    """Sessions / count windows (and the test-only (a,b)->a-b function) fail loudly: no CPU fallback."""
+    with pytest.raises(pkg.ScottyError):
         case(lambda: pkg.SlicingWindowOperator(device=0))
 
 
 # ---------------------------------------------------------------- seeded random configurations
+def _not_pow2(x):
+    # a power-of-two size/slide makes the reference loop forever (see test_reference_hang_config_rejected)
+    return x + 1 if x & (x - 1) == 0 else x
+
+
 def _random_cfg(rng, value_type):
     wins = []
     for _ in range(int(rng.integers(1, 5))):
         k = int(rng.integers(0, 3))
         if k == 0:
-            wins.append(Tumbling(Time, int(rng.integers(3, 60))))
+            wins.append(Tumbling(Time, _not_pow2(int(rng.integers(3, 60)))))
         elif k == 1:
             size = int(rng.integers(5, 90))
-            wins.append(Sliding(Time, size, int(rng.integers(1, size + 1))))
+            wins.append(Sliding(Time, size, _not_pow2(int(rng.integers(2, size + 1)))))
         else:
             wins.append(FixedBand(Time, int(rng.integers(0, 300)), int(rng.integers(1, 200))))
     aggs = {"i32": [SUM, COUNT, MIN, MAX], "i64": [SUM_I64, COUNT, MIN_I64, MAX_I64],
@@ -72,6 +77,20 @@ def test_random_streams_match_oracle(seed):
 
 
 # ---------------------------------------------------------------- edge semantics of the reference
+@pytest.mark.parametrize("win", [Tumbling(Time, 16), Sliding(Time, 100, 64), Tumbling(Time, 1)])
+def test_reference_hang_config_rejected(pkg, win):
+    """With a power-of-two size/slide, assignNextWindowStart(Long.MAX_VALUE) wraps to exactly Long.MIN_VALUE,
+    which calculateNextFixedEdge treats as 'unset' again: the reference spins forever in determineSlices
+    (S/StreamSlicer.java:65-69, :103-116).  The oracle reports ORC_ERR_HANG; the product refuses loudly."""
+    from oracle.oracle import ERR_HANG, JavaError
+    gpu, ora = build_ops(dict(windows=[win, Tumbling(Time, 10)], aggs=[SUM], lateness=5))
+    with pytest.raises(JavaError) as ei:
+        ora.processElement(1, 100)
+    assert ei.value.code == ERR_HANG
+    with pytest.raises(pkg.UnsupportedError):
+        gpu.processElements(np.array([100], dtype=np.int64), np.array([1], dtype=np.int32))
+
+
 @pytest.mark.parametrize("ts0,lateness", [(0, 1000), (3, 1000), (999, 1000), (1000, 1000), (5000, 1000),
                                           (7, 1), (10, 1), (12345, 0), (20, 5)])
 def test_first_tuple_edge_walk(ts0, lateness):
