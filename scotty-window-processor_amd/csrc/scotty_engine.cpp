@@ -495,7 +495,7 @@ int maybe_extend_grid(scotty_op* op, bool force) {
   const int64_t remaining = (int64_t)op->grid.size() - j0;
   const int64_t last = op->grid.back();
   const int64_t margin = std::max<int64_t>(16 * op->last_span, 60000);
-  if (!force && remaining > op->gcap / 4 && jsub(last, m.prev_max) > margin) return SCOTTY_OK;
+  if (!force && remaining > 1024 && jsub(last, m.prev_max) > margin) return SCOTTY_OK;
   const int64_t n_pending = op->grid[j0];
   const int64_t need_to = std::max(m.batch_max, m.prev_max);
   build_grid(op, n_pending, jadd(need_to, std::max<int64_t>(64 * op->last_span, 600000)));

@@ -134,7 +134,7 @@ def test_too_late_tuples_are_dropped_and_counted(pkg):
     vals = np.ones(len(ts), dtype=np.int32)
     gpu, ora = build_ops(cfg)
     run_schedule(gpu, ora, ts, vals, [("push", 0, 3), ("wm", 190), ("push", 3, 8), ("wm", 400)])
-    assert gpu.droppedCount() == 2 and gpu.last_status == pkg.SCOTTY_WARN_LATE_DROPPED
+    assert gpu.droppedCount() == 3 and gpu.last_status == pkg.SCOTTY_WARN_LATE_DROPPED
 
 
 def test_int32_wraparound_sum():
@@ -147,8 +147,8 @@ def test_int32_wraparound_sum():
 
 
 def test_f64_min_max_nan_and_signed_zero():
-    cfg = dict(windows=[Tumbling(Time, 4)], aggs=[MIN_F64, MAX_F64, SUM_F64], lateness=10)
-    ts = np.arange(16, dtype=np.int64)
+    cfg = dict(windows=[Tumbling(Time, 5)], aggs=[MIN_F64, MAX_F64, SUM_F64], lateness=10)
+    ts = np.arange(16, dtype=np.int64) * 5 // 4
     vals = np.array([1.0, -0.0, 0.0, 2.0, np.nan, 1.0, 3.0, -5.0, 0.0, -0.0, -0.0, 0.0,
                      np.inf, -np.inf, 1e300, -1e300], dtype=np.float64)
     gpu, ora = build_ops(cfg, "f64")
@@ -157,7 +157,7 @@ def test_f64_min_max_nan_and_signed_zero():
     ora.processElements(ts, np.zeros(16, dtype=np.int64), vals)
     a = gpu.processWatermark(100)
     b = ora.processWatermark(100)
-    assert len(a) == len(b) == 25
+    assert len(a) == len(b) == 20
     for x, y in zip(a, b):
         assert x.hasValue() == y.hasValue()
         for p, q in zip(x.getAggValues()[:2], y.getAggValues()[:2]):
@@ -181,9 +181,9 @@ def test_config2_1000_random_tumbling_sum_count():
 
 
 def test_config3_sliding_1000_concurrent_out_of_order_min_max():
-    ts, vals = product().workloads.stream(2_000_000, 40, t0=1000, ooo_frac=0.2, max_delay=500, seed=7)  # 50 s
+    ts, vals = product().workloads.stream(3_000_000, 25, t0=1000, ooo_frac=0.2, max_delay=500, seed=7)  # 120 s
     gpu, ora = build_ops(dict(windows=[Sliding(Time, 60_000, 60)], aggs=[MIN, MAX, COUNT], lateness=1000))
-    sched = interval_schedule(ts, 50, lag=500)
+    sched = interval_schedule(ts, 120, lag=500)
     assert run_schedule(gpu, ora, ts, vals, sched) > 0
 
 
