@@ -11,7 +11,8 @@
 
 namespace scotty {
 
-constexpr int TILE = 4096;        // tuples per arrival-order tile (tilemax granularity)
+constexpr int TILE_MIN = 4096;    // tuples per arrival-order tile (tilemax granularity), power of two
+constexpr int NT_MAX = 8192;      // tiles per micro-batch held in the commit kernel's LDS
 constexpr int WCAP = 1024;        // cells in a workgroup's LDS window
 constexpr int NPART = 3;          // partial slots per slice/cell: 0 sum, 1 min, 2 max
 
@@ -51,12 +52,14 @@ struct IngestArgs {
   // tile maxima
   long long* tilemax;
   DevMeta* meta;
-  int64_t per_wave;          // tuples per wave (multiple of TILE)
+  int64_t per_wave;          // tuples per wave (multiple of tile)
+  int64_t tile;              // tuples per tile (power of two >= TILE_MIN, nT <= NT_MAX)
 };
 
 struct CommitArgs {
   const int64_t* ts;
   int64_t n;
+  int64_t tile;
   int64_t max_lateness;
   int64_t scap;              // slice capacity
   const int64_t* grid;

@@ -300,7 +300,7 @@ int alloc_all(scotty_op* op) {
 }
 
 int ensure_tiles(scotty_op* op, int64_t n) {
-  int64_t nt = (n + TILE - 1) / TILE + 1;
+  int64_t nt = (n + TILE_MIN - 1) / TILE_MIN + 1;
   if (nt <= op->tcap) return SCOTTY_OK;
   HIPCHK(hipStreamSynchronize(op->stream));
   if (op->d_tilemax) HIPCHK(hipFree(op->d_tilemax));
@@ -397,12 +397,16 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
   for (int k = 0; k < NPART; k++) ia.c_part[k] = op->d_cpart[k];
   ia.tilemax = op->d_tilemax;
   ia.meta = op->d_meta;
-  // ~4 workgroups per CU on 256 CUs; each wave streams a TILE-aligned contiguous range
+  // tile: power of two >= TILE_MIN with at most NT_MAX tiles (the commit kernel keeps them in LDS)
+  int64_t tile = TILE_MIN;
+  while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
+  // ~4 workgroups per CU on 256 CUs; each wave streams a tile-aligned contiguous range
   const int64_t target_blocks = 1024;
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
-  per_wave = ((per_wave + TILE - 1) / TILE) * TILE;
-  if (per_wave < TILE) per_wave = TILE;
+  per_wave = ((per_wave + tile - 1) / tile) * tile;
+  if (per_wave < tile) per_wave = tile;
   ia.per_wave = per_wave;
+  ia.tile = tile;
   const int64_t nblocks = (n + per_wave * 4 - 1) / (per_wave * 4);
   std::pair<hipEvent_t, hipEvent_t> ev{};
   if (op->timing) {
@@ -424,6 +428,7 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
   CommitArgs ca{};
   ca.ts = d_ts;
   ca.n = n;
+  ca.tile = tile;
   ca.max_lateness = op->max_lateness;
   ca.scap = op->scap;
   ca.grid = op->d_grid;

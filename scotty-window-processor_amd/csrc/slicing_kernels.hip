@@ -374,9 +374,9 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       }
     }
     const int64_t done = s + 256;
-    if (((done - w0) % TILE) == 0 || done >= w1) {
+    if (((done - w0) & (a.tile - 1)) == 0 || done >= w1) {
       int64_t tm = wmax64(tile_max);
-      if (lane == 0) a.tilemax[s / TILE] = tm;
+      if (lane == 0) a.tilemax[s / a.tile] = tm;
       tile_max = INT64_MIN;
     }
   }
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
 }
 
 // ================================================================ 2. commit (single workgroup)
-__device__ __forceinline__ int64_t lower_bound_i64(const long long* a, int64_t n, int64_t x) {  // first a[i] >= x
+__device__ __forceinline__ int64_t lower_bound_lds(const long long* a, int64_t n, int64_t x) {  // first a[i] >= x
   int64_t lo = 0, hi = n;
   while (lo < hi) {
     int64_t mid = (lo + hi) >> 1;
@@ -410,8 +410,32 @@ __device__ __forceinline__ int64_t lower_bound_i64(const long long* a, int64_t n
   return lo;
 }
 
+// Block-wide (1024 threads) inclusive scan helpers.  `wtot` is LDS scratch of 16 entries.
+__device__ __forceinline__ int64_t block_incl_max(int64_t v, long long* wtot, int lane, int wid) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = (int64_t)__shfl_up((long long)v, o);
+    if (lane >= o) v = max(v, u);
+  }
+  if (lane == 63) wtot[wid] = v;
+  __syncthreads();
+  if (wid == 0) {
+    int64_t t = lane < 16 ? (int64_t)wtot[lane] : INT64_MIN;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int64_t u = (int64_t)__shfl_up((long long)t, o);
+      if (lane >= o) t = max(t, u);
+    }
+    if (lane < 16) wtot[lane] = t;
+  }
+  __syncthreads();
+  if (wid > 0) v = max(v, (int64_t)wtot[wid - 1]);
+  return v;
+}
+
 __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
-  __shared__ long long s_red[1024];
+  __shared__ long long s_p[NT_MAX];   // tile maxima -> prefix maxima (arrival order)
+  __shared__ long long s_w[32];
   __shared__ int64_t sc[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) {
@@ -427,32 +451,32 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
   const int64_t* g = a.grid + j0;
   const int64_t L = a.max_lateness;
+  const int64_t tile = a.tile;
 
-  // ---- (a) prefix max over tile maxima (arrival order)
-  const int64_t nT = (a.n + TILE - 1) / TILE;
-  const int64_t ch = (nT + 1023) / 1024;
-  const int64_t t0 = tid * ch, t1 = min(nT, t0 + ch);
-  long long lm = INT64_MIN;
-  for (int64_t t = t0; t < t1; t++) lm = max(lm, a.tilemax[t]);
-  s_red[tid] = lm;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive max scan (Hillis-Steele)
-    long long v = tid >= o ? s_red[tid - o] : INT64_MIN;
-    __syncthreads();
-    s_red[tid] = max(s_red[tid], v);
-    __syncthreads();
+  // ---- (a) prefix max over tile maxima, in LDS: 8 consecutive tiles per thread
+  const int64_t nT = (a.n + tile - 1) / tile;
+  int64_t loc[8];
+  int64_t run = INT64_MIN;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int64_t t = (int64_t)tid * 8 + j;
+    run = max(run, t < nT ? (int64_t)a.tilemax[t] : INT64_MIN);
+    loc[j] = run;
   }
-  long long run = tid > 0 ? s_red[tid - 1] : INT64_MIN;
-  for (int64_t t = t0; t < t1; t++) {
-    run = max(run, a.tilemax[t]);
-    a.pmax[t] = run;
+  const int64_t incl = block_incl_max(run, s_w, lane, wid);
+  const int64_t excl_thread = (int64_t)__shfl_up((long long)incl, 1);
+  int64_t carry = lane == 0 ? (wid > 0 ? (int64_t)s_w[wid - 1] : INT64_MIN) : excl_thread;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int64_t t = (int64_t)tid * 8 + j;
+    if (t < nT) s_p[t] = max(carry, loc[j]);
   }
-  const int64_t batch_max = max(prev_max, (int64_t)s_red[1023]);
   __syncthreads();
+  const int64_t batch_max = max(prev_max, nT > 0 ? (int64_t)s_p[nT - 1] : INT64_MIN);
 
   // ---- (b) candidates: grid points g[k] <= batch_max (k < kc)
   if (tid == 0) {
-    int64_t lo = 0, hi = kc;  // count of g[k] <= batch_max
+    int64_t lo = 0, hi = kc;
     while (lo < hi) {
       int64_t mid = (lo + hi) >> 1;
       if (g[mid] <= batch_max) lo = mid + 1; else hi = mid;
@@ -472,8 +496,8 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   if (!ovf) {
     for (int64_t k = tid; k < ncand; k += 1024) {
       const int64_t gk = g[k];
-      const int64_t ts_ = lower_bound_i64(a.pmax, nT, gk);
-      const int64_t pprev = ts_ > 0 ? max(prev_max, (int64_t)a.pmax[ts_ - 1]) : prev_max;
+      const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
+      const int64_t pprev = ts_ > 0 ? max(prev_max, (int64_t)s_p[ts_ - 1]) : prev_max;
       const int64_t tm = a.tilemax[ts_];
       int f;
       if (k == 0 || g[k - 1] <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < L) f = 1;
@@ -486,31 +510,30 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     for (int64_t k = wid; k < ncand; k += 16) {
       if (a.flag[k] != 2) continue;
       const int64_t gk = g[k];
-      const int64_t ts_ = lower_bound_i64(a.pmax, nT, gk);
-      int64_t r = ts_ > 0 ? max(prev_max, (int64_t)a.pmax[ts_ - 1]) : prev_max;
-      const int64_t e0 = ts_ * TILE, e1 = min(a.n, e0 + TILE);
+      const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
+      int64_t r = ts_ > 0 ? max(prev_max, (int64_t)s_p[ts_ - 1]) : prev_max;
+      const int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
       int64_t e = INT64_MIN, m = INT64_MIN;
       for (int64_t base = e0; base < e1; base += 64) {
         const int64_t i = base + lane;
         const int64_t v = i < e1 ? a.ts[i] : INT64_MIN;
-        // inclusive prefix max within the wave
-        int64_t incl = v;
+        int64_t inc = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-          int64_t u = (int64_t)__shfl_up((long long)incl, o);
-          if (lane >= o) incl = max(incl, u);
+          int64_t u = (int64_t)__shfl_up((long long)inc, o);
+          if (lane >= o) inc = max(inc, u);
         }
-        int64_t excl = (int64_t)__shfl_up((long long)incl, 1);
-        if (lane == 0) excl = INT64_MIN;
-        excl = max(excl, r);
+        int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
+        if (lane == 0) ex = INT64_MIN;
+        ex = max(ex, r);
         const unsigned long long hit = __ballot(v >= gk);
         if (hit) {
           const int f = __ffsll((long long)hit) - 1;
           e = rl64(v, f);
-          m = rl64(excl, f);
+          m = rl64(ex, f);
           break;
         }
-        r = max(r, rl64(incl, 63));
+        r = max(r, rl64(inc, 63));
       }
       if (lane == 0) {
         const bool emit = (int64_t)((uint64_t)e - (uint64_t)gk) < L || g[k - 1] <= m;
@@ -520,28 +543,29 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   }
   __syncthreads();
 
-  // ---- (d) rank = inclusive prefix count of emitted edges
+  // ---- (d) rank = inclusive prefix count of emitted edges (ballot/popcount per wave)
   int64_t n_emit = 0;
   if (!ovf) {
-    long long carry = 0;
+    int64_t base_cnt = 0;
     for (int64_t base = 0; base < ncand; base += 1024) {
       const int64_t k = base + tid;
-      const int f = (k < ncand && a.flag[k] == 1) ? 1 : 0;
-      s_red[tid] = f;
+      const bool f = k < ncand && a.flag[k] == 1;
+      const unsigned long long bal = __ballot(f);
+      const int in_wave = __popcll(bal & ((2ull << lane) - 1));  // inclusive within the wave
+      if (lane == 0) s_w[wid] = __popcll(bal);
       __syncthreads();
-      for (int o = 1; o < 1024; o <<= 1) {
-        long long v = tid >= o ? s_red[tid - o] : 0;
-        __syncthreads();
-        s_red[tid] += v;
-        __syncthreads();
-      }
-      if (k < ncand) a.rank[k] = (int32_t)(carry + s_red[tid]);
-      carry += s_red[1023];
+      int64_t before = 0;
+      for (int w = 0; w < wid; w++) before += s_w[w];
+      int64_t tot = 0;
+      for (int w = 0; w < 16; w++) tot += s_w[w];
+      if (k < ncand) a.rank[k] = (int32_t)(base_cnt + before + in_wave);
+      base_cnt += tot;
       __syncthreads();
     }
-    n_emit = carry;
+    n_emit = base_cnt;
     if (tail + n_emit > a.scap) ovf = 2;
   }
+  __syncthreads();
 
   if (!ovf) {
     // ---- (e) append new slices (SliceManager.appendSlice: tStart = edge, tLast = tStart, empty partial)
