@@ -19,7 +19,7 @@
 #include "device_common.h"
 
 namespace scotty {
-hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st);
+hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_windows(const WindowArgs& a, hipStream_t st);
 hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st);
@@ -120,6 +120,8 @@ struct scotty_op {
   std::vector<void*> owned;  // staging copies of host pushes
   int64_t push_seq = 0;
   uint64_t dropped = 0, processed = 0;
+
+  int ingest_mode = -1;  // tuning knob (scotty_tune), -1 = default variant
 
   // ---- timing
   bool timing = false;
@@ -419,7 +421,7 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
     }
     HIPCHK(hipEventRecord(ev.first, op->stream));
   }
-  HIPCHK(launch_ingest(ia, op->vt, op->need, nblocks, op->stream));
+  HIPCHK(launch_ingest(ia, op->vt, op->need, nblocks, op->stream, op->ingest_mode));
   if (op->timing) {
     HIPCHK(hipEventRecord(ev.second, op->stream));
     op->ev_pending.push_back(ev);
@@ -833,6 +835,16 @@ int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, ui
   if (launches) *launches = op->t_launches;
   if (tuples) *tuples = op->t_tuples;
   return SCOTTY_OK;
+}
+
+// Undeclared tuning hook (not part of the ABI contract): "ingest_mode" selects an ingest-kernel variant.
+int scotty_tune(scotty_op* op, const char* key, int64_t value) {
+  if (!op || !key) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "ingest_mode") == 0) {
+    op->ingest_mode = (int)value;
+    return SCOTTY_OK;
+  }
+  return SCOTTY_ERR_ARG;
 }
 
 int scotty_sync(scotty_op* op) {

@@ -186,7 +186,9 @@ __device__ __forceinline__ void glb_add(const IngestArgs& a, int64_t c, uint64_t
 }
 
 // ================================================================ 1. ingest
-template <int VT, int NEED>
+// MODE bit0: software-pipelined (next step's loads in flight while the current step is combined)
+// MODE bit1: non-temporal loads for the once-read tuple columns
+template <int VT, int NEED, int MODE>
 __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   using V = typename ValT<VT>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -306,79 +308,123 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     }
   };
 
-  for (int64_t s = w0; s < w1; s += 256) {
-    const bool full = s + 256 <= w1;
-    int64_t t[4];
-    V v[4];
+  constexpr bool PIPE = (MODE & 1) != 0;
+  constexpr bool NTL = (MODE & 2) != 0;
+  const V* vp = (const V*)a.val;
+  typedef long long v2i64 __attribute__((ext_vector_type(2)));
+  typedef int v2i32 __attribute__((ext_vector_type(2)));
+  auto ld2 = [&](const void* p) -> v2i64 {
+    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(p));
+    else return *reinterpret_cast<const v2i64*>(p);
+  };
+  auto ld2i = [&](const void* p) -> v2i32 {
+    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const v2i32*>(p));
+    else return *reinterpret_cast<const v2i32*>(p);
+  };
+  struct Step {
+    v2i64 ta, tb;
+    typename std::conditional<VT == VT_I32, v2i32, v2i64>::type va, vb;
+  };
+  auto load_step = [&](int64_t s, Step& st) {
     const int64_t i0 = s + 2 * lane, i1 = s + 128 + 2 * lane;
-    if (full) {
-      const longlong2 ta = *reinterpret_cast<const longlong2*>(a.ts + i0);
-      const longlong2 tb = *reinterpret_cast<const longlong2*>(a.ts + i1);
-      t[0] = ta.x; t[1] = ta.y; t[2] = tb.x; t[3] = tb.y;
-      const V* vp = (const V*)a.val;
-      if (VT == VT_I32) {
-        const int2 va = *reinterpret_cast<const int2*>(vp + i0);
-        const int2 vb = *reinterpret_cast<const int2*>(vp + i1);
-        v[0] = (V)va.x; v[1] = (V)va.y; v[2] = (V)vb.x; v[3] = (V)vb.y;
-      } else {
-        const longlong2 va = *reinterpret_cast<const longlong2*>(vp + i0);
-        const longlong2 vb = *reinterpret_cast<const longlong2*>(vp + i1);
-        if (VT == VT_I64) {
-          v[0] = (V)va.x; v[1] = (V)va.y; v[2] = (V)vb.x; v[3] = (V)vb.y;
-        } else {
-          v[0] = (V)__longlong_as_double(va.x); v[1] = (V)__longlong_as_double(va.y);
-          v[2] = (V)__longlong_as_double(vb.x); v[3] = (V)__longlong_as_double(vb.y);
-        }
-      }
-      // move the wave's current cell forward when the stream has advanced past it
-      const int64_t x = rl64(t[3], 63);
-      if (x >= hi && x >= first_start && (x < h_end || h_end == INT64_MAX)) {
-        flush();
-        int64_t c;
-        if (x >= tw0 && x < twn) {
-          int64_t l = 0, h = wn;
-          while (h - l > 1) {
-            int64_t mid = (l + h) >> 1;
-            if (w.tw[mid] <= x) l = mid; else h = mid;
-          }
-          c = wbase + l;
-          lo = w.tw[l];
-          hi = w.tw[l + 1];
-        } else {
-          c = cv.find(x);
-          lo = cv.start(c);
-          hi = cv.start(c + 1);
-        }
-        cstar = uni64(c);
-        lo = uni64(lo);
-        hi = uni64(hi);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        tile_max = max(tile_max, t[j]);
-        if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
-        else slow(t[j], v[j]);
-      }
+    st.ta = ld2(a.ts + i0);
+    st.tb = ld2(a.ts + i1);
+    if constexpr (VT == VT_I32) {
+      st.va = ld2i(vp + i0);
+      st.vb = ld2i(vp + i1);
     } else {
-      const V* vp = (const V*)a.val;
-      const int64_t idx[4] = {i0, i0 + 1, i1, i1 + 1};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (idx[j] < w1) {
-          int64_t tj = a.ts[idx[j]];
-          V vj = vp[idx[j]];
-          tile_max = max(tile_max, tj);
-          if (tj >= lo && tj < hi) acc.add(tj, vj);
-          else slow(tj, vj);
-        }
-      }
+      st.va = ld2(vp + i0);
+      st.vb = ld2(vp + i1);
     }
+  };
+  auto unpack = [&](const Step& st, int64_t (&t)[4], V (&v)[4]) {
+    t[0] = st.ta.x; t[1] = st.ta.y; t[2] = st.tb.x; t[3] = st.tb.y;
+    if constexpr (VT == VT_F64) {
+      v[0] = __longlong_as_double(st.va.x); v[1] = __longlong_as_double(st.va.y);
+      v[2] = __longlong_as_double(st.vb.x); v[3] = __longlong_as_double(st.vb.y);
+    } else {
+      v[0] = (V)st.va.x; v[1] = (V)st.va.y; v[2] = (V)st.vb.x; v[3] = (V)st.vb.y;
+    }
+  };
+  // one full step of 256 tuples (4 per lane) already in registers
+  auto process_full = [&](const int64_t (&t)[4], const V (&v)[4]) {
+    // move the wave's current cell forward when the stream has advanced past it
+    const int64_t x = rl64(t[3], 63);
+    if (x >= hi && x >= first_start && (x < h_end || h_end == INT64_MAX)) {
+      flush();
+      int64_t c;
+      if (x >= tw0 && x < twn) {
+        int64_t l = 0, h = wn;
+        while (h - l > 1) {
+          int64_t mid = (l + h) >> 1;
+          if (w.tw[mid] <= x) l = mid; else h = mid;
+        }
+        c = wbase + l;
+        lo = w.tw[l];
+        hi = w.tw[l + 1];
+      } else {
+        c = cv.find(x);
+        lo = cv.start(c);
+        hi = cv.start(c + 1);
+      }
+      cstar = uni64(c);
+      lo = uni64(lo);
+      hi = uni64(hi);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      tile_max = max(tile_max, t[j]);
+      if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
+      else slow(t[j], v[j]);
+    }
+  };
+  auto tile_done = [&](int64_t s) {
     const int64_t done = s + 256;
     if (((done - w0) & (a.tile - 1)) == 0 || done >= w1) {
       int64_t tm = wmax64(tile_max);
       if (lane == 0) a.tilemax[s / a.tile] = tm;
       tile_max = INT64_MIN;
     }
+  };
+  const int64_t w1_full = w0 + ((w1 - w0) / 256) * 256;  // end of the full steps
+  if constexpr (PIPE) {
+    Step cur, nxt;
+    if (w0 < w1_full) load_step(w0, cur);
+    for (int64_t s = w0; s < w1_full; s += 256) {
+      if (s + 256 < w1_full) load_step(s + 256, nxt);
+      int64_t t[4];
+      V v[4];
+      unpack(cur, t, v);
+      process_full(t, v);
+      tile_done(s);
+      cur = nxt;
+    }
+  } else {
+    for (int64_t s = w0; s < w1_full; s += 256) {
+      Step cur;
+      load_step(s, cur);
+      int64_t t[4];
+      V v[4];
+      unpack(cur, t, v);
+      process_full(t, v);
+      tile_done(s);
+    }
+  }
+  if (w1_full < w1) {  // ragged tail of the wave's range
+    const int64_t s = w1_full;
+    const int64_t i0 = s + 2 * lane, i1 = s + 128 + 2 * lane;
+    const int64_t idx[4] = {i0, i0 + 1, i1, i1 + 1};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (idx[j] < w1) {
+        int64_t tj = a.ts[idx[j]];
+        V vj = vp[idx[j]];
+        tile_max = max(tile_max, tj);
+        if (tj >= lo && tj < hi) acc.add(tj, vj);
+        else slow(tj, vj);
+      }
+    }
+    tile_done(s);
   }
   flush();
   {
@@ -721,30 +767,41 @@ __global__ void first_ge_kernel(const int64_t* ts, int64_t n, int64_t x, unsigne
 }
 
 // ---------------------------------------------------------------- host-side launch wrappers
-template <int VT, int NEED>
+template <int VT, int NEED, int MODE>
 static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStream_t st) {
   size_t lds = 128 + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP;
   for (int k = 0; k < NPART; k++)
     if (NEED & (1 << k)) lds += 8 * WCAP;
-  hipLaunchKernelGGL((ingest_kernel<VT, NEED>), dim3((unsigned)nblocks), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((ingest_kernel<VT, NEED, MODE>), dim3((unsigned)nblocks), dim3(256), lds, st, a);
   return hipGetLastError();
 }
+
+constexpr int DEFAULT_MODE = 2;  // non-temporal loads, no software pipelining (A/B: profiles/r01/ab_ingest_modes.json)
 
 template <int VT>
 static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
   switch (need) {
-    case 0: return launch_ingest_t<VT, 0>(a, nblocks, st);
-    case 1: return launch_ingest_t<VT, 1>(a, nblocks, st);
-    case 2: return launch_ingest_t<VT, 2>(a, nblocks, st);
-    case 3: return launch_ingest_t<VT, 3>(a, nblocks, st);
-    case 4: return launch_ingest_t<VT, 4>(a, nblocks, st);
-    case 5: return launch_ingest_t<VT, 5>(a, nblocks, st);
-    case 6: return launch_ingest_t<VT, 6>(a, nblocks, st);
-    default: return launch_ingest_t<VT, 7>(a, nblocks, st);
+    case 0: return launch_ingest_t<VT, 0, DEFAULT_MODE>(a, nblocks, st);
+    case 1: return launch_ingest_t<VT, 1, DEFAULT_MODE>(a, nblocks, st);
+    case 2: return launch_ingest_t<VT, 2, DEFAULT_MODE>(a, nblocks, st);
+    case 3: return launch_ingest_t<VT, 3, DEFAULT_MODE>(a, nblocks, st);
+    case 4: return launch_ingest_t<VT, 4, DEFAULT_MODE>(a, nblocks, st);
+    case 5: return launch_ingest_t<VT, 5, DEFAULT_MODE>(a, nblocks, st);
+    case 6: return launch_ingest_t<VT, 6, DEFAULT_MODE>(a, nblocks, st);
+    default: return launch_ingest_t<VT, 7, DEFAULT_MODE>(a, nblocks, st);
   }
 }
 
-hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st) {
+// mode < 0: default; mode 0..3 selects a variant for the (int32, SUM) configuration (A/B tuning)
+hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode) {
+  if (mode >= 0 && vt == VT_I32 && need == NEED_SUM) {
+    switch (mode) {
+      case 0: return launch_ingest_t<VT_I32, NEED_SUM, 0>(a, nblocks, st);
+      case 1: return launch_ingest_t<VT_I32, NEED_SUM, 1>(a, nblocks, st);
+      case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
+      default: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
+    }
+  }
   if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);
   if (vt == VT_I64) return launch_ingest_vt<VT_I64>(a, need, nblocks, st);
   return launch_ingest_vt<VT_F64>(a, need, nblocks, st);
