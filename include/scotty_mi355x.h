@@ -60,7 +60,9 @@ extern "C" {
 #define SCOTTY_MAX_AGGS 8
 
 /* ---- create flags */
-#define SCOTTY_FLAG_KEYED 0x1u /* reserved: keyed operator (one logical operator per key) */
+#define SCOTTY_FLAG_KEYED 0x1u /* keyed operator: one logical SlicingWindowOperator per uint32 key, all with the
+                                  same windows / functions / lateness, as the Flink connector builds them
+                                  (flink-connector/.../KeyedScottyWindowOperator.java:41-66) */
 
 typedef struct scotty_op scotty_op;
 
@@ -78,6 +80,8 @@ typedef struct {
   const int32_t* measure;
   const uint8_t* has_value;
   const int64_t* values[SCOTTY_MAX_AGGS];
+  const uint32_t* key; /* keyed ops: key of row i (rows of one key are contiguous, in the reference's order);
+                          NULL for non-keyed ops */
 } scotty_windows;
 
 /* new SlicingWindowOperator(stateFactory)  (S/SlicingWindowOperator.java:30-37) */
@@ -102,8 +106,23 @@ int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, s
  * stay valid and unmodified until the next scotty_process_watermark() returns. */
 int scotty_process_elements_device(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n);
 
-/* WindowOperator.processWatermark(wm) (C/WindowOperator.java:19).  Blocks until results are ready. */
+/* Keyed micro-batch: processElement(element, ts) of the key's operator, for every tuple in arrival order
+ * (KeyedScottyWindowOperator.processElement, flink-connector/.../KeyedScottyWindowOperator.java:56-66).
+ * A key seen for the first time gets a fresh operator (:57-60).  Host memory, consumed before return. */
+int scotty_process_keyed_elements(scotty_op* op, const uint32_t* key, const int64_t* ts, const void* val, size_t n);
+/* Same, device pointers resident in HBM (valid until the call returns; 16-byte aligned). */
+int scotty_process_keyed_elements_device(scotty_op* op, const uint32_t* d_key, const int64_t* d_ts,
+                                         const void* d_val, size_t n);
+
+/* WindowOperator.processWatermark(wm) (C/WindowOperator.java:19).  Blocks until results are ready.
+ * Keyed ops: processWatermark(wm) of every key's operator (KeyedScottyWindowOperator.java:72-86); all
+ * windows are returned (the connector's hasValue() filter, :80, is the caller's). */
 int scotty_process_watermark(scotty_op* op, int64_t watermark_ts, scotty_windows* out);
+/* Same, but the result columns stay in HBM (device pointers, valid until the next call on the op).
+ * Exact-engine ops only (keyed, or with session / count windows); others return SCOTTY_ERR_UNSUPPORTED. */
+int scotty_process_watermark_device(scotty_op* op, int64_t watermark_ts, scotty_windows* out);
+/* Number of keys (operators) of a keyed op. */
+int64_t scotty_key_count(scotty_op* op);
 
 /* Counters: tuples dropped as too late since creation; tuples processed. */
 uint64_t scotty_dropped_count(scotty_op* op);
@@ -116,6 +135,10 @@ int64_t scotty_slice_count(scotty_op* op);
  * milliseconds and launch count since the last reset. */
 int scotty_enable_timing(scotty_op* op, int on);
 int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, uint64_t* tuples);
+
+/* Tuning knobs (not semantics): "slice_capacity" / "session_capacity" per operator of the exact engine
+ * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only). */
+int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */
 int scotty_sync(scotty_op* op);

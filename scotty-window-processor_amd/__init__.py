@@ -25,6 +25,7 @@ LIB_PATH = os.path.join(_HERE, "libscotty_mi355x.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "scotty_mi355x.h")
 
 SCOTTY_OK, SCOTTY_WARN_LATE_DROPPED = 0, 1
+FLAG_KEYED = 0x1
 ERRORS = {-1: "SCOTTY_ERR_ARG", -2: "SCOTTY_ERR_UNSUPPORTED", -3: "SCOTTY_ERR_HIP", -4: "SCOTTY_ERR_STATE",
           -5: "SCOTTY_ERR_INDEX", -6: "SCOTTY_ERR_NOMEM"}
 VALUE_I32, VALUE_I64, VALUE_F64 = 0, 1, 2
@@ -105,7 +106,8 @@ class scotty_windows(ctypes.Structure):
     _fields_ = [("n_windows", ctypes.c_size_t), ("n_aggs", ctypes.c_int32),
                 ("start", ctypes.POINTER(ctypes.c_int64)), ("end", ctypes.POINTER(ctypes.c_int64)),
                 ("measure", ctypes.POINTER(ctypes.c_int32)), ("has_value", ctypes.POINTER(ctypes.c_uint8)),
-                ("values", ctypes.POINTER(ctypes.c_int64) * MAX_AGGS)]
+                ("values", ctypes.POINTER(ctypes.c_int64) * MAX_AGGS),
+                ("key", ctypes.POINTER(ctypes.c_uint32))]
 
 
 _lib = None
@@ -135,6 +137,11 @@ def lib():
             "scotty_process_elements": (ctypes.c_int, [P, P, P, ctypes.c_size_t]),
             "scotty_process_elements_device": (ctypes.c_int, [P, P, P, ctypes.c_size_t]),
             "scotty_process_watermark": (ctypes.c_int, [P, i64, ctypes.POINTER(scotty_windows)]),
+            "scotty_process_watermark_device": (ctypes.c_int, [P, i64, ctypes.POINTER(scotty_windows)]),
+            "scotty_process_keyed_elements": (ctypes.c_int, [P, P, P, P, ctypes.c_size_t]),
+            "scotty_process_keyed_elements_device": (ctypes.c_int, [P, P, P, P, ctypes.c_size_t]),
+            "scotty_key_count": (i64, [P]),
+            "scotty_tune": (ctypes.c_int, [P, ctypes.c_char_p, i64]),
             "scotty_dropped_count": (u64, [P]),
             "scotty_processed_count": (u64, [P]),
             "scotty_slice_count": (i64, [P]),
@@ -191,10 +198,12 @@ def _kind_of(fn):
 class SlicingWindowOperator:
     """de.tub.dima.scotty.slicing.SlicingWindowOperator backed by libscotty_mi355x.so."""
 
+    _flags = 0
+
     def __init__(self, device=0, value_type=VALUE_I32):
         self._l = lib()
         self._h = ctypes.c_void_p()
-        rc = self._l.scotty_create(ctypes.byref(self._h), device, value_type, 0)
+        rc = self._l.scotty_create(ctypes.byref(self._h), device, value_type, self._flags)
         if rc != 0:
             raise ScottyError(rc, "scotty_create failed (no MI355X / HIP device?)")
         self.value_type = value_type
@@ -218,6 +227,10 @@ class SlicingWindowOperator:
             msg = self._l.scotty_last_error(self._h).decode()
             raise (UnsupportedError if rc == -2 else ScottyError)(rc, msg)
         return rc
+
+    def tune(self, key, value):
+        """Capacity knobs of the exact engine ("slice_capacity", "session_capacity"), before the first push."""
+        self._check(self._l.scotty_tune(self._h, key.encode(), int(value)))
 
     # ---- WindowOperator API
     def addWindowAssigner(self, window):
@@ -287,6 +300,13 @@ class SlicingWindowOperator:
             res.append(AggregateWindow(int(start[i]), int(end[i]), int(meas[i]), bool(has[i]), vals))
         return res
 
+    def processWatermarkDevice(self, watermark_ts):
+        """processWatermark with the result columns left in HBM (exact engine): returns (n_windows, status)."""
+        self._flush()
+        out = scotty_windows()
+        st = self._check(self._l.scotty_process_watermark_device(self._h, watermark_ts, ctypes.byref(out)))
+        return out.n_windows, st
+
     def processWatermarkRaw(self, watermark_ts):
         """processWatermark without building Python objects: returns (n_windows, status)."""
         self._flush()
@@ -315,5 +335,59 @@ class SlicingWindowOperator:
 
     def sync(self):
         self._check(self._l.scotty_sync(self._h))
+
+class KeyedSlicingWindowOperator(SlicingWindowOperator):
+    """One SlicingWindowOperator per uint32 key, all configured alike -- the per-key HashMap of
+    flink-connector/.../KeyedScottyWindowOperator.java:21-86, on the GPU as one keyed engine.
+
+    processElements(keys, ts, values) feeds every key's operator in arrival order; processWatermark(wm)
+    returns [(key, AggregateWindow)] of every key's operator (rows of one key contiguous, in the
+    reference's order).  KeyedScottyWindowOperator only forwards hasValue() windows (:80): use
+    collect(wm) for exactly that stream."""
+
+    _flags = FLAG_KEYED
+
+    def processElement(self, element, ts, key=0):
+        self._buf_ts.append(ts)
+        self._buf_v.append(element)
+        self._buf_k = getattr(self, "_buf_k", [])
+        self._buf_k.append(key)
+
+    def _flush(self):
+        if self._buf_ts:
+            ts, v, k = self._buf_ts, self._buf_v, self._buf_k
+            self._buf_ts, self._buf_v, self._buf_k = [], [], []
+            self.processElements(k, ts, v)
+
+    def processElements(self, keys, ts, values):
+        self._flush()
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        dt = {VALUE_I32: np.int32, VALUE_I64: np.int64, VALUE_F64: np.float64}[self.value_type]
+        v = np.ascontiguousarray(values, dtype=dt)
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        assert len(ts) == len(v) == len(k)
+        if len(ts):
+            self._check(self._l.scotty_process_keyed_elements(self._h, k.ctypes.data, ts.ctypes.data,
+                                                              v.ctypes.data, len(ts)))
+
+    def processElementsDevice(self, key_ptr, ts_ptr, val_ptr, n):
+        self._flush()
+        self._check(self._l.scotty_process_keyed_elements_device(self._h, key_ptr, ts_ptr, val_ptr, n))
+
+    def _windows(self, out):
+        n = out.n_windows
+        if n == 0:
+            return []
+        keys = np.ctypeslib.as_array(out.key, shape=(n,)).copy()
+        ws = SlicingWindowOperator._windows(self, out)
+        return [(int(k), w) for k, w in zip(keys, ws)]
+
+    def collect(self, watermark_ts):
+        """What KeyedScottyWindowOperator.processWatermark forwards: hasValue() windows only (:79-82)."""
+        return [(k, w) for k, w in self.processWatermark(watermark_ts) if w.hasValue()]
+
+    def keyCount(self):
+        return self._l.scotty_key_count(self._h)
+
 
 from . import workloads  # noqa: E402,F401

@@ -1,0 +1,132 @@
+// exact_common.h -- data layout of the exact ("replay") engine, shared by host and gfx950 kernels.
+//
+// The exact engine runs the reference operator's per-tuple state machine (S/StreamSlicer.java:36-141,
+// S/SliceManager.java:27-192, C/windowType/SessionWindow.java:40-116) for MANY operators at once: one
+// wavefront owns one operator (one key of a keyed stream, or the single operator of a non-keyed stream)
+// and walks that operator's micro-batch in arrival order, 64 tuples at a time.  Tuples whose effect
+// commutes (no slice edge, no session modification) are reduced cooperatively per slice; the rare tuples
+// that change structure ("events") are executed exactly, wave-uniformly.  It serves every configuration
+// the grid path (slicing_kernels.hip) does not: session windows, count windows and keyed operators.
+//
+// HBM layout (SoA, operator-major):
+//   XState   [n_ops]            StreamSlicer / WindowManager scalars of each operator
+//   slices   [n_ops * sc]       tStart tEnd tLast tFirst cStart cLast (i64), type (i32), cnt + 3 partials
+//   sessions [n_ops * nctx * sesscap]  active sessions (start, end) of each SessionContext
+//   cfg                         windows + functions shared by all operators (same for every key, as the
+//                               Flink connector builds every per-key operator identically,
+//                               flink-connector/.../KeyedScottyWindowOperator.java:41-49)
+#pragma once
+#include <stdint.h>
+
+#include "device_common.h"
+
+namespace scotty {
+
+constexpr int XMAXCTX = 4;        // session windows per operator
+constexpr int XMAXMODS = 8;       // WindowModifications produced by one updateContext call (<= 4 in practice)
+constexpr int SCOTTY_MAX_AGGS_ = 8;  // == SCOTTY_MAX_AGGS
+
+// Slice.Type (S/slice/Slice.java:86-121): Fixed, or Flexible(counter).  Stored in an int32:
+// XTYPE_FIXED, or the flexible counter; bit 30 marks a LazySlice (SliceFactory.createSlice, :17-22).
+constexpr int32_t XTYPE_FIXED = (int32_t)0x80000000;
+constexpr int32_t XTYPE_LAZY = 0x40000000;
+
+// exception codes of the reference, recorded per operator
+enum : int32_t {
+  XERR_NONE = 0,
+  XERR_INDEX = 1,        // IndexOutOfBoundsException (tuple dropped; counted)
+  XERR_UNSUPPORTED = 2,  // LazySlice record movement (not on the MI355X path yet) -- fatal
+  XERR_SLICE_CAP = 3,    // per-operator slice capacity exceeded -- fatal
+  XERR_SESS_CAP = 4,     // per-context session capacity exceeded -- fatal
+  XERR_HANG = 5,         // reference would loop forever in StreamSlicer (power-of-two size/slide) -- fatal
+  XERR_WM_INDEX = 6,     // processWatermark threw (empty session context / count trigger) -- fatal for the call
+};
+
+struct XCfg {
+  int32_t n_cf;           // context-free windows (registration order)
+  int32_t n_ctx;          // context-aware (session) windows (registration order)
+  int32_t has_fixed, has_ctx, has_count, has_time, session_case, lazy;
+  int32_t need, vt;
+  int32_t sc;             // slice capacity per operator
+  int32_t sesscap;        // session capacity per context per operator
+  int32_t ctx_alloc;      // session contexts allocated per operator (>= n_ctx)
+  int64_t max_lateness, max_fixed;
+  int64_t gap[XMAXCTX];
+  int32_t ctx_measure[XMAXCTX];
+  int32_t n_aggs;
+  int32_t agg_kind[SCOTTY_MAX_AGGS_];   // SCOTTY_AGG_* of include/scotty_mi355x.h, registration order
+  // context-free windows, SoA [n_cf]
+  const int32_t* cf_kind;
+  const int32_t* cf_measure;
+  const int64_t* cf_a;
+  const int64_t* cf_b;
+};
+
+struct XState {          // 128 B
+  int64_t maxEventTime, nextEdgeTs, nextEdgeCount, currentCount;   // S/StreamSlicer.java:10-14, WindowManager
+  int64_t lastWatermark, lastCount;                                 // S/WindowManager.java:18-33
+  int32_t head, tail;                                               // retained slices [head, tail) of the op
+  int32_t started, unsorted;                                        // store non-empty; tStart order broken
+  int32_t err, key;                                                 // fatal error; key of this op
+  int32_t nsess[XMAXCTX];
+  uint64_t dropped;                                                 // tuples whose processing threw
+  int64_t wlo, whi;                                                 // watermark: slice scan range
+  int32_t pending, pad;                                             // batch deferred: capacity too small
+};
+
+struct XSlices {
+  int64_t *ts, *te, *tl, *tf, *cs, *cl;
+  int32_t* ty;
+  unsigned long long* cnt;
+  unsigned long long* p[NPART];
+};
+
+struct XSess {
+  int64_t *start, *end;
+};
+
+// one micro-batch, arrival ordered; ops[] lists the operators that have tuples, seg[op] = [begin, end)
+struct XBatchArgs {
+  const int64_t* ts;
+  const void* val;
+  const int32_t* op_of;     // nullable: operator of each sorted tuple (keyed) -- unused by the replay itself
+  const int64_t* seg_begin; // [n_ops] (null: the single operator owns [0, n))
+  const int64_t* seg_end;
+  int64_t n;
+  int32_t n_ops;
+  const XCfg* cfg;
+  XState* st;
+  XSlices sl;
+  XSess ss;
+  int32_t rec_stride;       // keyed: tuples are AoS records (ts at +0, value at +8, op at +rec_stride-4)
+  int32_t retry;            // process only ops marked pending by an earlier launch
+  unsigned long long* need; // [2] capacity pre-check: max slices / sessions an op may need (atomicMax)
+};
+
+struct XWmArgs {
+  const XCfg* cfg;
+  XState* st;
+  XSlices sl;
+  XSess ss;
+  int32_t n_ops;
+  int64_t wm;
+  // pass 1 output: windows per op; pass 2 input: exclusive offsets
+  int64_t* wcount;
+  const int64_t* woff;
+  // pass 2 outputs (rows)
+  int64_t* w_start;
+  int64_t* w_end;
+  int32_t* w_meas;
+  int32_t* w_op;
+  int32_t* err_flag;
+  unsigned long long* dropped_total;   // count pass: sum of XState.dropped
+  int32_t* op_err;                     // count pass: OR of (1 << XState.err)
+  // pass 3 outputs: lowered values (AggregateWindowState.getAggValues, S/state/AggregateWindowState.java:41-49)
+  uint8_t* has_value;
+  int64_t* values[SCOTTY_MAX_AGGS_];
+  uint32_t* w_key;                      // key of the row's op (keyed)
+  const uint32_t* slot_key;            // nullable
+  int64_t n_rows;
+};
+
+}  // namespace scotty

@@ -1,0 +1,590 @@
+// exact_engine.cpp -- host side of the exact ("replay") engine: operator table, keyed batching, watermark
+// result assembly.  Per-tuple work runs only in gfx950 kernels (exact_kernels.hip, keyed_kernels.hip);
+// the host sequences launches on the op's stream and owns the window/function configuration, like the
+// reference's WindowManager registration (S/WindowManager.java:121-151).
+#include "exact_engine.h"
+
+#include <algorithm>
+#include <cstddef>
+#include <cstring>
+
+namespace scotty {
+hipError_t launch_replay(const XBatchArgs& a, int vt, hipStream_t st);
+hipError_t launch_wm_count(const XWmArgs& a, hipStream_t st);
+hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
+hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st);
+hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
+hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
+hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
+                             uint32_t* new_pos, unsigned long long* new_count, int32_t* full, hipStream_t st);
+hipError_t launch_key_assign(unsigned long long* table, const uint32_t* new_pos, int64_t n_new, int64_t base,
+                             uint32_t* slot_key, hipStream_t st);
+hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask,
+                         hipStream_t st);
+hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
+                       uint32_t* slot, hipStream_t st);
+hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
+                               int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
+                               void** result, hipStream_t st);
+hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end, hipStream_t st);
+int64_t sort_tile();
+}  // namespace scotty
+
+namespace scotty {
+
+#define XCHK(expr)                                                         \
+  do {                                                                     \
+    hipError_t _e = (expr);                                                \
+    if (_e != hipSuccess) {                                                \
+      err = std::string(#expr ": ") + hipGetErrorString(_e);               \
+      failed = true;                                                       \
+      return SCOTTY_ERR_HIP;                                               \
+    }                                                                      \
+  } while (0)
+
+namespace {
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  return hipMalloc((void**)p, count * sizeof(T));
+}
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+int agg_need(int kind) {
+  switch (kind) {
+    case SCOTTY_AGG_SUM_I32: case SCOTTY_AGG_SUM_I64: case SCOTTY_AGG_SUM_F64: return NEED_SUM;
+    case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MIN_I64: case SCOTTY_AGG_MIN_F64: return NEED_MIN;
+    case SCOTTY_AGG_MAX_I32: case SCOTTY_AGG_MAX_I64: case SCOTTY_AGG_MAX_F64: return NEED_MAX;
+    default: return 0;
+  }
+}
+int bits_for(int64_t n) {  // bits to represent n-1
+  int b = 0;
+  while (b < 40 && ((int64_t)1 << b) < n) b++;
+  return b;
+}
+}  // namespace
+
+XEngine::~XEngine() { release(); }
+
+void XEngine::release() {
+  dfree(d_cfg); dfree(d_cf_kind); dfree(d_cf_meas); dfree(d_cf_a); dfree(d_cf_b);
+  dfree(d_st);
+  dfree(sl.ts); dfree(sl.te); dfree(sl.tl); dfree(sl.tf); dfree(sl.cs); dfree(sl.cl); dfree(sl.ty); dfree(sl.cnt);
+  for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  dfree(ss.start); dfree(ss.end);
+  dfree(d_need); dfree(d_table); dfree(d_newpos); dfree(d_newcnt); dfree(d_full); dfree(d_slot_key);
+  dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32); dfree(d_seg_b); dfree(d_seg_e);
+  dfree(d_wcount); dfree(d_woff); dfree(d_scan64); dfree(d_misc);
+  dfree(d_w_start); dfree(d_w_end); dfree(d_w_meas); dfree(d_w_op); dfree(d_w_key); dfree(d_has);
+  for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
+  if (h_misc) (void)hipHostFree(h_misc);
+  d_cfg = nullptr;
+  d_st = nullptr;
+  h_misc = nullptr;
+}
+
+int XEngine::init(int dev, hipStream_t st, int value_type, bool is_keyed, std::string& e_out) {
+  device = dev;
+  stream = st;
+  vt = value_type;
+  keyed = is_keyed;
+  (void)e_out;
+  XCHK(dalloc(&d_cfg, 1));
+  XCHK(dalloc(&d_misc, 8));
+  XCHK(hipHostMalloc((void**)&h_misc, 8 * sizeof(int64_t), hipHostMallocDefault));
+  XCHK(dalloc(&d_newcnt, 1));
+  XCHK(dalloc(&d_full, 1));
+  XCHK(dalloc(&d_need, 2));
+  return SCOTTY_OK;
+}
+
+// WindowManager.addWindowAssigner / addAggregation / setMaxLateness (S/WindowManager.java:121-202)
+int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness) {
+  XCfg c{};
+  std::vector<int32_t> kind, meas;
+  std::vector<int64_t> a, b;
+  int nctx = 0;
+  bool has_ctx = false, session_case = false;
+  int64_t max_fixed = 0;
+  for (const XWinDef& w : wins) {
+    if (w.kind == SCOTTY_WIN_SESSION) {
+      if (nctx >= XMAXCTX) {
+        err = "more than 4 session windows per operator are not supported on the MI355X path";
+        return SCOTTY_ERR_UNSUPPORTED;
+      }
+      session_case = !has_ctx || session_case;
+      has_ctx = true;
+      c.gap[nctx] = w.a;
+      c.ctx_measure[nctx] = w.measure;
+      nctx++;
+    } else {
+      kind.push_back(w.kind);
+      meas.push_back(w.measure);
+      a.push_back(w.a);
+      b.push_back(w.b);
+      max_fixed = std::max(max_fixed, w.kind == SCOTTY_WIN_FIXED_BAND ? w.b : w.a);  // clearDelay
+    }
+    if (w.measure == SCOTTY_MEASURE_COUNT) c.has_count = 1;
+    else c.has_time = 1;
+  }
+  c.n_cf = (int32_t)kind.size();
+  c.n_ctx = nctx;
+  c.has_fixed = c.n_cf > 0;
+  c.has_ctx = has_ctx;
+  c.session_case = session_case;
+  c.max_lateness = max_lateness;
+  c.max_fixed = max_fixed;
+  // SliceFactory.createSlice (S/slice/SliceFactory.java:17-22)
+  c.lazy = !(!c.has_count && (!has_ctx || session_case) && max_lateness > 0);
+  c.vt = vt;
+  c.need = 0;
+  c.n_aggs = (int32_t)aggs.size();
+  for (size_t i = 0; i < aggs.size(); i++) {
+    c.agg_kind[i] = aggs[i];
+    c.need |= agg_need(aggs[i]);
+  }
+  // capacities
+  if (sc == 0) {
+    if (!keyed) {
+      sc = sc_override > 0 ? sc_override : (1 << 20);
+    } else if (sc_override > 0) {
+      sc = sc_override;
+    } else {
+      int64_t min_step = INT64_MAX;
+      for (const XWinDef& w : wins) {
+        if (w.kind == SCOTTY_WIN_TUMBLING) min_step = std::min(min_step, w.a);
+        if (w.kind == SCOTTY_WIN_SLIDING) min_step = std::min(min_step, w.b);
+      }
+      int64_t est = 128;
+      if (min_step != INT64_MAX && min_step > 0 && !has_ctx && !c.has_count)
+        est = (max_fixed + std::max<int64_t>(max_lateness, 0)) / min_step + 24;
+      int64_t p = 32;
+      while (p < est && p < 1024) p <<= 1;  // grown on demand (replay capacity pre-check)
+      sc = (int32_t)p;
+    }
+  }
+  if (sesscap == 0) sesscap = sess_override > 0 ? sess_override : (keyed ? 64 : 4096);
+  c.sc = sc;
+  c.sesscap = sesscap;
+  c.ctx_alloc = ctx_alloc;
+  // context-free window table
+  dfree(d_cf_kind); dfree(d_cf_meas); dfree(d_cf_a); dfree(d_cf_b);
+  d_cf_kind = nullptr; d_cf_meas = nullptr; d_cf_a = nullptr; d_cf_b = nullptr;
+  XCHK(dalloc(&d_cf_kind, kind.size()));
+  XCHK(dalloc(&d_cf_meas, kind.size()));
+  XCHK(dalloc(&d_cf_a, kind.size()));
+  XCHK(dalloc(&d_cf_b, kind.size()));
+  if (!kind.empty()) {
+    XCHK(hipMemcpyAsync(d_cf_kind, kind.data(), kind.size() * 4, hipMemcpyHostToDevice, stream));
+    XCHK(hipMemcpyAsync(d_cf_meas, meas.data(), meas.size() * 4, hipMemcpyHostToDevice, stream));
+    XCHK(hipMemcpyAsync(d_cf_a, a.data(), a.size() * 8, hipMemcpyHostToDevice, stream));
+    XCHK(hipMemcpyAsync(d_cf_b, b.data(), b.size() * 8, hipMemcpyHostToDevice, stream));
+  }
+  c.cf_kind = d_cf_kind;
+  c.cf_measure = d_cf_meas;
+  c.cf_a = d_cf_a;
+  c.cf_b = d_cf_b;
+  cfg = c;
+  XCHK(hipMemcpyAsync(d_cfg, &cfg, sizeof(XCfg), hipMemcpyHostToDevice, stream));
+  if (nctx > ctx_alloc) {  // session windows registered (possibly mid-stream): widen the per-op session table
+    int rc = grow_caps(sc, sesscap, nctx);
+    if (rc) return rc;
+  }
+  XCHK(hipStreamSynchronize(stream));
+  if (!keyed && n_ops == 0) {
+    int rc = grow_ops(1);
+    if (rc) return rc;
+    XCHK(launch_xstate_init(d_st, 0, 1, nullptr, stream));
+    n_ops = 1;
+  }
+  return SCOTTY_OK;
+}
+
+int XEngine::grow_ops(int64_t need) {
+  if (need <= ops_cap) return SCOTTY_OK;
+  int64_t cap = std::max<int64_t>(ops_cap * 2, keyed ? 1024 : 1);
+  while (cap < need) cap *= 2;
+  XCHK(hipStreamSynchronize(stream));
+  auto grow = [&](auto** p, int64_t per_op) -> hipError_t {
+    using T = std::remove_pointer_t<std::remove_reference_t<decltype(*p)>>;
+    T* np = nullptr;
+    hipError_t e = dalloc(&np, (size_t)(cap * per_op));
+    if (e != hipSuccess) return e;
+    if (*p && n_ops > 0) {
+      e = hipMemcpyAsync(np, *p, (size_t)(n_ops * per_op) * sizeof(T), hipMemcpyDeviceToDevice, stream);
+      if (e != hipSuccess) return e;
+    }
+    if (*p) {
+      (void)hipStreamSynchronize(stream);
+      dfree(*p);
+    }
+    *p = np;
+    return hipSuccess;
+  };
+  XCHK(grow(&d_st, 1));
+  XCHK(grow(&sl.ts, sc)); XCHK(grow(&sl.te, sc)); XCHK(grow(&sl.tl, sc)); XCHK(grow(&sl.tf, sc));
+  XCHK(grow(&sl.cs, sc)); XCHK(grow(&sl.cl, sc)); XCHK(grow(&sl.ty, sc)); XCHK(grow(&sl.cnt, sc));
+  for (int k = 0; k < NPART; k++) XCHK(grow(&sl.p[k], sc));
+  if (ctx_alloc > 0) {
+    XCHK(grow(&ss.start, (int64_t)ctx_alloc * sesscap));
+    XCHK(grow(&ss.end, (int64_t)ctx_alloc * sesscap));
+  }
+  if (keyed) XCHK(grow(&d_slot_key, 1));
+  XCHK(hipStreamSynchronize(stream));
+  ops_cap = cap;
+  return SCOTTY_OK;
+}
+
+// Re-lay out the per-op slice / session tables with larger capacities (row = one op, 2-D copies).
+int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx) {
+  int64_t nsc = sc, nss = sesscap;
+  while (nsc < need_sc) nsc *= 2;
+  while (nss < need_sess) nss *= 2;
+  const int32_t nctx = std::max(ctx_alloc, need_ctx);
+  if (nsc > (1 << 26) || nss > (1 << 24)) {
+    err = "per-operator slice / session capacity would exceed the supported maximum";
+    failed = true;
+    return SCOTTY_ERR_NOMEM;
+  }
+  XCHK(hipStreamSynchronize(stream));
+  const int64_t rows = std::max<int64_t>(ops_cap, 1);
+  auto relayout = [&](auto** p, int64_t old_w, int64_t new_w, int64_t nrows, int64_t copy_rows) -> hipError_t {
+    using T = std::remove_pointer_t<std::remove_reference_t<decltype(*p)>>;
+    T* np = nullptr;
+    hipError_t e = dalloc(&np, (size_t)(nrows * new_w));
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(np, 0, (size_t)(nrows * new_w) * sizeof(T), stream);
+    if (e != hipSuccess) return e;
+    if (*p && copy_rows > 0 && old_w > 0) {
+      e = hipMemcpy2DAsync(np, new_w * sizeof(T), *p, old_w * sizeof(T), old_w * sizeof(T), copy_rows,
+                           hipMemcpyDeviceToDevice, stream);
+      if (e != hipSuccess) return e;
+      (void)hipStreamSynchronize(stream);
+    }
+    dfree(*p);
+    *p = np;
+    return hipSuccess;
+  };
+  if (nsc != sc && sl.ts) {
+    XCHK(relayout(&sl.ts, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.te, sc, nsc, rows, n_ops));
+    XCHK(relayout(&sl.tl, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.tf, sc, nsc, rows, n_ops));
+    XCHK(relayout(&sl.cs, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.cl, sc, nsc, rows, n_ops));
+    XCHK(relayout(&sl.ty, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.cnt, sc, nsc, rows, n_ops));
+    for (int k = 0; k < NPART; k++) XCHK(relayout(&sl.p[k], sc, nsc, rows, n_ops));
+  }
+  if (nss != sesscap || nctx != ctx_alloc) {
+    // row = one op: ctx_alloc contexts x sesscap sessions; re-pitch contexts first, then widen each context
+    int64_t* ns_start = nullptr;
+    int64_t* ns_end = nullptr;
+    XCHK(dalloc(&ns_start, (size_t)(rows * nctx * nss)));
+    XCHK(dalloc(&ns_end, (size_t)(rows * nctx * nss)));
+    XCHK(hipMemsetAsync(ns_start, 0, (size_t)(rows * nctx * nss) * 8, stream));
+    XCHK(hipMemsetAsync(ns_end, 0, (size_t)(rows * nctx * nss) * 8, stream));
+    if (ss.start && ctx_alloc > 0 && n_ops > 0) {
+      for (int c = 0; c < ctx_alloc; c++) {
+        XCHK(hipMemcpy2DAsync(ns_start + (int64_t)c * nss, (size_t)nctx * nss * 8, ss.start + (int64_t)c * sesscap,
+                              (size_t)ctx_alloc * sesscap * 8, (size_t)sesscap * 8, n_ops, hipMemcpyDeviceToDevice,
+                              stream));
+        XCHK(hipMemcpy2DAsync(ns_end + (int64_t)c * nss, (size_t)nctx * nss * 8, ss.end + (int64_t)c * sesscap,
+                              (size_t)ctx_alloc * sesscap * 8, (size_t)sesscap * 8, n_ops, hipMemcpyDeviceToDevice,
+                              stream));
+      }
+      XCHK(hipStreamSynchronize(stream));
+    }
+    dfree(ss.start);
+    dfree(ss.end);
+    ss.start = ns_start;
+    ss.end = ns_end;
+  }
+  sc = (int32_t)nsc;
+  sesscap = (int32_t)nss;
+  ctx_alloc = nctx;
+  cfg.sc = sc;
+  cfg.sesscap = sesscap;
+  cfg.ctx_alloc = ctx_alloc;
+  XCHK(hipMemcpyAsync(d_cfg, &cfg, sizeof(XCfg), hipMemcpyHostToDevice, stream));
+  XCHK(hipStreamSynchronize(stream));
+  return SCOTTY_OK;
+}
+
+int XEngine::ensure_batch(int64_t n) {
+  if (n <= bcap) return SCOTTY_OK;
+  XCHK(hipStreamSynchronize(stream));
+  int64_t cap = std::max<int64_t>(n, 1 << 16);
+  dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32);
+  const int rec = vt == VT_I32 ? 16 : 24;
+  XCHK(dalloc(&d_slot, cap));
+  XCHK(dalloc((unsigned char**)&d_recA, cap * rec));
+  XCHK(dalloc((unsigned char**)&d_recB, cap * rec));
+  const int64_t nb = (cap + sort_tile() - 1) / sort_tile();
+  XCHK(dalloc(&d_hist, 256 * nb));
+  XCHK(dalloc(&d_scan32, 256 * nb / 512 + 64));
+  XCHK(dalloc(&d_newpos, cap));
+  bcap = cap;
+  return SCOTTY_OK;
+}
+
+int XEngine::ensure_table(int64_t keys_needed) {
+  uint64_t want = 1024;
+  while ((int64_t)want < 2 * keys_needed) want <<= 1;
+  if (want <= tcap) return SCOTTY_OK;
+  unsigned long long* nt = nullptr;
+  XCHK(dalloc(&nt, want));
+  XCHK(hipMemsetAsync(nt, 0, want * 8, stream));
+  if (d_table) {
+    XCHK(launch_rehash(d_table, tcap, nt, want - 1, stream));
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_table);
+  }
+  d_table = nt;
+  tcap = want;
+  return SCOTTY_OK;
+}
+
+int XEngine::check_ready() {
+  if (failed) return SCOTTY_ERR_STATE;
+  return SCOTTY_OK;
+}
+
+XBatchArgs XEngine::batch_args() const {
+  XBatchArgs a{};
+  a.cfg = d_cfg;
+  a.st = d_st;
+  a.sl = sl;
+  a.ss = ss;
+  a.n_ops = (int32_t)n_ops;
+  return a;
+}
+
+int XEngine::push(const int64_t* d_ts, const void* d_val, int64_t n) {
+  if (n <= 0) return SCOTTY_OK;
+  XBatchArgs a = batch_args();
+  a.ts = d_ts;
+  a.val = d_val;
+  a.n = n;
+  a.rec_stride = 0;
+  XCHK(launch_replay(a, vt, stream));
+  return SCOTTY_OK;
+}
+
+int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n) {
+  if (n <= 0) return SCOTTY_OK;
+  int rc = ensure_batch(n);
+  if (rc) return rc;
+  rc = ensure_table(n_ops + std::min<int64_t>(n, 1 << 24));
+  if (rc) return rc;
+  // 1. new keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator()))
+  XCHK(hipMemsetAsync(d_newcnt, 0, 8, stream));
+  XCHK(hipMemsetAsync(d_full, 0, 4, stream));
+  XCHK(launch_key_insert(d_key, n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, stream));
+  XCHK(hipMemcpyAsync(h_misc, d_newcnt, 8, hipMemcpyDeviceToHost, stream));
+  XCHK(hipMemcpyAsync(h_misc + 1, d_full, 4, hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  const int64_t n_new = h_misc[0];
+  if ((int32_t)h_misc[1] != 0) {
+    err = "key hash table full";
+    failed = true;
+    return SCOTTY_ERR_NOMEM;
+  }
+  if (n_new > 0) {
+    rc = grow_ops(n_ops + n_new);
+    if (rc) return rc;
+    XCHK(launch_key_assign(d_table, d_newpos, n_new, n_ops, d_slot_key, stream));
+    XCHK(launch_xstate_init(d_st, n_ops, n_ops + n_new, d_slot_key, stream));
+    h_slot_key.resize(n_ops + n_new);
+    XCHK(hipMemcpyAsync(h_slot_key.data() + n_ops, d_slot_key + n_ops, n_new * 4, hipMemcpyDeviceToHost, stream));
+    n_ops += n_new;
+    if ((int64_t)2 * n_ops > (int64_t)tcap) {
+      rc = ensure_table(n_ops);
+      if (rc) return rc;
+    }
+  }
+  // 2. per-tuple slot, stable sort by slot (arrival order kept within each key), segments
+  XCHK(launch_slot(d_key, n, d_table, tcap - 1, d_slot, stream));
+  const int rec = vt == VT_I32 ? 16 : 24;
+  void* sorted = nullptr;
+  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_slot, n, bits_for(n_ops), d_recA, d_recB, d_hist, d_scan32, &sorted,
+                           stream));
+  if (seg_cap < n_ops) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_seg_b);
+    dfree(d_seg_e);
+    seg_cap = std::max<int64_t>(ops_cap, 1024);
+    XCHK(dalloc(&d_seg_b, seg_cap));
+    XCHK(dalloc(&d_seg_e, seg_cap));
+  }
+  XCHK(hipMemsetAsync(d_seg_b, 0, n_ops * 8, stream));
+  XCHK(hipMemsetAsync(d_seg_e, 0, n_ops * 8, stream));
+  XCHK(launch_seg(rec, sorted, n, d_seg_b, d_seg_e, stream));
+  // 3. per-key replay; ops whose capacities might overflow are deferred, the tables grown, and relaunched
+  XBatchArgs a = batch_args();
+  a.ts = (const int64_t*)sorted;
+  a.val = nullptr;
+  a.n = n;
+  a.seg_begin = d_seg_b;
+  a.seg_end = d_seg_e;
+  a.rec_stride = rec;
+  a.need = d_need;
+  for (int attempt = 0; attempt < 6; attempt++) {
+    XCHK(hipMemsetAsync(d_need, 0, 16, stream));
+    a.retry = attempt > 0;
+    a.sl = sl;
+    a.ss = ss;
+    XCHK(launch_replay(a, vt, stream));
+    XCHK(hipMemcpyAsync(h_misc, d_need, 16, hipMemcpyDeviceToHost, stream));
+    XCHK(hipStreamSynchronize(stream));
+    if (h_misc[0] == 0 && h_misc[1] == 0) return SCOTTY_OK;
+    rc = grow_caps(std::max<int64_t>(h_misc[0], sc), std::max<int64_t>(h_misc[1], sesscap), ctx_alloc);
+    if (rc) return rc;
+  }
+  err = "capacity growth did not converge";
+  failed = true;
+  return SCOTTY_ERR_NOMEM;
+}
+
+int XEngine::ensure_rows(int64_t rows) {
+  if (rows <= rcap) return SCOTTY_OK;
+  XCHK(hipStreamSynchronize(stream));
+  dfree(d_w_start); dfree(d_w_end); dfree(d_w_meas); dfree(d_w_op); dfree(d_w_key); dfree(d_has);
+  for (int k = 0; k < SCOTTY_MAX_AGGS; k++) {
+    dfree(d_vals[k]);
+    d_vals[k] = nullptr;
+  }
+  const int64_t cap = std::max<int64_t>(rows + rows / 2, 1024);
+  XCHK(dalloc(&d_w_start, cap));
+  XCHK(dalloc(&d_w_end, cap));
+  XCHK(dalloc(&d_w_meas, cap));
+  XCHK(dalloc(&d_w_op, cap));
+  XCHK(dalloc(&d_w_key, cap));
+  XCHK(dalloc(&d_has, cap));
+  for (int k = 0; k < cfg.n_aggs; k++) XCHK(dalloc(&d_vals[k], cap));
+  rcap = cap;
+  return SCOTTY_OK;
+}
+
+int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
+  r.n = 0;
+  r.dropped = 0;
+  r.start.clear(); r.end.clear(); r.meas.clear(); r.has.clear(); r.key.clear();
+  r.vals.assign(cfg.n_aggs, {});
+  if (n_ops == 0) return SCOTTY_OK;
+  if (wcap < n_ops) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_wcount); dfree(d_woff); dfree(d_scan64);
+    wcap = std::max<int64_t>(ops_cap, 1024);
+    XCHK(dalloc(&d_wcount, wcap));
+    XCHK(dalloc(&d_woff, wcap));
+    XCHK(dalloc(&d_scan64, wcap / 512 + 64));
+  }
+  XWmArgs a{};
+  a.cfg = d_cfg;
+  a.st = d_st;
+  a.sl = sl;
+  a.ss = ss;
+  a.n_ops = (int32_t)n_ops;
+  a.wm = wm;
+  a.wcount = d_wcount;
+  a.woff = d_woff;
+  a.err_flag = (int32_t*)(d_misc + 0);
+  a.dropped_total = (unsigned long long*)(d_misc + 1);
+  a.op_err = (int32_t*)(d_misc + 2);
+  a.slot_key = keyed ? d_slot_key : nullptr;
+  XCHK(hipMemsetAsync(d_misc, 0, 3 * 8, stream));
+  XCHK(launch_wm_count(a, stream));
+  XCHK(launch_scan_i64(d_wcount, d_woff, n_ops, d_scan64, stream));
+  XCHK(hipMemcpyAsync(h_misc, d_misc, 3 * 8, hipMemcpyDeviceToHost, stream));
+  XCHK(hipMemcpyAsync(h_misc + 3, d_woff + n_ops - 1, 8, hipMemcpyDeviceToHost, stream));
+  XCHK(hipMemcpyAsync(h_misc + 4, d_wcount + n_ops - 1, 8, hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  r.dropped = (uint64_t)h_misc[1];
+  const int32_t op_err = (int32_t)h_misc[2];
+  if (op_err & ~(1 << XERR_INDEX)) {
+    failed = true;
+    if (op_err & (1 << XERR_UNSUPPORTED))
+      err = "a LazySlice (count windows / maxLateness<=0 / non-session context windows) would move records "
+            "(out-of-order tuple): not implemented on the MI355X path yet";
+    else if (op_err & (1 << XERR_SLICE_CAP))
+      err = "per-operator slice capacity exceeded (scotty_tune \"slice_capacity\")";
+    else if (op_err & (1 << XERR_SESS_CAP))
+      err = "per-context session capacity exceeded (scotty_tune \"session_capacity\")";
+    else if (op_err & (1 << XERR_HANG))
+      err = "the reference StreamSlicer loops forever on this configuration (calculateNextFixedEdge returns "
+            "Long.MIN_VALUE for a power-of-two time window size/slide, S/StreamSlicer.java:103-116)";
+    else
+      err = "operator failed";
+    return (op_err & (1 << XERR_HANG)) || (op_err & (1 << XERR_UNSUPPORTED)) ? SCOTTY_ERR_UNSUPPORTED
+                                                                               : SCOTTY_ERR_NOMEM;
+  }
+  if ((int32_t)h_misc[0] & 1) {
+    err = "processWatermark threw IndexOutOfBoundsException (empty session context / count trigger before the "
+          "oldest slice, S/WindowManager.java:98-118)";
+    return SCOTTY_ERR_INDEX;
+  }
+  const int64_t rows = h_misc[3] + h_misc[4];
+  int rc = ensure_rows(rows);
+  if (rc) return rc;
+  a.w_start = d_w_start;
+  a.w_end = d_w_end;
+  a.w_meas = d_w_meas;
+  a.w_op = d_w_op;
+  a.has_value = d_has;
+  for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
+  a.w_key = d_w_key;
+  a.n_rows = rows;
+  XCHK(launch_wm_emit(a, stream));
+  XCHK(launch_wm_agg(a, stream));
+  r.n = rows;
+  r.d_start = d_w_start;
+  r.d_end = d_w_end;
+  r.d_meas = d_w_meas;
+  r.d_key = d_w_key;
+  r.d_has = d_has;
+  for (int k = 0; k < cfg.n_aggs; k++) r.d_vals[k] = d_vals[k];
+  if (to_host && rows > 0) {
+    r.start.resize(rows); r.end.resize(rows); r.meas.resize(rows); r.has.resize(rows); r.key.resize(rows);
+    r.vals.assign(cfg.n_aggs, std::vector<int64_t>(rows));
+    XCHK(hipMemcpyAsync(r.start.data(), d_w_start, rows * 8, hipMemcpyDeviceToHost, stream));
+    XCHK(hipMemcpyAsync(r.end.data(), d_w_end, rows * 8, hipMemcpyDeviceToHost, stream));
+    XCHK(hipMemcpyAsync(r.meas.data(), d_w_meas, rows * 4, hipMemcpyDeviceToHost, stream));
+    XCHK(hipMemcpyAsync(r.has.data(), d_has, rows, hipMemcpyDeviceToHost, stream));
+    XCHK(hipMemcpyAsync(r.key.data(), d_w_key, rows * 4, hipMemcpyDeviceToHost, stream));
+    for (int k = 0; k < cfg.n_aggs; k++)
+      XCHK(hipMemcpyAsync(r.vals[k].data(), d_vals[k], rows * 8, hipMemcpyDeviceToHost, stream));
+  }
+  XCHK(hipMemcpyAsync(h_misc, d_misc, 8, hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  if ((int32_t)h_misc[0] & 2) {
+    err = "processWatermark threw IndexOutOfBoundsException in LazyAggregateStore.aggregate (getSlice(-1))";
+    return SCOTTY_ERR_INDEX;
+  }
+  return SCOTTY_OK;
+}
+
+int XEngine::set_last_watermark(int64_t lw) {
+  if (n_ops < 1) return SCOTTY_OK;
+  XCHK(hipMemcpyAsync((unsigned char*)d_st + offsetof(XState, lastWatermark), &lw, 8, hipMemcpyHostToDevice, stream));
+  XCHK(hipStreamSynchronize(stream));
+  return SCOTTY_OK;
+}
+
+int XEngine::slice_count(int64_t op, int64_t* out) {
+  if (op < 0 || op >= n_ops) {
+    *out = 0;
+    return SCOTTY_OK;
+  }
+  XState s;
+  XCHK(hipMemcpy(&s, d_st + op, sizeof(XState), hipMemcpyDeviceToHost));
+  *out = s.tail - s.head;
+  return SCOTTY_OK;
+}
+
+int XEngine::read_states(std::vector<XState>& out) {
+  out.resize(n_ops);
+  if (n_ops) XCHK(hipMemcpy(out.data(), d_st, n_ops * sizeof(XState), hipMemcpyDeviceToHost));
+  return SCOTTY_OK;
+}
+
+}  // namespace scotty

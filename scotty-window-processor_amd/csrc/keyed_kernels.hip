@@ -1,0 +1,395 @@
+// keyed_kernels.hip -- gfx950 kernels that turn an arrival-ordered keyed micro-batch into per-operator
+// segments for the exact engine (exact_kernels.hip).
+//
+// The reference keeps one SlicingWindowOperator per key in a HashMap and feeds each key's tuples in
+// arrival order (flink-connector/.../KeyedScottyWindowOperator.java:56-66).  Here:
+//   1. key_insert / key_assign: a device open-addressing hash table maps each key to a dense operator slot
+//      (new keys get the next free slots: the HashMap.put of initWindowOperator, :57-60);
+//   2. slot_kernel: slot of every tuple;
+//   3. an LDS-staged, stable LSD radix sort of the (ts, value, slot) records by slot, 8 bits per pass:
+//      radix_hist (per-tile digit counts) -> scan -> radix_scatter (tile ranked stably in LDS with
+//      wave ballots, written out as contiguous per-digit runs).  Stability keeps every key's tuples in
+//      arrival order, which the reference's out-of-order handling depends on;
+//   4. seg_kernel: [begin, end) of every operator's run.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "exact_common.h"
+
+namespace scotty {
+namespace k {
+
+constexpr int RB = 8;                 // radix bits per pass
+constexpr int RADIX = 1 << RB;
+constexpr int SORT_THREADS = 256;
+constexpr int SORT_ITEMS = 8;
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;  // 2048 records per tile
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {  // murmur3 finaliser
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+// ---------------------------------------------------------------- hash table
+// entry: (key+1) << 32 | slot; 0 = empty; slot 0xFFFFFFFF = inserted in this batch, slot not yet assigned
+__global__ void key_insert_kernel(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
+                                  uint32_t* new_pos, unsigned long long* new_count, int32_t* full) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t tag = ((uint64_t)keys[i] + 1) << 32;
+    uint64_t h = hash32(keys[i]) & mask;
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+      unsigned long long e = table[h];
+      if ((e & 0xFFFFFFFF00000000ull) == tag) break;
+      if (e == 0) {
+        const unsigned long long prev = atomicCAS(&table[h], 0ull, (unsigned long long)(tag | 0xFFFFFFFFull));
+        if (prev == 0) {
+          const unsigned long long p = atomicAdd(new_count, 1ull);
+          new_pos[p] = (uint32_t)h;
+          break;
+        }
+        if ((prev & 0xFFFFFFFF00000000ull) == tag) break;
+      }
+      h = (h + 1) & mask;
+      if (probe == mask) atomicOr(full, 1);
+    }
+  }
+}
+
+__global__ void key_assign_kernel(unsigned long long* table, const uint32_t* new_pos, int64_t n_new, int64_t base,
+                                  uint32_t* slot_key) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_new; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = new_pos[i];
+    const unsigned long long e = table[h];
+    const uint32_t key = (uint32_t)((e >> 32) - 1);
+    table[h] = (e & 0xFFFFFFFF00000000ull) | (unsigned long long)(uint32_t)(base + i);
+    slot_key[base + i] = key;
+  }
+}
+
+__global__ void rehash_kernel(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)old_n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long e = old_t[i];
+    if (e == 0) continue;
+    uint64_t h = hash32((uint32_t)((e >> 32) - 1)) & mask;
+    while (atomicCAS(&nt[h], 0ull, e) != 0ull) h = (h + 1) & mask;
+  }
+}
+
+__global__ void slot_kernel(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
+                            uint32_t* slot) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t tag = ((uint64_t)keys[i] + 1) << 32;
+    uint64_t h = hash32(keys[i]) & mask;
+    unsigned long long e;
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+      e = table[h];
+      if ((e & 0xFFFFFFFF00000000ull) == tag) break;
+      h = (h + 1) & mask;
+    }
+    slot[i] = (uint32_t)e;
+  }
+}
+
+// ---------------------------------------------------------------- records
+// REC = 16: {ts i64, val i32, slot u32};  REC = 24: {ts i64, val 64-bit, slot u32, pad}
+template <int REC>
+struct Rec;
+template <>
+struct __attribute__((packed, aligned(16))) Rec<16> {
+  int64_t ts;
+  int32_t v;
+  uint32_t slot;
+};
+template <>
+struct __attribute__((packed, aligned(8))) Rec<24> {
+  int64_t ts;
+  int64_t v;
+  uint32_t slot;
+  uint32_t pad;
+};
+
+template <int REC>
+__device__ __forceinline__ Rec<REC> make_rec(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i) {
+  Rec<REC> r;
+  r.ts = ts[i];
+  if constexpr (REC == 16) r.v = ((const int32_t*)val)[i];
+  else { r.v = ((const int64_t*)val)[i]; r.pad = 0; }
+  r.slot = slot[i];
+  return r;
+}
+
+// FIRST: input is SoA (ts, val, slot arrays); else AoS records
+template <int REC, bool FIRST>
+__global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>* in, const int64_t* ts,
+                                                                   const void* val, const uint32_t* slot, int64_t n,
+                                                                   int shift, int32_t* hist, int64_t nblocks) {
+  __shared__ int32_t cnt[RADIX];
+  const int tid = threadIdx.x;
+  for (int d = tid; d < RADIX; d += SORT_THREADS) cnt[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; r++) {
+    const int64_t i = base + r * SORT_THREADS + tid;
+    if (i < n) {
+      const uint32_t s = FIRST ? slot[i] : in[i].slot;
+      atomicAdd(&cnt[(s >> shift) & (RADIX - 1)], 1);
+    }
+  }
+  __syncthreads();
+  for (int d = tid; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = cnt[d];
+}
+
+template <int REC, bool FIRST>
+__global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<REC>* in, const int64_t* ts,
+                                                                      const void* val, const uint32_t* slot,
+                                                                      int64_t n, int shift, const int32_t* offs,
+                                                                      int64_t nblocks, Rec<REC>* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  Rec<REC>* stage = (Rec<REC>*)smem;                                       // [SORT_TILE]
+  int32_t* wc = (int32_t*)(smem + sizeof(Rec<REC>) * SORT_TILE);          // [4][RADIX]
+  int32_t* run = wc + 4 * RADIX;                                           // [RADIX]
+  int32_t* tstart = run + RADIX;                                           // [RADIX] tile digit starts
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+  for (int d = tid; d < RADIX; d += SORT_THREADS) {
+    run[d] = 0;
+    tstart[d] = 0;
+  }
+  __syncthreads();
+  // load (striped: item r of thread t is element r*256+t, i.e. arrival order = (r, wave, lane))
+  Rec<REC> item[SORT_ITEMS];
+  int32_t dig[SORT_ITEMS];
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; r++) {
+    const int64_t i = base + r * SORT_THREADS + tid;
+    if (i < n) {
+      item[r] = FIRST ? make_rec<REC>(ts, val, slot, i) : in[i];
+      dig[r] = (item[r].slot >> shift) & (RADIX - 1);
+      atomicAdd(&tstart[dig[r]], 1);
+    } else {
+      dig[r] = -1;
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the tile's digit counts (RADIX == SORT_THREADS)
+  {
+    const int32_t v = tstart[tid];
+    int32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wc[wid] = inc;
+    __syncthreads();
+    int32_t add = 0;
+    for (int w = 0; w < wid; w++) add += wc[w];
+    __syncthreads();
+    tstart[tid] = inc - v + add;
+  }
+  for (int d = tid; d < 4 * RADIX; d += SORT_THREADS) wc[d] = 0;
+  __syncthreads();
+  // stable ranking, round by round
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; r++) {
+    const int d = dig[r];
+    unsigned long long peers = __ballot(d >= 0);
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+      const unsigned long long bb = __ballot(d >= 0 && ((d >> b) & 1));
+      peers &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const int rank = __popcll(peers & ((1ull << lane) - 1));
+    const bool leader = d >= 0 && rank == 0;
+    if (leader) wc[wid * RADIX + d] = __popcll(peers);
+    __syncthreads();
+    if (d >= 0) {
+      int32_t pos = tstart[d] + run[d] + rank;
+      for (int w = 0; w < wid; w++) pos += wc[w * RADIX + d];
+      stage[pos] = item[r];
+    }
+    __syncthreads();
+    {
+      const int dd = tid;  // RADIX == SORT_THREADS
+      run[dd] += wc[dd] + wc[RADIX + dd] + wc[2 * RADIX + dd] + wc[3 * RADIX + dd];
+      wc[dd] = wc[RADIX + dd] = wc[2 * RADIX + dd] = wc[3 * RADIX + dd] = 0;
+    }
+    __syncthreads();
+  }
+  // write out per-digit runs
+  const int64_t cnt_tile = min((int64_t)SORT_TILE, n - base);
+  for (int i = tid; i < cnt_tile; i += SORT_THREADS) {
+    const Rec<REC> rr = stage[i];
+    const int d = (rr.slot >> shift) & (RADIX - 1);
+    const int64_t g = (int64_t)offs[(int64_t)d * nblocks + blockIdx.x] + (i - tstart[d]);
+    out[g] = rr;
+  }
+}
+
+template <int REC>
+__global__ void seg_kernel(const Rec<REC>* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t s = recs[i].slot;
+    if (i == 0 || recs[i - 1].slot != s) seg_begin[s] = i;
+    if (i == n - 1 || recs[i + 1].slot != s) seg_end[s] = i + 1;
+  }
+}
+
+// ---------------------------------------------------------------- scans (int32 and int64, exclusive)
+template <typename T>
+__global__ __launch_bounds__(1024) void scan_block_kernel(const T* in, T* out, int64_t n, T* block_sums) {
+  __shared__ T ws[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + tid;
+  const T v = i < n ? in[i] : (T)0;
+  T inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) ws[wid] = inc;
+  __syncthreads();
+  T add = 0;
+  for (int w = 0; w < wid; w++) add += ws[w];
+  if (i < n) out[i] = inc - v + add;
+  if (tid == 1023) block_sums[blockIdx.x] = inc + add;
+}
+template <typename T>
+__global__ void scan_add_kernel(T* out, int64_t n, const T* block_off) {
+  const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (i < n) out[i] += block_off[blockIdx.x];
+}
+
+}  // namespace k
+
+// ---------------------------------------------------------------- host wrappers
+// exclusive scan in place-capable (in may equal out); tmp needs >= 2 * ceil(n/1024) + ... elements (recursive)
+template <typename T>
+static hipError_t scan_rec(const T* in, T* out, int64_t n, T* tmp, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nb = (n + 1023) / 1024;
+  T* sums = tmp;
+  T* rest = tmp + nb;
+  hipLaunchKernelGGL(k::scan_block_kernel<T>, dim3((unsigned)nb), dim3(1024), 0, st, in, out, n, sums);
+  if (nb > 1) {
+    hipError_t e = scan_rec<T>(sums, sums, nb, rest, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k::scan_add_kernel<T>, dim3((unsigned)nb), dim3(1024), 0, st, out, n, sums);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st) {
+  return scan_rec<int64_t>(in, out, n, tmp, st);
+}
+hipError_t launch_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t st) {
+  return scan_rec<int32_t>(in, out, n, tmp, st);
+}
+
+static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
+
+hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
+                             uint32_t* new_pos, unsigned long long* new_count, int32_t* full, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k::key_insert_kernel, dim3(grid_for(n)), dim3(256), 0, st, keys, n, table, mask, new_pos,
+                     new_count, full);
+  return hipGetLastError();
+}
+hipError_t launch_key_assign(unsigned long long* table, const uint32_t* new_pos, int64_t n_new, int64_t base,
+                             uint32_t* slot_key, hipStream_t st) {
+  if (n_new <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k::key_assign_kernel, dim3(grid_for(n_new)), dim3(256), 0, st, table, new_pos, n_new, base,
+                     slot_key);
+  return hipGetLastError();
+}
+hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k::rehash_kernel, dim3(grid_for((int64_t)old_n)), dim3(256), 0, st, old_t, old_n, nt, mask);
+  return hipGetLastError();
+}
+hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
+                       uint32_t* slot, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k::slot_kernel, dim3(grid_for(n)), dim3(256), 0, st, keys, n, table, mask, slot);
+  return hipGetLastError();
+}
+
+int64_t sort_tile() { return k::SORT_TILE; }
+
+// Stable sort of the batch by slot into records (AoS, rec bytes 16 or 24).  bufA/bufB: n records each;
+// hist/offs: RADIX * ceil(n / tile) int32; scan_tmp: int32 scratch.  Result lands in *result.
+hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
+                               int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
+                               void** result, hipStream_t st) {
+  const int64_t nb = (n + k::SORT_TILE - 1) / k::SORT_TILE;
+  int passes = (slot_bits + k::RB - 1) / k::RB;
+  if (passes < 1) passes = 1;
+  void* src = nullptr;
+  void* dst = bufA;
+  for (int p = 0; p < passes; p++) {
+    const int shift = p * k::RB;
+    const size_t lds = (size_t)rec * k::SORT_TILE + 4 * (4 * k::RADIX + 2 * k::RADIX);
+    if (rec == 16) {
+      using R = k::Rec<16>;
+      if (p == 0) {
+        hipLaunchKernelGGL((k::radix_hist_kernel<16, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb);
+      } else {
+        hipLaunchKernelGGL((k::radix_hist_kernel<16, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                           (const R*)src, ts, val, slot, n, shift, hist, nb);
+      }
+      hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
+      if (e != hipSuccess) return e;
+      if (p == 0) {
+        hipLaunchKernelGGL((k::radix_scatter_kernel<16, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds, st,
+                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst);
+      } else {
+        hipLaunchKernelGGL((k::radix_scatter_kernel<16, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds,
+                           st, (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst);
+      }
+    } else {
+      using R = k::Rec<24>;
+      if (p == 0) {
+        hipLaunchKernelGGL((k::radix_hist_kernel<24, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb);
+      } else {
+        hipLaunchKernelGGL((k::radix_hist_kernel<24, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                           (const R*)src, ts, val, slot, n, shift, hist, nb);
+      }
+      hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
+      if (e != hipSuccess) return e;
+      if (p == 0) {
+        hipLaunchKernelGGL((k::radix_scatter_kernel<24, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds, st,
+                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst);
+      } else {
+        hipLaunchKernelGGL((k::radix_scatter_kernel<24, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds,
+                           st, (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst);
+      }
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    src = dst;
+    dst = (dst == bufA) ? bufB : bufA;
+  }
+  *result = src;
+  return hipSuccess;
+}
+
+hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (rec == 16)
+    hipLaunchKernelGGL(k::seg_kernel<16>, dim3(grid_for(n)), dim3(256), 0, st, (const k::Rec<16>*)recs, n, seg_begin,
+                       seg_end);
+  else
+    hipLaunchKernelGGL(k::seg_kernel<24>, dim3(grid_for(n)), dim3(256), 0, st, (const k::Rec<24>*)recs, n, seg_begin,
+                       seg_end);
+  return hipGetLastError();
+}
+
+}  // namespace scotty

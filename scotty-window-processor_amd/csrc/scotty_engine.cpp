@@ -17,6 +17,7 @@
 
 #include "../../include/scotty_mi355x.h"
 #include "device_common.h"
+#include "exact_engine.h"
 
 namespace scotty {
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
@@ -122,6 +123,17 @@ struct scotty_op {
   uint64_t dropped = 0, processed = 0;
 
   int ingest_mode = -1;  // tuning knob (scotty_tune), -1 = default variant
+
+  // ---- engine selection: the grid path (context-free time windows, non-keyed) or the exact engine
+  //      (keyed ops, session windows, count windows); decided at the first push
+  bool keyed = false;
+  int mode = 0;                       // 0 undecided, 1 grid, 2 exact
+  std::vector<XWinDef> xwins;         // every window, registration order
+  XEngine* x = nullptr;
+  int32_t x_sc = 0, x_sess = 0;       // capacity knobs
+  uint64_t x_pushed = 0;
+  std::vector<uint32_t> r_key;
+  XResult xr;
 
   // ---- timing
   bool timing = false;
@@ -563,13 +575,13 @@ int scotty_create(scotty_op** out, int device, int value_type, uint32_t flags) {
   if (!out) return SCOTTY_ERR_ARG;
   *out = nullptr;
   if (value_type < VT_I32 || value_type > VT_F64) return SCOTTY_ERR_ARG;
-  if (flags & SCOTTY_FLAG_KEYED) return SCOTTY_ERR_UNSUPPORTED;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SCOTTY_ERR_HIP;
   if (device < 0 || device >= ndev) return SCOTTY_ERR_ARG;
   scotty_op* op = new scotty_op();
   op->device = device;
   op->vt = value_type;
+  op->keyed = (flags & SCOTTY_FLAG_KEYED) != 0;
   int rc = alloc_all(op);
   if (rc) {
     scotty_destroy(op);
@@ -594,6 +606,7 @@ void scotty_destroy(scotty_op* op) {
   if (op->h_obuf) (void)hipHostFree(op->h_obuf);
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  delete op->x;
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
 }
@@ -608,10 +621,22 @@ int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b
     return fail(op, SCOTTY_ERR_ARG, "unknown window kind / measure");
   if ((kind == SCOTTY_WIN_TUMBLING && a <= 0) || (kind == SCOTTY_WIN_SLIDING && (a <= 0 || b <= 0)))
     return fail(op, SCOTTY_ERR_ARG, "window size / slide must be positive");
-  if (kind == SCOTTY_WIN_SESSION)
-    return fail(op, SCOTTY_ERR_UNSUPPORTED, "SessionWindow is not implemented on the MI355X path yet");
-  if (measure == SCOTTY_MEASURE_COUNT)
-    return fail(op, SCOTTY_ERR_UNSUPPORTED, "count-measure windows are not implemented on the MI355X path yet");
+  if (kind == SCOTTY_WIN_SESSION && a < 0) return fail(op, SCOTTY_ERR_ARG, "session gap must be >= 0");
+  const bool exact_only = kind == SCOTTY_WIN_SESSION || measure == SCOTTY_MEASURE_COUNT;
+  if (op->mode == 2) {  // exact engine: reconfigure (windows may be added mid-stream, S/WindowManager.java:121-147)
+    op->xwins.push_back({kind, measure, a, b});
+    int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
+    if (rc) {
+      op->xwins.pop_back();
+      return fail(op, rc, op->x->err);
+    }
+    return SCOTTY_OK;
+  }
+  if (exact_only && op->mode == 1)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED,
+                "session / count window added after elements were processed by the context-free grid path");
+  op->xwins.push_back({kind, measure, a, b});
+  if (exact_only) return SCOTTY_OK;
   CFWin w{kind, a, b};
   const bool had_fixed = op->has_fixed;
   if (op->started && !had_fixed)
@@ -642,8 +667,8 @@ int scotty_add_aggregation(scotty_op* op, int kind) {
   if (vt == -2) return fail(op, SCOTTY_ERR_ARG, "unknown aggregation kind");
   if (vt >= 0 && vt != op->vt) return fail(op, SCOTTY_ERR_ARG, "aggregation kind does not match the value type");
   if ((int)op->aggs.size() >= SCOTTY_MAX_AGGS) return fail(op, SCOTTY_ERR_ARG, "too many aggregations");
-  if (op->started && (agg_need(kind) & ~op->need))
-    return fail(op, SCOTTY_ERR_UNSUPPORTED, "aggregation needing a new partial added after elements were processed");
+  if (op->mode != 0)  // existing slices would lack the new function's state (S/state/AggregateState.java:44-50)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "aggregation added after elements were processed");
   op->aggs.push_back(kind);
   op->need |= agg_need(kind);
   return (int)op->aggs.size() - 1;
@@ -652,12 +677,50 @@ int scotty_add_aggregation(scotty_op* op, int kind) {
 int scotty_set_max_lateness(scotty_op* op, int64_t l) {
   if (!op) return SCOTTY_ERR_ARG;
   op->max_lateness = l;
+  if (op->mode == 2) {
+    int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
+    if (rc) return fail(op, rc, op->x->err);
+  }
+  return SCOTTY_OK;
+}
+
+// First push: the grid path serves non-keyed ops whose windows are all context-free time windows; every
+// other configuration runs on the exact engine.
+static int decide_mode(scotty_op* op) {
+  if (op->mode != 0) return SCOTTY_OK;
+  bool exact = op->keyed;
+  for (const XWinDef& w : op->xwins)
+    if (w.kind == SCOTTY_WIN_SESSION || w.measure == SCOTTY_MEASURE_COUNT) exact = true;
+  if (!exact) {
+    op->mode = 1;
+    return SCOTTY_OK;
+  }
+  op->x = new XEngine();
+  op->x->sc_override = op->x_sc;
+  op->x->sess_override = op->x_sess;
+  std::string e;
+  int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
+  if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
+  if (!rc && !op->keyed && op->last_watermark != -1) rc = op->x->set_last_watermark(op->last_watermark);
+  if (rc) {
+    op->failed = true;
+    return fail(op, rc, op->x->err);
+  }
+  op->mode = 2;
   return SCOTTY_OK;
 }
 
 static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, const int64_t* h_ts0) {
   if (n <= 0) return SCOTTY_OK;
-  int rc;
+  int rc = decide_mode(op);
+  if (rc) return rc;
+  if (op->mode == 2) {
+    op->pending.push_back({d_ts, d_val, n, op->push_seq++});
+    op->x_pushed += (uint64_t)n;
+    rc = op->x->push(d_ts, d_val, n);
+    if (rc) return fail(op, rc, op->x->err);
+    return SCOTTY_OK;
+  }
   if (!op->started) {
     int64_t ts0;
     if (h_ts0) ts0 = *h_ts0;
@@ -670,11 +733,14 @@ static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int6
   return enqueue_push(op, d_ts, d_val, n, seq);
 }
 
+static size_t value_bytes(const scotty_op* op) { return op->vt == VT_I32 ? 4 : 8; }
+
 int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, size_t n) {
   if (!op || (n && (!ts || !val))) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->keyed) return fail(op, SCOTTY_ERR_ARG, "keyed operator: use scotty_process_keyed_elements");
   if (n == 0) return SCOTTY_OK;
-  const size_t vb = op->vt == VT_I32 ? 4 : 8;
+  const size_t vb = value_bytes(op);
   void* d = nullptr;
   HIPCHK(hipMalloc(&d, n * 8 + n * vb + 16));
   int64_t* d_ts = (int64_t*)d;
@@ -689,14 +755,110 @@ int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, s
 int scotty_process_elements_device(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n) {
   if (!op || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->keyed) return fail(op, SCOTTY_ERR_ARG, "keyed operator: use scotty_process_keyed_elements_device");
   if (((uintptr_t)d_ts & 15) || ((uintptr_t)d_val & 15))
     return fail(op, SCOTTY_ERR_ARG, "device buffers must be 16-byte aligned");
   return push_impl(op, d_ts, d_val, (int64_t)n, nullptr);
 }
 
+static int keyed_push(scotty_op* op, const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n) {
+  int rc = decide_mode(op);
+  if (rc) return rc;
+  op->x_pushed += (uint64_t)n;
+  rc = op->x->push_keyed(d_key, d_ts, d_val, n);
+  if (rc) return fail(op, rc, op->x->err);
+  return SCOTTY_OK;
+}
+
+int scotty_process_keyed_elements(scotty_op* op, const uint32_t* key, const int64_t* ts, const void* val, size_t n) {
+  if (!op || (n && (!ts || !val || !key))) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (!op->keyed) return fail(op, SCOTTY_ERR_ARG, "not a keyed operator (create with SCOTTY_FLAG_KEYED)");
+  if (n == 0) return SCOTTY_OK;
+  const size_t vb = value_bytes(op);
+  const size_t o_val = ((n * 8 + 15) / 16) * 16, o_key = o_val + ((n * vb + 15) / 16) * 16;
+  void* d = nullptr;
+  HIPCHK(hipMalloc(&d, o_key + n * 4 + 16));
+  HIPCHK(hipMemcpyAsync(d, ts, n * 8, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync((unsigned char*)d + o_val, val, n * vb, hipMemcpyHostToDevice, op->stream));
+  HIPCHK(hipMemcpyAsync((unsigned char*)d + o_key, key, n * 4, hipMemcpyHostToDevice, op->stream));
+  int rc = keyed_push(op, (const uint32_t*)((unsigned char*)d + o_key), (const int64_t*)d,
+                      (unsigned char*)d + o_val, (int64_t)n);
+  (void)hipStreamSynchronize(op->stream);
+  (void)hipFree(d);
+  return rc;
+}
+
+int scotty_process_keyed_elements_device(scotty_op* op, const uint32_t* d_key, const int64_t* d_ts,
+                                         const void* d_val, size_t n) {
+  if (!op || (n && (!d_ts || !d_val || !d_key))) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (!op->keyed) return fail(op, SCOTTY_ERR_ARG, "not a keyed operator (create with SCOTTY_FLAG_KEYED)");
+  if (n == 0) return SCOTTY_OK;
+  return keyed_push(op, d_key, d_ts, d_val, (int64_t)n);
+}
+
+// watermark of the exact engine
+static int exact_watermark(scotty_op* op, int64_t wm, scotty_windows* out, bool to_host) {
+  XResult& r = op->xr;
+  const uint64_t dropped_before = op->dropped;
+  int rc = op->x->watermark(wm, r, to_host);
+  if (rc) return fail(op, rc, op->x->err);
+  op->dropped = r.dropped;
+  op->processed = op->x_pushed - r.dropped;
+  for (void* p : op->owned) (void)hipFree(p);
+  op->owned.clear();
+  op->pending.clear();
+  if (out) {
+    std::memset(out, 0, sizeof(*out));
+    out->n_windows = (size_t)r.n;
+    out->n_aggs = (int32_t)op->aggs.size();
+    if (to_host) {
+      out->start = r.start.data();
+      out->end = r.end.data();
+      out->measure = r.meas.data();
+      out->has_value = r.has.data();
+      for (size_t k = 0; k < op->aggs.size() && k < r.vals.size(); k++) out->values[k] = r.vals[k].data();
+      out->key = op->keyed ? r.key.data() : nullptr;
+    } else {
+      out->start = r.d_start;
+      out->end = r.d_end;
+      out->measure = r.d_meas;
+      out->has_value = r.d_has;
+      for (size_t k = 0; k < op->aggs.size(); k++) out->values[k] = r.d_vals[k];
+      out->key = op->keyed ? r.d_key : nullptr;
+    }
+  }
+  if (op->dropped > dropped_before) {
+    op->err = "tuples older than the oldest retained slice were dropped (reference: IndexOutOfBoundsException)";
+    return SCOTTY_WARN_LATE_DROPPED;
+  }
+  return SCOTTY_OK;
+}
+
+int scotty_process_watermark_device(scotty_op* op, int64_t wm, scotty_windows* out) {
+  if (!op) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->mode != 2) {
+    if (op->mode == 0 && op->keyed) {  // keyed op without any tuple yet: no operators, no windows
+      if (out) std::memset(out, 0, sizeof(*out));
+      return SCOTTY_OK;
+    }
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "device results are provided by the exact engine only");
+  }
+  return exact_watermark(op, wm, out, false);
+}
+
+int64_t scotty_key_count(scotty_op* op) { return (op && op->x) ? op->x->key_count() : 0; }
+
 int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
   if (!op) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->mode == 2) return exact_watermark(op, wm, out, true);
+  if (op->keyed) {  // keyed op without any tuple yet: no per-key operators exist
+    if (out) std::memset(out, 0, sizeof(*out));
+    return SCOTTY_OK;
+  }
   int rc;
   const uint64_t dropped_before = op->dropped;
   // WindowManager.processWatermark (S/WindowManager.java:41-80)
@@ -815,7 +977,14 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
 uint64_t scotty_dropped_count(scotty_op* op) { return op ? op->dropped : 0; }
 uint64_t scotty_processed_count(scotty_op* op) { return op ? op->processed : 0; }
 int64_t scotty_slice_count(scotty_op* op) {
-  if (!op || !op->started) return 0;
+  if (!op) return 0;
+  if (op->mode == 2) {
+    if (op->keyed) return -1;
+    int64_t c = 0;
+    if (op->x->slice_count(0, &c)) return -1;
+    return c;
+  }
+  if (!op->started) return 0;
   if (sync_snapshot(op)) return -1;
   return op->h_snap->tail - op->h_snap->head;
 }
@@ -837,11 +1006,16 @@ int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, ui
   return SCOTTY_OK;
 }
 
-// Undeclared tuning hook (not part of the ABI contract): "ingest_mode" selects an ingest-kernel variant.
+// Tuning knobs (include/scotty_mi355x.h): capacities of the exact engine, grid ingest variant.
 int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (!op || !key) return SCOTTY_ERR_ARG;
   if (std::strcmp(key, "ingest_mode") == 0) {
     op->ingest_mode = (int)value;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "slice_capacity") == 0 || std::strcmp(key, "session_capacity") == 0) {
+    if (op->mode != 0 || value <= 0 || value > (1 << 26)) return SCOTTY_ERR_ARG;
+    (key[1] == 'l' ? op->x_sc : op->x_sess) = (int32_t)value;
     return SCOTTY_OK;
   }
   return SCOTTY_ERR_ARG;

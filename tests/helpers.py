@@ -97,3 +97,62 @@ def interval_schedule(ts, n_intervals, lag, pushes_per_interval=1):
         if hi > 0:
             sched.append(("wm", int(ts[:hi].max()) - lag))
     return sched
+
+
+class KeyedOracle:
+    """One OracleOperator per key, created on the key's first tuple with the same windows / functions /
+    lateness -- the HashMap of flink-connector/.../KeyedScottyWindowOperator.java:21-66.  Test checker."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.ops = {}      # key -> OracleOperator, insertion order = creation order
+        self.failed = 0
+
+    def _new(self):
+        from oracle.oracle import OracleOperator
+        op = OracleOperator()
+        for a in self.cfg["aggs"]:
+            op.addWindowFunction(a)
+        if self.cfg.get("lateness") is not None:
+            op.setMaxLateness(self.cfg["lateness"])
+        for w in self.cfg["windows"]:
+            op.addWindowAssigner(w)
+        return op
+
+    def processElements(self, keys, ts, vals):
+        import numpy as np
+        keys = np.asarray(keys)
+        for k in keys:  # creation order = first appearance
+            k = int(k)
+            if k not in self.ops:
+                self.ops[k] = self._new()
+        order = np.argsort(keys, kind="stable")
+        ks = keys[order]
+        bounds = np.flatnonzero(np.diff(ks)) + 1
+        for seg in np.split(np.arange(len(ks)), bounds):
+            if len(seg) == 0:
+                continue
+            idx = order[seg]
+            op = self.ops[int(ks[seg[0]])]
+            if vals.dtype.kind == "f":
+                self.failed += op.processElements(ts[idx], np.zeros(len(idx), dtype=np.int64), vals[idx])
+            else:
+                self.failed += op.processElements(ts[idx], vals[idx])
+
+    def processWatermark(self, wm):
+        # KeyedScottyWindowOperator.processWatermark loops over every key's operator (:77); an exception of
+        # one key's processWatermark propagates out of the loop
+        return {k: op.processWatermark(wm) for k, op in self.ops.items()}
+
+
+def same_keyed_windows(rows, expected, f64_cols=()):
+    """rows: [(key, AggregateWindow)] of the product; expected: {key: [AggregateWindow]} of the oracle.
+    Keys compare as a set (Java HashMap order is not a contract); windows of one key position by position."""
+    got = {}
+    for k, w in rows:
+        got.setdefault(k, []).append(w)
+    exp = {k: v for k, v in expected.items() if v}
+    assert set(got) == set(exp), ("keys", sorted(set(got) ^ set(exp))[:10])
+    for k in exp:
+        same_windows(got[k], exp[k], f64_cols=f64_cols)
+    return sum(len(v) for v in exp.values())

@@ -1,0 +1,214 @@
+"""Parity of the exact engine (session windows, count windows, keyed operators) on the MI355X against the
+CPU oracle: bit-exact window bounds, hasValue and integer aggregates (f64 sums within 1e-6 relative).
+
+Reference behaviour exercised: SessionWindow.SessionContext (C/windowType/SessionWindow.java:40-116),
+SliceManager.checkSliceEdges / splitSlice on out-of-order tuples (S/SliceManager.java:89-192), count
+edges (S/StreamSlicer.java:37-44, :88-101), count triggers (S/WindowManager.java:109-115) and the keyed
+connector's per-key operators (flink-connector/.../KeyedScottyWindowOperator.java:56-86)."""
+import numpy as np
+import pytest
+
+import junit_cases
+from helpers import product, build_ops, run_schedule, interval_schedule, KeyedOracle, same_keyed_windows
+from specs import Tumbling, Sliding, Session, FixedBand, Time, Count, SUM, COUNT, MIN, MAX, SUM_I64, \
+    MIN_I64, MAX_I64, SUM_F64, MIN_F64, MAX_F64
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    return product()
+
+
+# ---------------------------------------------------------------- the reference's golden values
+@pytest.mark.parametrize("case", junit_cases.SESSION + [junit_cases.tumbling_inOrderTestCount],
+                         ids=lambda c: c.__name__)
+def test_junit_session_and_count_golden_values_on_gpu(pkg, case):
+    case(lambda: pkg.SlicingWindowOperator(device=0))
+
+
+@pytest.mark.parametrize("case", [c for c in junit_cases.TUMBLING_COUNT if c is not junit_cases.tumbling_inOrderTestCount],
+                         ids=lambda c: c.__name__)
+def test_junit_lazy_count_out_of_order_fails_loudly(pkg, case):
+    """Out-of-order tuples with count windows move LazySlice records (S/SliceManager.java:77-85), and the
+    test-only (a,b)->a-b function has no GPU kind: both raise instead of falling back to the CPU."""
+    with pytest.raises(pkg.ScottyError):
+        case(lambda: pkg.SlicingWindowOperator(device=0))
+
+
+def _nz(x):  # a power-of-two size/slide makes the reference loop forever; avoid it in random configs
+    return x + 1 if x & (x - 1) == 0 else x
+
+
+def _aggs(rng, vt):
+    aggs = {"i32": [SUM, COUNT, MIN, MAX], "i64": [SUM_I64, COUNT, MIN_I64, MAX_I64],
+            "f64": [SUM_F64, COUNT, MIN_F64, MAX_F64]}[vt]
+    return [a for a in aggs if rng.random() < 0.7] or [aggs[0]]
+
+
+def _session_cfg(rng, vt):
+    wins = [Session(Time, int(rng.integers(3, 300)))]
+    if rng.random() < 0.3:
+        wins.append(Session(Time, int(rng.integers(3, 300))))
+    for _ in range(int(rng.integers(0, 3))):
+        if rng.random() < 0.5:
+            wins.append(Tumbling(Time, _nz(int(rng.integers(5, 200)))))
+        else:
+            size = int(rng.integers(10, 300))
+            wins.append(Sliding(Time, size, _nz(int(rng.integers(3, size + 1)))))
+    rng.shuffle(wins)
+    return dict(windows=wins, aggs=_aggs(rng, vt), lateness=int(rng.choice([1, 5, 50, 500, 1000])))
+
+
+def _gaps(rng, n, every, lo, hi):
+    return [(int(i), int(rng.integers(lo, hi))) for i in range(every, n, every)]
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_session_streams_match_oracle(seed):
+    rng = np.random.default_rng(7000 + seed)
+    vt = ["i32", "i32", "i64", "f64"][seed % 4]
+    cfg = _session_cfg(rng, vt)
+    n = int(rng.integers(100, 20_000))
+    rate = [0.05, 0.3, 1, 5][int(rng.integers(0, 4))]
+    gaps = _gaps(rng, n, int(rng.integers(50, 2000)), 50, 800)
+    ooo = [0.0, 0.05, 0.2][int(rng.integers(0, 3))]
+    ts, vals = product().workloads.stream(n, rate, t0=int(rng.integers(0, 3000)), ooo_frac=ooo,
+                                          max_delay=int(rng.integers(1, 300)), seed=seed, value_type=vt, gaps=gaps)
+    gpu, ora = build_ops(cfg, vt)
+    sched = interval_schedule(ts, int(rng.integers(1, 10)), lag=int(rng.integers(0, 300)),
+                              pushes_per_interval=int(rng.integers(1, 3)))
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
+    run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_count_windows_in_order_match_oracle(seed):
+    rng = np.random.default_rng(9100 + seed)
+    wins = [Tumbling(Count, int(rng.integers(1, 50)))]
+    if rng.random() < 0.5:
+        size = int(rng.integers(2, 60))
+        wins.append(Sliding(Count, size, int(rng.integers(1, size + 1))))
+    if rng.random() < 0.5:
+        wins.append(Tumbling(Time, _nz(int(rng.integers(5, 100)))))
+    if rng.random() < 0.3:
+        wins.append(Session(Time, int(rng.integers(5, 100))))
+    cfg = dict(windows=wins, aggs=[SUM, COUNT, MAX], lateness=int(rng.choice([1, 10, 1000])))
+    n = int(rng.integers(10, 5000))
+    ts, vals = product().workloads.stream(n, [0.5, 1, 3][seed % 3], t0=int(rng.integers(0, 500)), seed=seed,
+                                          gaps=_gaps(rng, n, 300, 10, 200))
+    gpu, ora = build_ops(cfg)
+    sched = interval_schedule(ts, int(rng.integers(1, 6)), lag=int(rng.integers(0, 20)))
+    run_schedule(gpu, ora, ts, vals, sched)
+
+
+def test_session_tumbling_mixed_config3_reduced():
+    """BASELINE configs[2] at reduced size: sliding + session, 20 % out-of-order (TimeStampGenerator-like,
+    delay U[1,500]), MIN/MAX; session silences every ~10 s of event time."""
+    n = 600_000
+    rate = 25
+    gaps = [(i, 1500) for i in range(250_000 // 1, n, 250_000)]
+    ts, vals = product().workloads.stream(n, rate, t0=1000, ooo_frac=0.2, max_delay=500, seed=33, gaps=gaps)
+    cfg = dict(windows=[Sliding(Time, 6000, 60), Session(Time, 1000)], aggs=[MIN, MAX, COUNT], lateness=1000)
+    gpu, ora = build_ops(cfg)
+    sched = interval_schedule(ts, 24, lag=500)
+    assert run_schedule(gpu, ora, ts, vals, sched) > 0
+
+
+# ---------------------------------------------------------------- keyed
+def _keyed_run(pkg, cfg, keys, ts, vals, sched, vt="i32", f64_cols=()):
+    vtc = {"i32": pkg.VALUE_I32, "i64": pkg.VALUE_I64, "f64": pkg.VALUE_F64}[vt]
+    gpu = pkg.KeyedSlicingWindowOperator(device=0, value_type=vtc)
+    for a in cfg["aggs"]:
+        gpu.addWindowFunction(a)
+    if cfg.get("lateness") is not None:
+        gpu.setMaxLateness(cfg["lateness"])
+    for w in cfg["windows"]:
+        gpu.addWindowAssigner(w)
+    ora = KeyedOracle(cfg)
+    total = 0
+    for step in sched:
+        if step[0] == "push":
+            lo, hi = step[1], step[2]
+            if hi > lo:
+                gpu.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                if vt == "f64":
+                    ora_vals = vals[lo:hi]
+                    ora.processElements(keys[lo:hi], ts[lo:hi], ora_vals)
+                else:
+                    ora.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        else:
+            from oracle.oracle import JavaError
+            try:
+                exp = ora.processWatermark(step[1])
+            except JavaError:
+                # a key's SessionContext is empty: activeWindows.get(0) throws in the reference
+                # (SessionWindow.java:107), which ends a Flink job; the product reports the same exception
+                with pytest.raises(pkg.ScottyError) as ei:
+                    gpu.processWatermark(step[1])
+                assert ei.value.code == -5  # SCOTTY_ERR_INDEX
+                return total
+            rows = gpu.processWatermark(step[1])
+            total += same_keyed_windows(rows, exp, f64_cols=f64_cols)
+            assert gpu.droppedCount() == ora.failed
+    assert gpu.keyCount() == len(ora.ops)
+    return total
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_keyed_streams_match_per_key_oracles(pkg, seed):
+    rng = np.random.default_rng(5300 + seed)
+    vt = ["i32", "i32", "i64", "f64"][seed % 4]
+    nkeys = int(rng.choice([1, 3, 50, 700, 5000]))
+    if seed % 3 == 0:
+        cfg = _session_cfg(rng, vt)
+    else:
+        wins = []
+        for _ in range(int(rng.integers(1, 4))):
+            if rng.random() < 0.5:
+                wins.append(Tumbling(Time, _nz(int(rng.integers(5, 200)))))
+            else:
+                size = int(rng.integers(10, 300))
+                wins.append(Sliding(Time, size, _nz(int(rng.integers(3, size + 1)))))
+        cfg = dict(windows=wins, aggs=_aggs(rng, vt), lateness=int(rng.choice([1, 5, 100, 1000])))
+    n = int(rng.integers(1000, 40_000))
+    ts, vals = product().workloads.stream(n, [0.5, 2, 10][seed % 3], t0=int(rng.integers(0, 1000)),
+                                          ooo_frac=[0.0, 0.2][seed % 2], max_delay=int(rng.integers(1, 200)),
+                                          seed=seed, value_type=vt)
+    keys = (rng.integers(0, nkeys, size=n) * 2654435761 % (2**32)).astype(np.uint32)
+    sched = interval_schedule(ts, int(rng.integers(1, 6)), lag=int(rng.integers(0, 100)),
+                              pushes_per_interval=int(rng.integers(1, 3)))
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
+    _keyed_run(pkg, cfg, keys, ts, vals, sched, vt=vt, f64_cols=f64_cols)
+
+
+def test_keyed_config4_reduced(pkg):
+    """BASELINE configs[3] at reduced size: SlidingWindow(60 s, 1 s) SUM, keys Random(42).nextInt-like
+    uniform over 20k keys, 90 s of event time, watermark every second."""
+    n = 1_800_000
+    ts, vals = product().workloads.stream(n, 20, t0=0, seed=42)
+    keys = np.random.default_rng(42).integers(0, 20_000, size=n).astype(np.uint32)
+    cfg = dict(windows=[Sliding(Time, 60_000, 1_000)], aggs=[SUM], lateness=1)
+    sched = interval_schedule(ts, 90, lag=0)
+    assert _keyed_run(pkg, cfg, keys, ts, vals, sched) > 20_000
+
+
+def test_keyed_large_batch_count_property(pkg):
+    """2^24 tuples over 100k keys in one push: tumbling windows partition each key's in-order stream, so
+    the COUNTs of all emitted windows add up to the tuple count."""
+    n = 1 << 24
+    rng = np.random.default_rng(8)
+    keys = rng.integers(0, 100_000, size=n).astype(np.uint32)
+    ts = np.arange(n, dtype=np.int64) // 1000
+    vals = rng.integers(-100, 100, size=n).astype(np.int32)
+    op = pkg.KeyedSlicingWindowOperator()
+    op.addWindowFunction(COUNT)
+    op.addWindowFunction(SUM)
+    op.addWindowAssigner(Tumbling(Time, 1001))
+    op.setMaxLateness(30_000)  # first watermark emits from max(0, wm - maxLateness) = 0 (WindowManager.java:43-44)
+    op.processElements(keys, ts, vals)
+    rows = op.processWatermark(int(ts.max()) + 2000)
+    assert op.keyCount() == len(np.unique(keys))
+    assert sum(w.getAggValues()[0] for _, w in rows if w.hasValue()) == n
+    assert sum(w.getAggValues()[1] for _, w in rows if w.hasValue()) == int(vals.astype(np.int64).sum())

@@ -27,13 +27,6 @@ def test_junit_golden_values_on_gpu(pkg, case):
     case(lambda: pkg.SlicingWindowOperator(device=0))
 
 
-@pytest.mark.parametrize("case", junit_cases.SESSION + junit_cases.TUMBLING_COUNT, ids=lambda c: c.__name__)
-def test_junit_session_and_count_not_yet_on_gpu(pkg, case):
-    """Sessions / count windows (and the test-only (a,b)->a-b function) fail loudly: no CPU fallback."""
-    with pytest.raises(pkg.ScottyError):
-        case(lambda: pkg.SlicingWindowOperator(device=0))
-
-
 # ---------------------------------------------------------------- seeded random configurations
 def _not_pow2(x):
     # a power-of-two size/slide makes the reference loop forever (see test_reference_hang_config_rejected)
