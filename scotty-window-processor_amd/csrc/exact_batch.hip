@@ -1,0 +1,1038 @@
+// exact_batch.hip -- batch-parallel exact path of a NON-keyed operator with session / count windows.
+//
+// The reference processes tuple after tuple (S/SlicingWindowOperator.java:41-44).  A micro-batch of one
+// operator is split into "simple" tuples, whose effect on the operator commutes, and "events", in three
+// steps over the whole chip:
+//
+//  classification (tiles of 4096 arrival-ordered tuples, all CUs) -- from the exclusive prefix max P of
+//  the batch (StreamSlicer.maxEventTime before each tuple) and the operator state at batch start:
+//   * in-order tuples (t >= P) are events iff they may cross the pending fixed edge (the pending edge after
+//     any processed in-order tuple te is nextGrid(te) = min_w assignNextWindowStart_w(te),
+//     S/StreamSlicer.java:55-84, :103-116), may open a flexible edge or a new session (the last session of
+//     every SessionContext always ends at maxEventTime: only in-order tuples extend it or start a newer
+//     one, C/windowType/SessionWindow.java:42-87), or hit a count edge (:37-44, :88-101);
+//   * out-of-order tuples are events unless they fall inside a session of every context (then
+//     updateContext is a no-op and checkSliceEdges gets no modification).  Sessions only grow or merge
+//     inside a micro-batch, so "inside" stays true whatever earlier events do.  The in-batch sessions form
+//     a chain of jumps of the running max by more than the gap; it is compacted per context.
+//  event pass (one wavefront, exact reference logic, exact_op.h) -- walks the compacted events in order.
+//   Before each event it re-applies the effect of the simple tuples since the previous event, all of which
+//   is a max (M = max ts in between): maxEventTime, the current slice's tLast and the last session's end.
+//   An out-of-order event of an operator with sessions may split / shift / merge older slices, so it ends a
+//   "segment": the simple tuples before it are applied first.
+//  apply (all CUs) -- simple tuples of a segment are lifted and combined into their slice: the last slice
+//   present at their arrival when t >= its tStart (slices appended later start above the running max), else
+//   the last slice with tStart <= t (LazyAggregateStore.findSliceIndexByTimestamp, :29-37).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "exact_op.h"
+
+namespace scotty {
+
+constexpr int XB_THREADS = 256;
+constexpr int XB_ITEMS = 16;
+constexpr int XB_TILE = XB_THREADS * XB_ITEMS;  // 4096 tuples per tile
+
+// batch-start snapshot of the operator, built by xb_prep_kernel (1 wave)
+struct XSnap {
+  int64_t p_start;         // maxEventTime (JMIN if no tuple yet)
+  int64_t n0;              // nextEdgeTs
+  int64_t nc0;             // nextEdgeCount
+  int64_t c0;              // currentCount
+  int64_t oldest;          // tStart of the oldest retained slice
+  int32_t started, unsorted, head, tail;
+  int64_t min_gap;
+  int32_t inv[XMAXCTX];    // last session ends at maxEventTime
+  int32_t ns[XMAXCTX];     // sessions per context
+  int64_t last_start[XMAXCTX], stored_end[XMAXCTX], lim[XMAXCTX];
+};
+
+// control block of the event pass / apply segments
+struct XBCtl {
+  int64_t ev_total;        // events of the batch
+  int64_t ev_next;         // next event to process
+  int64_t seg_start;       // first tuple of the current segment
+  int64_t seg_end;         // end of the segment to apply
+  int64_t ep_count;        // epoch entries of the current segment
+  int32_t stopped, done;
+  int32_t resume;          // the next event is the stop event of the previous segment
+  int32_t pad;
+  int64_t m_tail;          // max ts after the batch's last event (JMIN if none)
+};
+
+struct XBArgs {
+  const int64_t* ts;
+  const void* val;
+  int64_t n;
+  int64_t ntiles;
+  const XCfg* cfg;
+  XState* st;              // op 0
+  XSlices sl;
+  XSess ss;
+  XSnap* snap;
+  int64_t* reach;          // [XMAXCTX * sesscap] prefix max of (end + gap) over batch-start sessions
+  long long* tmax;         // [ntiles] tile max
+  long long* pcarry;       // [ntiles] exclusive prefix max carry
+  int64_t* ns_cnt;         // [XMAXCTX][ntiles] new sessions per tile -> exclusive offsets
+  int64_t* ns_tot;         // [XMAXCTX]
+  int64_t* ns_start;       // [XMAXCTX][ns_cap]
+  int64_t* ns_pb;          // [XMAXCTX][ns_cap]
+  int64_t ns_cap;
+  int64_t* ev_cnt;         // [ntiles] events per tile -> exclusive offsets
+  long long* seg_tail;     // [ntiles] max ts after the tile's last event (or tile max)
+  int32_t* seg_has;        // [ntiles] tile has an event
+  long long* m_carry;      // [ntiles] max ts since the last event before the tile
+  uint32_t* evbits;        // [n/32+1] event bitmap
+  int64_t* ev_pos;         // [ev_cap]
+  int64_t* ev_t;
+  int64_t* ev_v;
+  long long* ev_m;         // max ts strictly between the previous event and this one (JMIN if none)
+  int64_t ev_cap;
+  XBCtl* ctl;
+  int64_t* ep_pos;         // [ep_cap] epoch entries: event position, tail after it
+  int32_t* ep_tail;
+  int64_t ep_cap;
+  int32_t vt;
+  int32_t cfg_nctx_host;   // session windows (host copy, decides which passes run)
+  int64_t* sufmin;         // [sc] suffix minimum of tStart over [i, tail) (unsorted slice lists only)
+};
+
+namespace xb {
+using namespace x;
+
+__device__ __forceinline__ int64_t load_v(const XBArgs& a, int64_t i) {
+  if (a.vt == VT_I32) return (int64_t)((const int32_t*)a.val)[i];
+  return ((const int64_t*)a.val)[i];
+}
+
+// block-wide exclusive max over 256 threads (4 waves); wtot: LDS [4]
+__device__ __forceinline__ int64_t block_excl_max(int64_t v, long long* wtot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+    if (lane >= o) inc = max(inc, u);
+  }
+  if (lane == 63) wtot[wid] = inc;
+  __syncthreads();
+  int64_t before = JMIN;
+  for (int w = 0; w < wid; w++) before = max(before, (int64_t)wtot[w]);
+  int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
+  if (lane == 0) ex = JMIN;
+  __syncthreads();
+  return max(before, ex);
+}
+__device__ __forceinline__ int64_t block_excl_sum(int64_t v, long long* wtot, int64_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) wtot[wid] = inc;
+  __syncthreads();
+  int64_t before = 0, tot = 0;
+  for (int w = 0; w < 4; w++) {
+    if (w < wid) before += wtot[w];
+    tot += wtot[w];
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return before + inc - v;
+}
+
+// min over time-measure context-free windows of assignNextWindowStart(x) (lanes split the windows)
+__device__ __forceinline__ int64_t next_grid(const XCfg* c, int64_t xv) {
+  const int lane = threadIdx.x & 63;
+  int64_t e = JMAX;
+  for (int w = lane; w < c->n_cf; w += 64) {
+    if (c->cf_measure[w] != 0) continue;
+    const int k = c->cf_kind[w];
+    const int64_t a = c->cf_a[w], b = c->cf_b[w];
+    int64_t r;
+    if (k == 0) r = jsub(jadd(xv, a), jmod(xv, a));
+    else if (k == 1) r = jsub(jadd(xv, b), jmod(xv, b));
+    else if (xv == JMAX || xv < a) r = a;
+    else if (xv < jadd(a, b)) r = jadd(a, b);
+    else r = JMAX;
+    e = min(e, r);
+  }
+  return wmin(e);
+}
+__device__ __forceinline__ bool on_count_grid(const XCfg* c, int64_t cnt) {
+  for (int w = 0; w < c->n_cf; w++) {
+    if (c->cf_measure[w] != 1) continue;
+    const int k = c->cf_kind[w];
+    const int64_t a = c->cf_a[w], b = c->cf_b[w];
+    if (k == 0 && jmod(cnt, a) == 0) return true;
+    if (k == 1 && jmod(cnt, b) == 0) return true;
+    if (k == 2 && (cnt == a || cnt == jadd(a, b))) return true;
+  }
+  return false;
+}
+
+// Per-thread view of one tile: 16 contiguous tuples, their exclusive prefix max P, and the wave's grid bound.
+struct TileItems {
+  int64_t t[XB_ITEMS];
+  int64_t p[XB_ITEMS];  // exclusive prefix max (incl. carry and p_start)
+  int64_t g[XB_ITEMS];  // nextGrid(p): the pending fixed edge once n0 was crossed
+  int64_t base;         // index of item 0
+  int cnt;              // valid items
+};
+
+// per-lane nextGrid (serial over the windows): only recomputed when the running max reaches the cached edge
+__device__ __forceinline__ int64_t next_grid_lane(const XCfg* c, int64_t xv) {
+  int64_t e = JMAX;
+  for (int w = 0; w < c->n_cf; w++) {
+    if (c->cf_measure[w] != 0) continue;
+    const int k = c->cf_kind[w];
+    const int64_t a = c->cf_a[w], b = c->cf_b[w];
+    int64_t r;
+    if (k == 0) r = jsub(jadd(xv, a), jmod(xv, a));
+    else if (k == 1) r = jsub(jadd(xv, b), jmod(xv, b));
+    else if (xv == JMAX || xv < a) r = a;
+    else if (xv < jadd(a, b)) r = jadd(a, b);
+    else r = JMAX;
+    e = min(e, r);
+  }
+  return e;
+}
+
+constexpr int XB_LDS = XB_TILE / XB_ITEMS * (XB_ITEMS + 1);  // padded: thread rows of 17 words
+
+// coalesced striped loads into LDS, read back as 16 contiguous items per thread (row pad avoids bank conflicts)
+__device__ __forceinline__ void stage_tile(const int64_t* src, int64_t n, int64_t tile, long long* tb) {
+  const int64_t base = tile * XB_TILE;
+#pragma unroll
+  for (int r = 0; r < XB_ITEMS; r++) {
+    const int e = r * XB_THREADS + threadIdx.x;
+    const int64_t i = base + e;
+    tb[(e >> 4) * (XB_ITEMS + 1) + (e & 15)] = i < n ? src[i] : JMIN;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void load_tile(const XBArgs& a, int64_t tile, TileItems& it, long long* wtot,
+                                          bool want_grid, long long* tb) {
+  const XSnap& sn = *a.snap;
+  it.base = tile * XB_TILE + (int64_t)threadIdx.x * XB_ITEMS;
+  it.cnt = (int)max((int64_t)0, min((int64_t)XB_ITEMS, a.n - it.base));
+  stage_tile(a.ts, a.n, tile, tb);
+  int64_t run = JMIN;
+#pragma unroll
+  for (int j = 0; j < XB_ITEMS; j++) {
+    it.t[j] = j < it.cnt ? (int64_t)tb[threadIdx.x * (XB_ITEMS + 1) + j] : JMIN;
+    it.p[j] = run;  // local exclusive
+    run = max(run, it.t[j]);
+  }
+  const int64_t before = block_excl_max(run, wtot);
+  const int64_t carry = max((int64_t)a.pcarry[tile], sn.p_start);
+  const int64_t pre = max(carry, before);
+#pragma unroll
+  for (int j = 0; j < XB_ITEMS; j++) it.p[j] = max(pre, it.p[j]);
+  // nextGrid(x) is constant on [x, nextGrid(x)) and P is non-decreasing along the thread's items
+  int64_t gcur = JMIN;
+  const bool grid = want_grid && a.cfg->has_fixed && a.cfg->has_time;
+#pragma unroll
+  for (int j = 0; j < XB_ITEMS; j++) {
+    if (!grid || j >= it.cnt) {
+      it.g[j] = JMAX;
+      continue;
+    }
+    const int64_t pj = it.p[j];
+    if (pj < 0) {  // assignNextWindowStart bounds the pending edge only for non-negative times (Java %)
+      it.g[j] = JMIN;
+      continue;
+    }
+    if (gcur == JMIN || pj >= gcur) gcur = next_grid_lane(a.cfg, pj);
+    it.g[j] = gcur;
+  }
+}
+
+// in-order classification (depends on P only).  Returns event; sets new-session bits per context.
+__device__ __forceinline__ bool inorder_event(const XBArgs& a, int64_t t, int64_t p, int64_t g, int64_t pos,
+                                              int& nsmask, int64_t* pb) {
+  const XSnap& sn = *a.snap;
+  const XCfg* c = a.cfg;
+  bool ev = false;
+  nsmask = 0;
+  if (c->has_time) {
+    if (c->has_fixed) {
+      if ((sn.n0 == JMIN && p == sn.p_start) || (p < sn.n0 && t >= sn.n0) || (p >= sn.n0 && t >= g)) ev = true;
+    }
+    if (c->n_ctx > 0) {
+      if (t >= jadd(p, sn.min_gap)) ev = true;
+      // calculateNextFlexEdge (S/StreamSlicer.java:118-130): te >= max(maxEventTime, pending edge) + gap, in
+      // Java long arithmetic -- with no time window the pending edge is Long.MAX_VALUE and the sum wraps, so
+      // every in-order tuple opens a flexible slice.  Pending edge here: n0 until crossed, then nextGrid(P).
+      const int64_t pend = !c->has_fixed ? JMIN : (p < sn.n0 ? sn.n0 : g);
+      const int64_t tc = max(p, pend);
+      for (int k = 0; k < c->n_ctx; k++)
+        if (t >= jadd(tc, c->gap[k])) ev = true;
+    }
+  }
+  for (int k = 0; k < c->n_ctx; k++) {
+    const bool first_io = p == sn.p_start;
+    if (!sn.inv[k] && first_io) ev = true;
+    if (t <= sn.lim[k]) ev = true;
+    const int64_t gap = c->gap[k];
+    bool nw;
+    int64_t before;
+    if (!sn.inv[k] && first_io) {
+      nw = sn.ns[k] == 0 || t > jadd(sn.stored_end[k], gap);
+      before = sn.ns[k] == 0 ? JMIN : sn.stored_end[k];
+    } else {
+      nw = t > jadd(p, gap);
+      before = p;
+    }
+    if (nw) {
+      nsmask |= 1 << k;
+      pb[k] = before;
+    }
+  }
+  if (c->has_count) {
+    const int64_t cnt = jadd(sn.c0, pos);
+    if (sn.nc0 == JMIN || cnt == sn.nc0 || (cnt > sn.nc0 && on_count_grid(c, cnt))) ev = true;
+  }
+  if (!sn.started && pos == 0) ev = true;
+  return ev;
+}
+
+// ------------------------------------------------------------------------------------------- kernels
+__global__ void xb_prep_kernel(XBArgs a) {
+  const int lane = threadIdx.x;
+  const XCfg* c = a.cfg;
+  XState s = *a.st;
+  XSnap sn{};
+  sn.p_start = s.maxEventTime;
+  sn.n0 = s.nextEdgeTs;
+  sn.nc0 = s.nextEdgeCount;
+  sn.c0 = s.currentCount;
+  sn.started = s.tail > s.head;
+  sn.unsorted = s.unsorted;
+  sn.head = s.head;
+  sn.tail = s.tail;
+  sn.oldest = JMAX;  // findSliceIndexByTimestamp(t) == -1 <=> t < min tStart (the list may be unsorted)
+  for (int i = s.head + lane; i < s.tail; i += 64) sn.oldest = min(sn.oldest, a.sl.ts[i]);
+  sn.oldest = wmin(sn.oldest);
+  sn.min_gap = JMAX;
+  for (int k = 0; k < c->n_ctx; k++) {
+    sn.min_gap = min(sn.min_gap, c->gap[k]);
+    const int64_t* st_ = a.ss.start + (int64_t)k * c->sesscap;
+    const int64_t* en_ = a.ss.end + (int64_t)k * c->sesscap;
+    const int ns = s.nsess[k];
+    sn.ns[k] = ns;
+    sn.last_start[k] = ns > 0 ? st_[ns - 1] : JMAX;
+    sn.stored_end[k] = ns > 0 ? en_[ns - 1] : JMIN;
+    sn.inv[k] = ns > 0 && en_[ns - 1] == s.maxEventTime;
+    int64_t lim = JMIN;
+    // reach prefix (sequential; sessions per context are few) -- lane 0 writes
+    for (int i = 0; i < ns; i++) {
+      lim = max(lim, jadd(en_[i], c->gap[k]));
+      if (lane == 0) a.reach[(int64_t)k * c->sesscap + i] = lim;
+    }
+    int64_t lim2 = JMIN;
+    for (int i = 0; i < ns - 1; i++) lim2 = max(lim2, jadd(en_[i], c->gap[k]));
+    sn.lim[k] = lim2;
+  }
+  if (lane == 0) *a.snap = sn;
+}
+
+__global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
+  __shared__ long long wtot[4];
+  const int64_t base = (int64_t)blockIdx.x * XB_TILE;
+  int64_t m = JMIN;
+#pragma unroll
+  for (int r = 0; r < XB_ITEMS; r++) {
+    const int64_t i = base + r * XB_THREADS + threadIdx.x;
+    if (i < a.n) m = max(m, a.ts[i]);
+  }
+  m = wmax(m);
+  if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) a.tmax[blockIdx.x] = max(max(wtot[0], wtot[1]), max(wtot[2], wtot[3]));
+}
+
+// single workgroup: exclusive carries over tiles (prefix max of tile maxima)
+__global__ __launch_bounds__(1024) void xb_carry_kernel(XBArgs a) {
+  __shared__ long long wt[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int64_t carry = JMIN;
+  for (int64_t b0 = 0; b0 < a.ntiles; b0 += 1024) {
+    const int64_t i = b0 + tid;
+    const int64_t v = i < a.ntiles ? (int64_t)a.tmax[i] : JMIN;
+    int64_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+      if (lane >= o) inc = max(inc, u);
+    }
+    if (lane == 63) wt[wid] = inc;
+    __syncthreads();
+    int64_t before = carry;
+    for (int w = 0; w < wid; w++) before = max(before, (int64_t)wt[w]);
+    int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
+    if (lane == 0) ex = JMIN;
+    if (i < a.ntiles) a.pcarry[i] = max(before, ex);
+    int64_t tot = carry;
+    for (int w = 0; w < 16; w++) tot = max(tot, (int64_t)wt[w]);
+    __syncthreads();
+    carry = tot;
+  }
+}
+
+// pass 1: count new-session in-order tuples per context and tile
+__global__ __launch_bounds__(XB_THREADS) void xb_nscount_kernel(XBArgs a) {
+  __shared__ long long wtot[4];
+  __shared__ long long tb[XB_LDS];
+  TileItems it;
+  load_tile(a, blockIdx.x, it, wtot, true, tb);
+  int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
+  for (int j = 0; j < it.cnt; j++) {
+    if (it.t[j] < it.p[j]) continue;
+    int nsm;
+    int64_t pb[XMAXCTX];
+    (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm, pb);
+    for (int k = 0; k < a.cfg->n_ctx; k++)
+      if (nsm & (1 << k)) cnt[k]++;
+  }
+  for (int k = 0; k < a.cfg->n_ctx; k++) {
+    int64_t tot;
+    (void)block_excl_sum(cnt[k], wtot, &tot);
+    if (threadIdx.x == 0) a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x] = tot;
+  }
+}
+
+// single workgroup: exclusive scan of per-tile counts (rows of length ntiles), totals to tot[row]
+__global__ __launch_bounds__(1024) void xb_rows_scan_kernel(int64_t* cnt, int64_t ntiles, int rows, int64_t* tot) {
+  __shared__ long long wt[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int r = 0; r < rows; r++) {
+    int64_t* c = cnt + (int64_t)r * ntiles;
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < ntiles; b0 += 1024) {
+      const int64_t i = b0 + tid;
+      const int64_t v = i < ntiles ? c[i] : 0;
+      int64_t inc = v;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+        if (lane >= o) inc += u;
+      }
+      if (lane == 63) wt[wid] = inc;
+      __syncthreads();
+      int64_t before = carry;
+      for (int w = 0; w < wid; w++) before += wt[w];
+      if (i < ntiles) c[i] = before + inc - v;
+      int64_t t = carry;
+      for (int w = 0; w < 16; w++) t += wt[w];
+      __syncthreads();
+      carry = t;
+    }
+    if (tid == 0 && tot) tot[r] = carry;
+  }
+}
+
+// pass 2: write the per-context chains of in-batch new sessions (start, end of the previous session)
+__global__ __launch_bounds__(XB_THREADS) void xb_nswrite_kernel(XBArgs a) {
+  __shared__ long long wtot[4];
+  __shared__ long long tb[XB_LDS];
+  TileItems it;
+  load_tile(a, blockIdx.x, it, wtot, true, tb);
+  int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
+  for (int j = 0; j < it.cnt; j++) {
+    if (it.t[j] < it.p[j]) continue;
+    int nsm;
+    int64_t pb[XMAXCTX];
+    (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm, pb);
+    for (int k = 0; k < a.cfg->n_ctx; k++)
+      if (nsm & (1 << k)) cnt[k]++;
+  }
+  for (int k = 0; k < a.cfg->n_ctx; k++) {
+    int64_t off = block_excl_sum(cnt[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+    for (int j = 0; j < it.cnt; j++) {
+      if (it.t[j] < it.p[j]) continue;
+      int nsm;
+      int64_t pb[XMAXCTX];
+      (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm, pb);
+      if (nsm & (1 << k)) {
+        if (off < a.ns_cap) {
+          a.ns_start[(int64_t)k * a.ns_cap + off] = it.t[j];
+          a.ns_pb[(int64_t)k * a.ns_cap + off] = pb[k];
+        }
+        off++;
+      }
+    }
+  }
+}
+
+// is out-of-order tuple t (before it: m in-batch new sessions of context k, running max p) inside a session
+__device__ __forceinline__ bool ooo_inside(const XBArgs& a, int k, int64_t t, int64_t p, int64_t m) {
+  const XSnap& sn = *a.snap;
+  const XCfg* c = a.cfg;
+  const int64_t* nss = a.ns_start + (int64_t)k * a.ns_cap;
+  const int64_t* nsp = a.ns_pb + (int64_t)k * a.ns_cap;
+  if (m > 0 && t >= nss[0]) {
+    int64_t lo = 0, hi = m;  // last idx < m with nss[idx] <= t
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (nss[mid] <= t) lo = mid; else hi = mid;
+    }
+    const int64_t end = lo + 1 < m ? nsp[lo + 1] : p;
+    return t <= end;
+  }
+  const int ns = sn.ns[k];
+  if (ns == 0) return false;
+  // the batch-start last session, extended by the in-order tuples
+  const int64_t end0 = m > 0 ? nsp[0] : ((sn.inv[k] || p > sn.p_start) ? p : sn.stored_end[k]);
+  if (t >= sn.last_start[k]) return t <= end0 && t > sn.lim[k];
+  // settled sessions of the batch start: first session within reach of t must contain it (getSession)
+  const int64_t* st_ = a.ss.start + (int64_t)k * c->sesscap;
+  const int64_t* en_ = a.ss.end + (int64_t)k * c->sesscap;
+  const int64_t* rch = a.reach + (int64_t)k * c->sesscap;
+  int lo = 0, hi = ns - 1;  // last settled index with start <= t
+  if (hi <= 0 || st_[0] > t) return false;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (st_[mid] <= t) lo = mid; else hi = mid;
+  }
+  return t <= en_[lo] && (lo == 0 || rch[lo - 1] < t);
+}
+
+__device__ __forceinline__ bool classify(const XBArgs& a, int64_t t, int64_t p, int64_t g, int64_t pos,
+                                         const int64_t* ns_before) {
+  const XSnap& sn = *a.snap;
+  const XCfg* c = a.cfg;
+  if (t >= p) {
+    int nsm;
+    int64_t pb[XMAXCTX];
+    return inorder_event(a, t, p, g, pos, nsm, pb);
+  }
+  if (!sn.started) return true;
+  if (t < sn.oldest || c->has_count) return true;
+  if (c->n_ctx > 0) {
+    if (c->lazy) return true;
+    for (int k = 0; k < c->n_ctx; k++)
+      if (!ooo_inside(a, k, t, p, ns_before[k])) return true;
+  }
+  return false;
+}
+
+// pass 3: classify every tuple; event bitmap; per-tile event counts and segmented-max aggregates
+__global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
+  __shared__ long long wtot[4];
+  __shared__ long long tb[XB_LDS];
+  TileItems it;
+  load_tile(a, blockIdx.x, it, wtot, true, tb);
+  const XCfg* c = a.cfg;
+  // new sessions before each item: carry (exclusive offsets of the tile) + local exclusive count
+  int64_t nsb[XMAXCTX] = {0, 0, 0, 0};
+  int64_t loc[XMAXCTX] = {0, 0, 0, 0};
+  int nsm_item[XB_ITEMS];
+  for (int j = 0; j < it.cnt; j++) {
+    nsm_item[j] = 0;
+    if (it.t[j] >= it.p[j]) {
+      int64_t pb[XMAXCTX];
+      (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm_item[j], pb);
+      for (int k = 0; k < c->n_ctx; k++)
+        if (nsm_item[j] & (1 << k)) loc[k]++;
+    }
+  }
+  for (int k = 0; k < c->n_ctx; k++)
+    nsb[k] = block_excl_sum(loc[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+  uint32_t bits = 0;
+  int64_t nev = 0;
+  int64_t tail_m = JMIN;  // max after this thread's last event
+  bool has = false;
+  for (int j = 0; j < it.cnt; j++) {
+    const bool ev = classify(a, it.t[j], it.p[j], it.g[j], it.base + j, nsb);
+    for (int k = 0; k < c->n_ctx; k++)
+      if (nsm_item[j] & (1 << k)) nsb[k]++;
+    if (ev) {
+      bits |= 1u << j;
+      nev++;
+      has = true;
+      tail_m = JMIN;
+    } else {
+      tail_m = max(tail_m, it.t[j]);
+    }
+  }
+  // bitmap: 16 bits per thread, two threads per word
+  {
+    const uint32_t mine = bits & 0xFFFFu;
+    const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1);
+    if ((threadIdx.x & 1) == 0 && it.base < a.n) a.evbits[it.base >> 5] = mine | (other << 16);
+  }
+  int64_t tot;
+  (void)block_excl_sum(nev, wtot, &tot);
+  // segmented max: the tile's "max after its last event" = fold over threads in order
+  __shared__ long long s_tail[XB_THREADS];
+  __shared__ int s_has[XB_THREADS];
+  s_tail[threadIdx.x] = tail_m;
+  s_has[threadIdx.x] = has;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t m = JMIN;
+    int any = 0;
+    for (int i = 0; i < XB_THREADS; i++) {
+      if (s_has[i]) {
+        m = s_tail[i];
+        any = 1;
+      } else {
+        m = max(m, (int64_t)s_tail[i]);
+      }
+    }
+    a.ev_cnt[blockIdx.x] = tot;
+    a.seg_tail[blockIdx.x] = m;
+    a.seg_has[blockIdx.x] = any;
+  }
+}
+
+// single workgroup: carries of the segmented max over tiles (same operator as in xb_evwrite_kernel)
+__global__ __launch_bounds__(1024) void xb_mcarry_kernel(XBArgs a) {
+  __shared__ long long st_[16];
+  __shared__ int sh_[16];
+  const int tid = threadIdx.x, ln = tid & 63, wd = tid >> 6;
+  int64_t cm = JMIN;  // carry into the current chunk
+  for (int64_t b0 = 0; b0 < a.ntiles; b0 += 1024) {
+    const int64_t k = b0 + tid;
+    int hh = k < a.ntiles ? a.seg_has[k] : 0;
+    int64_t tt = k < a.ntiles ? (int64_t)a.seg_tail[k] : JMIN;
+    const int h0 = hh;
+    const int64_t t0 = tt;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int h2 = __shfl_up(hh, o);
+      const int64_t t2 = (int64_t)__shfl_up((long long)tt, o);
+      if (ln >= o) {
+        tt = hh ? tt : max(t2, tt);
+        hh = hh | h2;
+      }
+    }
+    if (ln == 63) {
+      st_[wd] = tt;
+      sh_[wd] = hh;
+    }
+    __syncthreads();
+    // exclusive value for tile k
+    int hx = 0;
+    int64_t tx = JMIN;
+    {
+      const int hp = __shfl_up(hh, 1);
+      const int64_t tp = (int64_t)__shfl_up((long long)tt, 1);
+      if (ln > 0) {
+        hx = hp;
+        tx = tp;
+      }
+    }
+    for (int w = wd - 1; w >= 0 && !hx; w--) {
+      tx = max(tx, (int64_t)st_[w]);
+      hx = sh_[w];
+    }
+    const int64_t ex = hx ? tx : max(cm, tx);
+    if (k < a.ntiles) a.m_carry[k] = ex;
+    // carry for the next chunk: fold the whole chunk
+    int64_t nc = cm;
+    for (int w = 0; w < 16; w++) nc = sh_[w] ? (int64_t)st_[w] : max(nc, (int64_t)st_[w]);
+    (void)h0;
+    (void)t0;
+    __syncthreads();
+    cm = nc;
+  }
+  if (tid == 0) a.ctl->m_tail = cm;
+}
+
+// pass 4: write the compacted events (position, ts, value, max ts since the previous event)
+__global__ __launch_bounds__(XB_THREADS) void xb_evwrite_kernel(XBArgs a) {
+  __shared__ long long wtot[4];
+  __shared__ long long s_tail[XB_THREADS];
+  __shared__ int s_has[XB_THREADS];
+  __shared__ long long tb[XB_LDS];
+  stage_tile(a.ts, a.n, blockIdx.x, tb);
+  const int64_t base = (int64_t)blockIdx.x * XB_TILE + (int64_t)threadIdx.x * XB_ITEMS;
+  const int cnt = (int)max((int64_t)0, min((int64_t)XB_ITEMS, a.n - base));
+  uint32_t bits = 0;
+  if (base < a.n) bits = (a.evbits[base >> 5] >> ((base & 31))) & 0xFFFFu;
+  int64_t t[XB_ITEMS];
+  int64_t tail_m = JMIN;
+  bool has = false;
+  int64_t nev = 0;
+  for (int j = 0; j < cnt; j++) {
+    t[j] = tb[threadIdx.x * (XB_ITEMS + 1) + j];
+    if ((bits >> j) & 1) {
+      has = true;
+      tail_m = JMIN;
+      nev++;
+    } else {
+      tail_m = max(tail_m, t[j]);
+    }
+  }
+  int64_t off = block_excl_sum(nev, wtot, nullptr) + a.ev_cnt[blockIdx.x];
+  // carry into this thread: segmented max over the previous threads of the tile (reset at a thread with an
+  // event), seeded with the tile carry -- an exclusive scan with the operator (h1,t1)o(h2,t2) =
+  // (h1|h2, h2 ? t2 : max(t1,t2))
+  int64_t m;
+  {
+    const int ln = threadIdx.x & 63, wd = threadIdx.x >> 6;
+    int hh = has ? 1 : 0;
+    int64_t tt = tail_m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int h2 = __shfl_up(hh, o);
+      const int64_t t2 = (int64_t)__shfl_up((long long)tt, o);
+      if (ln >= o) {
+        tt = hh ? tt : max(t2, tt);
+        hh = hh | h2;
+      }
+    }
+    s_tail[threadIdx.x] = tt;  // inclusive within the wave
+    s_has[threadIdx.x] = hh;
+    __syncthreads();
+    // exclusive: previous lane's inclusive, then previous waves, then tile carry
+    int hx = ln > 0 ? s_has[threadIdx.x - 1] : 0;
+    int64_t tx = ln > 0 ? (int64_t)s_tail[threadIdx.x - 1] : JMIN;
+    for (int w = wd - 1; w >= 0 && !hx; w--) {
+      const int h2 = s_has[w * 64 + 63];
+      const int64_t t2 = s_tail[w * 64 + 63];
+      tx = max(tx, t2);
+      hx = h2;
+    }
+    m = hx ? tx : max((int64_t)a.m_carry[blockIdx.x], tx);
+  }
+  for (int j = 0; j < cnt; j++) {
+    if ((bits >> j) & 1) {
+      if (off < a.ev_cap) {
+        a.ev_pos[off] = base + j;
+        a.ev_t[off] = t[j];
+        a.ev_v[off] = load_v(a, base + j);
+        a.ev_m[off] = m;
+      }
+      off++;
+      m = JMIN;
+    } else {
+      m = max(m, t[j]);
+    }
+  }
+}
+
+// Effect of the simple tuples since the previous event (or batch start): every part of it is a max of their
+// timestamps m -- StreamSlicer.maxEventTime, the current slice's tLast (they land in it iff m >= its tStart)
+// and the end of each context's last session (simple in-order tuples only extend it).
+__device__ __forceinline__ void reconstruct(Op& o, const XCfg* cfg, int64_t m) {
+  if (m == JMIN) return;
+  o.s.maxEventTime = max(o.s.maxEventTime, m);
+  if (o.s.tail > o.s.head) {
+    const int cur = o.s.tail - 1;
+    if (m >= o.ts[cur] && m > o.tl[cur]) o.tl[cur] = m;
+  }
+  for (int c = 0; c < cfg->n_ctx; c++) {
+    const int ns = o.s.nsess[c];
+    if (ns > 0 && m > o.se[c][ns - 1]) o.se[c][ns - 1] = m;
+  }
+}
+
+// event pass: one wavefront walks the events with the reference logic (exact_op.h)
+__global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
+  const int lane = threadIdx.x;
+  const XCfg* cfg = a.cfg;
+  XBCtl ctl = *a.ctl;
+  Op o;
+  o.bind(cfg, a.sl, a.ss, 0, lane);
+  o.s = *a.st;
+  if (ctl.done || o.s.err) {
+    return;
+  }
+  // segment start: compaction is only safe here (slice indices are stable within a segment)
+  if (o.s.tail + 64 > cfg->sc && o.s.head > 0) {
+    o.move_range(0, o.s.head, o.s.tail - o.s.head);
+    o.s.tail -= o.s.head;
+    o.s.head = 0;
+  }
+  int64_t ep = 0;
+  if (lane == 0) {
+    a.ep_pos[0] = ctl.seg_start - 1;
+    a.ep_tail[0] = o.s.tail;
+  }
+  ep = 1;
+  int64_t e = ctl.ev_next;
+  bool first = true;
+  ctl.stopped = 0;
+  for (; e < ctl.ev_total; e++) {
+    const int64_t pos = a.ev_pos[e], t = a.ev_t[e], vb = a.ev_v[e], m = a.ev_m[e];
+    reconstruct(o, cfg, m);
+    o.s.currentCount = jadd(a.snap->c0, pos);
+    // an out-of-order event of an operator with sessions may split / shift / merge older slices: the simple
+    // tuples before it are applied first (segment end).  The stop event itself opens the next segment.
+    const bool stop_kind = (cfg->n_ctx > 0 && (t < o.s.maxEventTime || a.snap->min_gap == 0)) ||
+                           (!a.snap->started && !first);  // re-classify once the store exists
+    const bool cap = o.s.tail + 8 >= cfg->sc || ep + 2 >= a.ep_cap;
+    // the stop tuple of the previous round (position 0 of this round) is processed, never deferred again
+    if (!(first && ctl.resume && pos == 0) && (stop_kind || cap)) {
+      ctl.stopped = 1;
+      ctl.seg_end = pos;
+      break;
+    }
+    first = false;
+    o.exc = 0;
+    o.determine_slices(t);
+    if (!o.exc) o.manager_process(t, vb);
+    if (o.exc == XERR_INDEX) {
+      o.s.dropped++;
+      o.exc = 0;
+    } else if (o.exc) {
+      o.s.err = o.exc;
+      e++;
+      break;
+    }
+    __threadfence_block();
+    if (lane == 0) {
+      a.ep_pos[ep] = pos;
+      a.ep_tail[ep] = o.s.tail;
+    }
+    ep++;
+  }
+  if (!ctl.stopped) {
+    ctl.seg_end = -1;  // host: apply to n
+    ctl.done = e >= ctl.ev_total ? 1 : 0;
+    ctl.ev_next = e;
+    if (ctl.done && !o.s.err) {  // the simple tuples after the last event
+      reconstruct(o, cfg, ctl.m_tail);
+      o.s.currentCount = jadd(a.snap->c0, a.n);
+    }
+  } else {
+    ctl.ev_next = e;
+  }
+  ctl.ep_count = ep;
+  ctl.resume = 0;
+  __threadfence_block();
+  if (lane == 0) {
+    *a.st = o.s;
+    *a.ctl = ctl;
+  }
+}
+
+// apply the simple tuples of [seg_start, seg_end) (all CUs).  Each workgroup streams a contiguous range and
+// accumulates into an LDS window over the newest XW slices (LDS atomics), flushed once per touched slice;
+// wave-uniform runs (in-order tuples all in the current slice) are reduced in registers first.
+constexpr int XW = 256;
+
+template <int VT>
+__global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
+  __shared__ unsigned int w_cnt[XW];
+  __shared__ long long w_tl[XW], w_tf[XW], w_p1[XW], w_p2[XW];
+  __shared__ unsigned long long w_p0[XW];
+  const XBCtl& ctl = *a.ctl;
+  const int64_t s0 = ctl.seg_start;
+  const int64_t s1 = ctl.seg_end < 0 ? a.n : ctl.seg_end;
+  const int lane = threadIdx.x & 63;
+  const XCfg* cfg = a.cfg;
+  const int need = cfg->need;
+  const XState& st = *a.st;
+  const int head = st.head;
+  const int64_t nep = ctl.ep_count;
+  const int wtop = a.ep_tail[nep - 1];
+  const int wbase = max(head, wtop - XW);
+  for (int k = threadIdx.x; k < XW; k += 256) {
+    w_cnt[k] = 0;
+    w_tl[k] = JMIN;
+    w_tf[k] = JMAX;
+    w_p0[k] = 0;
+    w_p1[k] = ID_MIN;
+    w_p2[k] = ID_MAX;
+  }
+  __syncthreads();
+  const int64_t total = s1 - s0;
+  int64_t chunk = (total + gridDim.x - 1) / gridDim.x;
+  chunk = ((chunk + 255) / 256) * 256;
+  const int64_t b0 = s0 + (int64_t)blockIdx.x * chunk;
+  const int64_t b1 = min(s1, b0 + chunk);
+  const int64_t* sk = (st.unsorted & 1) ? a.sufmin : a.sl.ts;
+  for (int64_t i0 = b0; i0 < b1; i0 += 256) {
+    const int64_t i = i0 + threadIdx.x;
+    bool act = i < b1;
+    int64_t t = 0, vb = 0;
+    if (act) act = !((a.evbits[i >> 5] >> (i & 31)) & 1);
+    int si = -1;
+    if (act) {
+      t = a.ts[i];
+      if constexpr (VT == VT_I32) vb = (int64_t)((const int32_t*)a.val)[i];
+      else vb = ((const int64_t*)a.val)[i];
+      int64_t lo = 0, hi = nep;  // last epoch entry with pos < i: the last slice present at arrival
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.ep_pos[mid] < i) lo = mid; else hi = mid;
+      }
+      const int last = a.ep_tail[lo] - 1;
+      if (t >= a.sl.ts[last]) {
+        si = last;
+      } else {  // last slice in [head, last) with tStart <= t (suffix-min keys on an unsorted list)
+        int l = head, h = last;
+        while (l < h) {
+          const int mid = (l + h) >> 1;
+          if (sk[mid] <= t) l = mid + 1; else h = mid;
+        }
+        si = l - 1;
+      }
+      if (si < head) {  // cannot happen for a simple tuple (t >= oldest); counted, never silently lost
+        atomicAdd((int*)&a.ctl->pad, 1);
+        act = false;
+      }
+    }
+    const Lift lf = lift(VT, vb);
+    const unsigned long long am = __ballot(act);
+    if (!am) continue;
+    const int leader = __ffsll((long long)am) - 1;
+    const int s_lead = __builtin_amdgcn_readlane(si, leader);
+    const bool same = __ballot(act && si != s_lead) == 0;
+    int tgt = si;
+    unsigned int c_ = 1;
+    int64_t tmx = t, tmn = t, mn = lf.mn, mx = lf.mx;
+    uint64_t sw = lf.sum;
+    bool doit = act;
+    if (same) {
+      c_ = (unsigned int)__popcll(am);
+      tmx = wmax(act ? t : JMIN);
+      tmn = wmin(act ? t : JMAX);
+      if (need & NEED_SUM) {
+        if constexpr (VT == VT_F64) sw = (uint64_t)__double_as_longlong(wsumf(act ? __longlong_as_double(vb) : 0.0));
+        else sw = wsum(act ? lf.sum : 0);
+      }
+      if (need & NEED_MIN) mn = wmin(act ? lf.mn : ID_MIN);
+      if (need & NEED_MAX) mx = wmax(act ? lf.mx : ID_MAX);
+      tgt = s_lead;
+      doit = lane == leader;
+    }
+    if (doit) {
+      if (tgt >= wbase && tgt < wbase + XW) {
+        const int k = tgt - wbase;
+        atomicAdd(&w_cnt[k], c_);
+        atomicMax(&w_tl[k], (long long)tmx);
+        atomicMin(&w_tf[k], (long long)tmn);
+        if (need & NEED_SUM) {
+          if constexpr (VT == VT_F64) atomicAdd((double*)&w_p0[k], __longlong_as_double((long long)sw));
+          else atomicAdd(&w_p0[k], (unsigned long long)sw);
+        }
+        if (need & NEED_MIN) atomicMin(&w_p1[k], (long long)mn);
+        if (need & NEED_MAX) atomicMax(&w_p2[k], (long long)mx);
+      } else {
+        atomicAdd(&a.sl.cnt[tgt], (unsigned long long)c_);
+        atomicAdd((unsigned long long*)&a.sl.cl[tgt], (unsigned long long)c_);
+        atomicMax((long long*)&a.sl.tl[tgt], (long long)tmx);
+        atomicMin((long long*)&a.sl.tf[tgt], (long long)tmn);
+        if (need & NEED_SUM) {
+          if constexpr (VT == VT_F64) atomicAdd((double*)&a.sl.p[0][tgt], __longlong_as_double((long long)sw));
+          else atomicAdd(&a.sl.p[0][tgt], (unsigned long long)sw);
+        }
+        if (need & NEED_MIN) atomicMin((long long*)&a.sl.p[1][tgt], (long long)mn);
+        if (need & NEED_MAX) atomicMax((long long*)&a.sl.p[2][tgt], (long long)mx);
+      }
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < XW; k += 256) {
+    const unsigned int c_ = w_cnt[k];
+    if (!c_) continue;
+    const int s_ = wbase + k;
+    atomicAdd(&a.sl.cnt[s_], (unsigned long long)c_);
+    atomicAdd((unsigned long long*)&a.sl.cl[s_], (unsigned long long)c_);
+    atomicMax((long long*)&a.sl.tl[s_], w_tl[k]);
+    atomicMin((long long*)&a.sl.tf[s_], w_tf[k]);
+    if (need & NEED_SUM) {
+      if constexpr (VT == VT_F64) atomicAdd((double*)&a.sl.p[0][s_], __longlong_as_double((long long)w_p0[k]));
+      else atomicAdd(&a.sl.p[0][s_], w_p0[k]);
+    }
+    if (need & NEED_MIN) atomicMin((long long*)&a.sl.p[1][s_], w_p1[k]);
+    if (need & NEED_MAX) atomicMax((long long*)&a.sl.p[2][s_], w_p2[k]);
+  }
+}
+
+// suffix minimum of tStart over the op's slices (only when the list is unsorted), one workgroup
+__global__ __launch_bounds__(1024) void xb_sufmin_kernel(XBArgs a) {
+  __shared__ long long wt[16];
+  const XState& st = *a.st;
+  if (!(st.unsorted & 1)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int64_t carry = JMAX;
+  for (int64_t top = st.tail; top > st.head; top -= 1024) {
+    const int64_t i = top - 1 - tid;  // thread 0 = rightmost
+    const int64_t v = i >= st.head ? a.sl.ts[i] : JMAX;
+    int64_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+      if (lane >= o) inc = min(inc, u);
+    }
+    if (lane == 63) wt[wid] = inc;
+    __syncthreads();
+    int64_t before = carry;
+    for (int w = 0; w < wid; w++) before = min(before, (int64_t)wt[w]);
+    if (i >= st.head) a.sufmin[i] = min(before, inc);
+    int64_t tot = carry;
+    for (int w = 0; w < 16; w++) tot = min(tot, (int64_t)wt[w]);
+    __syncthreads();
+    carry = tot;
+  }
+}
+
+// after an apply: the next segment starts at the stop event
+__global__ void xb_next_segment_kernel(XBArgs a) {
+  if (threadIdx.x != 0) return;
+  XBCtl c = *a.ctl;
+  if (c.stopped) {
+    c.seg_start = c.seg_end;
+    c.resume = 1;
+  } else {
+    c.seg_start = a.n;
+    c.done = 1;
+  }
+  *a.ctl = c;
+}
+
+}  // namespace xb
+
+// ---------------------------------------------------------------- host wrappers
+int64_t xb_tile() { return XB_TILE; }
+size_t xb_snap_bytes() { return sizeof(XSnap); }
+size_t xb_ctl_bytes() { return sizeof(XBCtl); }
+
+hipError_t xb_classify_phase(XBArgs& a, int phase, hipStream_t st) {
+  const unsigned nt = (unsigned)a.ntiles;
+  switch (phase) {
+    case 0:  // snapshot + tile maxima + carries + new-session counts + scan
+      hipLaunchKernelGGL(xb::xb_prep_kernel, dim3(1), dim3(64), 0, st, a);
+      hipLaunchKernelGGL(xb::xb_tilemax_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
+      hipLaunchKernelGGL(xb::xb_carry_kernel, dim3(1), dim3(1024), 0, st, a);
+      if (a.cfg_nctx_host > 0) {
+        hipLaunchKernelGGL(xb::xb_nscount_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
+        hipLaunchKernelGGL(xb::xb_rows_scan_kernel, dim3(1), dim3(1024), 0, st, a.ns_cnt, a.ntiles,
+                           a.cfg_nctx_host, a.ns_tot);
+      }
+      break;
+    case 1:  // new-session chains, classification, event counts
+      if (a.cfg_nctx_host > 0) hipLaunchKernelGGL(xb::xb_nswrite_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
+      hipLaunchKernelGGL(xb::xb_classify_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
+      hipLaunchKernelGGL(xb::xb_rows_scan_kernel, dim3(1), dim3(1024), 0, st, a.ev_cnt, a.ntiles, 1,
+                         &a.ctl->ev_total);
+      hipLaunchKernelGGL(xb::xb_mcarry_kernel, dim3(1), dim3(1024), 0, st, a);
+      break;
+    case 2:  // compacted events
+      hipLaunchKernelGGL(xb::xb_evwrite_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
+      break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t xb_events(XBArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(xb::xb_events_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t xb_apply(XBArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(xb::xb_sufmin_kernel, dim3(1), dim3(1024), 0, st, a);
+  const int64_t blocks = std::min<int64_t>((a.n + 4095) / 4096, 2048);
+  if (a.vt == VT_I32) hipLaunchKernelGGL(xb::xb_apply_kernel<VT_I32>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (a.vt == VT_I64) hipLaunchKernelGGL(xb::xb_apply_kernel<VT_I64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(xb::xb_apply_kernel<VT_F64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(xb::xb_next_segment_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace scotty

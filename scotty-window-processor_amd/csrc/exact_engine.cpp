@@ -30,6 +30,54 @@ hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, 
 int64_t sort_tile();
 }  // namespace scotty
 
+// batch-parallel path (exact_batch.hip): the argument block mirrors XBArgs there
+namespace scotty {
+struct XSnap;
+struct XBCtl;
+struct XBArgs {
+  const int64_t* ts;
+  const void* val;
+  int64_t n;
+  int64_t ntiles;
+  const XCfg* cfg;
+  XState* st;
+  XSlices sl;
+  XSess ss;
+  XSnap* snap;
+  int64_t* reach;
+  long long* tmax;
+  long long* pcarry;
+  int64_t* ns_cnt;
+  int64_t* ns_tot;
+  int64_t* ns_start;
+  int64_t* ns_pb;
+  int64_t ns_cap;
+  int64_t* ev_cnt;
+  long long* seg_tail;
+  int32_t* seg_has;
+  long long* m_carry;
+  uint32_t* evbits;
+  int64_t* ev_pos;
+  int64_t* ev_t;
+  int64_t* ev_v;
+  long long* ev_m;
+  int64_t ev_cap;
+  XBCtl* ctl;
+  int64_t* ep_pos;
+  int32_t* ep_tail;
+  int64_t ep_cap;
+  int32_t vt;
+  int32_t cfg_nctx_host;
+  int64_t* sufmin;
+};
+hipError_t xb_classify_phase(XBArgs& a, int phase, hipStream_t st);
+hipError_t xb_events(XBArgs& a, hipStream_t st);
+hipError_t xb_apply(XBArgs& a, hipStream_t st);
+int64_t xb_tile();
+size_t xb_snap_bytes();
+size_t xb_ctl_bytes();
+}  // namespace scotty
+
 namespace scotty {
 
 #define XCHK(expr)                                                         \
@@ -81,6 +129,10 @@ void XEngine::release() {
   dfree(d_w_start); dfree(d_w_end); dfree(d_w_meas); dfree(d_w_op); dfree(d_w_key); dfree(d_has);
   for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
   if (h_misc) (void)hipHostFree(h_misc);
+  dfree(xb_snap); dfree(xb_ctl); dfree(xb_reach); dfree(xb_tmax); dfree(xb_pcarry); dfree(xb_segtail);
+  dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
+  dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
+  dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
   d_cfg = nullptr;
   d_st = nullptr;
   h_misc = nullptr;
@@ -370,6 +422,153 @@ int XEngine::push(const int64_t* d_ts, const void* d_val, int64_t n) {
   return SCOTTY_OK;
 }
 
+// Non-keyed micro-batch: classify (all CUs) -> compacted events (one wave, exact) -> apply (all CUs).  A
+// round ends at the first out-of-order event that may modify sessions / older slices; the rest of the batch
+// is then classified again against the updated operator (rounds are rare: record-breaking session growth).
+int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
+  const size_t vb = vt == VT_I32 ? 4 : 8;
+  int64_t pos0 = 0;
+  last_events = 0;
+  last_segments = 0;
+  for (int64_t round = 0; pos0 < n; round++) {
+    int64_t stop = -1;
+    int rc = push_round(d_ts + pos0, (const unsigned char*)d_val + pos0 * vb, n - pos0, round > 0, &stop);
+    if (rc) return rc;
+    last_segments++;
+    if (stop < 0) break;
+    if (stop == 0 && round > 0 && false) {
+      err = "event pass made no progress";
+      failed = true;
+      return SCOTTY_ERR_STATE;
+    }
+    pos0 += stop;
+    if (round > 4 * n + 16) {
+      err = "event pass made no progress";
+      failed = true;
+      return SCOTTY_ERR_STATE;
+    }
+  }
+  return SCOTTY_OK;
+}
+
+int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool resume, int64_t* stop_at) {
+  *stop_at = -1;
+  if (n <= 0) return SCOTTY_OK;
+  const int64_t T = xb_tile();
+  const int64_t nt = (n + T - 1) / T;
+  if (!xb_snap) {
+    XCHK(dalloc((unsigned char**)&xb_snap, xb_snap_bytes()));
+    XCHK(dalloc((unsigned char**)&xb_ctl, xb_ctl_bytes()));
+    XCHK(dalloc(&xb_nstot, XMAXCTX));
+  }
+  if (nt > xb_tcap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(xb_tmax); dfree(xb_pcarry); dfree(xb_segtail); dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_evcnt);
+    dfree(xb_seghas);
+    const int64_t c = std::max<int64_t>(nt, 64);
+    XCHK(dalloc(&xb_tmax, c)); XCHK(dalloc(&xb_pcarry, c)); XCHK(dalloc(&xb_segtail, c));
+    XCHK(dalloc(&xb_mcarry, c)); XCHK(dalloc(&xb_nscnt, (size_t)c * XMAXCTX)); XCHK(dalloc(&xb_evcnt, c));
+    XCHK(dalloc(&xb_seghas, c));
+    xb_tcap = c;
+  }
+  if (n > xb_ncap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(xb_bits);
+    XCHK(dalloc(&xb_bits, (size_t)(n / 32 + 2)));
+    xb_ncap = n;
+  }
+  if (sc > xb_sufcap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(xb_sufmin);
+    xb_sufcap = sc;
+    XCHK(dalloc(&xb_sufmin, xb_sufcap));
+  }
+  if ((int64_t)XMAXCTX * sesscap > xb_reachcap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(xb_reach);
+    xb_reachcap = (int64_t)XMAXCTX * std::max<int32_t>(sesscap, 1);
+    XCHK(dalloc(&xb_reach, xb_reachcap));
+  }
+  XBArgs a{};
+  a.ts = d_ts;
+  a.val = d_val;
+  a.n = n;
+  a.ntiles = nt;
+  a.cfg = d_cfg;
+  a.st = d_st;
+  a.sl = sl;
+  a.ss = ss;
+  a.snap = (XSnap*)xb_snap;
+  a.reach = xb_reach;
+  a.tmax = xb_tmax;
+  a.pcarry = xb_pcarry;
+  a.ns_cnt = xb_nscnt;
+  a.ns_tot = xb_nstot;
+  a.ev_cnt = xb_evcnt;
+  a.seg_tail = xb_segtail;
+  a.seg_has = xb_seghas;
+  a.m_carry = xb_mcarry;
+  a.evbits = xb_bits;
+  a.ctl = (XBCtl*)xb_ctl;
+  a.vt = vt;
+  a.cfg_nctx_host = cfg.n_ctx;
+  a.sufmin = xb_sufmin;
+  XCHK(hipMemsetAsync(xb_ctl, 0, xb_ctl_bytes(), stream));
+  if (resume) {
+    const int32_t one = 1;
+    XCHK(hipMemcpyAsync((unsigned char*)xb_ctl + 48, &one, 4, hipMemcpyHostToDevice, stream));  // XBCtl.resume
+  }
+  XCHK(xb_classify_phase(a, 0, stream));
+  if (cfg.n_ctx > 0) {
+    XCHK(hipMemcpyAsync(h_misc, xb_nstot, 8 * cfg.n_ctx, hipMemcpyDeviceToHost, stream));
+    XCHK(hipStreamSynchronize(stream));
+    int64_t mx = 1;
+    for (int k = 0; k < cfg.n_ctx; k++) mx = std::max<int64_t>(mx, h_misc[k]);
+    if (mx > xb_nscap) {
+      dfree(xb_nsstart); dfree(xb_nspb);
+      xb_nscap = std::max<int64_t>(mx, 1024);
+      XCHK(dalloc(&xb_nsstart, (size_t)xb_nscap * XMAXCTX));
+      XCHK(dalloc(&xb_nspb, (size_t)xb_nscap * XMAXCTX));
+    }
+  }
+  a.ns_start = xb_nsstart;
+  a.ns_pb = xb_nspb;
+  a.ns_cap = xb_nscap;
+  XCHK(xb_classify_phase(a, 1, stream));
+  XCHK(hipMemcpyAsync(h_misc, xb_ctl, 8, hipMemcpyDeviceToHost, stream));  // XBCtl.ev_total
+  XCHK(hipStreamSynchronize(stream));
+  const int64_t nev = h_misc[0];
+  if (nev + 4 > xb_evcap) {
+    dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_evm); dfree(xb_eppos); dfree(xb_eptail);
+    xb_evcap = std::max<int64_t>(nev + 4, 4096);
+    XCHK(dalloc(&xb_evpos, xb_evcap)); XCHK(dalloc(&xb_evt, xb_evcap)); XCHK(dalloc(&xb_evv, xb_evcap));
+    XCHK(dalloc(&xb_evm, xb_evcap)); XCHK(dalloc(&xb_eppos, xb_evcap + 4)); XCHK(dalloc(&xb_eptail, xb_evcap + 4));
+  }
+  a.ev_pos = xb_evpos;
+  a.ev_t = xb_evt;
+  a.ev_v = xb_evv;
+  a.ev_m = xb_evm;
+  a.ev_cap = xb_evcap;
+  a.ep_pos = xb_eppos;
+  a.ep_tail = xb_eptail;
+  a.ep_cap = xb_evcap + 4;
+  XCHK(xb_classify_phase(a, 2, stream));
+  last_events += nev;
+  XCHK(xb_events(a, stream));
+  XCHK(xb_apply(a, stream));
+  XCHK(hipMemcpyAsync(h_misc, xb_ctl, 48, hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  const int32_t stopped = ((const int32_t*)(h_misc + 5))[0];
+  if (stopped) *stop_at = h_misc[3];  // XBCtl.seg_end
+  XCHK(hipMemcpy(h_misc, (unsigned char*)xb_ctl + 52, 4, hipMemcpyDeviceToHost));
+  if (*(int32_t*)h_misc) {
+    err = "internal: simple tuple without a slice (" + std::to_string(*(int32_t*)h_misc) + ")";
+    failed = true;
+    return SCOTTY_ERR_STATE;
+  }
+  return SCOTTY_OK;
+}
+
 int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n) {
   if (n <= 0) return SCOTTY_OK;
   int rc = ensure_batch(n);
@@ -578,6 +777,42 @@ int XEngine::slice_count(int64_t op, int64_t* out) {
   XState s;
   XCHK(hipMemcpy(&s, d_st + op, sizeof(XState), hipMemcpyDeviceToHost));
   *out = s.tail - s.head;
+  return SCOTTY_OK;
+}
+
+int XEngine::debug_dump(int64_t op, std::vector<int64_t>& out) {
+  out.clear();
+  if (op < 0 || op >= n_ops) return SCOTTY_ERR_ARG;
+  XState s;
+  XCHK(hipMemcpy(&s, d_st + op, sizeof(XState), hipMemcpyDeviceToHost));
+  const int64_t S = s.tail - s.head, b = op * (int64_t)sc + s.head;
+  out.push_back(S);
+  std::vector<int64_t> tmp(std::max<int64_t>(S, 1));
+  std::vector<int32_t> ty(std::max<int64_t>(S, 1));
+  auto col = [&](const void* p) -> int {
+    XCHK(hipMemcpy(tmp.data(), (const int64_t*)p + b, S * 8, hipMemcpyDeviceToHost));
+    out.insert(out.end(), tmp.begin(), tmp.begin() + S);
+    return SCOTTY_OK;
+  };
+  if (S > 0) {
+    if (col(sl.ts) || col(sl.te) || col(sl.tl) || col(sl.cnt) || col(sl.cs) || col(sl.cl)) return SCOTTY_ERR_HIP;
+    XCHK(hipMemcpy(ty.data(), sl.ty + b, S * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < S; i++) out.push_back(ty[i]);
+  }
+  out.push_back(cfg.n_ctx);
+  for (int c = 0; c < cfg.n_ctx; c++) {
+    const int ns = s.nsess[c];
+    out.push_back(ns);
+    const int64_t sb = (op * ctx_alloc + c) * (int64_t)sesscap;
+    std::vector<int64_t> a(std::max(ns, 1)), e(std::max(ns, 1));
+    if (ns) {
+      XCHK(hipMemcpy(a.data(), ss.start + sb, ns * 8, hipMemcpyDeviceToHost));
+      XCHK(hipMemcpy(e.data(), ss.end + sb, ns * 8, hipMemcpyDeviceToHost));
+    }
+    for (int i = 0; i < ns; i++) { out.push_back(a[i]); out.push_back(e[i]); }
+  }
+  out.push_back(s.maxEventTime); out.push_back(s.nextEdgeTs); out.push_back(s.currentCount);
+  out.push_back(s.unsorted); out.push_back(s.head); out.push_back(s.tail);
   return SCOTTY_OK;
 }
 

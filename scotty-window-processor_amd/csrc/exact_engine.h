@@ -39,15 +39,20 @@ class XEngine {
   int configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness);
   int push(const int64_t* d_ts, const void* d_val, int64_t n);
   int push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n);
+  int push_batch(const int64_t* d_ts, const void* d_val, int64_t n);  // non-keyed, batch-parallel
+  int push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool resume, int64_t* stop_at);
+  int64_t last_events = 0, last_segments = 0;                          // statistics of the last push
   int watermark(int64_t wm, XResult& r, bool to_host);
   int slice_count(int64_t op, int64_t* out);
   int read_states(std::vector<XState>& out);
+  int debug_dump(int64_t op, std::vector<int64_t>& out);  // slices + sessions of one op (tests / debugging)
   int64_t key_count() const { return keyed ? n_ops : 0; }
   int set_last_watermark(int64_t lw);  // non-keyed: watermarks seen before the first tuple
 
   std::string err;
   bool failed = false;
   int32_t sc_override = 0, sess_override = 0;
+  bool serial = false;  // non-keyed: single-wavefront replay instead of the batch-parallel path (A/B)
 
  private:
   void release();
@@ -98,6 +103,21 @@ class XEngine {
   uint32_t* d_w_key = nullptr;
   uint8_t* d_has = nullptr;
   int64_t* d_vals[SCOTTY_MAX_AGGS] = {};
+  // batch-parallel non-keyed path (exact_batch.hip)
+  int64_t xb_tcap = 0, xb_ncap = 0, xb_nscap = 0, xb_evcap = 0, xb_reachcap = 0;
+  void* xb_snap = nullptr;
+  void* xb_ctl = nullptr;
+  int64_t* xb_reach = nullptr;
+  long long *xb_tmax = nullptr, *xb_pcarry = nullptr, *xb_segtail = nullptr, *xb_mcarry = nullptr;
+  int64_t *xb_nscnt = nullptr, *xb_nstot = nullptr, *xb_nsstart = nullptr, *xb_nspb = nullptr;
+  int64_t* xb_evcnt = nullptr;
+  int32_t* xb_seghas = nullptr;
+  uint32_t* xb_bits = nullptr;
+  int64_t *xb_evpos = nullptr, *xb_evt = nullptr, *xb_evv = nullptr, *xb_eppos = nullptr;
+  long long* xb_evm = nullptr;
+  int32_t* xb_eptail = nullptr;
+  int64_t* xb_sufmin = nullptr;
+  int64_t xb_sufcap = 0;
 };
 
 }  // namespace scotty

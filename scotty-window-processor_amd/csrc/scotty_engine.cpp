@@ -131,6 +131,7 @@ struct scotty_op {
   std::vector<XWinDef> xwins;         // every window, registration order
   XEngine* x = nullptr;
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
+  bool x_serial = false;
   uint64_t x_pushed = 0;
   std::vector<uint32_t> r_key;
   XResult xr;
@@ -698,6 +699,7 @@ static int decide_mode(scotty_op* op) {
   op->x = new XEngine();
   op->x->sc_override = op->x_sc;
   op->x->sess_override = op->x_sess;
+  op->x->serial = op->x_serial;
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
   if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
@@ -717,7 +719,7 @@ static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int6
   if (op->mode == 2) {
     op->pending.push_back({d_ts, d_val, n, op->push_seq++});
     op->x_pushed += (uint64_t)n;
-    rc = op->x->push(d_ts, d_val, n);
+    rc = op->x->serial ? op->x->push(d_ts, d_val, n) : op->x->push_batch(d_ts, d_val, n);
     if (rc) return fail(op, rc, op->x->err);
     return SCOTTY_OK;
   }
@@ -1013,12 +1015,33 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     op->ingest_mode = (int)value;
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "exact_serial") == 0) {
+    if (op->mode != 0) return SCOTTY_ERR_ARG;
+    op->x_serial = value != 0;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "slice_capacity") == 0 || std::strcmp(key, "session_capacity") == 0) {
     if (op->mode != 0 || value <= 0 || value > (1 << 26)) return SCOTTY_ERR_ARG;
     (key[1] == 'l' ? op->x_sc : op->x_sess) = (int32_t)value;
     return SCOTTY_OK;
   }
   return SCOTTY_ERR_ARG;
+}
+
+// Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds).
+int64_t scotty_debug_stat(scotty_op* op, int which) {
+  if (!op || !op->x) return -1;
+  return which == 0 ? op->x->last_events : op->x->last_segments;
+}
+
+// Internal (not in the header): state of one operator of the exact engine, for tests and debugging.
+int64_t scotty_debug_dump(scotty_op* op, int64_t key_slot, int64_t* out, int64_t cap) {
+  if (!op || !op->x) return SCOTTY_ERR_STATE;
+  std::vector<int64_t> v;
+  int rc = op->x->debug_dump(key_slot, v);
+  if (rc) return rc;
+  for (int64_t i = 0; i < (int64_t)v.size() && i < cap; i++) out[i] = v[i];
+  return (int64_t)v.size();
 }
 
 int scotty_sync(scotty_op* op) {

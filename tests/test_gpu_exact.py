@@ -103,6 +103,38 @@ def test_count_windows_in_order_match_oracle(seed):
     run_schedule(gpu, ora, ts, vals, sched)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_batch_parallel_path_equals_serial_replay(pkg, seed):
+    """The batch-parallel non-keyed path (exact_batch.hip) and the single-wavefront replay (exact_kernels.hip)
+    must leave identical results -- larger streams than the oracle comparisons, many events and segments."""
+    rng = np.random.default_rng(4400 + seed)
+    cfg = _session_cfg(rng, "i32")
+    n = 400_000
+    gaps = _gaps(rng, n, int(rng.integers(5_000, 50_000)), 100, 3000)
+    ts, vals = product().workloads.stream(n, [2, 10, 40][seed % 3], t0=500, ooo_frac=[0.05, 0.2][seed % 2],
+                                          max_delay=int(rng.integers(10, 600)), seed=seed, gaps=gaps)
+    ops = []
+    for serial in (0, 1):
+        op = pkg.SlicingWindowOperator(device=0)
+        op.tune("exact_serial", serial)
+        for a in cfg["aggs"]:
+            op.addWindowFunction(a)
+        op.setMaxLateness(cfg["lateness"])
+        for w in cfg["windows"]:
+            op.addWindowAssigner(w)
+        ops.append(op)
+    sched = interval_schedule(ts, 6, lag=300, pushes_per_interval=2)
+    from helpers import same_windows
+    for step in sched:
+        if step[0] == "push":
+            for op in ops:
+                op.processElements(ts[step[1]:step[2]], vals[step[1]:step[2]])
+        else:
+            a, b = ops[0].processWatermark(step[1]), ops[1].processWatermark(step[1])
+            same_windows(a, b)
+            assert ops[0].droppedCount() == ops[1].droppedCount()
+
+
 def test_session_tumbling_mixed_config3_reduced():
     """BASELINE configs[2] at reduced size: sliding + session, 20 % out-of-order (TimeStampGenerator-like,
     delay U[1,500]), MIN/MAX; session silences every ~10 s of event time."""
