@@ -62,6 +62,75 @@ def cpu_baseline(sizes, rate_per_ms, budget_s=12.0):
                                                                                     rate_per_ms, k)}
 
 
+def extra_c3(pkg, dev, batch, steps):
+    """BASELINE configs[2] (C3): SlidingWindow(60 s, 60 ms) + SessionWindow(1 s gap), MIN_I32 + MAX_I32, 20 %
+    out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; exact engine
+    (exact_batch.hip).  Inputs resident in HBM; results stay in HBM (processWatermarkDevice)."""
+    import torch
+    rate = max(1, batch // 1000)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    op = pkg.SlicingWindowOperator(device=dev.index)
+    op.addWindowFunction(pkg.AGG_MIN_I32)
+    op.addWindowFunction(pkg.AGG_MAX_I32)
+    op.setMaxLateness(1000)
+    op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 60))
+    op.addWindowAssigner(pkg.SessionWindow(pkg.WindowMeasure.Time, 1000))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    times, rows = [], 0
+    for s in range(steps + 2):
+        ts = base + s * 1000 + 1000
+        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        d = torch.randint(1, 501, (batch,), device=dev, generator=g)
+        ts = torch.where(late, torch.clamp(ts - d, min=1), ts).contiguous()
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(s * 1000 + 1000 + (batch - 1) // rate - 500)
+        torch.cuda.synchronize(dev)
+        if s >= 2:  # the first batch builds the store (first-tuple edge walk, session start)
+            times.append(time.perf_counter() - t0)
+            rows += n
+    return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
+                        "(delay U[1,500] ms), lag 500 ms, non-keyed, exact engine",
+            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
+
+
+def extra_c4(pkg, dev, batch, keys, steps):
+    """BASELINE configs[3] (C4), one GPU's shard: SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys,
+    maxLateness 1 (Flink connector default); 61 s of warm-up so every step emits each key's window."""
+    import torch
+    rate = max(1, batch // 1000)
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    op = pkg.KeyedSlicingWindowOperator(device=dev.index)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.setMaxLateness(1)
+    op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    warm = 61
+    times, rows = [], 0
+    for s in range(warm + steps):
+        k = torch.randint(0, keys, (batch,), device=dev, dtype=torch.int32, generator=g)
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        ts = base + s * 1000
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op.processElementsDevice(k.data_ptr(), ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
+        torch.cuda.synchronize(dev)
+        if s >= warm:
+            times.append(time.perf_counter() - t0)
+            rows += n
+    return {"workload": "C4 (one shard): keyed SlidingWindow(60s,1s) SUM_I32, %d uniform keys, maxLateness=1, "
+                        "results left in HBM" % keys,
+            "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
+            "ms_per_step": 1e3 * sum(times) / len(times), "value": batch * len(times) / sum(times),
+            "unit": "tuples/s", "windows_emitted": rows}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,6 +138,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C4 secondary measurements")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -167,6 +237,10 @@ def main():
                          "kernel": "ingest_kernel<VT_I32,NEED_SUM>", "algorithmic_bytes_per_launch":
                              B * BYTES_PER_TUPLE, "avg_launch_ms": avg_ms, "launches": launches},
         }
+        if not args.no_extra and world == 1:
+            del batches
+            torch.cuda.empty_cache()
+            res["extra"] = {"c3": extra_c3(pkg, dev, 1 << 26, 5), "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5)}
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(sizes, rate)
         print(json.dumps(res), flush=True)

@@ -252,6 +252,31 @@ __device__ __forceinline__ void load_tile(const XBArgs& a, int64_t tile, TileIte
   }
 }
 
+// in-order tuple t (t >= p): contexts in which it starts a new session (the chain of in-batch sessions), and
+// the end of the session before it
+__device__ __forceinline__ int newsess_bits(const XBArgs& a, int64_t t, int64_t p, int64_t* pb) {
+  const XSnap& sn = *a.snap;
+  const XCfg* c = a.cfg;
+  int nsmask = 0;
+  for (int k = 0; k < c->n_ctx; k++) {
+    const int64_t gap = c->gap[k];
+    bool nw;
+    int64_t before;
+    if (!sn.inv[k] && p == sn.p_start) {
+      nw = sn.ns[k] == 0 || t > jadd(sn.stored_end[k], gap);
+      before = sn.ns[k] == 0 ? JMIN : sn.stored_end[k];
+    } else {
+      nw = t > jadd(p, gap);
+      before = p;
+    }
+    if (nw) {
+      nsmask |= 1 << k;
+      pb[k] = before;
+    }
+  }
+  return nsmask;
+}
+
 // in-order classification (depends on P only).  Returns event; sets new-session bits per context.
 __device__ __forceinline__ bool inorder_event(const XBArgs& a, int64_t t, int64_t p, int64_t g, int64_t pos,
                                               int& nsmask, int64_t* pb) {
@@ -275,24 +300,10 @@ __device__ __forceinline__ bool inorder_event(const XBArgs& a, int64_t t, int64_
     }
   }
   for (int k = 0; k < c->n_ctx; k++) {
-    const bool first_io = p == sn.p_start;
-    if (!sn.inv[k] && first_io) ev = true;
+    if (!sn.inv[k] && p == sn.p_start) ev = true;
     if (t <= sn.lim[k]) ev = true;
-    const int64_t gap = c->gap[k];
-    bool nw;
-    int64_t before;
-    if (!sn.inv[k] && first_io) {
-      nw = sn.ns[k] == 0 || t > jadd(sn.stored_end[k], gap);
-      before = sn.ns[k] == 0 ? JMIN : sn.stored_end[k];
-    } else {
-      nw = t > jadd(p, gap);
-      before = p;
-    }
-    if (nw) {
-      nsmask |= 1 << k;
-      pb[k] = before;
-    }
   }
+  nsmask = newsess_bits(a, t, p, pb);
   if (c->has_count) {
     const int64_t cnt = jadd(sn.c0, pos);
     if (sn.nc0 == JMIN || cnt == sn.nc0 || (cnt > sn.nc0 && on_count_grid(c, cnt))) ev = true;
@@ -388,13 +399,12 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nscount_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
   TileItems it;
-  load_tile(a, blockIdx.x, it, wtot, true, tb);
+  load_tile(a, blockIdx.x, it, wtot, false, tb);
   int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
   for (int j = 0; j < it.cnt; j++) {
     if (it.t[j] < it.p[j]) continue;
-    int nsm;
     int64_t pb[XMAXCTX];
-    (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm, pb);
+    const int nsm = newsess_bits(a, it.t[j], it.p[j], pb);
     for (int k = 0; k < a.cfg->n_ctx; k++)
       if (nsm & (1 << k)) cnt[k]++;
   }
@@ -439,13 +449,12 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nswrite_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
   TileItems it;
-  load_tile(a, blockIdx.x, it, wtot, true, tb);
+  load_tile(a, blockIdx.x, it, wtot, false, tb);
   int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
   for (int j = 0; j < it.cnt; j++) {
     if (it.t[j] < it.p[j]) continue;
-    int nsm;
     int64_t pb[XMAXCTX];
-    (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm, pb);
+    const int nsm = newsess_bits(a, it.t[j], it.p[j], pb);
     for (int k = 0; k < a.cfg->n_ctx; k++)
       if (nsm & (1 << k)) cnt[k]++;
   }
@@ -453,9 +462,8 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nswrite_kernel(XBArgs a) {
     int64_t off = block_excl_sum(cnt[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
     for (int j = 0; j < it.cnt; j++) {
       if (it.t[j] < it.p[j]) continue;
-      int nsm;
       int64_t pb[XMAXCTX];
-      (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm, pb);
+      const int nsm = newsess_bits(a, it.t[j], it.p[j], pb);
       if (nsm & (1 << k)) {
         if (off < a.ns_cap) {
           a.ns_start[(int64_t)k * a.ns_cap + off] = it.t[j];
@@ -530,11 +538,12 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   int64_t nsb[XMAXCTX] = {0, 0, 0, 0};
   int64_t loc[XMAXCTX] = {0, 0, 0, 0};
   int nsm_item[XB_ITEMS];
+  uint32_t io_ev = 0;  // in-order events, evaluated once
   for (int j = 0; j < it.cnt; j++) {
     nsm_item[j] = 0;
     if (it.t[j] >= it.p[j]) {
       int64_t pb[XMAXCTX];
-      (void)inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm_item[j], pb);
+      if (inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm_item[j], pb)) io_ev |= 1u << j;
       for (int k = 0; k < c->n_ctx; k++)
         if (nsm_item[j] & (1 << k)) loc[k]++;
     }
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   int64_t tail_m = JMIN;  // max after this thread's last event
   bool has = false;
   for (int j = 0; j < it.cnt; j++) {
-    const bool ev = classify(a, it.t[j], it.p[j], it.g[j], it.base + j, nsb);
+    const bool ev = it.t[j] >= it.p[j] ? ((io_ev >> j) & 1) != 0 : classify(a, it.t[j], it.p[j], it.g[j], it.base + j, nsb);
     for (int k = 0; k < c->n_ctx; k++)
       if (nsm_item[j] & (1 << k)) nsb[k]++;
     if (ev) {
