@@ -2,11 +2,13 @@
 
 Workload (N=1): 1000 concurrent tumbling windows with sizes from BenchmarkRunner.randomTumbling(1000,1,20)
 (java.util.Random(10)), SUM_I32 + COUNT, in-order synthetic stream, maxLateness 1 (Flink connector default).
-One step = one watermark interval: a micro-batch of --batch tuples covering 1 s of event time, resident in
-HBM before the timed region, pushed through the C-ABI (ingest + edge commit kernels) followed by
-processWatermark (window assembly + GC + results to host).  N>1: one process per GPU, each rank runs an
-independent operator on its own key-hash shard (weak scaling, no collective on the data path); value is
-the aggregate over ranks divided by the max-over-ranks time.
+One step = one watermark interval: a micro-batch of --batch tuples per GPU covering 1 s of event time,
+resident in HBM before the timed region, pushed through the C-ABI (ingest + edge commit kernels) followed by
+processWatermark (window assembly + GC + results to host).  N>1: one process per GPU; the ONE non-keyed C2
+stream is sharded by arrival (= time) range -- rank r holds chunk r of every global micro-batch of N*batch
+tuples -- and one RCCL all-gather over xGMI per micro-batch exchanges the ranks' first-crossing records and
+slice partials; every rank then holds the same slice store and emits the same windows.
+Weak scaling: tuples per GPU fixed; value = all ranks' tuples / max-over-ranks time.
 
 Prints ONE JSON line (rank 0).  cpu_baseline = the CPU restatement of SlicingWindowOperator (oracle/),
 single thread, on a bounded sample of the same workload.
@@ -139,6 +141,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C4 secondary measurements")
+    ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -155,21 +158,27 @@ def main():
 
     sizes = pkg.workloads.random_tumbling_sizes(1000, 1, 20, seed=10)
     B = args.batch
-    rate = max(1, B // 1000)  # tuples per ms of event time
+    sharded = world > 1 or args.shard
+    if sharded and not dist:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get("MASTER_PORT", "29511"),
+                                rank=0, world_size=1)
+    G = world
+    rate = max(1, (B * G) // 1000)  # tuples per ms of event time of the global stream
     nsteps = args.steps + args.warmup
 
-    # ---- inputs resident in HBM before the timed region (one batch per step)
+    # ---- inputs resident in HBM before the timed region: this rank's arrival chunk of every global batch
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     batches = []
-    base = torch.arange(B, device=dev, dtype=torch.int64) // rate
+    base = (torch.arange(B, device=dev, dtype=torch.int64) + rank * B) // rate
     for s in range(nsteps):
         ts = base + s * 1000
         vals = torch.randint(-2**31, 2**31, (B,), device=dev, dtype=torch.int32, generator=gen)
-        batches.append((ts, vals, int(s * 1000 + (B - 1) // rate)))
+        batches.append((ts, vals, int(s * 1000 + (B * G - 1) // rate)))
     torch.cuda.synchronize(dev)
 
-    op = pkg.SlicingWindowOperator(device=local)
+    op = pkg.ShardedSlicingWindowOperator(device=local) if sharded else pkg.SlicingWindowOperator(device=local)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.addWindowFunction(pkg.AGG_COUNT)
     op.setMaxLateness(1)
@@ -179,7 +188,10 @@ def main():
 
     def step(i):
         ts, vals, wm = batches[i]
-        op.processElementsDevice(ts.data_ptr(), vals.data_ptr(), B)
+        if sharded:
+            op.processChunk(ts.data_ptr(), vals.data_ptr(), B, 0)
+        else:
+            op.processElementsDevice(ts.data_ptr(), vals.data_ptr(), B)
         nw, _ = op.processWatermarkRaw(wm)
         return nw
 
@@ -227,11 +239,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32 values / int64 timestamps",
-            "data": "synthetic (in-HBM, seeded): ts = step*1000 + i//%d ms, int32 uniform values" % rate,
+            "data": "synthetic (in-HBM, seeded): global stream ts = step*1000 + i//%d ms, int32 uniform values" % rate,
             "config": {"workload": "C2: 1000 concurrent tumbling windows, sizes randomTumbling(1000,1,20) "
                                    "java.util.Random(10), SUM_I32+COUNT, in-order, maxLateness=1",
-                       "tuples_per_step": B, "event_ms_per_step": 1000, "windows_emitted": n_windows,
-                       "parallelism": "key-shard x%d (one operator per GPU)" % world},
+                       "tuples_per_step": B * world, "tuples_per_step_per_gpu": B, "event_ms_per_step": 1000,
+                       "windows_emitted": n_windows,
+                       "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch"
+                                       % world) if sharded else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "ingest_kernel<VT_I32,NEED_SUM>", "algorithmic_bytes_per_launch":

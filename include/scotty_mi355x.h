@@ -121,6 +121,21 @@ int scotty_process_watermark(scotty_op* op, int64_t watermark_ts, scotty_windows
 /* Same, but the result columns stay in HBM (device pointers, valid until the next call on the op).
  * Exact-engine ops only (keyed, or with session / count windows); others return SCOTTY_ERR_UNSUPPORTED. */
 int scotty_process_watermark_device(scotty_op* op, int64_t watermark_ts, scotty_windows* out);
+/* ---- time/arrival-range sharding of ONE non-keyed stream over G ranks (one GPU each).
+ * Every rank creates the same operator (same windows, functions, lateness) and, per micro-batch, holds a
+ * contiguous arrival chunk of the global batch (chunk r precedes chunk r+1 in arrival order).  Per batch:
+ *   1. scotty_shard_push(op, chunk, ts0, xbuf): ingest the chunk, write this rank's exchange record into the
+ *      caller's device buffer xbuf of scotty_shard_xbytes(op) bytes (same size on every rank);
+ *      ts0 = timestamp of the global first tuple (only read on the op's first batch: the first-edge walk);
+ *   2. the caller all-gathers the G records in rank order into one device buffer (RCCL / NCCL all_gather);
+ *   3. scotty_shard_commit(op, gathered, G): every rank decides the same slice edges (StreamSlicer rule from
+ *      the global first crossings, S/StreamSlicer.java:55-116) and folds every rank's partials.
+ * Watermarks then run unchanged (and identically) on every rank.  Context-free time windows only (the grid
+ * path); other configurations return SCOTTY_ERR_UNSUPPORTED. */
+size_t scotty_shard_xbytes(scotty_op* op);
+int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0, void* d_xbuf);
+int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world);
+
 /* Number of keys (operators) of a keyed op. */
 int64_t scotty_key_count(scotty_op* op);
 

@@ -142,6 +142,9 @@ def lib():
             "scotty_process_keyed_elements_device": (ctypes.c_int, [P, P, P, P, ctypes.c_size_t]),
             "scotty_key_count": (i64, [P]),
             "scotty_tune": (ctypes.c_int, [P, ctypes.c_char_p, i64]),
+            "scotty_shard_xbytes": (ctypes.c_size_t, [P]),
+            "scotty_shard_push": (ctypes.c_int, [P, P, P, ctypes.c_size_t, i64, P]),
+            "scotty_shard_commit": (ctypes.c_int, [P, P, ctypes.c_int]),
             "scotty_dropped_count": (u64, [P]),
             "scotty_processed_count": (u64, [P]),
             "scotty_slice_count": (i64, [P]),
@@ -300,6 +303,17 @@ class SlicingWindowOperator:
             res.append(AggregateWindow(int(start[i]), int(end[i]), int(meas[i]), bool(has[i]), vals))
         return res
 
+    # ---- time/arrival-range sharding of one non-keyed stream (include/scotty_mi355x.h, scotty_shard_*)
+    def shardXBytes(self):
+        return self._l.scotty_shard_xbytes(self._h)
+
+    def shardPush(self, ts_ptr, val_ptr, n, ts0, xbuf_ptr):
+        self._flush()
+        self._check(self._l.scotty_shard_push(self._h, ts_ptr, val_ptr, n, ts0, xbuf_ptr))
+
+    def shardCommit(self, gathered_ptr, world):
+        self._check(self._l.scotty_shard_commit(self._h, gathered_ptr, world))
+
     def processWatermarkDevice(self, watermark_ts):
         """processWatermark with the result columns left in HBM (exact engine): returns (n_windows, status)."""
         self._flush()
@@ -388,6 +402,53 @@ class KeyedSlicingWindowOperator(SlicingWindowOperator):
 
     def keyCount(self):
         return self._l.scotty_key_count(self._h)
+
+
+class ShardedSlicingWindowOperator:
+    """One non-keyed stream over the ranks of a torch.distributed group, one GPU each:
+    every rank holds the same SlicingWindowOperator and feeds a contiguous arrival chunk of each global
+    micro-batch; one all-gather of the per-rank exchange records (RCCL over xGMI for backend "nccl"; host
+    staging for "gloo") joins them, and every rank then holds the identical slice store, so processWatermark
+    is purely local.  Context-free time windows only."""
+
+    def __init__(self, device=0, value_type=VALUE_I32, group=None):
+        import torch
+        import torch.distributed as dist
+        self.dist, self.torch, self.group = dist, torch, group
+        self.op = SlicingWindowOperator(device=device, value_type=value_type)
+        self.world = dist.get_world_size(group)
+        self.dev = torch.device("cuda", device)
+        self.staged = dist.get_backend(group) != "nccl"
+        self._xb = None
+
+    def __getattr__(self, name):  # addWindowAssigner, addWindowFunction, setMaxLateness, processWatermark...
+        return getattr(self.op, name)
+
+    def _bufs(self):
+        if self._xb is None:
+            words = self.op.shardXBytes() // 8
+            t = self.torch
+            self._xb = t.empty(words, dtype=t.int64, device=self.dev)
+            self._gb = t.empty(words * self.world, dtype=t.int64, device=self.dev)
+            if self.staged:
+                self._hx = t.empty(words, dtype=t.int64)
+                self._hg = t.empty(words * self.world, dtype=t.int64)
+        return self._xb, self._gb
+
+    def processChunk(self, ts_ptr, val_ptr, n, ts0=0):
+        """This rank's arrival chunk of the next global micro-batch (device pointers); ts0 = the global first
+        tuple's timestamp (read on the very first batch only)."""
+        xb, gb = self._bufs()
+        self.op.shardPush(ts_ptr, val_ptr, n, ts0, xb.data_ptr())
+        if self.staged:
+            self._hx.copy_(xb)
+            self.dist.all_gather_into_tensor(self._hg, self._hx, group=self.group)
+            gb.copy_(self._hg)
+            self.torch.cuda.synchronize(self.dev)
+        else:
+            self.dist.all_gather_into_tensor(gb, xb, group=self.group)
+            self.torch.cuda.current_stream(self.dev).synchronize()  # the commit runs on the op's own stream
+        self.op.shardCommit(gb.data_ptr(), self.world)
 
 
 from . import workloads  # noqa: E402,F401

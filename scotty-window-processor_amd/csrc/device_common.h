@@ -97,4 +97,37 @@ struct WindowArgs {
   int vt;
 };
 
+// Time/arrival-range sharding of one non-keyed micro-batch over G ranks: rank r ingests
+// arrival chunk r into the replicated cell layout, exports its first-crossing records and touched cells
+// (ShardArgs.xbuf, identical size on every rank), the caller all-gathers the records, and every rank commits
+// the same slice edges and partials.  Exchange record of one rank, int64 words:
+//   [0..15]   header: chunk max, late tuples, horizon-overflow tuples, touched cells, local candidates, n
+//   cells     kc_cap x {cell index, cnt, tmax, sum, min, max}
+//   cands     kg_cap x {a local tuple reaches g (0/1), local part of the edge rule (0/1)}
+constexpr int SHARD_HDR = 16;
+struct ShardArgs {
+  const int64_t* ts;
+  int64_t n;
+  int64_t tile;
+  int64_t max_lateness;
+  int64_t scap;
+  const int64_t* grid;
+  long long* tilemax;
+  int64_t* s_tstart;
+  int64_t* s_tlast;
+  unsigned long long* s_cnt;
+  unsigned long long* s_part[NPART];
+  unsigned long long* c_cnt;
+  long long* c_tmax;
+  unsigned long long* c_part[NPART];
+  DevMeta* meta;
+  int32_t* rank_buf;          // scratch [kg_cap]
+  int32_t* flag_buf;          // scratch [kg_cap]
+  int64_t kc_cap, kg_cap;
+  int64_t* xbuf;              // export: this rank's record
+  const int64_t* gathered;    // commit: world records
+  int32_t world;
+  int need, vt;
+};
+
 }  // namespace scotty

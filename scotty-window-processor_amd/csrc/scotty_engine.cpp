@@ -26,6 +26,8 @@ hipError_t launch_windows(const WindowArgs& a, hipStream_t st);
 hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st);
 hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
 hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st);
+hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st);
+hipError_t launch_shard_commit(const ShardArgs& a, hipStream_t st);
 }  // namespace scotty
 
 using namespace scotty;
@@ -134,6 +136,11 @@ struct scotty_op {
   bool x_serial = false;
   uint64_t x_pushed = 0;
   std::vector<uint32_t> r_key;
+  // sharded grid path (scotty_shard_*)
+  int64_t shard_kc = 2048, shard_kg = 1024;
+  int32_t* d_shrank = nullptr;
+  int32_t* d_shflag = nullptr;
+  int64_t shard_tile = TILE_MIN, shard_n = 0;
   XResult xr;
 
   // ---- timing
@@ -397,8 +404,8 @@ int sync_snapshot(scotty_op* op) {
   return SCOTTY_OK;
 }
 
-// Runs the ingest + commit launches of one micro-batch (no host synchronisation).
-int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t seq) {
+// Ingest launch of one micro-batch (no host synchronisation); *tile_out = the arrival tile size used.
+int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t* tile_out) {
   int rc = ensure_tiles(op, n);
   if (rc) return rc;
   IngestArgs ia{};
@@ -440,6 +447,15 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
     op->ev_pending.push_back(ev);
     op->t_tuples += n;
   }
+  *tile_out = tile;
+  return SCOTTY_OK;
+}
+
+// Runs the ingest + commit launches of one micro-batch (no host synchronisation).
+int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t seq) {
+  int64_t tile = TILE_MIN;
+  int rc = enqueue_ingest(op, d_ts, d_val, n, &tile);
+  if (rc) return rc;
   CommitArgs ca{};
   ca.ts = d_ts;
   ca.n = n;
@@ -529,6 +545,9 @@ int replay_after_overflow(scotty_op* op) {
     DevMeta& m = *op->h_snap;
     if (!m.overflow) return SCOTTY_OK;
     if (m.overflow == 2) return fail(op, SCOTTY_ERR_NOMEM, "slice capacity exceeded");
+    if (m.overflow == 3)
+      return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharded batch exceeded the exchange capacity or the edge-grid horizon "
+                                              "(scotty_tune \"shard_cells\" / \"shard_cands\")");
     const int64_t failed = m.failed_push;
     int64_t zero = 0;
     HIPCHK(hipMemcpyAsync(&op->d_meta->overflow, &zero, 8, hipMemcpyHostToDevice, op->stream));
@@ -608,6 +627,7 @@ void scotty_destroy(scotty_op* op) {
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
+  F(op->d_shrank); F(op->d_shflag);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
 }
@@ -851,6 +871,80 @@ int scotty_process_watermark_device(scotty_op* op, int64_t wm, scotty_windows* o
   return exact_watermark(op, wm, out, false);
 }
 
+static int64_t shard_words(const scotty_op* op) { return SHARD_HDR + 6 * op->shard_kc + 2 * op->shard_kg; }
+
+size_t scotty_shard_xbytes(scotty_op* op) { return op ? (size_t)shard_words(op) * 8 : 0; }
+
+static ShardArgs shard_args(scotty_op* op) {
+  ShardArgs a{};
+  a.tile = op->shard_tile;
+  a.max_lateness = op->max_lateness;
+  a.scap = op->scap;
+  a.grid = op->d_grid;
+  a.tilemax = op->d_tilemax;
+  a.s_tstart = op->d_tstart;
+  a.s_tlast = op->d_tlast;
+  a.s_cnt = op->d_scnt;
+  for (int k = 0; k < NPART; k++) a.s_part[k] = op->d_spart[k];
+  a.c_cnt = op->d_ccnt;
+  a.c_tmax = op->d_ctmax;
+  for (int k = 0; k < NPART; k++) a.c_part[k] = op->d_cpart[k];
+  a.meta = op->d_meta;
+  a.rank_buf = op->d_shrank;
+  a.flag_buf = op->d_shflag;
+  a.kc_cap = op->shard_kc;
+  a.kg_cap = op->shard_kg;
+  a.need = op->need;
+  a.vt = op->vt;
+  return a;
+}
+
+int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0, void* d_xbuf) {
+  if (!op || !d_xbuf || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->keyed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "keyed operators shard by key: no exchange needed");
+  int rc = decide_mode(op);
+  if (rc) return rc;
+  if (op->mode != 1)
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs context-free time windows only (the grid path)");
+  if (!op->has_fixed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs at least one context-free window");
+  if (!op->d_shrank) {
+    HIPCHK(hipMalloc(&op->d_shrank, op->shard_kg * 4));
+    HIPCHK(hipMalloc(&op->d_shflag, op->shard_kg * 4));
+  }
+  if (!op->started) {
+    rc = start_stream(op, ts0);
+    if (rc) return rc;
+  }
+  int64_t tile = TILE_MIN;
+  if (n > 0) {
+    rc = enqueue_ingest(op, d_ts, d_val, (int64_t)n, &tile);
+    if (rc) return rc;
+  } else {
+    HIPCHK(hipMemsetAsync(op->d_tilemax, 0xFF, 8, op->stream));
+  }
+  op->shard_tile = tile;
+  op->shard_n = (int64_t)n;
+  ShardArgs a = shard_args(op);
+  a.ts = d_ts;
+  a.n = (int64_t)n;
+  a.xbuf = (int64_t*)d_xbuf;
+  HIPCHK(launch_shard_export(a, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));  // the record is complete when the caller starts the all-gather
+  return SCOTTY_OK;
+}
+
+int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world) {
+  if (!op || !d_gathered || world < 1 || world > 64) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->mode != 1 || !op->d_shrank) return fail(op, SCOTTY_ERR_STATE, "scotty_shard_push must come first");
+  ShardArgs a = shard_args(op);
+  a.gathered = (const int64_t*)d_gathered;
+  a.world = world;
+  HIPCHK(launch_shard_commit(a, op->stream));
+  return SCOTTY_OK;
+}
+
 int64_t scotty_key_count(scotty_op* op) { return (op && op->x) ? op->x->key_count() : 0; }
 
 int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
@@ -1013,6 +1107,11 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (!op || !key) return SCOTTY_ERR_ARG;
   if (std::strcmp(key, "ingest_mode") == 0) {
     op->ingest_mode = (int)value;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "shard_cells") == 0 || std::strcmp(key, "shard_cands") == 0) {
+    if (op->d_shrank || value < 16 || value > (1 << 22)) return SCOTTY_ERR_ARG;
+    (key[6] == 'c' && key[7] == 'e' ? op->shard_kc : op->shard_kg) = value;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "exact_serial") == 0) {

@@ -766,6 +766,297 @@ __global__ void first_ge_kernel(const int64_t* ts, int64_t n, int64_t x, unsigne
     if (ts[i] >= x) atomicMin(out_idx, (unsigned long long)i);
 }
 
+// ================================================================ 4. sharded micro-batch
+// Export (one workgroup per rank, after the local ingest): the rank's chunk max, for every grid point g of
+// the effective grid below it the first local tuple e >= g and the local running max before it (the inputs
+// of StreamSlicer.determineSlices' edge rule, S/StreamSlicer.java:55-84), and its touched cells.
+__global__ __launch_bounds__(1024) void shard_export_kernel(ShardArgs a) {
+  __shared__ long long s_p[NT_MAX];
+  __shared__ long long s_w[32];
+  __shared__ int64_t sc[16];
+  __shared__ int s_cnt[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) {
+    const DevMeta& m = *a.meta;
+    sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount;
+    sc[5] = (int64_t)m.late_push; sc[6] = (int64_t)m.overflow_push;
+  }
+  __syncthreads();
+  const int64_t head = sc[1], tail = sc[2], j0 = sc[3], gcount = sc[4];
+  const int64_t c_old = tail - head;
+  int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+  if (kc < 0) kc = 0;
+  const int64_t* g = a.grid + j0;
+  const int64_t tile = a.tile;
+  // local prefix max over tile maxima (no carry: the other ranks' maxima come in the exchange)
+  const int64_t nT = (a.n + tile - 1) / tile;
+  int64_t loc[8];
+  int64_t run = INT64_MIN;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int64_t t = (int64_t)tid * 8 + j;
+    run = max(run, t < nT ? (int64_t)a.tilemax[t] : INT64_MIN);
+    loc[j] = run;
+  }
+  const int64_t incl = block_incl_max(run, s_w, lane, wid);
+  const int64_t excl_thread = (int64_t)__shfl_up((long long)incl, 1);
+  const int64_t carry = lane == 0 ? (wid > 0 ? (int64_t)s_w[wid - 1] : INT64_MIN) : excl_thread;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int64_t t = (int64_t)tid * 8 + j;
+    if (t < nT) s_p[t] = max(carry, loc[j]);
+  }
+  __syncthreads();
+  const int64_t cmax = nT > 0 ? (int64_t)s_p[nT - 1] : INT64_MIN;
+  if (tid == 0) {
+    int64_t lo = 0, hi = kc;  // local candidates: grid points <= chunk max
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (g[mid] <= cmax) lo = mid + 1; else hi = mid;
+    }
+    sc[8] = lo;
+  }
+  __syncthreads();
+  const int64_t nc = sc[8];
+  int64_t* hdr = a.xbuf;
+  int64_t* xcells = a.xbuf + SHARD_HDR;
+  int64_t* xcand = xcells + 6 * a.kc_cap;
+  // Local part of the edge rule for every local candidate g_k: with m = max(pre_r, m_loc) the rule
+  // g_{k-1} <= m || e - g_k < maxLateness splits into f_loc = (g_{k-1} <= m_loc || e - g_k < L), decided
+  // here, and g_{k-1} <= pre_r, decided at commit.  Tile bounds decide f_loc except in rare ambiguous cases,
+  // which scan the crossing tile exactly (as commit_kernel does).
+  for (int64_t k = tid; k < min(nc, a.kg_cap); k += 1024) {
+    const int64_t gk = g[k];
+    const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
+    const int64_t pprev = ts_ > 0 ? (int64_t)s_p[ts_ - 1] : INT64_MIN;
+    const int64_t tm = a.tilemax[ts_];
+    int f;
+    if (k == 0 || g[k - 1] <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < a.max_lateness) f = 1;
+    else f = 2;
+    xcand[2 * k] = 1;  // found
+    xcand[2 * k + 1] = f;
+  }
+  __syncthreads();
+  for (int64_t k = wid; k < min(nc, a.kg_cap); k += 16) {
+    if (xcand[2 * k + 1] != 2) continue;
+    const int64_t gk = g[k];
+    const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
+    int64_t r = ts_ > 0 ? (int64_t)s_p[ts_ - 1] : INT64_MIN;
+    const int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
+    int64_t e = INT64_MIN, m = INT64_MIN;
+    for (int64_t base = e0; base < e1; base += 64) {
+      const int64_t i = base + lane;
+      const int64_t v = i < e1 ? a.ts[i] : INT64_MIN;
+      int64_t inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+        if (lane >= o) inc = max(inc, u);
+      }
+      int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
+      if (lane == 0) ex = INT64_MIN;
+      ex = max(ex, r);
+      const unsigned long long hit = __ballot(v >= gk);
+      if (hit) {
+        const int f = __ffsll((long long)hit) - 1;
+        e = rl64(v, f);
+        m = rl64(ex, f);
+        break;
+      }
+      r = max(r, rl64(inc, 63));
+    }
+    if (lane == 0) xcand[2 * k + 1] = ((int64_t)((uint64_t)e - (uint64_t)gk) < a.max_lateness || g[k - 1] <= m) ? 1 : 0;
+  }
+  for (int64_t k = nc + tid; k < a.kg_cap; k += 1024) {
+    xcand[2 * k] = 0;  // no local tuple reaches g_k
+    xcand[2 * k + 1] = 0;
+  }
+  // touched cells (tuples <= chunk max fall in cells [0, c_old + nc]) -> compacted records; cells reset
+  const int64_t ncell = min(c_old + nc + 1, c_old + kc);
+  int64_t written = 0;
+  for (int64_t base = 0; base < ncell; base += 1024) {
+    const int64_t c = base + tid;
+    const bool have = c < ncell && a.c_cnt[c] != 0;
+    const unsigned long long bal = __ballot(have);
+    if (lane == 0) s_cnt[wid] = __popcll(bal);
+    __syncthreads();
+    int64_t before = written;
+    for (int w = 0; w < wid; w++) before += s_cnt[w];
+    int64_t tot = 0;
+    for (int w = 0; w < 16; w++) tot += s_cnt[w];
+    if (have) {
+      const int64_t o = before + __popcll(bal & ((1ull << lane) - 1));
+      if (o < a.kc_cap) {
+        int64_t* rec = xcells + 6 * o;
+        rec[0] = c;
+        rec[1] = (int64_t)a.c_cnt[c];
+        rec[2] = a.c_tmax[c];
+        rec[3] = (int64_t)a.c_part[0][c];
+        rec[4] = (int64_t)a.c_part[1][c];
+        rec[5] = (int64_t)a.c_part[2][c];
+      }
+      a.c_cnt[c] = 0;
+      a.c_tmax[c] = INT64_MIN;
+      a.c_part[0][c] = 0;
+      a.c_part[1][c] = (unsigned long long)PART_ID_MIN;
+      a.c_part[2][c] = (unsigned long long)PART_ID_MAX;
+    }
+    written += tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    hdr[0] = cmax;
+    hdr[1] = sc[5];
+    hdr[2] = sc[6];
+    hdr[3] = written;
+    hdr[4] = nc;
+    hdr[5] = a.n;
+    for (int i = 6; i < SHARD_HDR; i++) hdr[i] = 0;
+    DevMeta& m = *a.meta;
+    m.late_push = 0;
+    m.overflow_push = 0;
+  }
+}
+
+// Commit (one workgroup, identical on every rank): global first crossings -> slice edges, append, fold.
+__global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
+  __shared__ long long s_pre[64];  // pre_r = max(prev_max, chunk max of ranks < r)
+  __shared__ int64_t sc[16];
+  __shared__ long long s_w[32];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t xw = SHARD_HDR + 6 * a.kc_cap + 2 * a.kg_cap;
+  if (tid == 0) {
+    DevMeta& m = *a.meta;
+    sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount; sc[5] = m.prev_max;
+    int64_t pre = m.prev_max, late = 0, ovf = 0, ntot = 0, bad = 0;
+    for (int r = 0; r < a.world; r++) {
+      const int64_t* h = a.gathered + r * xw;
+      s_pre[r] = pre;
+      pre = max(pre, h[0]);
+      late += h[1];
+      ovf += h[2];
+      ntot += h[5];
+      if (h[3] > a.kc_cap || h[4] > a.kg_cap) bad = 1;
+    }
+    sc[6] = pre;  // batch max
+    sc[7] = late;
+    sc[9] = ovf;
+    sc[10] = ntot;
+    sc[11] = bad;
+  }
+  __syncthreads();
+  const int64_t head = sc[1], tail = sc[2], j0 = sc[3], gcount = sc[4];
+  const int64_t batch_max = sc[6];
+  const int64_t c_old = tail - head;
+  int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+  if (kc < 0) kc = 0;
+  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
+  const int64_t* g = a.grid + j0;
+  if (tid == 0) {
+    int64_t lo = 0, hi = kc;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (g[mid] <= batch_max) lo = mid + 1; else hi = mid;
+    }
+    sc[8] = lo;
+    if (h_end != INT64_MAX && batch_max >= h_end) sc[9] = max(sc[9], (int64_t)1);
+  }
+  __syncthreads();
+  const int64_t ncand = sc[8];
+  int ovf = (sc[9] != 0 || sc[11] != 0 || ncand > a.kg_cap) ? 1 : 0;
+  const int64_t L = a.max_lateness;
+  // edge decision per candidate from the owning (first) rank's crossing
+  if (!ovf) {
+    for (int64_t k = tid; k < ncand; k += 1024) {
+      const int64_t gk = g[k];
+      int f = 0;
+      for (int r = 0; r < a.world; r++) {  // the first rank reaching g_k owns its first crossing
+        const int64_t* xc = a.gathered + r * xw + SHARD_HDR + 6 * a.kc_cap;
+        if (xc[2 * k] == 0) continue;
+        f = (k == 0 || xc[2 * k + 1] == 1 || g[k - 1] <= (int64_t)s_pre[r]) ? 1 : 0;
+        break;
+      }
+      a.flag_buf[k] = f;
+    }
+  }
+  __syncthreads();
+  int64_t n_emit = 0;
+  if (!ovf) {
+    int64_t base_cnt = 0;
+    for (int64_t base = 0; base < ncand; base += 1024) {
+      const int64_t k = base + tid;
+      const bool f = k < ncand && a.flag_buf[k] == 1;
+      const unsigned long long bal = __ballot(f);
+      const int in_wave = __popcll(bal & ((2ull << lane) - 1));
+      if (lane == 0) s_w[wid] = __popcll(bal);
+      __syncthreads();
+      int64_t before = 0;
+      for (int w = 0; w < wid; w++) before += s_w[w];
+      int64_t tot = 0;
+      for (int w = 0; w < 16; w++) tot += s_w[w];
+      if (k < ncand) a.rank_buf[k] = (int32_t)(base_cnt + before + in_wave);
+      base_cnt += tot;
+      __syncthreads();
+    }
+    n_emit = base_cnt;
+    if (tail + n_emit > a.scap) ovf = 2;
+  }
+  __syncthreads();
+  if (!ovf) {
+    for (int64_t k = tid; k < ncand; k += 1024) {  // SliceManager.appendSlice
+      if (a.flag_buf[k] == 1) {
+        const int64_t s = tail + a.rank_buf[k] - 1;
+        a.s_tstart[s] = g[k];
+        a.s_tlast[s] = g[k];
+        a.s_cnt[s] = 0;
+        a.s_part[0][s] = 0;
+        a.s_part[1][s] = (unsigned long long)PART_ID_MIN;
+        a.s_part[2][s] = (unsigned long long)PART_ID_MAX;
+      }
+    }
+    __syncthreads();
+    for (int r = 0; r < a.world; r++) {  // fold every rank's cells
+      const int64_t* h = a.gathered + r * xw;
+      const int64_t* xcells = h + SHARD_HDR;
+      const int64_t nrec = h[3];
+      for (int64_t i = tid; i < nrec; i += 1024) {
+        const int64_t* rec = xcells + 6 * i;
+        const int64_t c = rec[0];
+        int64_t s;
+        if (c < c_old) {
+          s = head + c;
+        } else {
+          const int32_t rk = a.rank_buf[c - c_old];
+          s = rk > 0 ? tail + rk - 1 : tail - 1;
+        }
+        atomicAdd(&a.s_cnt[s], (unsigned long long)rec[1]);
+        atomicMax((long long*)&a.s_tlast[s], (long long)rec[2]);
+        if (a.need & NEED_SUM) {
+          if (a.vt == VT_F64) atomicAdd((double*)&a.s_part[0][s], __longlong_as_double((long long)rec[3]));
+          else atomicAdd(&a.s_part[0][s], (unsigned long long)rec[3]);
+        }
+        if (a.need & NEED_MIN) atomicMin((long long*)&a.s_part[1][s], (long long)rec[4]);
+        if (a.need & NEED_MAX) atomicMax((long long*)&a.s_part[2][s], (long long)rec[5]);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    DevMeta& m = *a.meta;
+    m.batch_max = batch_max;
+    if (!ovf) {
+      m.tail = tail + n_emit;
+      m.j0 = j0 + ncand;
+      m.prev_max = batch_max;
+      m.n_emitted = n_emit;
+      m.late_total += (uint64_t)sc[7];
+      m.processed_total += (uint64_t)(sc[10] - sc[7]);
+    } else {
+      m.overflow = ovf == 2 ? 2 : 3;  // 3: shard horizon / exchange capacity exceeded (not replayable)
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host-side launch wrappers
 template <int VT, int NEED, int MODE>
 static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStream_t st) {
@@ -809,6 +1100,15 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
 
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(1024), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(shard_export_kernel, dim3(1), dim3(1024), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_shard_commit(const ShardArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(1024), 0, st, a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,23 @@
+"""Deterministic sharded-run cases shared by the worker ranks and the checking test (no GPU needed here)."""
+import numpy as np
+
+from helpers import product, interval_schedule
+from specs import Tumbling, Sliding, FixedBand, Time, SUM, COUNT, MIN, MAX
+
+
+def case(cid):
+    rng = np.random.default_rng(600 + cid)
+    wl = product().workloads
+    if cid == 0:   # C2-like: many tumbling windows, in-order
+        sizes = wl.random_tumbling_sizes(200, 1, 20, seed=10)
+        cfg = dict(windows=[Tumbling(Time, s) for s in sizes], aggs=[SUM, COUNT], lateness=1)
+        ts, vals = wl.stream(400_000, 20, t0=0, seed=cid)
+    elif cid == 1:  # sliding + tumbling, 20 % out-of-order across chunk boundaries
+        cfg = dict(windows=[Sliding(Time, 3000, 61), Tumbling(Time, 997)], aggs=[SUM, COUNT, MIN, MAX], lateness=800)
+        ts, vals = wl.stream(300_000, 25, t0=100, ooo_frac=0.2, max_delay=500, seed=cid)
+    else:           # lateness edge skipping on jumps + fixed band
+        cfg = dict(windows=[Tumbling(Time, 13), FixedBand(Time, 5000, 2000)], aggs=[SUM, MAX], lateness=3)
+        ts, vals = wl.stream(120_000, 2, t0=7, ooo_frac=0.05, max_delay=2, seed=cid,
+                             gaps=[(i, int(rng.integers(50, 900))) for i in range(5000, 120_000, 7000)])
+    sched = interval_schedule(ts, 6, lag=50 if cid != 1 else 500, pushes_per_interval=2)
+    return cfg, ts, vals, sched

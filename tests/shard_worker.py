@@ -1,0 +1,52 @@
+"""One rank of a sharded non-keyed run (launched by tests/test_gpu_shard.py through torch.distributed.run).
+Every rank feeds its arrival chunk of each global micro-batch; rank 0 writes the windows of every watermark."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+from helpers import product  # noqa: E402
+from shard_cases import case  # noqa: E402
+
+
+def main():
+    out, cid = sys.argv[1], int(sys.argv[2])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    pkg = product()
+    cfg, ts, vals, sched = case(cid)
+    op = pkg.ShardedSlicingWindowOperator(device=0)
+    for a in cfg["aggs"]:
+        op.addWindowFunction(a)
+    if cfg.get("lateness") is not None:
+        op.setMaxLateness(cfg["lateness"])
+    for w in cfg["windows"]:
+        op.addWindowAssigner(w)
+    dev = torch.device("cuda", 0)
+    res = []
+    for st in sched:
+        if st[0] == "push":
+            lo, hi = st[1], st[2]
+            cuts = np.linspace(lo, hi, world + 1).astype(np.int64)
+            a, b = int(cuts[rank]), int(cuts[rank + 1])
+            t = torch.tensor(ts[a:b], dtype=torch.int64, device=dev)
+            v = torch.tensor(vals[a:b], dtype=torch.int32, device=dev)
+            op.processChunk(t.data_ptr(), v.data_ptr(), b - a, int(ts[0]))
+            torch.cuda.synchronize(dev)
+        else:
+            ws = op.processWatermark(st[1])
+            res.append([list(w.key()[:4]) + [list(w.key()[4])] for w in ws] + [["dropped", op.droppedCount()]])
+    if rank == 0:
+        json.dump(res, open(out, "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

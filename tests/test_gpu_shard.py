@@ -1,0 +1,46 @@
+"""Time/arrival-range sharding of one non-keyed stream: 2 ranks (one process each, both on
+cuda:0, exchange over gloo with host staging -- the protocol is identical to RCCL device all-gathers) must
+produce exactly the windows the single-stream oracle produces, out-of-order tuples across chunk boundaries
+included."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from helpers import build_ops, same_windows, ROOT
+from shard_cases import case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cid", [0, 1, 2])
+def test_two_rank_sharded_stream_matches_oracle(tmp_path, cid):
+    out = str(tmp_path / "w.json")
+    port = str(29500 + cid + (os.getpid() % 400))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", port,
+                        os.path.join(ROOT, "tests", "shard_worker.py"), out, str(cid)],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.load(open(out))
+    cfg, ts, vals, sched = case(cid)
+    _, ora = build_ops(cfg)
+    k = 0
+    fails = 0
+    for st in sched:
+        if st[0] == "push":
+            fails += ora.processElements(ts[st[1]:st[2]], vals[st[1]:st[2]])
+        else:
+            exp = ora.processWatermark(st[1])
+            g = got[k]
+            k += 1
+            assert g[-1] == ["dropped", fails]
+            rows = g[:-1]
+            assert len(rows) == len(exp), (len(rows), len(exp))
+            for x, y in zip(rows, exp):
+                assert (x[0], x[1], x[2], bool(x[3])) == (y.getStart(), y.getEnd(), y.getMeasure(), y.hasValue()), (x, y)
+                assert x[4] == y.getAggValues(), (x, y)
+    assert k > 0
