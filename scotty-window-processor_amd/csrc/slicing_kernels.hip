@@ -964,11 +964,9 @@ __global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
   __syncthreads();
   const int64_t ncand = sc[8];
   int ovf = (sc[9] != 0 || sc[11] != 0 || ncand > a.kg_cap) ? 1 : 0;
-  const int64_t L = a.max_lateness;
   // edge decision per candidate from the owning (first) rank's crossing
   if (!ovf) {
     for (int64_t k = tid; k < ncand; k += 1024) {
-      const int64_t gk = g[k];
       int f = 0;
       for (int r = 0; r < a.world; r++) {  // the first rank reaching g_k owns its first crossing
         const int64_t* xc = a.gathered + r * xw + SHARD_HDR + 6 * a.kc_cap;
