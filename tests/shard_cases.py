@@ -15,6 +15,12 @@ def case(cid):
     elif cid == 1:  # sliding + tumbling, 20 % out-of-order across chunk boundaries
         cfg = dict(windows=[Sliding(Time, 3000, 61), Tumbling(Time, 997)], aggs=[SUM, COUNT, MIN, MAX], lateness=800)
         ts, vals = wl.stream(300_000, 25, t0=100, ooo_frac=0.2, max_delay=500, seed=cid)
+    elif cid == 3:  # sparse: tuples jump over grid points by more than maxLateness at chunk cuts
+        cfg = dict(windows=[Tumbling(Time, 5), Sliding(Time, 40, 7)], aggs=[SUM, COUNT], lateness=2)
+        ts, vals = wl.stream(6000, 0.25, t0=1000, ooo_frac=0.1, max_delay=3, seed=cid)
+        ts = ts + np.cumsum(rng.integers(0, 4, size=len(ts)))
+        sched = interval_schedule(ts, 40, lag=5, pushes_per_interval=3)
+        return cfg, ts, vals, sched
     else:           # lateness edge skipping on jumps + fixed band
         cfg = dict(windows=[Tumbling(Time, 13), FixedBand(Time, 5000, 2000)], aggs=[SUM, MAX], lateness=3)
         ts, vals = wl.stream(120_000, 2, t0=7, ooo_frac=0.05, max_delay=2, seed=cid,

@@ -15,7 +15,7 @@ from shard_cases import case
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cid", [0, 1, 2])
+@pytest.mark.parametrize("cid", [0, 1, 2, 3])
 def test_two_rank_sharded_stream_matches_oracle(tmp_path, cid):
     out = str(tmp_path / "w.json")
     port = str(29500 + cid + (os.getpid() % 400))
