@@ -152,7 +152,9 @@ int scotty_enable_timing(scotty_op* op, int on);
 int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, uint64_t* tuples);
 
 /* Tuning knobs (not semantics): "slice_capacity" / "session_capacity" per operator of the exact engine
- * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only). */
+ * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only), "exact_serial"
+ * (non-keyed: single-wavefront replay, A/B only), "keyed_lane" 0 (keyed: wavefront-per-key replay instead of
+ * the lane-per-key path for context-free time windows, A/B only), "shard_cells" / "shard_cands". */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */

@@ -13,6 +13,9 @@ hipError_t launch_replay(const XBatchArgs& a, int vt, hipStream_t st);
 hipError_t launch_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st);
+hipError_t launch_lane_replay(const XBatchArgs& a, int vt, hipStream_t st);
+hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
+hipError_t launch_lane_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
 hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
 hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
@@ -632,7 +635,7 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
     a.retry = attempt > 0;
     a.sl = sl;
     a.ss = ss;
-    XCHK(launch_replay(a, vt, stream));
+    XCHK(lane_mode() ? launch_lane_replay(a, vt, stream) : launch_replay(a, vt, stream));
     XCHK(hipMemcpyAsync(h_misc, d_need, 16, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
     if (h_misc[0] == 0 && h_misc[1] == 0) return SCOTTY_OK;
@@ -692,7 +695,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.op_err = (int32_t*)(d_misc + 2);
   a.slot_key = keyed ? d_slot_key : nullptr;
   XCHK(hipMemsetAsync(d_misc, 0, 3 * 8, stream));
-  XCHK(launch_wm_count(a, stream));
+  XCHK(lane_mode() ? launch_lane_wm_count(a, stream) : launch_wm_count(a, stream));
   XCHK(launch_scan_i64(d_wcount, d_woff, n_ops, d_scan64, stream));
   XCHK(hipMemcpyAsync(h_misc, d_misc, 3 * 8, hipMemcpyDeviceToHost, stream));
   XCHK(hipMemcpyAsync(h_misc + 3, d_woff + n_ops - 1, 8, hipMemcpyDeviceToHost, stream));
@@ -733,7 +736,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
   a.w_key = d_w_key;
   a.n_rows = rows;
-  XCHK(launch_wm_emit(a, stream));
+  XCHK(lane_mode() ? launch_lane_wm_emit(a, stream) : launch_wm_emit(a, stream));
   XCHK(launch_wm_agg(a, stream));
   r.n = rows;
   r.d_start = d_w_start;

@@ -53,6 +53,10 @@ class XEngine {
   bool failed = false;
   int32_t sc_override = 0, sess_override = 0;
   bool serial = false;  // non-keyed: single-wavefront replay instead of the batch-parallel path (A/B)
+  bool lane_off = false;  // keyed: force the wavefront-per-key replay even where the lane path applies (A/B)
+  bool lane_mode() const {  // keyed_lane.hip: context-free time windows on Eager slices only
+    return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && cfg.n_cf > 0;
+  }
 
  private:
   void release();

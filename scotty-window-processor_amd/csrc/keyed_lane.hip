@@ -1,0 +1,389 @@
+// keyed_lane.hip -- one LANE per key: the keyed exact engine's fast path for operators whose windows are all
+// context-free time windows (Tumbling / Sliding / FixedBand) on Eager slices -- the Flink connector's common
+// case and BASELINE configs[3] (C4).  For this subset the reference's per-tuple work is a short scalar state
+// machine (StreamSlicer.determineSlices, S/StreamSlicer.java:36-116, and SliceManager.processElement,
+// S/SliceManager.java:47-87, without context-aware windows): a wavefront per key (exact_kernels.hip) spends
+// 64 lanes on it, here one lane walks a key's ~16 tuples of a micro-batch with the current slice's partials
+// held in registers.  The state layout (XState, slice SoA) is the exact engine's, so configurations can move
+// between the two paths mid-stream.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "exact_common.h"
+
+namespace scotty {
+namespace ln {
+
+constexpr int64_t JMAX = INT64_MAX, JMIN = INT64_MIN;
+constexpr int64_t ID_MIN = INT64_MAX;
+constexpr int64_t ID_MAX = INT64_MIN;
+
+__device__ __forceinline__ int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+__device__ __forceinline__ int64_t jsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+__device__ __forceinline__ int64_t jmod(int64_t a, int64_t b) { return b == -1 ? 0 : a % b; }
+__device__ __forceinline__ int64_t f64_key(double d) {
+  const int64_t b = __double_as_longlong(d);
+  return b ^ ((b >> 63) & 0x7FFFFFFFFFFFFFFFLL);
+}
+
+// assignNextWindowStart (TumblingWindow.java:29-31, SlidingWindow.java:41-43, FixedBandWindow.java:37-48)
+__device__ __forceinline__ int64_t assign_next(const XCfg* c, int w, int64_t t) {
+  const int k = c->cf_kind[w];
+  const int64_t a = c->cf_a[w], b = c->cf_b[w];
+  if (k == 0) return jsub(jadd(t, a), jmod(t, a));
+  if (k == 1) return jsub(jadd(t, b), jmod(t, b));
+  if (t == JMAX || t < a) return a;
+  if (t >= a && t < jadd(a, b)) return jadd(a, b);
+  return JMAX;
+}
+
+// one key's slice list, indices relative to the op's region
+struct Lane {
+  int64_t *ts, *te, *tl, *tf, *cs, *cl;
+  int32_t* ty;
+  unsigned long long *cnt, *p0, *p1, *p2;
+  const XCfg* c;
+  XState s;
+  int vt, need;
+  // register copy of the current (last) slice's aggregation fields
+  int ci;
+  int64_t c_ts, c_tl, c_tf, c_cl;
+  uint64_t c_cnt, c_p0;
+  int64_t c_p1, c_p2;
+  bool err_hang;
+
+  __device__ void bind(const XCfg* cfg, const XSlices& sl, int64_t op) {
+    c = cfg;
+    const int64_t b = op * (int64_t)cfg->sc;
+    ts = sl.ts + b; te = sl.te + b; tl = sl.tl + b; tf = sl.tf + b; cs = sl.cs + b; cl = sl.cl + b;
+    ty = sl.ty + b; cnt = sl.cnt + b; p0 = sl.p[0] + b; p1 = sl.p[1] + b; p2 = sl.p[2] + b;
+    vt = cfg->vt;
+    need = cfg->need;
+    ci = -1;
+    err_hang = false;
+  }
+  __device__ void load_cur() {
+    ci = s.tail - 1;
+    if (ci < s.head) {
+      ci = -1;
+      return;
+    }
+    c_ts = ts[ci]; c_tl = tl[ci]; c_tf = tf[ci]; c_cl = cl[ci];
+    c_cnt = cnt[ci]; c_p0 = p0[ci]; c_p1 = (int64_t)p1[ci]; c_p2 = (int64_t)p2[ci];
+  }
+  __device__ void flush_cur() {
+    if (ci < 0) return;
+    tl[ci] = c_tl; tf[ci] = c_tf; cl[ci] = c_cl;
+    cnt[ci] = c_cnt; p0[ci] = c_p0; p1[ci] = (unsigned long long)c_p1; p2[ci] = (unsigned long long)c_p2;
+  }
+  // calculateNextFixedEdge (S/StreamSlicer.java:103-116), time windows
+  __device__ int64_t next_fixed_edge(int64_t te_) {
+    const int64_t cur = s.nextEdgeTs == JMIN ? JMAX : s.nextEdgeTs;
+    const int64_t t_c = max(jsub(te_, c->max_lateness), cur);
+    int64_t e = JMAX;
+    for (int w = 0; w < c->n_cf; w++)
+      if (c->cf_measure[w] == 0) e = min(e, assign_next(c, w, t_c));
+    return e;
+  }
+  // SliceManager.appendSlice (S/SliceManager.java:27-38)
+  __device__ void append(int64_t start, int32_t type) {
+    if (ci >= 0) {
+      flush_cur();
+      te[ci] = start;
+      ty[ci] = type;
+    }
+    const int i = s.tail;
+    ts[i] = start; te[i] = JMAX; cs[i] = s.currentCount; ty[i] = 1;
+    s.tail++;
+    ci = i;
+    c_ts = start; c_tl = start; c_tf = JMAX; c_cl = s.currentCount;
+    c_cnt = 0; c_p0 = 0; c_p1 = ID_MIN; c_p2 = ID_MAX;
+  }
+  __device__ void lift(int64_t vb, uint64_t& sw, int64_t& mn, int64_t& mx) const {
+    sw = (uint64_t)vb;
+    if (vt == VT_F64) {
+      const double d = __longlong_as_double(vb);
+      mn = d != d ? INT64_MIN : f64_key(d);
+      mx = d != d ? INT64_MAX : f64_key(d);
+    } else {
+      mn = vb;
+      mx = vb;
+    }
+  }
+  __device__ void add_cur(int64_t t, int64_t vb) {
+    uint64_t sw;
+    int64_t mn, mx;
+    lift(vb, sw, mn, mx);
+    c_tl = max(c_tl, t);
+    c_tf = min(c_tf, t);
+    c_cl = jadd(c_cl, 1);
+    c_cnt++;
+    if (need & NEED_SUM) {
+      if (vt == VT_F64) c_p0 = (uint64_t)__double_as_longlong(__longlong_as_double((long long)c_p0) +
+                                                             __longlong_as_double((long long)sw));
+      else c_p0 += sw;
+    }
+    if (need & NEED_MIN) c_p1 = min(c_p1, mn);
+    if (need & NEED_MAX) c_p2 = max(c_p2, mx);
+  }
+  __device__ void add_mem(int i, int64_t t, int64_t vb) {
+    uint64_t sw;
+    int64_t mn, mx;
+    lift(vb, sw, mn, mx);
+    tl[i] = max(tl[i], t);
+    tf[i] = min(tf[i], t);
+    cl[i] = jadd(cl[i], 1);
+    cnt[i] = cnt[i] + 1;
+    if (need & NEED_SUM) {
+      if (vt == VT_F64) p0[i] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)p0[i]) +
+                                                                        __longlong_as_double((long long)sw));
+      else p0[i] = p0[i] + sw;
+    }
+    if (need & NEED_MIN) p1[i] = (unsigned long long)min((int64_t)p1[i], mn);
+    if (need & NEED_MAX) p2[i] = (unsigned long long)max((int64_t)p2[i], mx);
+  }
+  // LazyAggregateStore.findSliceIndexByTimestamp (:29-37) on a sorted list: last slice with tStart <= t
+  __device__ int find_ts(int64_t t) const {
+    int lo = s.head, hi = s.tail;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ts[mid] <= t) lo = mid + 1; else hi = mid;
+    }
+    return lo - 1 >= s.head ? lo - 1 : -1;
+  }
+  // SlicingWindowOperator.processElement (S/SlicingWindowOperator.java:41-44) for this subset
+  __device__ void process(int64_t t, int64_t vb) {
+    if (c->has_time && t >= s.maxEventTime) {  // StreamSlicer.determineSlices, in-order branch
+      if (c->has_fixed && s.nextEdgeTs == JMIN) s.nextEdgeTs = next_fixed_edge(t);
+      while (c->has_fixed && t > s.nextEdgeTs) {
+        if (s.nextEdgeTs >= 0) append(s.nextEdgeTs, XTYPE_FIXED);
+        s.nextEdgeTs = next_fixed_edge(t);
+        if (s.nextEdgeTs == JMIN) {  // the reference loops forever here (power-of-two size / slide)
+          err_hang = true;
+          return;
+        }
+      }
+      if (s.nextEdgeTs == t) {
+        append(t, XTYPE_FIXED);
+        s.nextEdgeTs = next_fixed_edge(t);
+      }
+    }
+    s.currentCount = jadd(s.currentCount, 1);
+    s.maxEventTime = max(t, s.maxEventTime);
+    if (s.tail <= s.head) append(0, 1);  // SliceManager.processElement: empty store (:49-51)
+    s.started = 1;
+    if (t >= c_tl) {
+      add_cur(t, vb);
+    } else {
+      const int idx = find_ts(t);
+      if (idx < 0) {
+        s.dropped++;  // IndexOutOfBoundsException in the reference: the tuple is lost
+      } else if (idx == ci) {
+        add_cur(t, vb);
+      } else {
+        add_mem(idx, t, vb);
+      }
+    }
+  }
+};
+
+template <int VT>
+__global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
+  const XCfg* cfg = a.cfg;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; op < a.n_ops; op += stride) {
+    const int64_t b0 = a.seg_begin[op], b1 = a.seg_end[op];
+    if (b1 <= b0) continue;
+    Lane L;
+    L.bind(cfg, a.sl, op);
+    L.s = a.st[op];
+    if (L.s.err) continue;
+    if (a.retry && !L.s.pending) continue;
+    L.s.pending = 0;
+    const unsigned char* rec = (const unsigned char*)a.ts;
+    auto load = [&](int64_t i, int64_t& t, int64_t& vb) {
+      const unsigned char* r = rec + i * a.rec_stride;
+      t = *(const int64_t*)r;
+      if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
+      else vb = *(const int64_t*)(r + 8);
+    };
+    // capacity pre-check (same bound as the wavefront replay): defer the key, the host grows and retries
+    int64_t tmin = JMAX, tmax = JMIN;
+    for (int64_t i = b0; i < b1; i++) {
+      int64_t t, vb;
+      load(i, t, vb);
+      tmin = min(tmin, t);
+      tmax = max(tmax, t);
+    }
+    int64_t from = L.s.started ? max(L.s.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
+    if (from > tmax) from = tmax;
+    const double span = (double)tmax - (double)from;
+    double bound = 4.0;
+    for (int w = 0; w < cfg->n_cf; w++) {
+      const int k = cfg->cf_kind[w];
+      bound += k == 2 ? 2.0 : span / (double)(k == 0 ? cfg->cf_a[w] : cfg->cf_b[w]) + 2.0;
+    }
+    const double need_s = (double)(L.s.tail - L.s.head) + bound;
+    if (need_s > (double)cfg->sc) {
+      atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
+      L.s.pending = 1;
+      a.st[op] = L.s;
+      continue;
+    }
+    if ((double)L.s.tail + bound > (double)cfg->sc && L.s.head > 0) {  // compact [head, tail) to the front
+      const int n = L.s.tail - L.s.head, h = L.s.head;
+      for (int i = 0; i < n; i++) {
+        L.ts[i] = L.ts[h + i]; L.te[i] = L.te[h + i]; L.tl[i] = L.tl[h + i]; L.tf[i] = L.tf[h + i];
+        L.cs[i] = L.cs[h + i]; L.cl[i] = L.cl[h + i]; L.ty[i] = L.ty[h + i]; L.cnt[i] = L.cnt[h + i];
+        L.p0[i] = L.p0[h + i]; L.p1[i] = L.p1[h + i]; L.p2[i] = L.p2[h + i];
+      }
+      L.s.head = 0;
+      L.s.tail = n;
+    }
+    L.load_cur();
+    if (L.ci < 0) L.c_tl = JMIN;  // empty store: the first tuple appends
+    for (int64_t i = b0; i < b1 && !L.err_hang; i++) {
+      int64_t t, vb;
+      load(i, t, vb);
+      L.process(t, vb);
+    }
+    L.flush_cur();
+    if (L.err_hang) L.s.err = XERR_HANG;
+    a.st[op] = L.s;
+  }
+}
+
+// ---------------------------------------------------------------- watermark, one lane per key
+// Triggered context-free time windows of one key (S/WindowManager.java:104-118, C/windowType/*.triggerWindows)
+template <bool EMIT>
+__device__ int64_t lane_triggers(const XCfg* c, int64_t last, int64_t wm, int64_t* w_start, int64_t* w_end,
+                                 int32_t* w_meas, int32_t* w_op, int64_t off, int32_t op, int64_t& minTs,
+                                 int64_t& maxTs) {
+  int64_t k = 0;
+  auto emit = [&](int64_t st, int64_t en) {
+    if (EMIT) {
+      w_start[off + k] = st;
+      w_end[off + k] = en;
+      w_meas[off + k] = 0;
+      w_op[off + k] = op;
+    }
+    minTs = min(minTs, st);
+    maxTs = max(maxTs, en);
+    k++;
+  };
+  for (int w = 0; w < c->n_cf; w++) {
+    const int kind = c->cf_kind[w];
+    const int64_t a = c->cf_a[w], b = c->cf_b[w];
+    if (kind == 0) {
+      const int64_t ls = jsub(last, jmod(jadd(last, a), a));
+      for (int64_t ws = ls; jadd(ws, a) <= wm; ws = jadd(ws, a)) emit(ws, jadd(ws, a));
+    } else if (kind == 1) {
+      const int64_t ls = jsub(wm, jmod(jadd(wm, b), b));
+      for (int64_t ws = ls; jadd(ws, a) > last; ws = jsub(ws, b))
+        if (ws >= 0 && jadd(ws, a) <= jadd(wm, 1)) emit(ws, jadd(ws, a));
+    } else {
+      const int64_t e = jadd(a, b);
+      if (last <= e && e <= wm) emit(a, e);
+    }
+  }
+  return k;
+}
+
+__global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
+  const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (op >= a.n_ops) return;
+  const XState s = a.st[op];
+  if (s.dropped) atomicAdd(a.dropped_total, (unsigned long long)s.dropped);
+  if (s.err) atomicOr(a.op_err, 1 << s.err);
+  int64_t k = 0;
+  if (!s.err && s.tail > s.head) {
+    int64_t last = s.lastWatermark == -1 ? max((int64_t)0, jsub(a.wm, a.cfg->max_lateness)) : s.lastWatermark;
+    const int64_t oldest = a.sl.ts[op * (int64_t)a.cfg->sc + s.head];
+    if (last < oldest) last = oldest;
+    int64_t mn = JMAX, mx = 0;
+    k = lane_triggers<false>(a.cfg, last, a.wm, nullptr, nullptr, nullptr, nullptr, 0, 0, mn, mx);
+  }
+  a.wcount[op] = k;
+}
+
+__global__ __launch_bounds__(256) void lane_wm_emit_kernel(XWmArgs a) {
+  const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (op >= a.n_ops) return;
+  XState s = a.st[op];
+  if (s.err) return;
+  const XCfg* c = a.cfg;
+  if (s.lastWatermark == -1) s.lastWatermark = max((int64_t)0, jsub(a.wm, c->max_lateness));  // :43-44
+  if (s.tail <= s.head) {
+    s.lastWatermark = a.wm;
+    a.st[op] = s;
+    return;
+  }
+  const int64_t base = op * (int64_t)c->sc;
+  const int64_t* ts = a.sl.ts + base;
+  const int64_t* cs = a.sl.cs + base;
+  if (s.lastWatermark < ts[s.head]) s.lastWatermark = ts[s.head];
+  int64_t minTs = JMAX, maxTs = 0;
+  const int64_t k = lane_triggers<true>(c, s.lastWatermark, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, a.woff[op],
+                                        (int32_t)op, minTs, maxTs);
+  auto find_ts = [&](int64_t t) {
+    int lo = s.head, hi = s.tail;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (ts[mid] <= t) lo = mid + 1; else hi = mid;
+    }
+    return lo - 1 >= s.head ? lo - 1 : -1;
+  };
+  auto find_count = [&](int64_t cc) {
+    int lo = s.head, hi = s.tail;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cs[mid] <= cc) lo = mid + 1; else hi = mid;
+    }
+    return lo - 1 >= s.head ? lo - 1 : -1;
+  };
+  if (k > 0) {  // LazyAggregateStore.aggregate scan range (:83-90); no count windows: minCount = currentCount
+    const int S = s.tail - s.head;
+    auto rel = [&](int i) { return i < 0 ? -1 : i - s.head; };
+    int si = max(rel(find_ts(minTs)), 0);
+    si = min(si, rel(find_count(s.currentCount)));
+    int ei = min(S - 1, rel(find_ts(maxTs)));
+    ei = max(ei, rel(find_count(0)));
+    if (si < 0 && si <= ei) {
+      atomicOr(a.err_flag, 2);
+      si = 0;
+    }
+    s.wlo = s.head + si;
+    s.whi = s.head + ei + 1;
+  } else {
+    s.wlo = s.whi = s.head;
+  }
+  s.lastWatermark = a.wm;
+  s.lastCount = s.currentCount;
+  const int64_t t = jsub(jsub(a.wm, c->max_lateness), c->max_fixed);  // clearAfterWatermark (:82-95)
+  const int idx = find_ts(t);
+  if (idx > s.head) s.head = idx;
+  a.st[op] = s;
+}
+
+}  // namespace ln
+
+hipError_t launch_lane_replay(const XBatchArgs& a, int vt, hipStream_t st) {
+  if (a.n_ops <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((a.n_ops + 255) / 256, 65536);
+  if (vt == VT_I32) hipLaunchKernelGGL(ln::lane_replay_kernel<VT_I32>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (vt == VT_I64) hipLaunchKernelGGL(ln::lane_replay_kernel<VT_I64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ln::lane_replay_kernel<VT_F64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st) {
+  if (a.n_ops <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ln::lane_wm_count_kernel, dim3((unsigned)((a.n_ops + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_lane_wm_emit(const XWmArgs& a, hipStream_t st) {
+  if (a.n_ops <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ln::lane_wm_emit_kernel, dim3((unsigned)((a.n_ops + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace scotty

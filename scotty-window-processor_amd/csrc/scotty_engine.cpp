@@ -134,6 +134,7 @@ struct scotty_op {
   XEngine* x = nullptr;
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
+  bool x_lane_off = false;
   uint64_t x_pushed = 0;
   std::vector<uint32_t> r_key;
   // sharded grid path (scotty_shard_*)
@@ -720,6 +721,7 @@ static int decide_mode(scotty_op* op) {
   op->x->sc_override = op->x_sc;
   op->x->sess_override = op->x_sess;
   op->x->serial = op->x_serial;
+  op->x->lane_off = op->x_lane_off;
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
   if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
@@ -1117,6 +1119,11 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (std::strcmp(key, "exact_serial") == 0) {
     if (op->mode != 0) return SCOTTY_ERR_ARG;
     op->x_serial = value != 0;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "keyed_lane") == 0) {  // 0: wavefront-per-key replay even where the lane path applies
+    if (op->mode != 0) return SCOTTY_ERR_ARG;
+    op->x_lane_off = value == 0;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "slice_capacity") == 0 || std::strcmp(key, "session_capacity") == 0) {

@@ -198,7 +198,10 @@ def test_keyed_streams_match_per_key_oracles(pkg, seed):
     else:
         wins = []
         for _ in range(int(rng.integers(1, 4))):
-            if rng.random() < 0.5:
+            r = rng.random()
+            if r < 0.1:
+                wins.append(FixedBand(Time, int(rng.integers(0, 3000)), int(rng.integers(1, 2000))))
+            elif r < 0.5:
                 wins.append(Tumbling(Time, _nz(int(rng.integers(5, 200)))))
             else:
                 size = int(rng.integers(10, 300))
@@ -213,6 +216,54 @@ def test_keyed_streams_match_per_key_oracles(pkg, seed):
                               pushes_per_interval=int(rng.integers(1, 3)))
     f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
     _keyed_run(pkg, cfg, keys, ts, vals, sched, vt=vt, f64_cols=f64_cols)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_keyed_lane_path_equals_wavefront_replay(pkg, seed):
+    """Context-free time windows on Eager slices run lane-per-key (keyed_lane.hip); the wavefront-per-key
+    replay (exact_kernels.hip, tune "keyed_lane" 0) must leave the same rows -- larger streams and key counts
+    than the oracle comparisons, out-of-order tuples, drops and slice GC."""
+    rng = np.random.default_rng(6100 + seed)
+    vt = ["i32", "i64", "f64", "i32"][seed % 4]
+    vtc = {"i32": pkg.VALUE_I32, "i64": pkg.VALUE_I64, "f64": pkg.VALUE_F64}[vt]
+    wins = [Sliding(Time, int(rng.integers(200, 3000)), _nz(int(rng.integers(20, 200)))),
+            Tumbling(Time, _nz(int(rng.integers(30, 500))))][:1 + seed % 2]
+    if seed % 3 == 1:
+        wins.append(FixedBand(Time, int(rng.integers(0, 5000)), int(rng.integers(100, 5000))))
+    aggs = _aggs(rng, vt)
+    n = 300_000
+    ts, vals = product().workloads.stream(n, [1, 4, 20][seed % 3], t0=int(rng.integers(0, 1000)),
+                                          ooo_frac=[0.0, 0.3][seed % 2], max_delay=int(rng.integers(1, 400)),
+                                          seed=seed, value_type=vt)
+    nkeys = [10, 2_000, 30_000][seed % 3]
+    keys = rng.integers(0, nkeys, size=n).astype(np.uint32)
+    lateness = int(rng.choice([1, 50, 500]))
+    ops = []
+    for lane in (1, 0):
+        op = pkg.KeyedSlicingWindowOperator(device=0, value_type=vtc)
+        op.tune("keyed_lane", lane)
+        for a in aggs:
+            op.addWindowFunction(a)
+        op.setMaxLateness(lateness)
+        for w in wins:
+            op.addWindowAssigner(w)
+        ops.append(op)
+    f64_cols = [i for i, a in enumerate(aggs) if a == SUM_F64]
+    sched = interval_schedule(ts, 12, lag=int(rng.integers(0, 300)), pushes_per_interval=2)
+    total = 0
+    for step in sched:
+        if step[0] == "push":
+            if step[2] > step[1]:
+                for op in ops:
+                    op.processElements(keys[step[1]:step[2]], ts[step[1]:step[2]], vals[step[1]:step[2]])
+        else:
+            a, b = ops[0].processWatermark(step[1]), ops[1].processWatermark(step[1])
+            exp = {}
+            for k, w in b:
+                exp.setdefault(k, []).append(w)
+            total += same_keyed_windows(a, exp, f64_cols=f64_cols)
+            assert ops[0].droppedCount() == ops[1].droppedCount()
+    assert total > 0
 
 
 def test_keyed_config4_reduced(pkg):
