@@ -100,7 +100,7 @@ def extra_c3(pkg, dev, batch, steps):
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
 
 
-def extra_c4(pkg, dev, batch, keys, steps):
+def extra_c4(pkg, dev, batch, keys, steps, lane=True):
     """BASELINE configs[3] (C4), one GPU's shard: SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys,
     maxLateness 1 (Flink connector default); 61 s of warm-up so every step emits each key's window."""
     import torch
@@ -108,6 +108,8 @@ def extra_c4(pkg, dev, batch, keys, steps):
     g = torch.Generator(device=dev)
     g.manual_seed(42)
     op = pkg.KeyedSlicingWindowOperator(device=dev.index)
+    if not lane:
+        op.tune("keyed_lane", 0)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.setMaxLateness(1)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))

@@ -12,20 +12,21 @@ namespace scotty {
 hipError_t launch_replay(const XBatchArgs& a, int vt, hipStream_t st);
 hipError_t launch_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
-hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st);
-hipError_t launch_lane_replay(const XBatchArgs& a, int vt, hipStream_t st);
+hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group);
+hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st);
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
 hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
 hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
-                             uint32_t* new_pos, unsigned long long* new_count, int32_t* full, hipStream_t st);
+                             uint32_t* new_pos, unsigned long long* new_count, int32_t* full, uint32_t* slot,
+                             hipStream_t st);
 hipError_t launch_key_assign(unsigned long long* table, const uint32_t* new_pos, int64_t n_new, int64_t base,
                              uint32_t* slot_key, hipStream_t st);
 hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask,
                          hipStream_t st);
 hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
-                       uint32_t* slot, hipStream_t st);
+                       uint32_t* slot, bool fixup, hipStream_t st);
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
                                void** result, hipStream_t st);
@@ -581,7 +582,7 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
   // 1. new keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator()))
   XCHK(hipMemsetAsync(d_newcnt, 0, 8, stream));
   XCHK(hipMemsetAsync(d_full, 0, 4, stream));
-  XCHK(launch_key_insert(d_key, n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, stream));
+  XCHK(launch_key_insert(d_key, n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, d_slot, stream));
   XCHK(hipMemcpyAsync(h_misc, d_newcnt, 8, hipMemcpyDeviceToHost, stream));
   XCHK(hipMemcpyAsync(h_misc + 1, d_full, 4, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
@@ -604,8 +605,8 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
       if (rc) return rc;
     }
   }
-  // 2. per-tuple slot, stable sort by slot (arrival order kept within each key), segments
-  XCHK(launch_slot(d_key, n, d_table, tcap - 1, d_slot, stream));
+  // 2. slots of the tuples whose key was new, stable sort by slot (arrival order kept within each key), segments
+  if (n_new > 0) XCHK(launch_slot(d_key, n, d_table, tcap - 1, d_slot, true, stream));
   const int rec = vt == VT_I32 ? 16 : 24;
   void* sorted = nullptr;
   XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_slot, n, bits_for(n_ops), d_recA, d_recB, d_hist, d_scan32, &sorted,
@@ -635,7 +636,7 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
     a.retry = attempt > 0;
     a.sl = sl;
     a.ss = ss;
-    XCHK(lane_mode() ? launch_lane_replay(a, vt, stream) : launch_replay(a, vt, stream));
+    XCHK(lane_mode() ? launch_lane_replay(a, cfg, stream) : launch_replay(a, vt, stream));
     XCHK(hipMemcpyAsync(h_misc, d_need, 16, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
     if (h_misc[0] == 0 && h_misc[1] == 0) return SCOTTY_OK;
@@ -737,7 +738,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.w_key = d_w_key;
   a.n_rows = rows;
   XCHK(lane_mode() ? launch_lane_wm_emit(a, stream) : launch_wm_emit(a, stream));
-  XCHK(launch_wm_agg(a, stream));
+  XCHK(launch_wm_agg(a, stream, keyed ? 16 : 64));
   r.n = rows;
   r.d_start = d_w_start;
   r.d_end = d_w_end;

@@ -408,10 +408,18 @@ __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
   if (lane == 0) a.st[op] = o.s;
 }
 
-// one wave per emitted window: AggregateWindowState.containsSlice/addState over the op's scan range
+// G lanes per emitted window (G = 64: one wavefront; G = 16: four windows per wavefront, for the many short
+// scan ranges of keyed operators): AggregateWindowState.containsSlice/addState over the op's scan range
+template <int G, typename T, typename F>
+__device__ __forceinline__ T greduce(T v, F f) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v = f(v, (T)__shfl_xor(v, o));
+  return v;
+}
+template <int G>
 __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t wi = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   if (wi >= a.n_rows) return;
   const int64_t op = a.w_op[wi];
   const XState& st = a.st[op];
@@ -421,7 +429,9 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   int64_t lo = st.wlo, hi = st.whi;
   if (lo < 0) lo = 0;
   const int64_t* key = tmeas ? a.sl.ts + base : a.sl.cs + base;
-  if (!(st.unsorted & 3) || !tmeas) {  // narrow to start keys in [ws, we] (contained slices satisfy it)
+  // narrow to start keys in [ws, we] (contained slices satisfy it); a range of a few group widths is
+  // cheaper to scan than to bisect (the bisection is a chain of dependent loads)
+  if ((!(st.unsorted & 3) || !tmeas) && hi - lo > 4 * G) {
     int64_t l = lo, h = hi;
     while (l < h) {
       int64_t m = (l + h) >> 1;
@@ -440,7 +450,7 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   uint64_t cnt = 0, sw = 0;
   double sf = 0.0;
   int64_t mn = ID_MIN, mx = ID_MAX;
-  for (int64_t i = lo + lane; i < hi; i += 64) {
+  for (int64_t i = lo + lane; i < hi; i += G) {
     const int64_t s = base + i;
     const bool contains = tmeas ? (ws <= a.sl.ts[s] && we > a.sl.tl[s]) : (ws <= a.sl.cs[s] && we >= a.sl.cl[s]);
     if (!contains) continue;
@@ -454,11 +464,16 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
     if (need & NEED_MIN) mn = min(mn, (int64_t)a.sl.p[1][s]);
     if (need & NEED_MAX) mx = max(mx, (int64_t)a.sl.p[2][s]);
   }
-  cnt = wsum(cnt);
-  if (vt == VT_F64) sf = wsumf(sf);
-  else sw = wsum(sw);
-  mn = wmin(mn);
-  mx = wmax(mx);
+  auto add_u = [](unsigned long long x, unsigned long long y) { return x + y; };
+  auto min_i = [](long long x, long long y) { return x < y ? x : y; };
+  auto max_i = [](long long x, long long y) { return x > y ? x : y; };
+  cnt = greduce<G>((unsigned long long)cnt, add_u);
+  if (need & NEED_SUM) {
+    if (vt == VT_F64) sf = greduce<G>(sf, [](double x, double y) { return x + y; });
+    else sw = greduce<G>((unsigned long long)sw, add_u);
+  }
+  if (need & NEED_MIN) mn = greduce<G>((long long)mn, min_i);
+  if (need & NEED_MAX) mx = greduce<G>((long long)mx, max_i);
   if (lane == 0) {
     a.has_value[wi] = cnt ? 1 : 0;
     if (a.w_key) a.w_key[wi] = a.slot_key ? a.slot_key[op] : (uint32_t)op;
@@ -508,9 +523,12 @@ hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint3
   hipLaunchKernelGGL(x::xstate_init_kernel, dim3((unsigned)blocks), dim3(256), 0, st, st_, from, to, slot_key);
   return hipGetLastError();
 }
-hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st) {
+hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group) {
   if (a.n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(x::wm_agg_kernel, dim3((unsigned)((a.n_rows + 3) / 4)), dim3(256), 0, st, a);
+  if (group == 16)
+    hipLaunchKernelGGL(x::wm_agg_kernel<16>, dim3((unsigned)((a.n_rows + 15) / 16)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(x::wm_agg_kernel<64>, dim3((unsigned)((a.n_rows + 3) / 4)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

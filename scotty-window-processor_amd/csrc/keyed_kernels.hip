@@ -37,13 +37,19 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {  // murmur3 finaliser
 // ---------------------------------------------------------------- hash table
 // entry: (key+1) << 32 | slot; 0 = empty; slot 0xFFFFFFFF = inserted in this batch, slot not yet assigned
 __global__ void key_insert_kernel(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
-                                  uint32_t* new_pos, unsigned long long* new_count, int32_t* full) {
+                                  uint32_t* new_pos, unsigned long long* new_count, int32_t* full, uint32_t* slot) {
+  // also records each tuple's slot when its key already has one (0xFFFFFFFF: key new in this batch, fixed up by
+  // slot_kernel<true> after key_assign) -- in the steady state of a keyed stream one probe pass does both
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t tag = ((uint64_t)keys[i] + 1) << 32;
     uint64_t h = hash32(keys[i]) & mask;
+    uint32_t sl = 0xFFFFFFFFu;
     for (uint64_t probe = 0; probe <= mask; probe++) {
       unsigned long long e = table[h];
-      if ((e & 0xFFFFFFFF00000000ull) == tag) break;
+      if ((e & 0xFFFFFFFF00000000ull) == tag) {
+        sl = (uint32_t)e;
+        break;
+      }
       if (e == 0) {
         const unsigned long long prev = atomicCAS(&table[h], 0ull, (unsigned long long)(tag | 0xFFFFFFFFull));
         if (prev == 0) {
@@ -56,6 +62,7 @@ __global__ void key_insert_kernel(const uint32_t* keys, int64_t n, unsigned long
       h = (h + 1) & mask;
       if (probe == mask) atomicOr(full, 1);
     }
+    slot[i] = sl;
   }
 }
 
@@ -80,9 +87,11 @@ __global__ void rehash_kernel(const unsigned long long* old_t, uint64_t old_n, u
   }
 }
 
+template <bool FIXUP>
 __global__ void slot_kernel(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
                             uint32_t* slot) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (FIXUP && slot[i] != 0xFFFFFFFFu) continue;
     const uint64_t tag = ((uint64_t)keys[i] + 1) << 32;
     uint64_t h = hash32(keys[i]) & mask;
     unsigned long long e;
@@ -123,6 +132,41 @@ __device__ __forceinline__ Rec<REC> make_rec(const int64_t* ts, const void* val,
   return r;
 }
 
+// Register image of a record as plain 32-bit words (a packed struct copy would be lowered through scratch)
+template <int REC>
+struct RV;
+template <>
+struct RV<16> {
+  uint4 a;
+  __device__ uint32_t slot() const { return a.w; }
+  __device__ static RV load(const void* p, int64_t i) { return RV{((const uint4*)p)[i]}; }
+  __device__ void store(void* p, int64_t i) const { ((uint4*)p)[i] = a; }
+  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i) {
+    const uint64_t t = (uint64_t)ts[i];
+    return RV{make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)((const int32_t*)val)[i], slot[i])};
+  }
+};
+template <>
+struct RV<24> {
+  uint2 a, b, c;
+  __device__ uint32_t slot() const { return c.x; }
+  __device__ static RV load(const void* p, int64_t i) {
+    const uint2* q = (const uint2*)p + 3 * i;
+    return RV{q[0], q[1], q[2]};
+  }
+  __device__ void store(void* p, int64_t i) const {
+    uint2* q = (uint2*)p + 3 * i;
+    q[0] = a;
+    q[1] = b;
+    q[2] = c;
+  }
+  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i) {
+    const uint64_t t = (uint64_t)ts[i], v = (uint64_t)((const int64_t*)val)[i];
+    return RV{make_uint2((uint32_t)t, (uint32_t)(t >> 32)), make_uint2((uint32_t)v, (uint32_t)(v >> 32)),
+              make_uint2(slot[i], 0u)};
+  }
+};
+
 // FIRST: input is SoA (ts, val, slot arrays); else AoS records
 template <int REC, bool FIRST>
 __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>* in, const int64_t* ts,
@@ -145,90 +189,83 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>
   for (int d = tid; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = cnt[d];
 }
 
+// Stable scatter of one tile.  Each wavefront ranks its own contiguous 512-record sub-tile against
+// wave-private digit counters in LDS (8 ballots per record, no block barrier between rounds); one barrier
+// then turns the per-wave counts into tile positions.  Arrival order inside the tile = (wave, round, lane).
 template <int REC, bool FIRST>
 __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<REC>* in, const int64_t* ts,
                                                                       const void* val, const uint32_t* slot,
                                                                       int64_t n, int shift, const int32_t* offs,
                                                                       int64_t nblocks, Rec<REC>* out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  Rec<REC>* stage = (Rec<REC>*)smem;                                       // [SORT_TILE]
-  int32_t* wc = (int32_t*)(smem + sizeof(Rec<REC>) * SORT_TILE);          // [4][RADIX]
-  int32_t* run = wc + 4 * RADIX;                                           // [RADIX]
-  int32_t* tstart = run + RADIX;                                           // [RADIX] tile digit starts
+  void* stage = smem;                                                      // [SORT_TILE] records
+  int32_t* wc = (int32_t*)(smem + sizeof(Rec<REC>) * SORT_TILE);          // [4][RADIX] per-wave counters
+  int32_t* tot = wc + 4 * RADIX;                                           // [4] wave partial sums (scan)
+  int32_t* tstart = tot + RADIX;                                           // [RADIX] tile digit starts
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
-  for (int d = tid; d < RADIX; d += SORT_THREADS) {
-    run[d] = 0;
-    tstart[d] = 0;
-  }
-  __syncthreads();
-  // load (striped: item r of thread t is element r*256+t, i.e. arrival order = (r, wave, lane))
-  Rec<REC> item[SORT_ITEMS];
-  int32_t dig[SORT_ITEMS];
-#pragma unroll
-  for (int r = 0; r < SORT_ITEMS; r++) {
-    const int64_t i = base + r * SORT_THREADS + tid;
-    if (i < n) {
-      item[r] = FIRST ? make_rec<REC>(ts, val, slot, i) : in[i];
-      dig[r] = (item[r].slot >> shift) & (RADIX - 1);
-      atomicAdd(&tstart[dig[r]], 1);
-    } else {
-      dig[r] = -1;
-    }
-  }
-  __syncthreads();
-  // exclusive scan of the tile's digit counts (RADIX == SORT_THREADS)
-  {
-    const int32_t v = tstart[tid];
-    int32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t u = __shfl_up(inc, o);
-      if (lane >= o) inc += u;
-    }
-    if (lane == 63) wc[wid] = inc;
-    __syncthreads();
-    int32_t add = 0;
-    for (int w = 0; w < wid; w++) add += wc[w];
-    __syncthreads();
-    tstart[tid] = inc - v + add;
-  }
+  constexpr int WAVE_ITEMS = SORT_ITEMS * 64;
   for (int d = tid; d < 4 * RADIX; d += SORT_THREADS) wc[d] = 0;
   __syncthreads();
-  // stable ranking, round by round
+  RV<REC> item[SORT_ITEMS];
+  int32_t dig[SORT_ITEMS], rank[SORT_ITEMS];
+  int32_t* mine = wc + wid * RADIX;
+  const unsigned long long lt = (1ull << lane) - 1;
 #pragma unroll
   for (int r = 0; r < SORT_ITEMS; r++) {
-    const int d = dig[r];
+    const int64_t i = base + wid * WAVE_ITEMS + r * 64 + lane;
+    int d = -1;
+    if (i < n) {
+      item[r] = FIRST ? RV<REC>::make(ts, val, slot, i) : RV<REC>::load(in, i);
+      d = (item[r].slot() >> shift) & (RADIX - 1);
+    }
+    dig[r] = d;
     unsigned long long peers = __ballot(d >= 0);
 #pragma unroll
     for (int b = 0; b < RB; b++) {
       const unsigned long long bb = __ballot(d >= 0 && ((d >> b) & 1));
       peers &= ((d >> b) & 1) ? bb : ~bb;
     }
-    const int rank = __popcll(peers & ((1ull << lane) - 1));
-    const bool leader = d >= 0 && rank == 0;
-    if (leader) wc[wid * RADIX + d] = __popcll(peers);
-    __syncthreads();
-    if (d >= 0) {
-      int32_t pos = tstart[d] + run[d] + rank;
-      for (int w = 0; w < wid; w++) pos += wc[w * RADIX + d];
-      stage[pos] = item[r];
-    }
-    __syncthreads();
-    {
-      const int dd = tid;  // RADIX == SORT_THREADS
-      run[dd] += wc[dd] + wc[RADIX + dd] + wc[2 * RADIX + dd] + wc[3 * RADIX + dd];
-      wc[dd] = wc[RADIX + dd] = wc[2 * RADIX + dd] = wc[3 * RADIX + dd] = 0;
-    }
-    __syncthreads();
+    const int before = d >= 0 ? mine[d] : 0;
+    rank[r] = before + __popcll(peers & lt);
+    __builtin_amdgcn_wave_barrier();
+    if (d >= 0 && (peers & lt) == 0) mine[d] = before + __popcll(peers);
+    __builtin_amdgcn_wave_barrier();
   }
+  __syncthreads();
+  // digit tid: per-wave exclusive offsets and the tile's exclusive digit scan (RADIX == SORT_THREADS)
+  {
+    const int32_t c0 = wc[tid], c1 = wc[RADIX + tid], c2 = wc[2 * RADIX + tid], c3 = wc[3 * RADIX + tid];
+    const int32_t v = c0 + c1 + c2 + c3;
+    int32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) tot[wid] = inc;
+    __syncthreads();
+    int32_t add = 0;
+    for (int w = 0; w < wid; w++) add += tot[w];
+    const int32_t st0 = inc - v + add;
+    tstart[tid] = st0;
+    wc[tid] = st0;
+    wc[RADIX + tid] = st0 + c0;
+    wc[2 * RADIX + tid] = st0 + c0 + c1;
+    wc[3 * RADIX + tid] = st0 + c0 + c1 + c2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < SORT_ITEMS; r++)
+    if (dig[r] >= 0) item[r].store(stage, mine[dig[r]] + rank[r]);
+  __syncthreads();
   // write out per-digit runs
   const int64_t cnt_tile = min((int64_t)SORT_TILE, n - base);
   for (int i = tid; i < cnt_tile; i += SORT_THREADS) {
-    const Rec<REC> rr = stage[i];
-    const int d = (rr.slot >> shift) & (RADIX - 1);
+    const RV<REC> rr = RV<REC>::load(stage, i);
+    const int d = (rr.slot() >> shift) & (RADIX - 1);
     const int64_t g = (int64_t)offs[(int64_t)d * nblocks + blockIdx.x] + (i - tstart[d]);
-    out[g] = rr;
+    rr.store(out, g);
   }
 }
 
@@ -295,10 +332,11 @@ hipError_t launch_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* 
 static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
 
 hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
-                             uint32_t* new_pos, unsigned long long* new_count, int32_t* full, hipStream_t st) {
+                             uint32_t* new_pos, unsigned long long* new_count, int32_t* full, uint32_t* slot,
+                             hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k::key_insert_kernel, dim3(grid_for(n)), dim3(256), 0, st, keys, n, table, mask, new_pos,
-                     new_count, full);
+                     new_count, full, slot);
   return hipGetLastError();
 }
 hipError_t launch_key_assign(unsigned long long* table, const uint32_t* new_pos, int64_t n_new, int64_t base,
@@ -314,9 +352,10 @@ hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsign
   return hipGetLastError();
 }
 hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
-                       uint32_t* slot, hipStream_t st) {
+                       uint32_t* slot, bool fixup, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k::slot_kernel, dim3(grid_for(n)), dim3(256), 0, st, keys, n, table, mask, slot);
+  if (fixup) hipLaunchKernelGGL(k::slot_kernel<true>, dim3(grid_for(n)), dim3(256), 0, st, keys, n, table, mask, slot);
+  else hipLaunchKernelGGL(k::slot_kernel<false>, dim3(grid_for(n)), dim3(256), 0, st, keys, n, table, mask, slot);
   return hipGetLastError();
 }
 

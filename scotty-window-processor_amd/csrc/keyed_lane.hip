@@ -37,71 +37,75 @@ __device__ __forceinline__ int64_t assign_next(const XCfg* c, int w, int64_t t) 
   return JMAX;
 }
 
-// one key's slice list, indices relative to the op's region
+// One key's slice list.  The slice columns are the kernel argument's (uniform, SGPRs); a lane holds only its
+// key's base offset, the StreamSlicer / store scalars it changes, and the current slice's aggregation fields
+// (VGPR budget: the kernel is latency bound, occupancy is what hides the per-key record and slice loads).
+// MM: the operator has a MIN or MAX aggregation (partials p[1] / p[2] live).
+template <int VT, bool MM>
 struct Lane {
-  int64_t *ts, *te, *tl, *tf, *cs, *cl;
-  int32_t* ty;
-  unsigned long long *cnt, *p0, *p1, *p2;
   const XCfg* c;
-  XState s;
-  int vt, need;
-  // register copy of the current (last) slice's aggregation fields
-  int ci;
-  int64_t c_ts, c_tl, c_tf, c_cl;
+  XSlices sl;
+  int64_t b;  // op * sc
+  // XState fields the per-tuple path changes
+  int64_t maxEventTime, nextEdgeTs, currentCount;
+  int32_t head, tail, started;
+  uint32_t dropped;
+  // register copy of the current (last) slice
+  int32_t ci;
+  int64_t c_tl, c_tf, c_cl;
   uint64_t c_cnt, c_p0;
   int64_t c_p1, c_p2;
-  bool err_hang;
+  bool hang;
 
-  __device__ void bind(const XCfg* cfg, const XSlices& sl, int64_t op) {
-    c = cfg;
-    const int64_t b = op * (int64_t)cfg->sc;
-    ts = sl.ts + b; te = sl.te + b; tl = sl.tl + b; tf = sl.tf + b; cs = sl.cs + b; cl = sl.cl + b;
-    ty = sl.ty + b; cnt = sl.cnt + b; p0 = sl.p[0] + b; p1 = sl.p[1] + b; p2 = sl.p[2] + b;
-    vt = cfg->vt;
-    need = cfg->need;
-    ci = -1;
-    err_hang = false;
-  }
   __device__ void load_cur() {
-    ci = s.tail - 1;
-    if (ci < s.head) {
+    ci = tail - 1;
+    if (ci < head) {
       ci = -1;
+      c_tl = JMIN;  // empty store: the first tuple appends
       return;
     }
-    c_ts = ts[ci]; c_tl = tl[ci]; c_tf = tf[ci]; c_cl = cl[ci];
-    c_cnt = cnt[ci]; c_p0 = p0[ci]; c_p1 = (int64_t)p1[ci]; c_p2 = (int64_t)p2[ci];
+    const int64_t j = b + ci;
+    c_tl = sl.tl[j]; c_tf = sl.tf[j]; c_cl = sl.cl[j];
+    c_cnt = sl.cnt[j]; c_p0 = sl.p[0][j];
+    if (MM) {
+      c_p1 = (int64_t)sl.p[1][j];
+      c_p2 = (int64_t)sl.p[2][j];
+    }
   }
   __device__ void flush_cur() {
     if (ci < 0) return;
-    tl[ci] = c_tl; tf[ci] = c_tf; cl[ci] = c_cl;
-    cnt[ci] = c_cnt; p0[ci] = c_p0; p1[ci] = (unsigned long long)c_p1; p2[ci] = (unsigned long long)c_p2;
+    const int64_t j = b + ci;
+    sl.tl[j] = c_tl; sl.tf[j] = c_tf; sl.cl[j] = c_cl;
+    sl.cnt[j] = c_cnt; sl.p[0][j] = c_p0;
+    if (MM) {
+      sl.p[1][j] = (unsigned long long)c_p1;
+      sl.p[2][j] = (unsigned long long)c_p2;
+    }
   }
   // calculateNextFixedEdge (S/StreamSlicer.java:103-116), time windows
-  __device__ int64_t next_fixed_edge(int64_t te_) {
-    const int64_t cur = s.nextEdgeTs == JMIN ? JMAX : s.nextEdgeTs;
+  __device__ int64_t next_fixed_edge(int64_t te_) const {
+    const int64_t cur = nextEdgeTs == JMIN ? JMAX : nextEdgeTs;
     const int64_t t_c = max(jsub(te_, c->max_lateness), cur);
     int64_t e = JMAX;
-    for (int w = 0; w < c->n_cf; w++)
-      if (c->cf_measure[w] == 0) e = min(e, assign_next(c, w, t_c));
+    for (int w = 0; w < c->n_cf; w++) e = min(e, assign_next(c, w, t_c));  // all time-measured here
     return e;
   }
-  // SliceManager.appendSlice (S/SliceManager.java:27-38)
+  // SliceManager.appendSlice (S/SliceManager.java:27-38); a new slice starts Flexible(1), empty
   __device__ void append(int64_t start, int32_t type) {
     if (ci >= 0) {
       flush_cur();
-      te[ci] = start;
-      ty[ci] = type;
+      sl.te[b + ci] = start;
+      sl.ty[b + ci] = type;
     }
-    const int i = s.tail;
-    ts[i] = start; te[i] = JMAX; cs[i] = s.currentCount; ty[i] = 1;
-    s.tail++;
-    ci = i;
-    c_ts = start; c_tl = start; c_tf = JMAX; c_cl = s.currentCount;
+    const int64_t j = b + tail;
+    sl.ts[j] = start; sl.te[j] = JMAX; sl.cs[j] = currentCount; sl.ty[j] = 1;
+    ci = tail;
+    tail++;
+    c_tl = start; c_tf = JMAX; c_cl = currentCount;
     c_cnt = 0; c_p0 = 0; c_p1 = ID_MIN; c_p2 = ID_MAX;
   }
-  __device__ void lift(int64_t vb, uint64_t& sw, int64_t& mn, int64_t& mx) const {
-    sw = (uint64_t)vb;
-    if (vt == VT_F64) {
+  __device__ static void lift(int64_t vb, int64_t& mn, int64_t& mx) {
+    if (VT == VT_F64) {
       const double d = __longlong_as_double(vb);
       mn = d != d ? INT64_MIN : f64_key(d);
       mx = d != d ? INT64_MAX : f64_key(d);
@@ -110,147 +114,161 @@ struct Lane {
       mx = vb;
     }
   }
+  __device__ static uint64_t add_sum(uint64_t acc, int64_t vb) {
+    if (VT == VT_F64)
+      return (uint64_t)__double_as_longlong(__longlong_as_double((long long)acc) + __longlong_as_double(vb));
+    return acc + (uint64_t)vb;
+  }
+  // AbstractSlice.addElement + AggregateState.addElement on the current slice (registers)
   __device__ void add_cur(int64_t t, int64_t vb) {
-    uint64_t sw;
-    int64_t mn, mx;
-    lift(vb, sw, mn, mx);
     c_tl = max(c_tl, t);
     c_tf = min(c_tf, t);
     c_cl = jadd(c_cl, 1);
     c_cnt++;
-    if (need & NEED_SUM) {
-      if (vt == VT_F64) c_p0 = (uint64_t)__double_as_longlong(__longlong_as_double((long long)c_p0) +
-                                                             __longlong_as_double((long long)sw));
-      else c_p0 += sw;
+    if (c->need & NEED_SUM) c_p0 = add_sum(c_p0, vb);
+    if (MM) {
+      int64_t mn, mx;
+      lift(vb, mn, mx);
+      c_p1 = min(c_p1, mn);
+      c_p2 = max(c_p2, mx);
     }
-    if (need & NEED_MIN) c_p1 = min(c_p1, mn);
-    if (need & NEED_MAX) c_p2 = max(c_p2, mx);
   }
+  // ... on an older slice (out-of-order tuple), in HBM
   __device__ void add_mem(int i, int64_t t, int64_t vb) {
-    uint64_t sw;
-    int64_t mn, mx;
-    lift(vb, sw, mn, mx);
-    tl[i] = max(tl[i], t);
-    tf[i] = min(tf[i], t);
-    cl[i] = jadd(cl[i], 1);
-    cnt[i] = cnt[i] + 1;
-    if (need & NEED_SUM) {
-      if (vt == VT_F64) p0[i] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)p0[i]) +
-                                                                        __longlong_as_double((long long)sw));
-      else p0[i] = p0[i] + sw;
+    const int64_t j = b + i;
+    sl.tl[j] = max(sl.tl[j], t);
+    sl.tf[j] = min(sl.tf[j], t);
+    sl.cl[j] = jadd(sl.cl[j], 1);
+    sl.cnt[j] = sl.cnt[j] + 1;
+    if (c->need & NEED_SUM) sl.p[0][j] = add_sum(sl.p[0][j], vb);
+    if (MM) {
+      int64_t mn, mx;
+      lift(vb, mn, mx);
+      sl.p[1][j] = (unsigned long long)min((int64_t)sl.p[1][j], mn);
+      sl.p[2][j] = (unsigned long long)max((int64_t)sl.p[2][j], mx);
     }
-    if (need & NEED_MIN) p1[i] = (unsigned long long)min((int64_t)p1[i], mn);
-    if (need & NEED_MAX) p2[i] = (unsigned long long)max((int64_t)p2[i], mx);
   }
   // LazyAggregateStore.findSliceIndexByTimestamp (:29-37) on a sorted list: last slice with tStart <= t
   __device__ int find_ts(int64_t t) const {
-    int lo = s.head, hi = s.tail;
+    int lo = head, hi = tail;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (ts[mid] <= t) lo = mid + 1; else hi = mid;
+      if (sl.ts[b + mid] <= t) lo = mid + 1; else hi = mid;
     }
-    return lo - 1 >= s.head ? lo - 1 : -1;
+    return lo - 1 >= head ? lo - 1 : -1;
   }
   // SlicingWindowOperator.processElement (S/SlicingWindowOperator.java:41-44) for this subset
   __device__ void process(int64_t t, int64_t vb) {
-    if (c->has_time && t >= s.maxEventTime) {  // StreamSlicer.determineSlices, in-order branch
-      if (c->has_fixed && s.nextEdgeTs == JMIN) s.nextEdgeTs = next_fixed_edge(t);
-      while (c->has_fixed && t > s.nextEdgeTs) {
-        if (s.nextEdgeTs >= 0) append(s.nextEdgeTs, XTYPE_FIXED);
-        s.nextEdgeTs = next_fixed_edge(t);
-        if (s.nextEdgeTs == JMIN) {  // the reference loops forever here (power-of-two size / slide)
-          err_hang = true;
+    if (t >= maxEventTime) {  // StreamSlicer.determineSlices, in-order branch (:51-86)
+      if (nextEdgeTs == JMIN) nextEdgeTs = next_fixed_edge(t);
+      while (t > nextEdgeTs) {
+        if (nextEdgeTs >= 0) append(nextEdgeTs, XTYPE_FIXED);
+        nextEdgeTs = next_fixed_edge(t);
+        if (nextEdgeTs == JMIN) {  // the reference loops forever here (power-of-two size / slide)
+          hang = true;
           return;
         }
       }
-      if (s.nextEdgeTs == t) {
+      if (nextEdgeTs == t) {
         append(t, XTYPE_FIXED);
-        s.nextEdgeTs = next_fixed_edge(t);
+        nextEdgeTs = next_fixed_edge(t);
       }
     }
-    s.currentCount = jadd(s.currentCount, 1);
-    s.maxEventTime = max(t, s.maxEventTime);
-    if (s.tail <= s.head) append(0, 1);  // SliceManager.processElement: empty store (:49-51)
-    s.started = 1;
+    currentCount = jadd(currentCount, 1);  // WindowManager.incrementCount
+    maxEventTime = max(t, maxEventTime);
+    if (tail <= head) append(0, 1);  // SliceManager.processElement: empty store (:49-51)
+    started = 1;
     if (t >= c_tl) {
       add_cur(t, vb);
     } else {
       const int idx = find_ts(t);
-      if (idx < 0) {
-        s.dropped++;  // IndexOutOfBoundsException in the reference: the tuple is lost
-      } else if (idx == ci) {
-        add_cur(t, vb);
-      } else {
-        add_mem(idx, t, vb);
-      }
+      if (idx < 0) dropped++;  // IndexOutOfBoundsException in the reference: the tuple is lost
+      else if (idx == ci) add_cur(t, vb);
+      else add_mem(idx, t, vb);
     }
   }
 };
 
-template <int VT>
+template <int VT, bool MM>
 __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
   const XCfg* cfg = a.cfg;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; op < a.n_ops; op += stride) {
-    const int64_t b0 = a.seg_begin[op], b1 = a.seg_end[op];
-    if (b1 <= b0) continue;
-    Lane L;
-    L.bind(cfg, a.sl, op);
-    L.s = a.st[op];
-    if (L.s.err) continue;
-    if (a.retry && !L.s.pending) continue;
-    L.s.pending = 0;
-    const unsigned char* rec = (const unsigned char*)a.ts;
-    auto load = [&](int64_t i, int64_t& t, int64_t& vb) {
-      const unsigned char* r = rec + i * a.rec_stride;
-      t = *(const int64_t*)r;
-      if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
-      else vb = *(const int64_t*)(r + 8);
-    };
-    // capacity pre-check (same bound as the wavefront replay): defer the key, the host grows and retries
-    int64_t tmin = JMAX, tmax = JMIN;
-    for (int64_t i = b0; i < b1; i++) {
-      int64_t t, vb;
-      load(i, t, vb);
-      tmin = min(tmin, t);
-      tmax = max(tmax, t);
-    }
-    int64_t from = L.s.started ? max(L.s.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
-    if (from > tmax) from = tmax;
-    const double span = (double)tmax - (double)from;
-    double bound = 4.0;
-    for (int w = 0; w < cfg->n_cf; w++) {
-      const int k = cfg->cf_kind[w];
-      bound += k == 2 ? 2.0 : span / (double)(k == 0 ? cfg->cf_a[w] : cfg->cf_b[w]) + 2.0;
-    }
-    const double need_s = (double)(L.s.tail - L.s.head) + bound;
-    if (need_s > (double)cfg->sc) {
-      atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
-      L.s.pending = 1;
-      a.st[op] = L.s;
-      continue;
-    }
-    if ((double)L.s.tail + bound > (double)cfg->sc && L.s.head > 0) {  // compact [head, tail) to the front
-      const int n = L.s.tail - L.s.head, h = L.s.head;
-      for (int i = 0; i < n; i++) {
-        L.ts[i] = L.ts[h + i]; L.te[i] = L.te[h + i]; L.tl[i] = L.tl[h + i]; L.tf[i] = L.tf[h + i];
-        L.cs[i] = L.cs[h + i]; L.cl[i] = L.cl[h + i]; L.ty[i] = L.ty[h + i]; L.cnt[i] = L.cnt[h + i];
-        L.p0[i] = L.p0[h + i]; L.p1[i] = L.p1[h + i]; L.p2[i] = L.p2[h + i];
-      }
-      L.s.head = 0;
-      L.s.tail = n;
-    }
-    L.load_cur();
-    if (L.ci < 0) L.c_tl = JMIN;  // empty store: the first tuple appends
-    for (int64_t i = b0; i < b1 && !L.err_hang; i++) {
-      int64_t t, vb;
-      load(i, t, vb);
-      L.process(t, vb);
-    }
-    L.flush_cur();
-    if (L.err_hang) L.s.err = XERR_HANG;
-    a.st[op] = L.s;
+  const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (op >= a.n_ops) return;
+  const int64_t b0 = a.seg_begin[op], b1 = a.seg_end[op];
+  if (b1 <= b0) return;
+  XState* sp = a.st + op;
+  if (sp->err) return;
+  if (a.retry && !sp->pending) return;
+  const unsigned char* rec = (const unsigned char*)a.ts;
+  auto load = [&](int64_t i, int64_t& t, int64_t& vb) {
+    const unsigned char* r = rec + i * a.rec_stride;
+    t = *(const int64_t*)r;
+    if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
+    else vb = *(const int64_t*)(r + 8);
+  };
+  Lane<VT, MM> L;
+  L.c = cfg;
+  L.sl = a.sl;
+  L.b = op * (int64_t)cfg->sc;
+  L.maxEventTime = sp->maxEventTime;
+  L.nextEdgeTs = sp->nextEdgeTs;
+  L.currentCount = sp->currentCount;
+  L.head = sp->head;
+  L.tail = sp->tail;
+  L.started = sp->started;
+  L.dropped = 0;
+  L.hang = false;
+  // capacity pre-check (same bound as the wavefront replay): defer the key, the host grows and retries
+  int64_t tmin = JMAX, tmax = JMIN;
+  for (int64_t i = b0; i < b1; i++) {
+    int64_t t, vb;
+    load(i, t, vb);
+    tmin = min(tmin, t);
+    tmax = max(tmax, t);
   }
+  int64_t from = L.started ? max(L.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
+  if (from > tmax) from = tmax;
+  const double span = (double)tmax - (double)from;
+  double bound = 4.0;
+  for (int w = 0; w < cfg->n_cf; w++) {
+    const int k = cfg->cf_kind[w];
+    bound += k == 2 ? 2.0 : span / (double)(k == 0 ? cfg->cf_a[w] : cfg->cf_b[w]) + 2.0;
+  }
+  const double need_s = (double)(L.tail - L.head) + bound;
+  if (need_s > (double)cfg->sc) {
+    atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
+    sp->pending = 1;
+    return;
+  }
+  sp->pending = 0;
+  if ((double)L.tail + bound > (double)cfg->sc && L.head > 0) {  // compact [head, tail) to the front
+    const int n = L.tail - L.head;
+    const int64_t h = L.b + L.head, d = L.b;
+    const XSlices& q = a.sl;
+    for (int i = 0; i < n; i++) {
+      q.ts[d + i] = q.ts[h + i]; q.te[d + i] = q.te[h + i]; q.tl[d + i] = q.tl[h + i]; q.tf[d + i] = q.tf[h + i];
+      q.cs[d + i] = q.cs[h + i]; q.cl[d + i] = q.cl[h + i]; q.ty[d + i] = q.ty[h + i];
+      q.cnt[d + i] = q.cnt[h + i];
+      for (int p = 0; p < NPART; p++) q.p[p][d + i] = q.p[p][h + i];
+    }
+    L.head = 0;
+    L.tail = n;
+  }
+  L.load_cur();
+  for (int64_t i = b0; i < b1 && !L.hang; i++) {
+    int64_t t, vb;
+    load(i, t, vb);
+    L.process(t, vb);
+  }
+  L.flush_cur();
+  sp->maxEventTime = L.maxEventTime;
+  sp->nextEdgeTs = L.nextEdgeTs;
+  sp->currentCount = L.currentCount;
+  sp->head = L.head;
+  sp->tail = L.tail;
+  sp->started = L.started;
+  if (L.dropped) sp->dropped += L.dropped;
+  if (L.hang) sp->err = XERR_HANG;
 }
 
 // ---------------------------------------------------------------- watermark, one lane per key
@@ -367,12 +385,16 @@ __global__ __launch_bounds__(256) void lane_wm_emit_kernel(XWmArgs a) {
 
 }  // namespace ln
 
-hipError_t launch_lane_replay(const XBatchArgs& a, int vt, hipStream_t st) {
+hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
-  const int64_t blocks = std::min<int64_t>((a.n_ops + 255) / 256, 65536);
-  if (vt == VT_I32) hipLaunchKernelGGL(ln::lane_replay_kernel<VT_I32>, dim3((unsigned)blocks), dim3(256), 0, st, a);
-  else if (vt == VT_I64) hipLaunchKernelGGL(ln::lane_replay_kernel<VT_I64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(ln::lane_replay_kernel<VT_F64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
+  const bool mm = (host_cfg.need & (NEED_MIN | NEED_MAX)) != 0;
+  const int vt = host_cfg.vt;
+#define SCOTTY_LANE(V, M) hipLaunchKernelGGL((ln::lane_replay_kernel<V, M>), grid, block, 0, st, a)
+  if (vt == VT_I32) { if (mm) SCOTTY_LANE(VT_I32, true); else SCOTTY_LANE(VT_I32, false); }
+  else if (vt == VT_I64) { if (mm) SCOTTY_LANE(VT_I64, true); else SCOTTY_LANE(VT_I64, false); }
+  else { if (mm) SCOTTY_LANE(VT_F64, true); else SCOTTY_LANE(VT_F64, false); }
+#undef SCOTTY_LANE
   return hipGetLastError();
 }
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st) {
