@@ -64,10 +64,12 @@ def cpu_baseline(sizes, rate_per_ms, budget_s=12.0):
                                                                                     rate_per_ms, k)}
 
 
-def extra_c3(pkg, dev, batch, steps):
+def extra_c3(pkg, dev, batch, steps, warm=61):
     """BASELINE configs[2] (C3): SlidingWindow(60 s, 60 ms) + SessionWindow(1 s gap), MIN_I32 + MAX_I32, 20 %
     out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; exact engine
-    (exact_batch.hip).  Inputs resident in HBM; results stay in HBM (processWatermarkDevice)."""
+    (exact_batch.hip).  Every 10 s of event time the stream pauses for 1.5 s, so sessions close
+    (BenchmarkRunner.generateSessionGaps-like).  61 s of warm-up: every timed step emits its sliding windows.
+    Inputs resident in HBM; results stay in HBM (processWatermarkDevice)."""
     import torch
     rate = max(1, batch // 1000)
     g = torch.Generator(device=dev)
@@ -79,25 +81,84 @@ def extra_c3(pkg, dev, batch, steps):
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 60))
     op.addWindowAssigner(pkg.SessionWindow(pkg.WindowMeasure.Time, 1000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    times, rows, events = [], 0, 0
+    for s in range(warm + steps):
+        t_begin = s * 1000 + 1000 + (s // 10) * 1500
+        ts = base + t_begin
+        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        d = torch.randint(1, 501, (batch,), device=dev, generator=g)
+        ts = torch.where(late, torch.clamp(ts - d, min=t_begin - 500), ts).contiguous()
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(t_begin + (batch - 1) // rate - 500)
+        torch.cuda.synchronize(dev)
+        if s >= warm:
+            times.append(time.perf_counter() - t0)
+            rows += n
+    return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
+                        "(delay U[1,500] ms), lag 500 ms, 1.5 s pause every 10 s, non-keyed, exact engine",
+            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
+
+
+def c2s_windows(pkg):
+    """1000 concurrent sliding windows: sizes BenchmarkRunner.randomTumbling(1000,1,20) (java.util.Random(10)),
+    slide = size/20 (50..1000 ms; a power-of-two slide is bumped by 1 ms, as the reference would hang on it)."""
+    out = []
+    for size in pkg.workloads.random_tumbling_sizes(1000, 1, 20, seed=10):
+        slide = max(1, size // 20)
+        if slide & (slide - 1) == 0:
+            slide += 1
+        out.append((size, slide))
+    return out
+
+
+def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None):
+    """north_star target workload: 1000 concurrent sliding windows (c2s_windows), SUM_I32 + COUNT, 20 %
+    out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; grid path.  Warm-up until the
+    largest window (20 s) has been emitted, so every timed step assembles a full set of windows."""
+    import torch
+    rate = max(1, batch // 1000)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    op = pkg.SlicingWindowOperator(device=dev.index)
+    for k, v in (tune or {}).items():
+        op.tune(k, v)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.addWindowFunction(pkg.AGG_COUNT)
+    op.setMaxLateness(1000)
+    for size, slide in c2s_windows(pkg):
+        op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, size, slide))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     times, rows = [], 0
-    for s in range(steps + 2):
+    op.enableTiming(True)
+    for s in range(warm + steps):
         ts = base + s * 1000 + 1000
         late = torch.rand(batch, device=dev, generator=g) < 0.2
         d = torch.randint(1, 501, (batch,), device=dev, generator=g)
         ts = torch.where(late, torch.clamp(ts - d, min=1), ts).contiguous()
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        if s == warm:
+            op.enableTiming(False)
+            op.enableTiming(True)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
-        n, _ = op.processWatermarkDevice(s * 1000 + 1000 + (batch - 1) // rate - 500)
+        n, _ = op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
         torch.cuda.synchronize(dev)
-        if s >= 2:  # the first batch builds the store (first-tuple edge walk, session start)
+        if s >= warm:
             times.append(time.perf_counter() - t0)
             rows += n
-    return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
-                        "(delay U[1,500] ms), lag 500 ms, non-keyed, exact engine",
+    ingest_ms, launches, _ = op.ingestTiming()
+    avg_ms = ingest_ms / max(1, launches)
+    achieved = batch * BYTES_PER_TUPLE / (avg_ms * 1e-3) / 1e9
+    return {"workload": "C2s: 1000 concurrent sliding windows, sizes randomTumbling(1000,1,20) Random(10), slide "
+                        "size/20, SUM_I32+COUNT, 20% out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
-            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
+            "ingest": {"avg_launch_ms": avg_ms, "achieved_GBs": achieved, "frac": achieved / HBM_PEAK_GBS}}
 
 
 def extra_c4(pkg, dev, batch, keys, steps, lane=True):
@@ -256,7 +317,8 @@ def main():
         if not args.no_extra and world == 1:
             del batches
             torch.cuda.empty_cache()
-            res["extra"] = {"c3": extra_c3(pkg, dev, 1 << 26, 5), "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5)}
+            res["extra"] = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
+                            "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5)}
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(sizes, rate)
         print(json.dumps(res), flush=True)

@@ -14,6 +14,8 @@ namespace scotty {
 constexpr int TILE_MIN = 4096;    // tuples per arrival-order tile (tilemax granularity), power of two
 constexpr int NT_MAX = 8192;      // tiles per micro-batch held in the commit kernel's LDS
 constexpr int WCAP = 1024;        // cells in a workgroup's LDS window
+constexpr int64_t CIX_CAP = 1 << 20;  // entries of the cell index (ts bucket -> first cell), see cix_build_kernel
+constexpr int LCIX = 2048;        // cell-index entries staged in LDS for a workgroup's window
 constexpr int NPART = 3;          // partial slots per slice/cell: 0 sum, 1 min, 2 max
 
 enum : int { VT_I32 = 0, VT_I64 = 1, VT_F64 = 2 };
@@ -54,6 +56,9 @@ struct IngestArgs {
   DevMeta* meta;
   int64_t per_wave;          // tuples per wave (multiple of tile)
   int64_t tile;              // tuples per tile (power of two >= TILE_MIN, nT <= NT_MAX)
+  // cell index (built per push by cix_build_kernel): cix[k] = cell of ts cix_meta[0] + (k << cix_meta[1])
+  uint32_t* cix;
+  int64_t* cix_meta;         // [base, shift, n]
 };
 
 struct CommitArgs {

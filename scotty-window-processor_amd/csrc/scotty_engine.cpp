@@ -21,6 +21,7 @@
 
 namespace scotty {
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
+hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_windows(const WindowArgs& a, hipStream_t st);
 hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st);
@@ -99,6 +100,8 @@ struct scotty_op {
   long long* d_ctmax = nullptr;
   unsigned long long* d_cpart[NPART] = {};
   long long* d_tilemax = nullptr;
+  uint32_t* d_cix = nullptr;      // cell index (slicing_kernels.hip cix_build_kernel)
+  int64_t* d_cixmeta = nullptr;
   long long* d_pmax = nullptr;
   int32_t* d_rank = nullptr;
   int32_t* d_flag = nullptr;
@@ -125,6 +128,7 @@ struct scotty_op {
   uint64_t dropped = 0, processed = 0;
 
   int ingest_mode = -1;  // tuning knob (scotty_tune), -1 = default variant
+  int64_t ingest_blocks = 1024;  // tuning knob: target workgroups of the ingest launch (~4 per CU)
 
   // ---- engine selection: the grid path (context-free time windows, non-keyed) or the exact engine
   //      (keyed ops, session windows, count windows); decided at the first push
@@ -420,11 +424,18 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   for (int k = 0; k < NPART; k++) ia.c_part[k] = op->d_cpart[k];
   ia.tilemax = op->d_tilemax;
   ia.meta = op->d_meta;
+  if (!op->d_cix) {
+    HIPCHK(hipMalloc(&op->d_cix, CIX_CAP * 4));
+    HIPCHK(hipMalloc(&op->d_cixmeta, 4 * 8));
+  }
+  ia.cix = op->d_cix;
+  ia.cix_meta = op->d_cixmeta;
+  HIPCHK(launch_cix_build(ia, op->stream));
   // tile: power of two >= TILE_MIN with at most NT_MAX tiles (the commit kernel keeps them in LDS)
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
   // ~4 workgroups per CU on 256 CUs; each wave streams a tile-aligned contiguous range
-  const int64_t target_blocks = 1024;
+  const int64_t target_blocks = op->ingest_blocks;
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
   per_wave = ((per_wave + tile - 1) / tile) * tile;
   if (per_wave < tile) per_wave = tile;
@@ -628,7 +639,7 @@ void scotty_destroy(scotty_op* op) {
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
-  F(op->d_shrank); F(op->d_shflag);
+  F(op->d_shrank); F(op->d_shflag); F(op->d_cix); F(op->d_cixmeta);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
 }
@@ -1107,6 +1118,11 @@ int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, ui
 // Tuning knobs (include/scotty_mi355x.h): capacities of the exact engine, grid ingest variant.
 int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (!op || !key) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "ingest_blocks") == 0) {
+    if (value < 1 || value > (1 << 20)) return SCOTTY_ERR_ARG;
+    op->ingest_blocks = value;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "ingest_mode") == 0) {
     op->ingest_mode = (int)value;
     return SCOTTY_OK;

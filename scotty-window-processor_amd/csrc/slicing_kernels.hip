@@ -106,6 +106,61 @@ struct CellView {
   }
 };
 
+// Cell index: cix[k] = last cell with start <= base + (k << shift), built once per push over the whole cell
+// range [first cell start, horizon end) (cix_build_kernel).  A lookup is one load plus at most one compare when
+// shift == 0 (cell starts are distinct integers), instead of a ~16-step binary search through HBM / L2.
+struct CellIndex {
+  const uint32_t* cix;
+  int64_t base, n, ctot;
+  int shift;
+  // largest c with start(c) <= t; requires start(0) <= t (and t < h_end when the horizon is finite)
+  __device__ __forceinline__ int64_t find(const CellView& cv, int64_t t) const {
+    const uint64_t k = (uint64_t)(t - base) >> shift;
+    if (k >= (uint64_t)n) return ctot - 1;
+    int64_t lo = cix[k];
+    int64_t hi = k + 1 < (uint64_t)n ? (int64_t)cix[k + 1] + 1 : ctot;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cv.start(mid) <= t) lo = mid; else hi = mid;
+    }
+    return lo;
+  }
+};
+
+__global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
+  const DevMeta& m = *a.meta;
+  if (m.overflow != 0) return;
+  const int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
+  int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+  if (kc < 0) kc = 0;
+  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
+  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+  const int64_t ctot = cv.c_old + kc;
+  if (ctot <= 0) return;
+  const int64_t first = cv.start(0);
+  const int64_t span_end = h_end != INT64_MAX ? h_end : cv.start(ctot - 1) + 1;
+  const uint64_t span = (uint64_t)(span_end - first);
+  // about four buckets per cell: dense enough that a lookup rarely needs more than one compare, sparse enough
+  // that building it is O(cells) even when a few cells span most of the range
+  const uint64_t target = (uint64_t)min(CIX_CAP, max((int64_t)4096, 4 * ctot));
+  int shift = 0;
+  while ((span >> shift) >= target) shift++;
+  const int64_t n = (int64_t)(span >> shift) + 1;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) {
+    a.cix_meta[0] = first;
+    a.cix_meta[1] = shift;
+    a.cix_meta[2] = n;
+  }
+  // thread per cell: cell c owns the buckets whose point first + (k << shift) lies in [start(c), start(c+1))
+  const uint64_t round = ((uint64_t)1 << shift) - 1;
+  for (int64_t c = g; c < ctot; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k0 = c == 0 ? 0 : (int64_t)(((uint64_t)(cv.start(c) - first) + round) >> shift);
+    const int64_t k1 = c + 1 == ctot ? n : min(n, (int64_t)(((uint64_t)(cv.start(c + 1) - first) + round) >> shift));
+    for (int64_t k = k0; k < k1; k++) a.cix[k] = (uint32_t)c;
+  }
+}
+
 template <int VT>
 struct ValT;
 template <> struct ValT<VT_I32> { using T = int32_t; };
@@ -207,6 +262,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       w.part[k] = nullptr;
     }
   }
+  uint16_t* lcix = (uint16_t*)p;  // [LCIX] cell index entries of the window, relative to wbase
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -234,13 +290,32 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     sc[0] = m.overflow;
     sc[1] = head; sc[2] = tail; sc[3] = j0; sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
     sc[7] = wbase; sc[8] = wn;
+    const int64_t cbase = a.cix_meta[0], cshift = a.cix_meta[1], cn = a.cix_meta[2];
+    const int64_t twa = cv.start(wbase), twb = cv.start(wbase + wn);
+    // stage the cell index for the most recent part of the window (out-of-order tuples are mostly recent)
+    int64_t k0 = (int64_t)((uint64_t)(twa - cbase) >> cshift);
+    const int64_t kl = (int64_t)((uint64_t)(twb - 1 - cbase) >> cshift);
+    if (twb != INT64_MAX && kl + 2 - k0 > LCIX) k0 = kl + 2 - LCIX;
+    sc[9] = cbase; sc[10] = cshift; sc[11] = cn; sc[12] = k0;
+    sc[13] = (twb != INT64_MAX && twb > twa) ? kl - k0 + 2 : 0;  // staged entries (0: LDS binary search)
+    sc[14] = ctot;
   }
   __syncthreads();
   if (sc[0] != 0) return;  // an earlier push of this interval overflowed: nothing is committed until replay
-  const int64_t head = sc[1], tail = sc[2], j0 = sc[3], kc = sc[4], h_end = sc[5], first_start = sc[6];
-  const int64_t wbase = sc[7], wn = sc[8];
+  // block-uniform scalars: readfirstlane keeps them in SGPRs (an LDS load alone yields VGPRs)
+  const int64_t head = uni64(sc[1]), tail = uni64(sc[2]), j0 = uni64(sc[3]), kc = uni64(sc[4]);
+  const int64_t h_end = uni64(sc[5]), first_start = uni64(sc[6]);
+  const int64_t wbase = uni64(sc[7]), wn = uni64(sc[8]);
   const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+  const CellIndex cx{a.cix, uni64(sc[9]), uni64(sc[11]), uni64(sc[14]), (int)uni64(sc[10])};
+  const int64_t lk0 = uni64(sc[12]), lcn = uni64(sc[13]);
   for (int64_t i = tid; i <= wn; i += 256) w.tw[i] = cv.start(wbase + i);
+  for (int64_t i = tid; i < lcn; i += 256) {
+    const int64_t kk = lk0 + i;
+    int64_t v = kk < cx.n ? (int64_t)cx.cix[kk] : cx.ctot - 1;
+    v = min(max(v - wbase, (int64_t)0), wn - 1);
+    lcix[i] = (uint16_t)v;
+  }
   for (int64_t i = tid; i < wn; i += 256) {
     w.cnt[i] = 0;
     w.tmax[i] = INT64_MIN;
@@ -249,7 +324,21 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     if (NEED & NEED_MAX) w.part[2][i] = (unsigned long long)PART_ID_MAX;
   }
   __syncthreads();
-  const int64_t tw0 = w.tw[0], twn = w.tw[wn];
+  const int64_t tw0 = uni64(w.tw[0]), twn = uni64(w.tw[wn]);
+  // window cell of t (tw0 <= t < twn): staged cell index, else binary search over the window's starts
+  auto wfind = [&](int64_t t) -> int64_t {
+    int64_t l = 0, h = wn;
+    const int64_t i = (int64_t)((uint64_t)(t - cx.base) >> cx.shift) - lk0;
+    if (i >= 0 && i + 1 < lcn) {
+      l = lcix[i];
+      h = (int64_t)lcix[i + 1] + 1;
+    }
+    while (h - l > 1) {
+      int64_t mid = (l + h) >> 1;
+      if (w.tw[mid] <= t) l = mid; else h = mid;
+    }
+    return l;
+  };
 
   const int64_t w0 = b0 + (int64_t)wid * a.per_wave;
   const int64_t w1 = min(b1, w0 + a.per_wave);
@@ -286,19 +375,16 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     } else if (t >= h_end && h_end != INT64_MAX) {
       n_ovf++;
     } else if (t >= tw0 && t < twn) {
-      int64_t l = 0, h = wn;
-      while (h - l > 1) {
-        int64_t mid = (l + h) >> 1;
-        if (w.tw[mid] <= t) l = mid; else h = mid;
-      }
+      const int64_t l = (MODE & 8) ? 0 : wfind(t);  // MODE bits 2/3: timing probes only (wrong results)
       Acc<VT, NEED> one;
       one.reset();
       one.add(t, v);
       const uint64_t sw = one.sum_word();
       const double sf = one.sum_f();
-      lds_add<VT, NEED>(w, l, 1u, t, sw, sf, one.mn, one.mx);
+      if (!(MODE & 4)) lds_add<VT, NEED>(w, l, 1u, t, sw, sf, one.mn, one.mx);
+      else if (l == 12345678) w.cnt[0] = (uint32_t)sw;
     } else {
-      int64_t c = cv.find(t);
+      const int64_t c = cx.find(cv, t);
       Acc<VT, NEED> one;
       one.reset();
       one.add(t, v);
@@ -354,16 +440,12 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       flush();
       int64_t c;
       if (x >= tw0 && x < twn) {
-        int64_t l = 0, h = wn;
-        while (h - l > 1) {
-          int64_t mid = (l + h) >> 1;
-          if (w.tw[mid] <= x) l = mid; else h = mid;
-        }
+        const int64_t l = wfind(x);
         c = wbase + l;
         lo = w.tw[l];
         hi = w.tw[l + 1];
       } else {
-        c = cv.find(x);
+        c = cx.find(cv, x);
         lo = cv.start(c);
         hi = cv.start(c + 1);
       }
@@ -371,11 +453,19 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       lo = uni64(lo);
       hi = uni64(hi);
     }
+    uint32_t sm = 0;  // tuples outside the wave's current cell take the slow path, one code copy for all four
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       tile_max = max(tile_max, t[j]);
       if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
-      else slow(t[j], v[j]);
+      else sm |= 1u << j;
+    }
+    while (sm) {
+      const int j = __builtin_ctz(sm);
+      sm &= sm - 1;
+      const int64_t tj = j == 0 ? t[0] : j == 1 ? t[1] : j == 2 ? t[2] : t[3];
+      const V vj = j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+      slow(tj, vj);
     }
   };
   auto tile_done = [&](int64_t s) {
@@ -1058,7 +1148,7 @@ __global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
 // ---------------------------------------------------------------- host-side launch wrappers
 template <int VT, int NEED, int MODE>
 static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStream_t st) {
-  size_t lds = 128 + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP;
+  size_t lds = 128 + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP + 2 * LCIX;
   for (int k = 0; k < NPART; k++)
     if (NEED & (1 << k)) lds += 8 * WCAP;
   hipLaunchKernelGGL((ingest_kernel<VT, NEED, MODE>), dim3((unsigned)nblocks), dim3(256), lds, st, a);
@@ -1082,13 +1172,21 @@ static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblock
 }
 
 // mode < 0: default; mode 0..3 selects a variant for the (int32, SUM) configuration (A/B tuning)
+hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(cix_build_kernel, dim3(256), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode) {
   if (mode >= 0 && vt == VT_I32 && need == NEED_SUM) {
     switch (mode) {
       case 0: return launch_ingest_t<VT_I32, NEED_SUM, 0>(a, nblocks, st);
       case 1: return launch_ingest_t<VT_I32, NEED_SUM, 1>(a, nblocks, st);
       case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
-      default: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
+      case 3: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
+      case 6: return launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st);   // timing probe: no LDS atomics
+      case 10: return launch_ingest_t<VT_I32, NEED_SUM, 10>(a, nblocks, st); // timing probe: no cell lookup
+      default: return launch_ingest_t<VT_I32, NEED_SUM, 14>(a, nblocks, st); // timing probe: neither
     }
   }
   if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);

@@ -20,14 +20,18 @@ import bench  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["c3", "c4"])
+    ap.add_argument("which", choices=["c2s", "c3", "c4"])
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--wave", action="store_true", help="C4: wavefront-per-key replay (tune keyed_lane 0)")
+    ap.add_argument("--tune", action="append", default=[], help="C2s: scotty_tune key=value (repeatable)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    if args.which == "c3":
+    if args.which == "c2s":
+        tune = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune}
+        r = bench.extra_c2s(pkg, dev, args.batch or (1 << 27), args.steps, tune=tune)
+    elif args.which == "c3":
         r = bench.extra_c3(pkg, dev, args.batch or (1 << 26), args.steps)
     else:
         r = bench.extra_c4(pkg, dev, args.batch or (1 << 24), args.keys, args.steps, lane=not args.wave)
