@@ -115,7 +115,7 @@ def c2s_windows(pkg):
     return out
 
 
-def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None):
+def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
     """north_star target workload: 1000 concurrent sliding windows (c2s_windows), SUM_I32 + COUNT, 20 %
     out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; grid path.  Warm-up until the
     largest window (20 s) has been emitted, so every timed step assembles a full set of windows."""
@@ -136,7 +136,7 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None):
     op.enableTiming(True)
     for s in range(warm + steps):
         ts = base + s * 1000 + 1000
-        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        late = torch.rand(batch, device=dev, generator=g) < ooo
         d = torch.randint(1, 501, (batch,), device=dev, generator=g)
         ts = torch.where(late, torch.clamp(ts - d, min=1), ts).contiguous()
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
@@ -154,6 +154,9 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None):
     ingest_ms, launches, _ = op.ingestTiming()
     avg_ms = ingest_ms / max(1, launches)
     achieved = batch * BYTES_PER_TUPLE / (avg_ms * 1e-3) / 1e9
+    f = op._l.scotty_debug_grid_stat
+    f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int]
+    log("c2s: tuples added with global atomics since creation:", f(op._h, 0))
     return {"workload": "C2s: 1000 concurrent sliding windows, sizes randomTumbling(1000,1,20) Random(10), slide "
                         "size/20, SUM_I32+COUNT, 20% out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),

@@ -36,7 +36,7 @@ struct DevMeta {
   int64_t oldest_start;      // t_start[head] after the last GC (host mirror)
   uint64_t late_push, overflow_push;   // per-push counters (reset by the commit kernel)
   uint64_t late_total, processed_total;
-  int64_t pad[1];
+  uint64_t glb_slow;          // statistics: tuples the ingest kernel added with global atomics (outside the LDS window)
 };
 
 struct IngestArgs {

@@ -1150,6 +1150,14 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   return SCOTTY_ERR_ARG;
 }
 
+// Internal (not in the header): grid-path statistics (0: tuples added with global atomics since creation).
+int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
+  if (!op || op->mode != 1 || !op->d_meta) return -1;
+  DevMeta m;
+  if (hipMemcpy(&m, op->d_meta, sizeof(DevMeta), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return which == 0 ? (int64_t)m.glb_slow : -1;
+}
+
 // Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds).
 int64_t scotty_debug_stat(scotty_op* op, int which) {
   if (!op || !op->x) return -1;

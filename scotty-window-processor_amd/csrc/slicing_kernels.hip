@@ -271,6 +271,15 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   const int64_t b0 = (int64_t)blockIdx.x * per_block;
   const int64_t b1 = min(a.n, b0 + per_block);
 
+  // Window anchor: max ts over the block's first and last 64 tuples (a single endpoint may be an out-of-order
+  // tuple; a window placed below the block's in-order front sends most of its late tuples to global atomics)
+  if (tid < 64) {
+    int64_t x = INT64_MIN;
+    if (b0 + tid < b1) x = max(a.ts[b0 + tid], a.ts[b1 - 1 - tid]);
+    x = wmax64(x);
+    if (tid == 0) sc[15] = x;
+  }
+  __syncthreads();
   if (tid == 0) {
     const DevMeta& m = *a.meta;
     int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
@@ -280,7 +289,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
     int64_t ctot = cv.c_old + kc;
     int64_t first_start = cv.start(0);
-    int64_t x = max(a.ts[b0], a.ts[b1 - 1]);
+    int64_t x = sc[15];
     int64_t chi;
     if (x < first_start) chi = 0;
     else if (x >= h_end) chi = ctot - 1;
@@ -346,7 +355,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   Acc<VT, NEED> acc;
   acc.reset();
   int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
-  uint32_t n_late = 0, n_ovf = 0;
+  uint32_t n_late = 0, n_ovf = 0, n_glb = 0;
   int64_t tile_max = INT64_MIN;
 
   auto flush = [&]() {
@@ -375,15 +384,15 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     } else if (t >= h_end && h_end != INT64_MAX) {
       n_ovf++;
     } else if (t >= tw0 && t < twn) {
-      const int64_t l = (MODE & 8) ? 0 : wfind(t);  // MODE bits 2/3: timing probes only (wrong results)
+      const int64_t l = wfind(t);
       Acc<VT, NEED> one;
       one.reset();
       one.add(t, v);
       const uint64_t sw = one.sum_word();
       const double sf = one.sum_f();
-      if (!(MODE & 4)) lds_add<VT, NEED>(w, l, 1u, t, sw, sf, one.mn, one.mx);
-      else if (l == 12345678) w.cnt[0] = (uint32_t)sw;
+      lds_add<VT, NEED>(w, l, 1u, t, sw, sf, one.mn, one.mx);
     } else {
+      n_glb++;
       const int64_t c = cx.find(cv, t);
       Acc<VT, NEED> one;
       one.reset();
@@ -518,7 +527,8 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   }
   flush();
   {
-    uint32_t nl = wsum32(n_late), no = wsum32(n_ovf);
+    uint32_t nl = wsum32(n_late), no = wsum32(n_ovf), ng = wsum32(n_glb);
+    if (lane == 0 && ng) atomicAdd((unsigned long long*)&a.meta->glb_slow, (unsigned long long)ng);
     if (lane == 0 && (nl | no)) {
       if (nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
       if (no) atomicAdd((unsigned long long*)&a.meta->overflow_push, (unsigned long long)no);
@@ -1183,10 +1193,7 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
       case 0: return launch_ingest_t<VT_I32, NEED_SUM, 0>(a, nblocks, st);
       case 1: return launch_ingest_t<VT_I32, NEED_SUM, 1>(a, nblocks, st);
       case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
-      case 3: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
-      case 6: return launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st);   // timing probe: no LDS atomics
-      case 10: return launch_ingest_t<VT_I32, NEED_SUM, 10>(a, nblocks, st); // timing probe: no cell lookup
-      default: return launch_ingest_t<VT_I32, NEED_SUM, 14>(a, nblocks, st); // timing probe: neither
+      default: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
     }
   }
   if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);

@@ -25,12 +25,13 @@ def main():
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--wave", action="store_true", help="C4: wavefront-per-key replay (tune keyed_lane 0)")
+    ap.add_argument("--ooo", type=float, default=0.2, help="C2s: out-of-order fraction")
     ap.add_argument("--tune", action="append", default=[], help="C2s: scotty_tune key=value (repeatable)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.which == "c2s":
         tune = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune}
-        r = bench.extra_c2s(pkg, dev, args.batch or (1 << 27), args.steps, tune=tune)
+        r = bench.extra_c2s(pkg, dev, args.batch or (1 << 27), args.steps, tune=tune, ooo=args.ooo)
     elif args.which == "c3":
         r = bench.extra_c3(pkg, dev, args.batch or (1 << 26), args.steps)
     else:
