@@ -164,13 +164,16 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
             "ingest": {"avg_launch_ms": avg_ms, "achieved_GBs": achieved, "frac": achieved / HBM_PEAK_GBS}}
 
 
-def extra_c4(pkg, dev, batch, keys, steps, lane=True):
-    """BASELINE configs[3] (C4), one GPU's shard: SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys,
-    maxLateness 1 (Flink connector default); 61 s of warm-up so every step emits each key's window."""
+def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None):
+    """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
+    connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
+    with no collective -- rank r owns the keys k with k mod world == r (what an upstream keyBy delivers), `keys`
+    is the global key count, `batch` the tuples per rank per step (weak scaling); the timed region is bracketed
+    by barriers and the max over ranks is taken."""
     import torch
     rate = max(1, batch // 1000)
     g = torch.Generator(device=dev)
-    g.manual_seed(42)
+    g.manual_seed(42 + rank)
     op = pkg.KeyedSlicingWindowOperator(device=dev.index)
     if not lane:
         op.tune("keyed_lane", 0)
@@ -179,12 +182,15 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True):
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     warm = 61
-    times, rows = [], 0
+    shard_keys = max(1, keys // world)
+    times, rows, elapsed = [], 0, 0.0
     for s in range(warm + steps):
-        k = torch.randint(0, keys, (batch,), device=dev, dtype=torch.int32, generator=g)
+        k = torch.randint(0, shard_keys, (batch,), device=dev, dtype=torch.int32, generator=g) * world + rank
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         ts = base + s * 1000
         torch.cuda.synchronize(dev)
+        if dist is not None and s == warm:
+            dist.barrier()
         t0 = time.perf_counter()
         op.processElementsDevice(k.data_ptr(), ts.data_ptr(), v.data_ptr(), batch)
         n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
@@ -192,11 +198,18 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True):
         if s >= warm:
             times.append(time.perf_counter() - t0)
             rows += n
-    return {"workload": "C4 (one shard): keyed SlidingWindow(60s,1s) SUM_I32, %d uniform keys, maxLateness=1, "
-                        "results left in HBM" % keys,
-            "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
-            "ms_per_step": 1e3 * sum(times) / len(times), "value": batch * len(times) / sum(times),
-            "unit": "tuples/s", "windows_emitted": rows}
+    elapsed = sum(times)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    return {"workload": "C4: keyed SlidingWindow(60s,1s) SUM_I32, %d uniform keys%s, maxLateness=1, results left "
+                        "in HBM" % (keys, " key-hash sharded over %d GPUs (no collective)" % world if world > 1 else ""),
+            "tuples_per_step": batch * world, "tuples_per_step_per_gpu": batch, "steps": steps,
+            "keys_per_gpu": op.keyCount(), "ms_per_step": 1e3 * elapsed / len(times),
+            "value": batch * world * len(times) / elapsed, "unit": "tuples/s", "scaling": "weak",
+            "windows_emitted_rank0": rows}
 
 
 def main():
@@ -317,11 +330,18 @@ def main():
                          "kernel": "ingest_kernel<VT_I32,NEED_SUM>", "algorithmic_bytes_per_launch":
                              B * BYTES_PER_TUPLE, "avg_launch_ms": avg_ms, "launches": launches},
         }
-        if not args.no_extra and world == 1:
-            del batches
-            torch.cuda.empty_cache()
-            res["extra"] = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
-                            "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5)}
+    if not args.no_extra:
+        del batches
+        del op
+        torch.cuda.empty_cache()
+        if world == 1:
+            extra = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
+                     "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5)}
+        else:  # every rank takes part: key-hash sharded C4, no collective on the data path
+            extra = {"c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5, rank=rank, world=world, dist=dist)}
+        if rank == 0:
+            res["extra"] = extra
+    if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(sizes, rate)
         print(json.dumps(res), flush=True)

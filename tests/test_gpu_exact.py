@@ -295,3 +295,50 @@ def test_keyed_large_batch_count_property(pkg):
     assert op.keyCount() == len(np.unique(keys))
     assert sum(w.getAggValues()[0] for _, w in rows if w.hasValue()) == n
     assert sum(w.getAggValues()[1] for _, w in rows if w.hasValue()) == int(vals.astype(np.int64).sum())
+
+
+def test_keyed_hash_sharding_equals_single_operator(pkg):
+    """SURVEY §8(e) keyed: ranks own disjoint key sets (hash(key) mod G) and need no collective.  G=3 keyed
+    operators fed by a key partition of one stream (the arrival order of each key kept) leave exactly the rows
+    of one operator fed the whole stream."""
+    rng = np.random.default_rng(77)
+    n = 200_000
+    ts, vals = product().workloads.stream(n, 4, t0=100, ooo_frac=0.2, max_delay=300, seed=77)
+    keys = rng.integers(0, 5000, size=n).astype(np.uint32)
+    wins = [Sliding(Time, 2000, 250), Tumbling(Time, 700)]
+
+    def make():
+        op = pkg.KeyedSlicingWindowOperator(device=0)
+        op.addWindowFunction(SUM)
+        op.addWindowFunction(MAX)
+        op.setMaxLateness(500)
+        for w in wins:
+            op.addWindowAssigner(w)
+        return op
+
+    G = 3
+    shard = (keys.astype(np.uint64) * 2654435761 >> 7) % G  # any key hash; the SPE's keyBy in production
+    whole, parts = make(), [make() for _ in range(G)]
+    sched = interval_schedule(ts, 8, lag=400)
+    total = 0
+    for step in sched:
+        if step[0] == "push":
+            lo, hi = step[1], step[2]
+            if hi <= lo:
+                continue
+            whole.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+            for r in range(G):
+                m = shard[lo:hi] == r
+                if m.any():
+                    parts[r].processElements(keys[lo:hi][m], ts[lo:hi][m], vals[lo:hi][m])
+        else:
+            exp = {}
+            for k, w in whole.processWatermark(step[1]):
+                exp.setdefault(k, []).append(w)
+            got = []
+            for r in range(G):
+                got += parts[r].processWatermark(step[1])
+            total += same_keyed_windows(got, exp)
+    assert sum(p.keyCount() for p in parts) == whole.keyCount()
+    assert sum(p.droppedCount() for p in parts) == whole.droppedCount()
+    assert total > 0
