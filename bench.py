@@ -164,6 +164,39 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
             "ingest": {"avg_launch_ms": avg_ms, "achieved_GBs": achieved, "frac": achieved / HBM_PEAK_GBS}}
 
 
+def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20_000_000):
+    """BASELINE configs[4] (C5), one GPU: count-based windows, BenchmarkRunner.randomCount(n, lo, hi)
+    (TumblingWindow(Count, size), java.util.Random(10)), SUM_I32 + COUNT, in-order non-keyed stream,
+    maxLateness 1.  Count windows make every slice a LazySlice (S/slice/SliceFactory.java:17-22)."""
+    import torch
+    rate = max(1, batch // 1000)
+    g = torch.Generator(device=dev)
+    g.manual_seed(9)
+    op = pkg.SlicingWindowOperator(device=dev.index)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.addWindowFunction(pkg.AGG_COUNT)
+    op.setMaxLateness(1)
+    for size in pkg.workloads.random_count_sizes(n_windows, lo, hi, seed=10):
+        op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, size))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    times, rows = [], 0
+    for s in range(warm + steps):
+        ts = base + s * 1000
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
+        torch.cuda.synchronize(dev)
+        if s >= warm:
+            times.append(time.perf_counter() - t0)
+            rows += n
+    return {"workload": "C5 (one GPU): %d tumbling count windows, sizes randomCount(%d,%d,%d) Random(10), "
+                        "SUM_I32+COUNT, in-order, maxLateness=1" % (n_windows, n_windows, lo, hi),
+            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
+
+
 def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None):
     """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
     connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
@@ -336,7 +369,7 @@ def main():
         torch.cuda.empty_cache()
         if world == 1:
             extra = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
-                     "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5)}
+                     "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5), "c5": extra_c5(pkg, dev, 1 << 27, 5)}
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
             extra = {"c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5, rank=rank, world=world, dist=dist)}
         if rank == 0:

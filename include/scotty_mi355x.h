@@ -119,7 +119,8 @@ int scotty_process_keyed_elements_device(scotty_op* op, const uint32_t* d_key, c
  * windows are returned (the connector's hasValue() filter, :80, is the caller's). */
 int scotty_process_watermark(scotty_op* op, int64_t watermark_ts, scotty_windows* out);
 /* Same, but the result columns stay in HBM (device pointers, valid until the next call on the op).
- * Exact-engine ops only (keyed, or with session / count windows); others return SCOTTY_ERR_UNSUPPORTED. */
+ * Exact-engine and count-path ops (keyed, or with session / count windows); grid-path ops (context-free time
+ * windows only) return SCOTTY_ERR_UNSUPPORTED. */
 int scotty_process_watermark_device(scotty_op* op, int64_t watermark_ts, scotty_windows* out);
 /* ---- time/arrival-range sharding of ONE non-keyed stream over G ranks (one GPU each).
  * Every rank creates the same operator (same windows, functions, lateness) and, per micro-batch, holds a
@@ -154,7 +155,8 @@ int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, ui
 /* Tuning knobs (not semantics): "slice_capacity" / "session_capacity" per operator of the exact engine
  * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only), "exact_serial"
  * (non-keyed: single-wavefront replay, A/B only), "keyed_lane" 0 (keyed: wavefront-per-key replay instead of
- * the lane-per-key path for context-free time windows, A/B only), "shard_cells" / "shard_cands". */
+ * the lane-per-key path for context-free time windows, A/B only), "count_path" 0 (count-window operators on the
+ * exact engine instead of the count path, A/B only), "ingest_blocks", "shard_cells" / "shard_cands". */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */

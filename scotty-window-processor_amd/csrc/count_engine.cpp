@@ -1,0 +1,433 @@
+// count_engine.cpp -- host side of the count-window path (count_common.h).  The host tracks the count and the
+// pending count edge exactly (edges are a function of counts), launches one push as a chain of kernels without
+// synchronising, and synchronises once per watermark (count trigger) plus once for the results.
+#include "count_engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace scotty {
+
+hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, int64_t* scan_tmp,
+                             long long* premax_tmp, hipStream_t st, hipEvent_t ingest_start, hipEvent_t ingest_end);
+hipError_t launch_count_wm_find(const CWmArgs& a, hipStream_t st);
+hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st);
+hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st);
+
+#define CCHK(x)                                                      \
+  do {                                                               \
+    hipError_t e_ = (x);                                             \
+    if (e_ != hipSuccess) {                                          \
+      err = std::string("HIP: ") + hipGetErrorString(e_) + " at " #x; \
+      failed = true;                                                 \
+      return SCOTTY_ERR_HIP;                                         \
+    }                                                                \
+  } while (0)
+
+namespace {
+constexpr int64_t JMAX = INT64_MAX, JMIN = INT64_MIN;
+constexpr int64_t MAX_PUSH = (int64_t)1 << 28;       // tuples per launch chain (step prefix max: 2 levels)
+constexpr int64_t MAX_EDGES_PER_PUSH = (int64_t)1 << 26;
+int64_t jadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+int64_t jsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+int64_t jmod(int64_t a, int64_t b) { return b == -1 ? 0 : a % b; }
+template <typename T>
+hipError_t dalloc(T** p, int64_t n) {
+  return hipMalloc((void**)p, (size_t)std::max<int64_t>(n, 1) * sizeof(T));
+}
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+// assignNextWindowStart of a count window (C/windowType/TumblingWindow.java:29-31, SlidingWindow.java:41-43,
+// FixedBandWindow.java:37-48): smallest grid point > t
+int64_t assign_next(const CWin& w, int64_t t) {
+  if (w.kind == SCOTTY_WIN_TUMBLING) return jsub(jadd(t, w.a), jmod(t, w.a));
+  if (w.kind == SCOTTY_WIN_SLIDING) return jsub(jadd(t, w.b), jmod(t, w.b));
+  if (t == JMAX || t < w.a) return w.a;
+  if (t >= w.a && t < jadd(w.a, w.b)) return jadd(w.a, w.b);
+  return JMAX;
+}
+// grid points of w in [lo, hi) (as marked by count_mark_kernel)
+int64_t points_in(const CWin& w, int64_t lo, int64_t hi) {
+  if (lo >= hi) return 0;
+  if (w.kind == SCOTTY_WIN_FIXED_BAND) {
+    int64_t c = 0;
+    if (w.a > 0 && w.a >= lo && w.a < hi) c++;
+    const int64_t e = jadd(w.a, w.b);
+    if (e > 0 && e >= lo && e < hi) c++;
+    return c;
+  }
+  const int64_t step = w.kind == SCOTTY_WIN_TUMBLING ? w.a : w.b;
+  const int64_t first = lo <= 0 ? step : ((lo + step - 1) / step) * step;
+  if (first >= hi) return 0;
+  return (hi - 1 - first) / step + 1;
+}
+}  // namespace
+
+CEngine::~CEngine() {
+  (void)hipSetDevice(device);
+  if (stream) (void)hipStreamSynchronize(stream);
+  dfree(d_meta);
+  if (h_meta) (void)hipHostFree(h_meta);
+  dfree(d_wins);
+  dfree(sl.ts); dfree(sl.tl); dfree(sl.cs); dfree(sl.cnt);
+  for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  dfree(cells.cnt); dfree(cells.tl); dfree(cells.tf); dfree(cells.e_pos); dfree(cells.e_ts);
+  for (int k = 0; k < NPART; k++) dfree(cells.p[k]);
+  dfree(d_bits); dfree(d_stepc); dfree(d_stepbase); dfree(d_scan); dfree(d_stepmax); dfree(d_steppre);
+  dfree(d_premax);
+  dfree(d_wstart); dfree(d_wend); dfree(d_meas); dfree(d_has);
+  for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
+  dfree(d_pre_cnt); dfree(d_pre_sum); dfree(d_bsum);
+}
+
+int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
+  device = dev;
+  stream = st;
+  vt = vt_;
+  if (hipMalloc((void**)&d_meta, sizeof(CMeta)) != hipSuccess ||
+      hipHostMalloc((void**)&h_meta, sizeof(CMeta), hipHostMallocDefault) != hipSuccess) {
+    e = "count engine: out of memory";
+    return SCOTTY_ERR_NOMEM;
+  }
+  CMeta m{};
+  m.prev_max = JMIN;
+  *h_meta = m;
+  if (hipMemcpy(d_meta, &m, sizeof(CMeta), hipMemcpyHostToDevice) != hipSuccess) {
+    e = "count engine: HIP error";
+    return SCOTTY_ERR_HIP;
+  }
+  return SCOTTY_OK;
+}
+
+int CEngine::configure(const std::vector<XWinDef>& ws, const std::vector<int>& ag, int64_t lateness) {
+  std::vector<CWin> nw;
+  int64_t mf = 0;
+  for (const XWinDef& w : ws) {
+    if (w.kind == SCOTTY_WIN_SESSION || w.measure != SCOTTY_MEASURE_COUNT)
+      return fail(SCOTTY_ERR_UNSUPPORTED, "count path: only context-free count windows");
+    CWin c{};
+    c.kind = w.kind;
+    c.a = w.a;
+    c.b = w.b;
+    nw.push_back(c);
+    mf = std::max(mf, w.kind == SCOTTY_WIN_FIXED_BAND ? w.b : w.a);  // clearDelay (C/windowType/*.java)
+  }
+  // mid-stream additions: the pending edge keeps its value (StreamSlicer recomputes it only at the next edge)
+  wins = nw;
+  max_fixed = mf;
+  aggs = ag;
+  max_lateness = lateness;
+  need = 0;
+  prefix = !aggs.empty();
+  for (int k : aggs) {
+    if (k == SCOTTY_AGG_SUM_I32 || k == SCOTTY_AGG_SUM_I64 || k == SCOTTY_AGG_SUM_F64) need |= NEED_SUM;
+    if (k == SCOTTY_AGG_MIN_I32 || k == SCOTTY_AGG_MIN_I64 || k == SCOTTY_AGG_MIN_F64) need |= NEED_MIN;
+    if (k == SCOTTY_AGG_MAX_I32 || k == SCOTTY_AGG_MAX_I64 || k == SCOTTY_AGG_MAX_F64) need |= NEED_MAX;
+    if (k != SCOTTY_AGG_SUM_I32 && k != SCOTTY_AGG_SUM_I64 && k != SCOTTY_AGG_COUNT) prefix = false;
+  }
+  dfree(d_wins);
+  d_wins = nullptr;
+  CCHK(dalloc(&d_wins, (int64_t)wins.size()));
+  if (!wins.empty())
+    CCHK(hipMemcpyAsync(d_wins, wins.data(), wins.size() * sizeof(CWin), hipMemcpyHostToDevice, stream));
+  CCHK(hipStreamSynchronize(stream));
+  return SCOTTY_OK;
+}
+
+int64_t CEngine::next_point(int64_t x) const {
+  int64_t e = JMAX;
+  for (const CWin& w : wins) e = std::min(e, assign_next(w, x - 1));
+  return e;
+}
+
+// slices: keep [head, tail) and room for `need` more; reallocates and moves the retained range to index 0
+int CEngine::grow_slices(int64_t need_more) {
+  CCHK(hipMemcpyAsync(h_meta, d_meta, sizeof(CMeta), hipMemcpyDeviceToHost, stream));
+  CCHK(hipStreamSynchronize(stream));
+  const int64_t head = h_meta->head, tail = h_meta->tail, S = tail - head;
+  if (tail + need_more <= scap) {
+    tail_ub = tail;
+    head_lb = head;
+    return SCOTTY_OK;
+  }
+  const int64_t ncap = std::max<int64_t>({(S + need_more) * 2, scap, 4096});
+  CSlices n{};
+  CCHK(dalloc(&n.ts, ncap));
+  CCHK(dalloc(&n.tl, ncap));
+  CCHK(dalloc(&n.cs, ncap));
+  CCHK(dalloc(&n.cnt, ncap));
+  for (int k = 0; k < NPART; k++) CCHK(dalloc(&n.p[k], ncap));
+  if (S > 0) {
+    CCHK(hipMemcpyAsync(n.ts, sl.ts + head, S * 8, hipMemcpyDeviceToDevice, stream));
+    CCHK(hipMemcpyAsync(n.tl, sl.tl + head, S * 8, hipMemcpyDeviceToDevice, stream));
+    CCHK(hipMemcpyAsync(n.cs, sl.cs + head, S * 8, hipMemcpyDeviceToDevice, stream));
+    CCHK(hipMemcpyAsync(n.cnt, sl.cnt + head, S * 8, hipMemcpyDeviceToDevice, stream));
+    for (int k = 0; k < NPART; k++)
+      CCHK(hipMemcpyAsync(n.p[k], sl.p[k] + head, S * 8, hipMemcpyDeviceToDevice, stream));
+  }
+  h_meta->head = 0;
+  h_meta->tail = S;
+  CCHK(hipMemcpyAsync(d_meta, h_meta, sizeof(CMeta), hipMemcpyHostToDevice, stream));
+  CCHK(hipStreamSynchronize(stream));
+  dfree(sl.ts); dfree(sl.tl); dfree(sl.cs); dfree(sl.cnt);
+  for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  sl = n;
+  scap = ncap;
+  tail_ub = S;
+  head_lb = 0;
+  return SCOTTY_OK;
+}
+
+int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t ev0, hipEvent_t ev1) {
+  if (failed) return SCOTTY_ERR_STATE;
+  const size_t vb = vt == VT_I32 ? 4 : 8;
+  while (n > MAX_PUSH) {  // keep one launch chain within the step prefix-max depth
+    int rc = push(d_ts, d_val, MAX_PUSH, nullptr, nullptr);
+    if (rc) return rc;
+    d_ts += MAX_PUSH;
+    d_val = (const unsigned char*)d_val + MAX_PUSH * vb;
+    n -= MAX_PUSH;
+  }
+  if (n <= 0) return SCOTTY_OK;
+  // edges of this batch: the pending edge and every union grid point after it below count + n
+  int64_t mark_from, extra = -1;
+  if (pending == JMIN) {  // the stream's first tuple appends the first slice (S/StreamSlicer.java:37-43)
+    extra = count;
+    mark_from = next_point(count + 1);
+  } else {
+    mark_from = pending;
+  }
+  const int64_t lo = std::max(count, mark_from), hi = count + n;
+  int64_t ebound = extra >= 0 ? 1 : 0, maxp = 0;
+  for (const CWin& w : wins) {
+    const int64_t p = points_in(w, lo, hi);
+    ebound += p;
+    maxp = std::max(maxp, p);
+  }
+  if (ebound > MAX_EDGES_PER_PUSH)
+    return fail(SCOTTY_ERR_UNSUPPORTED, "count windows create more than 2^26 slices in one micro-batch");
+  // capacities
+  const int64_t nwords = (n + 31) / 32, nsteps = (n + CSTEP - 1) / CSTEP;
+  if (nwords > bcap) {
+    dfree(d_bits);
+    bcap = nwords + nwords / 4 + 64;
+    CCHK(dalloc(&d_bits, bcap));
+  }
+  if (nsteps > stcap) {
+    dfree(d_stepc); dfree(d_stepbase); dfree(d_scan); dfree(d_stepmax); dfree(d_steppre); dfree(d_premax);
+    stcap = nsteps + nsteps / 4 + 64;
+    CCHK(dalloc(&d_stepc, stcap));
+    CCHK(dalloc(&d_stepbase, stcap));
+    CCHK(dalloc(&d_scan, stcap / 512 + 64));
+    CCHK(dalloc(&d_stepmax, stcap));
+    CCHK(dalloc(&d_steppre, stcap));
+    CCHK(dalloc(&d_premax, stcap / 1024 + 64));
+  }
+  if (ebound + 1 > ccap) {
+    dfree(cells.cnt); dfree(cells.tl); dfree(cells.tf); dfree(cells.e_pos); dfree(cells.e_ts);
+    for (int k = 0; k < NPART; k++) dfree(cells.p[k]);
+    ccap = ebound + 1 + (ebound + 1) / 4 + 64;
+    CCHK(dalloc(&cells.cnt, ccap));
+    CCHK(dalloc(&cells.tl, ccap));
+    CCHK(dalloc(&cells.tf, ccap));
+    CCHK(dalloc(&cells.e_pos, ccap));
+    CCHK(dalloc(&cells.e_ts, ccap));
+    for (int k = 0; k < NPART; k++) CCHK(dalloc(&cells.p[k], ccap));
+  }
+  if (tail_ub + ebound > scap) {
+    int rc = grow_slices(ebound);
+    if (rc) return rc;
+  }
+  CCHK(hipMemsetAsync(d_bits, 0, nwords * 4, stream));
+  CPushArgs a{};
+  a.ts = d_ts;
+  a.val = d_val;
+  a.n = n;
+  a.bits = d_bits;
+  a.nwords = nwords;
+  a.C = count;
+  a.mark_from = mark_from;
+  a.extra_point = extra;
+  a.wins = d_wins;
+  a.n_wins = (int32_t)wins.size();
+  a.need = need;
+  a.vt = vt;
+  a.stepc = d_stepc;
+  a.stepbase = d_stepbase;
+  a.stepmax = d_stepmax;
+  a.steppre = d_steppre;
+  a.nsteps = nsteps;
+  a.per_wave = std::max<int64_t>(1, (nsteps + 4095) / 4096);  // ~1024 workgroups of 4 waves
+  a.cells = cells;
+  a.cell_cap = ebound + 1;
+  a.sl = sl;
+  a.meta = d_meta;
+  CCHK(launch_count_push(a, maxp, d_scan, d_premax, stream, ev0, ev1));
+  count += n;
+  pending = (pending != JMIN && pending >= count) ? pending : next_point(count);
+  tail_ub += ebound;
+  started = true;
+  return SCOTTY_OK;
+}
+
+// ContextFreeWindow.triggerWindows of every count window with (lastCount, cend + 1), registration order
+// (S/WindowManager.java:104-118; C/windowType/TumblingWindow.java:34-39, SlidingWindow.java:50-57,
+// FixedBandWindow.java:51-57)
+void CEngine::trigger(int64_t last, int64_t cur) {
+  rows.clear();
+  for (const CWin& w : wins) {
+    if (w.kind == SCOTTY_WIN_TUMBLING) {
+      const int64_t size = w.a;
+      const int64_t ls = jsub(last, jmod(jadd(last, size), size));
+      for (int64_t s = ls; jadd(s, size) <= cur; s = jadd(s, size)) rows.push_back({s, jadd(s, size)});
+    } else if (w.kind == SCOTTY_WIN_SLIDING) {
+      const int64_t size = w.a, slide = w.b;
+      const int64_t ls = jsub(cur, jmod(jadd(cur, slide), slide));
+      for (int64_t s = ls; jadd(s, size) > last; s = jsub(s, slide))
+        if (s >= 0 && jadd(s, size) <= jadd(cur, 1)) rows.push_back({s, jadd(s, size)});
+    } else {
+      const int64_t e = jadd(w.a, w.b);
+      if (last <= e && e <= cur) rows.push_back({w.a, e});
+    }
+  }
+}
+
+int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
+  r.n = 0;
+  r.start.clear(); r.end.clear(); r.meas.clear(); r.has.clear(); r.key.clear();
+  r.vals.assign(aggs.size(), {});
+  if (failed) return SCOTTY_ERR_STATE;
+  // WindowManager.processWatermark (S/WindowManager.java:41-80)
+  if (last_wm == -1) last_wm = std::max<int64_t>(0, jsub(wm, max_lateness));
+  if (!started) {
+    last_wm = wm;
+    r.dropped = dropped_;
+    return SCOTTY_OK;
+  }
+  CWmArgs a{};
+  a.sl = sl;
+  a.meta = d_meta;
+  a.wm = wm;
+  CCHK(launch_count_wm_find(a, stream));
+  CCHK(hipMemcpyAsync(h_meta, d_meta, sizeof(CMeta), hipMemcpyDeviceToHost, stream));
+  CCHK(hipStreamSynchronize(stream));
+  dropped_ = h_meta->late_total;
+  r.dropped = dropped_;
+  if (h_meta->err & 1)
+    return fail(SCOTTY_ERR_UNSUPPORTED,
+                "a tuple older than its count slice would be inserted into an earlier LazySlice and shift records "
+                "(S/SliceManager.java:64-85): not implemented on the MI355X count path");
+  if (h_meta->err)
+    return fail(SCOTTY_ERR_STATE, "internal: count path lost tuples");
+  tail_ub = h_meta->tail;
+  head_lb = h_meta->head;
+  if (h_meta->wm_status == 1) {
+    last_wm = wm;
+    return SCOTTY_OK;
+  }
+  if (last_wm < h_meta->oldest) last_wm = h_meta->oldest;
+  if (h_meta->wm_status == 2) {
+    err = "processWatermark threw IndexOutOfBoundsException (count trigger: watermark before the oldest slice, "
+          "S/WindowManager.java:109-112)";
+    return SCOTTY_ERR_INDEX;
+  }
+  trigger(last_count, jadd(h_meta->cend, 1));
+  const int64_t nw = (int64_t)rows.size();
+  int64_t min_c = count, max_c = 0;
+  for (const Row& w : rows) {
+    min_c = std::min(min_c, w.start);
+    max_c = std::max(max_c, w.end);
+  }
+  if (nw > wcap) {
+    dfree(d_wstart); dfree(d_wend); dfree(d_meas); dfree(d_has);
+    for (int k = 0; k < SCOTTY_MAX_AGGS; k++) {
+      dfree(d_vals[k]);
+      d_vals[k] = nullptr;
+    }
+    wcap = nw + nw / 2 + 1024;
+    CCHK(dalloc(&d_wstart, wcap));
+    CCHK(dalloc(&d_wend, wcap));
+    CCHK(dalloc(&d_meas, wcap));
+    CCHK(dalloc(&d_has, wcap));
+    for (size_t k = 0; k < aggs.size(); k++) CCHK(dalloc(&d_vals[k], wcap));
+    std::vector<int32_t> ones(wcap, SCOTTY_MEASURE_COUNT);
+    CCHK(hipMemcpyAsync(d_meas, ones.data(), wcap * 4, hipMemcpyHostToDevice, stream));
+    CCHK(hipStreamSynchronize(stream));
+  }
+  const int64_t S_ub = tail_ub - head_lb + 2;
+  if (prefix && S_ub > pcap) {
+    dfree(d_pre_cnt); dfree(d_pre_sum); dfree(d_bsum);
+    pcap = S_ub + S_ub / 2 + 1024;
+    CCHK(dalloc(&d_pre_cnt, pcap));
+    CCHK(dalloc(&d_pre_sum, pcap));
+    CCHK(dalloc(&d_bsum, 2 * (pcap / 1024 + 2)));
+  }
+  h_start.resize(nw);
+  h_end.resize(nw);
+  for (int64_t i = 0; i < nw; i++) {
+    h_start[i] = rows[i].start;
+    h_end[i] = rows[i].end;
+  }
+  if (nw > 0) {
+    CCHK(hipMemcpyAsync(d_wstart, h_start.data(), nw * 8, hipMemcpyHostToDevice, stream));
+    CCHK(hipMemcpyAsync(d_wend, h_end.data(), nw * 8, hipMemcpyHostToDevice, stream));
+  }
+  a.min_count = min_c;
+  a.max_count = max_c;
+  a.gc_before = jsub(jsub(wm, max_lateness), max_fixed);
+  a.w_start = d_wstart;
+  a.w_end = d_wend;
+  a.nw = nw;
+  a.need = need;
+  a.vt = vt;
+  a.n_aggs = (int32_t)aggs.size();
+  a.prefix = prefix ? 1 : 0;
+  for (size_t k = 0; k < aggs.size(); k++) {
+    a.agg_kind[k] = aggs[k];
+    a.values[k] = d_vals[k];
+  }
+  a.pre_cnt = d_pre_cnt;
+  a.pre_sum = d_pre_sum;
+  a.has_value = d_has;
+  if (nw > 0) {  // LazyAggregateStore.aggregate runs only with windows (S/WindowManager.java:73-75)
+    CCHK(launch_count_wm_agg(a, (S_ub + 1023) / 1024 + 1, d_bsum, stream));
+    CCHK(hipMemcpyAsync(h_meta, d_meta, sizeof(CMeta), hipMemcpyDeviceToHost, stream));
+    CCHK(hipStreamSynchronize(stream));
+    if (h_meta->range_err) {
+      err = "processWatermark threw IndexOutOfBoundsException (LazyAggregateStore.aggregate: a window starts before "
+            "the oldest retained slice, S/aggregationstore/LazyAggregateStore.java:83-90)";
+      return SCOTTY_ERR_INDEX;
+    }
+  }
+  last_wm = wm;
+  last_count = count;
+  CCHK(launch_count_gc(a, stream));  // clearAfterWatermark(wm - maxLateness) (S/WindowManager.java:82-95)
+  r.n = nw;
+  r.d_start = d_wstart;
+  r.d_end = d_wend;
+  r.d_meas = d_meas;
+  r.d_key = nullptr;
+  r.d_has = d_has;
+  for (size_t k = 0; k < aggs.size(); k++) r.d_vals[k] = d_vals[k];
+  if (to_host && nw > 0) {
+    r.start = h_start;
+    r.end = h_end;
+    r.meas.assign(nw, SCOTTY_MEASURE_COUNT);
+    r.has.resize(nw);
+    r.vals.assign(aggs.size(), std::vector<int64_t>(nw));
+    CCHK(hipMemcpyAsync(r.has.data(), d_has, nw, hipMemcpyDeviceToHost, stream));
+    for (size_t k = 0; k < aggs.size(); k++)
+      CCHK(hipMemcpyAsync(r.vals[k].data(), d_vals[k], nw * 8, hipMemcpyDeviceToHost, stream));
+  }
+  CCHK(hipStreamSynchronize(stream));
+  return SCOTTY_OK;
+}
+
+int64_t CEngine::slice_count() {
+  if (hipMemcpyAsync(h_meta, d_meta, sizeof(CMeta), hipMemcpyDeviceToHost, stream) != hipSuccess) return -1;
+  if (hipStreamSynchronize(stream) != hipSuccess) return -1;
+  return h_meta->tail - h_meta->head;
+}
+
+}  // namespace scotty

@@ -1,0 +1,83 @@
+// count_engine.h -- host side of the count-window path (count_common.h, count_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/scotty_mi355x.h"
+#include "count_common.h"
+#include "exact_engine.h"
+
+namespace scotty {
+
+class CEngine {
+ public:
+  ~CEngine();
+  int init(int device, hipStream_t stream, int vt, std::string& err);
+  // WindowManager.addWindowAssigner / addAggregation / setMaxLateness (S/WindowManager.java:121-202)
+  int configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness);
+  int push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t ev0, hipEvent_t ev1);
+  int watermark(int64_t wm, XResult& r, bool to_host);
+  int set_last_watermark(int64_t lw) {
+    last_wm = lw;
+    return SCOTTY_OK;
+  }
+  int64_t slice_count();
+  uint64_t dropped() const { return dropped_; }
+
+  std::string err;
+  bool failed = false;
+
+ private:
+  int grow_slices(int64_t need);
+  int fail(int rc, const std::string& m) {
+    err = m;
+    failed = true;
+    return rc;
+  }
+  int64_t next_point(int64_t x) const;  // smallest union count-grid point >= x (x >= 1)
+  void trigger(int64_t last_count, int64_t cend1);
+
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int vt = VT_I32;
+  std::vector<CWin> wins;
+  std::vector<int> aggs;
+  int need = 0;
+  int64_t max_lateness = 1000, max_fixed = 0;
+  bool prefix = false;  // every aggregation an invertible integer kind
+  // StreamSlicer / WindowManager scalars the host tracks exactly (edges depend on counts only)
+  int64_t count = 0;           // WindowManager.currentCount
+  int64_t pending = INT64_MIN;  // StreamSlicer.min_next_edge_count
+  int64_t last_wm = -1, last_count = 0;
+  bool started = false;
+  uint64_t dropped_ = 0;
+  int64_t tail_ub = 0, head_lb = 0;  // slice range bounds between synchronisations
+  // device
+  CMeta* d_meta = nullptr;
+  CMeta* h_meta = nullptr;  // pinned
+  CWin* d_wins = nullptr;
+  int64_t scap = 0;
+  CSlices sl{};
+  int64_t ccap = 0;
+  CCells cells{};
+  int64_t bcap = 0, stcap = 0;
+  uint32_t* d_bits = nullptr;
+  int64_t *d_stepc = nullptr, *d_stepbase = nullptr, *d_scan = nullptr;
+  long long *d_stepmax = nullptr, *d_steppre = nullptr, *d_premax = nullptr;
+  // watermark
+  struct Row {
+    int64_t start, end;
+  };
+  std::vector<Row> rows;
+  int64_t wcap = 0, pcap = 0;
+  int64_t *d_wstart = nullptr, *d_wend = nullptr;
+  int32_t* d_meas = nullptr;
+  uint8_t* d_has = nullptr;
+  int64_t* d_vals[SCOTTY_MAX_AGGS] = {};
+  unsigned long long *d_pre_cnt = nullptr, *d_pre_sum = nullptr, *d_bsum = nullptr;
+  std::vector<int64_t> h_start, h_end;
+};
+
+}  // namespace scotty

@@ -1,0 +1,719 @@
+// count_kernels.hip -- gfx950 kernels of the count-window path (layout and derivation: count_common.h).
+//
+// One micro-batch:
+//   1. count_mark_kernel     edge bitmap over the batch's counts: the union grid of the windows'
+//                            assignNextWindowStart in count space from the pending edge on
+//                            (StreamSlicer.determineSlices / calculateNextFixedEdgeCount, S/StreamSlicer.java:36-44,
+//                            :88-101); one thread per grid point.
+//   2. count_stepc_kernel    edges per 256-tuple step (popcount) -> exclusive scan = cell of each step's start.
+//   3. count_ingest_kernel   the HBM pass (12 B/tuple): SliceManager.processElement + LazySlice.addElement +
+//                            AggregateValueState.addElement (S/SliceManager.java:47-87, S/slice/LazySlice.java:23-27);
+//                            a tuple's cell = edges at or before its index; register accumulators for the wave's
+//                            current cell, global atomics only in steps that contain an edge; step maxima of ts.
+//   4. count_edges_kernel    tStart of every new slice = max ts before its edge (S/StreamSlicer.java:39-41, :83):
+//                            prefix max over step maxima + an in-step wave scan; one wave per step with edges.
+//   5. count_append_kernel   SliceManager.appendSlice (S/SliceManager.java:27-38) for every edge, partials folded
+//                            into the open slice; the out-of-order check (a tuple older than its own slice).
+//   6. count_finish_kernel   StreamSlicer.maxEventTime, store tail.
+// Watermark (WindowManager.processWatermark, S/WindowManager.java:41-80):
+//   count_wm_find_kernel     the count trigger's cend (S/WindowManager.java:109-115) and the oldest slice start,
+//   count_wm_range_kernel    LazyAggregateStore.aggregate's scan range (S/aggregationstore/LazyAggregateStore.java:83-90),
+//   count_wm_agg_kernel<G>   AggregateWindowState.containsSlice/addState (S/state/AggregateWindowState.java:25-53)
+//                            per window: prefix-sum difference for invertible integer aggregates, else a G-lane scan,
+//   count_gc_kernel          clearAfterWatermark / removeSlices (S/WindowManager.java:82-95).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/scotty_mi355x.h"
+#include "count_common.h"
+#include "exact_op.h"
+
+namespace scotty {
+namespace ck {
+
+constexpr int64_t JMAX = INT64_MAX, JMIN = INT64_MIN;
+constexpr int64_t ID_MIN = INT64_MAX;  // identity of min partials
+constexpr int64_t ID_MAX = INT64_MIN;  // identity of max partials
+
+template <typename T, typename F>
+__device__ __forceinline__ T wred(T v, F f) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = f(v, (T)__shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int64_t uni(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// ---------------------------------------------------------------- 1. edge bitmap
+// blockIdx.y = window.  Points of window w in [lo, hi): tumbling multiples of size, sliding multiples of slide
+// (assignNextWindowStart, C/windowType/TumblingWindow.java:29-31, SlidingWindow.java:41-43), fixed band
+// start and start+size (FixedBandWindow.java:37-48).  0 is only an edge as the stream's first tuple.
+__global__ __launch_bounds__(256) void count_mark_kernel(CPushArgs a) {
+  const int w = blockIdx.y;
+  const CWin win = a.wins[w];
+  const int64_t lo = max(a.C, a.mark_from), hi = a.C + a.n;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  auto set = [&](int64_t c) {
+    const int64_t i = c - a.C;
+    atomicOr(&a.bits[i >> 5], 1u << (i & 31));
+  };
+  if (g == 0 && w == 0 && a.extra_point >= a.C && a.extra_point < hi) set(a.extra_point);
+  if (lo >= hi) return;
+  if (win.kind == SCOTTY_WIN_FIXED_BAND) {
+    if (g == 0) {
+      if (win.a >= lo && win.a < hi && win.a > 0) set(win.a);
+      const int64_t e = win.a + win.b;
+      if (e >= lo && e < hi && e > 0) set(e);
+    }
+    return;
+  }
+  const int64_t step = win.kind == SCOTTY_WIN_TUMBLING ? win.a : win.b;
+  const int64_t first = lo <= 0 ? step : ((lo + step - 1) / step) * step;
+  for (int64_t m = first + g * step; m < hi; m += (int64_t)gridDim.x * blockDim.x * step) set(m);
+}
+
+// ---------------------------------------------------------------- 2. edges per step
+__global__ void count_stepc_kernel(CPushArgs a) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.nsteps) return;
+  int64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int64_t wi = s * 8 + k;
+    if (wi < a.nwords) c += __popc(a.bits[wi]);
+  }
+  a.stepc[s] = c;
+}
+
+__global__ void count_cells_init_kernel(CCells c, int64_t n) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    c.cnt[j] = 0;
+    c.tl[j] = JMIN;
+    c.tf[j] = JMAX;
+    c.p[0][j] = 0;
+    c.p[1][j] = (unsigned long long)ID_MIN;
+    c.p[2][j] = (unsigned long long)ID_MAX;
+  }
+}
+
+// ---------------------------------------------------------------- 3. ingest
+template <int VT>
+struct Lifted {
+  uint64_t sw;
+  double sf;
+  int64_t mn, mx;
+};
+template <int VT>
+__device__ __forceinline__ void lift(int64_t vb, uint64_t& sw, int64_t& mn, int64_t& mx) {
+  if constexpr (VT == VT_F64) {
+    const double d = __longlong_as_double(vb);
+    sw = (uint64_t)vb;
+    mn = d != d ? INT64_MIN : x::f64_key(d);
+    mx = d != d ? INT64_MAX : x::f64_key(d);
+  } else {
+    sw = (uint64_t)vb;
+    mn = vb;
+    mx = vb;
+  }
+}
+
+template <int VT, int NEED>
+__device__ __forceinline__ void cell_add(const CCells& c, int64_t j, uint64_t n, int64_t tmax, int64_t tmin,
+                                         uint64_t sw, double sf, int64_t mn, int64_t mx) {
+  atomicAdd(&c.cnt[j], (unsigned long long)n);
+  atomicMax(&c.tl[j], (long long)tmax);
+  atomicMin(&c.tf[j], (long long)tmin);
+  if constexpr ((NEED & NEED_SUM) != 0) {
+    if constexpr (VT == VT_F64) atomicAdd((double*)&c.p[0][j], sf);
+    else atomicAdd(&c.p[0][j], (unsigned long long)sw);
+  }
+  if constexpr ((NEED & NEED_MIN) != 0) atomicMin((long long*)&c.p[1][j], (long long)mn);
+  if constexpr ((NEED & NEED_MAX) != 0) atomicMax((long long*)&c.p[2][j], (long long)mx);
+}
+
+template <int VT, int NEED>
+__global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t s0 = wave * a.per_wave;
+  const int64_t s1 = min(a.nsteps, s0 + a.per_wave);
+  if (s0 >= s1) return;
+  const int64_t first_start = uni(a.meta->first_start);
+  // per-lane accumulator of the wave's current cell
+  uint64_t cnt = 0, sw = 0;
+  double sf = 0.0;
+  int64_t tmax = JMIN, tmin = JMAX, mn = ID_MIN, mx = ID_MAX;
+  int64_t cur = -1;
+  uint32_t n_late = 0;
+  auto flush = [&]() {
+    const uint64_t c = wred(cnt, [](unsigned long long p, unsigned long long q) { return p + q; });
+    if (c != 0) {
+      const int64_t tm = wred(tmax, [](long long p, long long q) { return p > q ? p : q; });
+      const int64_t tn = wred(tmin, [](long long p, long long q) { return p < q ? p : q; });
+      uint64_t s = 0;
+      double f = 0.0;
+      if constexpr ((NEED & NEED_SUM) != 0) {
+        if constexpr (VT == VT_F64) f = wred(sf, [](double p, double q) { return p + q; });
+        else s = wred(sw, [](unsigned long long p, unsigned long long q) { return p + q; });
+      }
+      int64_t m1 = ID_MIN, m2 = ID_MAX;
+      if constexpr ((NEED & NEED_MIN) != 0) m1 = wred(mn, [](long long p, long long q) { return p < q ? p : q; });
+      if constexpr ((NEED & NEED_MAX) != 0) m2 = wred(mx, [](long long p, long long q) { return p > q ? p : q; });
+      if (lane == 0) cell_add<VT, NEED>(a.cells, cur, c, tm, tn, s, f, m1, m2);
+    }
+    cnt = 0; sw = 0; sf = 0.0; tmax = JMIN; tmin = JMAX; mn = ID_MIN; mx = ID_MAX;
+  };
+  auto add = [&](int64_t t, int64_t vb) {
+    uint64_t w;
+    int64_t l, h;
+    lift<VT>(vb, w, l, h);
+    cnt++;
+    tmax = max(tmax, t);
+    tmin = min(tmin, t);
+    if constexpr ((NEED & NEED_SUM) != 0) {
+      if constexpr (VT == VT_F64) sf += __longlong_as_double((long long)w);
+      else sw += w;
+    }
+    if constexpr ((NEED & NEED_MIN) != 0) mn = min(mn, l);
+    if constexpr ((NEED & NEED_MAX) != 0) mx = max(mx, h);
+  };
+  typedef long long v2i64 __attribute__((ext_vector_type(2)));
+  typedef int v2i32 __attribute__((ext_vector_type(2)));
+  for (int64_t s = s0; s < s1; s++) {
+    const int64_t base = s * CSTEP;
+    const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
+    int64_t t[4], v[4];
+    bool ok[4];
+    if (base + CSTEP <= a.n) {
+      const v2i64 ta = __builtin_nontemporal_load((const v2i64*)(a.ts + i0));
+      const v2i64 tb = __builtin_nontemporal_load((const v2i64*)(a.ts + i1));
+      t[0] = ta.x; t[1] = ta.y; t[2] = tb.x; t[3] = tb.y;
+      if constexpr (VT == VT_I32) {
+        const v2i32 va = __builtin_nontemporal_load((const v2i32*)((const int32_t*)a.val + i0));
+        const v2i32 vb = __builtin_nontemporal_load((const v2i32*)((const int32_t*)a.val + i1));
+        v[0] = va.x; v[1] = va.y; v[2] = vb.x; v[3] = vb.y;
+      } else {
+        const v2i64 va = __builtin_nontemporal_load((const v2i64*)((const int64_t*)a.val + i0));
+        const v2i64 vb = __builtin_nontemporal_load((const v2i64*)((const int64_t*)a.val + i1));
+        v[0] = va.x; v[1] = va.y; v[2] = vb.x; v[3] = vb.y;
+      }
+      ok[0] = ok[1] = ok[2] = ok[3] = true;
+    } else {  // ragged last step
+      const int64_t idx[4] = {i0, i0 + 1, i1, i1 + 1};
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        ok[j] = idx[j] < a.n;
+        t[j] = ok[j] ? a.ts[idx[j]] : JMIN;
+        if constexpr (VT == VT_I32) v[j] = ok[j] ? (int64_t)((const int32_t*)a.val)[idx[j]] : 0;
+        else v[j] = ok[j] ? ((const int64_t*)a.val)[idx[j]] : 0;
+      }
+    }
+    int64_t smax = JMIN;
+#pragma unroll
+    for (int j = 0; j < 4; j++) smax = max(smax, t[j]);
+    smax = wred(smax, [](long long p, long long q) { return p > q ? p : q; });
+    if (lane == 0) a.stepmax[s] = smax;
+    // edge words of the step (wave-uniform)
+    uint32_t wd[8];
+    uint32_t any = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int64_t wi = s * 8 + k;
+      wd[k] = wi < a.nwords ? __builtin_amdgcn_readfirstlane(a.bits[wi]) : 0u;
+      any |= wd[k];
+    }
+    const int64_t sb = uni(a.stepbase[s]);
+    if (any == 0) {
+      if (sb != cur) {
+        if (cur >= 0) flush();
+        cur = sb;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (!ok[j]) continue;
+        if (t[j] < first_start) n_late++;
+        else add(t[j], v[j]);
+      }
+      continue;
+    }
+    // a step with edges: the wave keeps the step's last cell in registers, other tuples go to their cell directly
+    int pre[9];
+    pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) pre[k + 1] = pre[k] + __popc(wd[k]);
+    const int64_t last = sb + pre[8];
+    if (last != cur) {
+      if (cur >= 0) flush();
+      cur = last;
+    }
+    const int off[4] = {2 * lane, 2 * lane + 1, 128 + 2 * lane, 129 + 2 * lane};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (!ok[j]) continue;
+      if (t[j] < first_start) {
+        n_late++;
+        continue;
+      }
+      const int o = off[j], q = o >> 5, b = o & 31;
+      const uint32_t mask = (uint32_t)((2ull << b) - 1);
+      const int64_t cell = sb + pre[q] + __popc(wd[q] & mask);
+      if (cell == cur) {
+        add(t[j], v[j]);
+      } else {
+        uint64_t w;
+        int64_t l, h;
+        lift<VT>(v[j], w, l, h);
+        cell_add<VT, NEED>(a.cells, cell, 1, t[j], t[j], w, __longlong_as_double((long long)w), l, h);
+      }
+    }
+  }
+  if (cur >= 0) flush();
+  const uint32_t nl = wred(n_late, [](uint32_t p, uint32_t q) { return p + q; });
+  if (lane == 0 && nl) atomicAdd((unsigned long long*)&a.meta->late_total, (unsigned long long)nl);
+}
+
+// ---------------------------------------------------------------- 4. edge positions and slice starts
+// prefix max over step maxima (inclusive, single pass per 1024-step block + block carry)
+__global__ __launch_bounds__(1024) void count_premax_block_kernel(const long long* in, long long* out, int64_t n,
+                                                                  long long* bsum) {
+  __shared__ long long wt[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + tid;
+  long long v = i < n ? in[i] : JMIN;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long u = __shfl_up(v, o);
+    if (lane >= o) v = max(v, u);
+  }
+  if (lane == 63) wt[wid] = v;
+  __syncthreads();
+  long long add = JMIN;
+  for (int w = 0; w < wid; w++) add = max(add, wt[w]);
+  v = max(v, add);
+  if (i < n) out[i] = v;
+  if (tid == 1023) bsum[blockIdx.x] = v;
+}
+__global__ void count_premax_carry_kernel(long long* out, int64_t n, const long long* bsum_incl) {
+  const int64_t b = blockIdx.x;
+  if (b == 0) return;
+  const long long c = bsum_incl[b - 1];
+  const int64_t i = b * 1024 + threadIdx.x;
+  if (i < n) out[i] = max(out[i], c);
+}
+
+__global__ __launch_bounds__(256) void count_edges_kernel(CPushArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (s >= a.nsteps) return;
+  if (a.stepc[s] == 0) return;
+  const int64_t base = s * CSTEP;
+  const int64_t prev = a.meta->prev_max;
+  long long before = s > 0 ? a.steppre[s - 1] : JMIN;
+  before = max(before, (long long)prev);
+  // lane l holds offsets 4l .. 4l+3
+  int64_t t[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int64_t i = base + 4 * lane + j;
+    t[j] = i < a.n ? a.ts[i] : JMIN;
+  }
+  int64_t lm = max(max(t[0], t[1]), max(t[2], t[3]));
+  int64_t ex = lm;  // exclusive prefix max over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = (int64_t)__shfl_up((long long)ex, o);
+    if (lane >= o) ex = max(ex, u);
+  }
+  ex = (int64_t)__shfl_up((long long)ex, 1);
+  if (lane == 0) ex = JMIN;
+  uint32_t wd[8];
+  int pre[9];
+  pre[0] = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int64_t wi = s * 8 + k;
+    wd[k] = wi < a.nwords ? a.bits[wi] : 0u;
+    pre[k + 1] = pre[k] + __popc(wd[k]);
+  }
+  const int64_t sb = a.stepbase[s];
+  int64_t run = max((int64_t)before, ex);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int o = 4 * lane + j, q = o >> 5, b = o & 31;
+    if ((wd[q] >> b) & 1u) {
+      const int64_t e = sb + pre[q] + __popc(wd[q] & ((1u << b) - 1u));  // edges strictly before o
+      a.cells.e_pos[e] = base + o;
+      // max ts of every tuple before the edge (StreamSlicer.maxEventTime); the stream's first tuple sets it to its
+      // own ts first (S/StreamSlicer.java:39-40)
+      a.cells.e_ts[e] = run == JMIN ? t[j] : run;
+    }
+    run = max(run, t[j]);
+  }
+}
+
+// ---------------------------------------------------------------- 5. append
+template <int VT>
+__global__ __launch_bounds__(256) void count_append_kernel(CPushArgs a) {
+  const CMeta& m = *a.meta;
+  const int64_t E = m.n_edges;
+  const int64_t head = m.head, tail = m.tail;
+  const CCells& c = a.cells;
+  const CSlices& sl = a.sl;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= E; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t n = c.cnt[j];
+    if (j == 0) {  // the slice open before the batch
+      if (n == 0) continue;
+      const int64_t k = tail - 1;
+      if (k < head) {
+        atomicOr((unsigned long long*)&a.meta->err, 2ull);  // internal: tuples without a slice
+        continue;
+      }
+      if (c.tf[0] < sl.ts[k]) atomicOr((unsigned long long*)&a.meta->err, 1ull);
+      sl.cnt[k] += n;
+      sl.tl[k] = max(sl.tl[k], (int64_t)c.tl[0]);
+      if (VT == VT_F64)
+        sl.p[0][k] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)sl.p[0][k]) +
+                                                             __longlong_as_double((long long)c.p[0][0]));
+      else
+        sl.p[0][k] += c.p[0][0];
+      sl.p[1][k] = (unsigned long long)min((int64_t)sl.p[1][k], (int64_t)c.p[1][0]);
+      sl.p[2][k] = (unsigned long long)max((int64_t)sl.p[2][k], (int64_t)c.p[2][0]);
+      continue;
+    }
+    const int64_t k = tail + j - 1;
+    const int64_t st = c.e_ts[j - 1];
+    if (n != 0 && c.tf[j] < st) atomicOr((unsigned long long*)&a.meta->err, 1ull);
+    sl.ts[k] = st;
+    sl.tl[k] = max(st, (int64_t)c.tl[j]);  // tLast starts at tStart (S/slice/AbstractSlice.java:15-23)
+    sl.cs[k] = a.C + c.e_pos[j - 1];
+    sl.cnt[k] = n;
+    sl.p[0][k] = c.p[0][j];
+    sl.p[1][k] = c.p[1][j];
+    sl.p[2][k] = c.p[2][j];
+  }
+}
+
+__global__ void count_nedges_kernel(CPushArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t last = a.nsteps - 1;
+  a.meta->n_edges = a.stepbase[last] + a.stepc[last];
+}
+
+__global__ void count_finish_kernel(CPushArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  m.tail += m.n_edges;
+  m.prev_max = max(m.prev_max, (int64_t)a.steppre[a.nsteps - 1]);
+}
+
+// first push of the stream: the oldest slice will be the one the first tuple opens (tStart = its ts)
+__global__ void count_first_start_kernel(CPushArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  m.first_start = m.tail > m.head ? a.sl.ts[m.head] : a.ts[0];
+}
+
+// ---------------------------------------------------------------- watermark
+__device__ __forceinline__ int64_t last_le(const int64_t* key, int64_t lo, int64_t hi, int64_t x) {
+  // last index in [lo, hi) with key <= x (key nondecreasing), lo - 1 if none
+  int64_t l = lo, h = hi;
+  while (l < h) {
+    const int64_t mid = (l + h) >> 1;
+    if (key[mid] <= x) l = mid + 1; else h = mid;
+  }
+  return l - 1;
+}
+
+__global__ void count_wm_find_kernel(CWmArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  const int64_t head = m.head, tail = m.tail;
+  m.range_err = 0;
+  if (tail <= head) {
+    m.wm_status = 1;
+    return;
+  }
+  m.oldest = a.sl.ts[head];
+  int64_t idx = last_le(a.sl.ts, head, tail, a.wm);  // findSliceIndexByTimestamp(wm)
+  if (idx < head) {
+    m.wm_status = 2;  // getSlice(-1)
+    return;
+  }
+  if (a.sl.tl[idx] >= a.wm && idx > head) idx--;
+  m.cend = a.sl.cs[idx] + (int64_t)a.sl.cnt[idx];  // cLast
+  m.wm_status = 0;
+}
+
+// LazyAggregateStore.aggregate start/end index (time terms with no time windows: minTs = MAX, maxTs = 0)
+__global__ void count_wm_range_kernel(CWmArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  const int64_t head = m.head, tail = m.tail, S = tail - head;
+  auto rel = [&](int64_t i) { return i < head ? (int64_t)-1 : i - head; };
+  // cLast is not stored; cStart is nondecreasing, findSliceIndexByCount = last slice with cStart <= c
+  int64_t si = max(rel(last_le(a.sl.ts, head, tail, JMAX)), (int64_t)0);
+  si = min(si, rel(last_le(a.sl.cs, head, tail, a.min_count)));
+  int64_t ei = min(S - 1, rel(last_le(a.sl.ts, head, tail, 0)));
+  ei = max(ei, rel(last_le(a.sl.cs, head, tail, a.max_count)));
+  if (si < 0 && si <= ei) {
+    m.range_err = 1;
+    si = 0;
+  }
+  m.r_lo = head + si;
+  m.r_hi = head + ei + 1;
+}
+
+// exclusive prefix sums of cnt and sum over [r_lo, r_hi): single-block chunks + carry (sizes here are the
+// retained slices a watermark touches)
+__global__ __launch_bounds__(1024) void count_pre_block_kernel(CWmArgs a, unsigned long long* bsum) {
+  __shared__ unsigned long long wt[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t lo = a.meta->r_lo, hi = a.meta->r_hi, n = hi - lo;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + tid;
+  unsigned long long vc = i < n ? a.sl.cnt[lo + i] : 0, vs = i < n ? a.sl.p[0][lo + i] : 0;
+  unsigned long long ic = vc, is = vs;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long uc = __shfl_up(ic, o), us = __shfl_up(is, o);
+    if (lane >= o) {
+      ic += uc;
+      is += us;
+    }
+  }
+  if (lane == 63) {
+    wt[0][wid] = ic;
+    wt[1][wid] = is;
+  }
+  __syncthreads();
+  unsigned long long ac = 0, as = 0;
+  for (int w = 0; w < wid; w++) {
+    ac += wt[0][w];
+    as += wt[1][w];
+  }
+  if (i < n) {
+    a.pre_cnt[i] = ic - vc + ac;
+    a.pre_sum[i] = is - vs + as;
+  }
+  if (tid == 1023) {
+    bsum[2 * blockIdx.x] = ic + ac;
+    bsum[2 * blockIdx.x + 1] = is + as;
+  }
+}
+// exclusive scan of the block sums (one workgroup, 1024 blocks per round) and the range total at index n
+__global__ __launch_bounds__(1024) void count_pre_bscan_kernel(CWmArgs a, unsigned long long* bsum, int64_t nblocks) {
+  __shared__ unsigned long long wt[2][16];
+  __shared__ unsigned long long carry[2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t n = a.meta->r_hi - a.meta->r_lo;
+  if (tid == 0) carry[0] = carry[1] = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < nblocks; b0 += 1024) {
+    const int64_t b = b0 + tid;
+    const unsigned long long vc = b < nblocks ? bsum[2 * b] : 0, vs = b < nblocks ? bsum[2 * b + 1] : 0;
+    unsigned long long ic = vc, is = vs;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long uc = __shfl_up(ic, o), us = __shfl_up(is, o);
+      if (lane >= o) {
+        ic += uc;
+        is += us;
+      }
+    }
+    if (lane == 63) {
+      wt[0][wid] = ic;
+      wt[1][wid] = is;
+    }
+    __syncthreads();
+    unsigned long long ac = carry[0], as = carry[1];
+    for (int w = 0; w < wid; w++) {
+      ac += wt[0][w];
+      as += wt[1][w];
+    }
+    if (b < nblocks) {
+      bsum[2 * b] = ic - vc + ac;  // exclusive
+      bsum[2 * b + 1] = is - vs + as;
+    }
+    __syncthreads();
+    if (tid == 1023) {
+      carry[0] = ic + ac;
+      carry[1] = is + as;
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && n >= 0) {
+    a.pre_cnt[n] = carry[0];
+    a.pre_sum[n] = carry[1];
+  }
+}
+__global__ __launch_bounds__(1024) void count_pre_add_kernel(CWmArgs a, const unsigned long long* bsum) {
+  const int64_t n = a.meta->r_hi - a.meta->r_lo;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (blockIdx.x == 0 || i >= n) return;
+  a.pre_cnt[i] += bsum[2 * blockIdx.x];
+  a.pre_sum[i] += bsum[2 * blockIdx.x + 1];
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void count_wm_agg_kernel(CWmArgs a) {
+  const int lane = threadIdx.x & (G - 1);
+  const int64_t wi = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  if (wi >= a.nw) return;
+  const int64_t ws = a.w_start[wi], we = a.w_end[wi];
+  const int64_t r_lo = a.meta->r_lo, r_hi = a.meta->r_hi;
+  // contained slices (AggregateWindowState.containsSlice, count measure: ws <= cStart && we >= cLast):
+  // cStart >= ws is a suffix, cLast = cStart + cnt <= we a prefix (both nondecreasing)
+  int64_t l = r_lo, h = r_hi;
+  while (l < h) {
+    const int64_t mid = (l + h) >> 1;
+    if (a.sl.cs[mid] < ws) l = mid + 1; else h = mid;
+  }
+  const int64_t lo = l;
+  l = lo;
+  h = r_hi;
+  while (l < h) {
+    const int64_t mid = (l + h) >> 1;
+    if (a.sl.cs[mid] + (int64_t)a.sl.cnt[mid] <= we) l = mid + 1; else h = mid;
+  }
+  const int64_t hi = l;
+  uint64_t cnt = 0, sw = 0;
+  double sf = 0.0;
+  int64_t mn = ID_MIN, mx = ID_MAX;
+  if (a.prefix) {
+    if (lane == 0 && hi > lo) {
+      cnt = a.pre_cnt[hi - r_lo] - a.pre_cnt[lo - r_lo];
+      sw = a.pre_sum[hi - r_lo] - a.pre_sum[lo - r_lo];
+    }
+  } else {
+    for (int64_t k = lo + lane; k < hi; k += G) {
+      const uint64_t c = a.sl.cnt[k];
+      if (c == 0) continue;
+      cnt += c;
+      if (a.need & NEED_SUM) {
+        if (a.vt == VT_F64) sf += __longlong_as_double((long long)a.sl.p[0][k]);
+        else sw += a.sl.p[0][k];
+      }
+      if (a.need & NEED_MIN) mn = min(mn, (int64_t)a.sl.p[1][k]);
+      if (a.need & NEED_MAX) mx = max(mx, (int64_t)a.sl.p[2][k]);
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+      cnt += (uint64_t)__shfl_xor((unsigned long long)cnt, o);
+      sw += (uint64_t)__shfl_xor((unsigned long long)sw, o);
+      sf += __shfl_xor(sf, o);
+      mn = min(mn, (int64_t)__shfl_xor((long long)mn, o));
+      mx = max(mx, (int64_t)__shfl_xor((long long)mx, o));
+    }
+  }
+  if (lane == 0) {
+    a.has_value[wi] = cnt ? 1 : 0;
+    const uint64_t sword = a.vt == VT_F64 && !a.prefix ? (uint64_t)__double_as_longlong(sf) : sw;
+    for (int k = 0; k < a.n_aggs; k++) a.values[k][wi] = cnt ? x::lower_value(a.agg_kind[k], cnt, sword, mn, mx) : 0;
+  }
+}
+
+__global__ void count_gc_kernel(CWmArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  if (m.tail <= m.head) return;
+  const int64_t idx = last_le(a.sl.ts, m.head, m.tail, a.gc_before);  // LazyAggregateStore.removeSlices
+  if (idx > m.head) m.head = idx;
+}
+
+}  // namespace ck
+
+// ---------------------------------------------------------------- launch wrappers
+template <int VT, int NEED>
+static void launch_ingest_cn(const CPushArgs& a, hipStream_t st) {
+  const int64_t waves = (a.nsteps + a.per_wave - 1) / a.per_wave;
+  hipLaunchKernelGGL((ck::count_ingest_kernel<VT, NEED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+}
+template <int VT>
+static void launch_ingest_cv(const CPushArgs& a, hipStream_t st) {
+  switch (a.need) {
+    case 0: launch_ingest_cn<VT, 0>(a, st); break;
+    case 1: launch_ingest_cn<VT, 1>(a, st); break;
+    case 2: launch_ingest_cn<VT, 2>(a, st); break;
+    case 3: launch_ingest_cn<VT, 3>(a, st); break;
+    case 4: launch_ingest_cn<VT, 4>(a, st); break;
+    case 5: launch_ingest_cn<VT, 5>(a, st); break;
+    case 6: launch_ingest_cn<VT, 6>(a, st); break;
+    default: launch_ingest_cn<VT, 7>(a, st); break;
+  }
+}
+
+hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
+
+// everything of one push after the bitmap was cleared; premax_tmp: >= nsteps/1024 + 2 words
+hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, int64_t* scan_tmp,
+                             long long* premax_tmp, hipStream_t st, hipEvent_t ingest_start,
+                             hipEvent_t ingest_end) {
+  if (a.n <= 0) return hipSuccess;
+  {
+    const int64_t th = std::max<int64_t>(1, std::min<int64_t>(max_points_per_window, 1 << 16));
+    const unsigned bx = (unsigned)((th + 255) / 256);
+    hipLaunchKernelGGL(ck::count_mark_kernel, dim3(bx, (unsigned)std::max(1, a.n_wins)), dim3(256), 0, st, a);
+  }
+  hipLaunchKernelGGL(ck::count_stepc_kernel, dim3((unsigned)((a.nsteps + 255) / 256)), dim3(256), 0, st, a);
+  hipError_t e = launch_scan_i64(a.stepc, a.stepbase, a.nsteps, scan_tmp, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ck::count_nedges_kernel, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(ck::count_cells_init_kernel, dim3((unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 4096)),
+                     dim3(256), 0, st, a.cells, a.cell_cap);
+  hipLaunchKernelGGL(ck::count_first_start_kernel, dim3(1), dim3(64), 0, st, a);
+  if (ingest_start) (void)hipEventRecord(ingest_start, st);
+  if (a.vt == VT_I32) launch_ingest_cv<VT_I32>(a, st);
+  else if (a.vt == VT_I64) launch_ingest_cv<VT_I64>(a, st);
+  else launch_ingest_cv<VT_F64>(a, st);
+  if (ingest_end) (void)hipEventRecord(ingest_end, st);
+  // step prefix max
+  const int64_t nb = (a.nsteps + 1023) / 1024;
+  hipLaunchKernelGGL(ck::count_premax_block_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.stepmax, a.steppre,
+                     a.nsteps, premax_tmp);
+  if (nb > 1) {
+    hipLaunchKernelGGL(ck::count_premax_block_kernel, dim3((unsigned)((nb + 1023) / 1024)), dim3(1024), 0, st,
+                       premax_tmp, premax_tmp, nb, premax_tmp + nb);
+    if (nb > 1024) return hipErrorInvalidValue;  // > 2^28 tuples per push: split the push
+    hipLaunchKernelGGL(ck::count_premax_carry_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.steppre, a.nsteps,
+                       premax_tmp);
+  }
+  hipLaunchKernelGGL(ck::count_edges_kernel, dim3((unsigned)((a.nsteps * 64 + 255) / 256)), dim3(256), 0, st, a);
+  const unsigned ab = (unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 8192);
+  if (a.vt == VT_F64) hipLaunchKernelGGL(ck::count_append_kernel<VT_F64>, dim3(ab), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(ck::count_append_kernel<VT_I32>, dim3(ab), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ck::count_finish_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_wm_find(const CWmArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(ck::count_wm_find_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+// range + (prefix sums) + per-window aggregation + GC; range_blocks = upper bound of (r_hi - r_lo + 1) / 1024
+hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st) {
+  hipLaunchKernelGGL(ck::count_wm_range_kernel, dim3(1), dim3(64), 0, st, a);
+  if (a.nw > 0) {
+    if (a.prefix) {
+      hipLaunchKernelGGL(ck::count_pre_block_kernel, dim3((unsigned)std::max<int64_t>(1, range_blocks)), dim3(1024), 0,
+                         st, a, bsum);
+      hipLaunchKernelGGL(ck::count_pre_bscan_kernel, dim3(1), dim3(1024), 0, st, a, bsum,
+                         std::max<int64_t>(1, range_blocks));
+      hipLaunchKernelGGL(ck::count_pre_add_kernel, dim3((unsigned)std::max<int64_t>(1, range_blocks)), dim3(1024), 0,
+                         st, a, bsum);
+    }
+    hipLaunchKernelGGL(ck::count_wm_agg_kernel<16>, dim3((unsigned)((a.nw + 15) / 16)), dim3(256), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(ck::count_gc_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace scotty

@@ -17,6 +17,7 @@
 
 #include "../../include/scotty_mi355x.h"
 #include "device_common.h"
+#include "count_engine.h"
 #include "exact_engine.h"
 
 namespace scotty {
@@ -136,9 +137,11 @@ struct scotty_op {
   int mode = 0;                       // 0 undecided, 1 grid, 2 exact
   std::vector<XWinDef> xwins;         // every window, registration order
   XEngine* x = nullptr;
+  CEngine* c = nullptr;  // mode 3: count-window path (count_engine.h)
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
   bool x_lane_off = false;
+  bool x_count_off = false;  // tuning: count-window operators on the exact engine instead of the count path
   uint64_t x_pushed = 0;
   std::vector<uint32_t> r_key;
   // sharded grid path (scotty_shard_*)
@@ -639,6 +642,7 @@ void scotty_destroy(scotty_op* op) {
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
+  delete op->c;
   F(op->d_shrank); F(op->d_shflag); F(op->d_cix); F(op->d_cixmeta);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
@@ -656,6 +660,18 @@ int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b
     return fail(op, SCOTTY_ERR_ARG, "window size / slide must be positive");
   if (kind == SCOTTY_WIN_SESSION && a < 0) return fail(op, SCOTTY_ERR_ARG, "session gap must be >= 0");
   const bool exact_only = kind == SCOTTY_WIN_SESSION || measure == SCOTTY_MEASURE_COUNT;
+  if (op->mode == 3) {  // count path: more count windows mid-stream (the pending count edge keeps its value)
+    if (kind == SCOTTY_WIN_SESSION || measure != SCOTTY_MEASURE_COUNT)
+      return fail(op, SCOTTY_ERR_UNSUPPORTED, "time / session window added to a count-window operator after elements "
+                                              "were processed");
+    op->xwins.push_back({kind, measure, a, b});
+    int rc = op->c->configure(op->xwins, op->aggs, op->max_lateness);
+    if (rc) {
+      op->xwins.pop_back();
+      return fail(op, rc, op->c->err);
+    }
+    return SCOTTY_OK;
+  }
   if (op->mode == 2) {  // exact engine: reconfigure (windows may be added mid-stream, S/WindowManager.java:121-147)
     op->xwins.push_back({kind, measure, a, b});
     int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
@@ -710,6 +726,10 @@ int scotty_add_aggregation(scotty_op* op, int kind) {
 int scotty_set_max_lateness(scotty_op* op, int64_t l) {
   if (!op) return SCOTTY_ERR_ARG;
   op->max_lateness = l;
+  if (op->mode == 3) {
+    int rc = op->c->configure(op->xwins, op->aggs, op->max_lateness);
+    if (rc) return fail(op, rc, op->c->err);
+  }
   if (op->mode == 2) {
     int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
     if (rc) return fail(op, rc, op->x->err);
@@ -726,6 +746,22 @@ static int decide_mode(scotty_op* op) {
     if (w.kind == SCOTTY_WIN_SESSION || w.measure == SCOTTY_MEASURE_COUNT) exact = true;
   if (!exact) {
     op->mode = 1;
+    return SCOTTY_OK;
+  }
+  bool count_only = !op->keyed && !op->xwins.empty() && !op->x_count_off;
+  for (const XWinDef& w : op->xwins)
+    if (w.kind == SCOTTY_WIN_SESSION || w.measure != SCOTTY_MEASURE_COUNT) count_only = false;
+  if (count_only) {  // count_common.h: edges are a function of counts, one micro-batch = segmented reduction
+    op->c = new CEngine();
+    std::string e;
+    int rc = op->c->init(op->device, op->stream, op->vt, e);
+    if (!rc) rc = op->c->configure(op->xwins, op->aggs, op->max_lateness);
+    if (!rc && op->last_watermark != -1) rc = op->c->set_last_watermark(op->last_watermark);
+    if (rc) {
+      op->failed = true;
+      return fail(op, rc, e.empty() ? op->c->err : e);
+    }
+    op->mode = 3;
     return SCOTTY_OK;
   }
   op->x = new XEngine();
@@ -749,6 +785,27 @@ static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int6
   if (n <= 0) return SCOTTY_OK;
   int rc = decide_mode(op);
   if (rc) return rc;
+  if (op->mode == 3) {
+    op->pending.push_back({d_ts, d_val, n, op->push_seq++});
+    op->x_pushed += (uint64_t)n;
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (op->timing) {
+      if (!op->ev_pool.empty()) {
+        ev = op->ev_pool.back();
+        op->ev_pool.pop_back();
+      } else {
+        HIPCHK(hipEventCreate(&ev.first));
+        HIPCHK(hipEventCreate(&ev.second));
+      }
+    }
+    rc = op->c->push(d_ts, d_val, n, ev.first, ev.second);
+    if (rc) return fail(op, rc, op->c->err);
+    if (op->timing) {
+      op->ev_pending.push_back(ev);
+      op->t_tuples += n;
+    }
+    return SCOTTY_OK;
+  }
   if (op->mode == 2) {
     op->pending.push_back({d_ts, d_val, n, op->push_seq++});
     op->x_pushed += (uint64_t)n;
@@ -837,8 +894,17 @@ int scotty_process_keyed_elements_device(scotty_op* op, const uint32_t* d_key, c
 static int exact_watermark(scotty_op* op, int64_t wm, scotty_windows* out, bool to_host) {
   XResult& r = op->xr;
   const uint64_t dropped_before = op->dropped;
-  int rc = op->x->watermark(wm, r, to_host);
-  if (rc) return fail(op, rc, op->x->err);
+  int rc = op->mode == 3 ? op->c->watermark(wm, r, to_host) : op->x->watermark(wm, r, to_host);
+  if (rc) return fail(op, rc, op->mode == 3 ? op->c->err : op->x->err);
+  if (op->mode == 3) {  // ingest-kernel timing of the interval (scotty_enable_timing)
+    for (auto& e : op->ev_pending) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) op->t_ms += ms;
+      op->t_launches++;
+      op->ev_pool.push_back(e);
+    }
+    op->ev_pending.clear();
+  }
   op->dropped = r.dropped;
   op->processed = op->x_pushed - r.dropped;
   for (void* p : op->owned) (void)hipFree(p);
@@ -874,12 +940,12 @@ static int exact_watermark(scotty_op* op, int64_t wm, scotty_windows* out, bool 
 int scotty_process_watermark_device(scotty_op* op, int64_t wm, scotty_windows* out) {
   if (!op) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
-  if (op->mode != 2) {
+  if (op->mode != 2 && op->mode != 3) {
     if (op->mode == 0 && op->keyed) {  // keyed op without any tuple yet: no operators, no windows
       if (out) std::memset(out, 0, sizeof(*out));
       return SCOTTY_OK;
     }
-    return fail(op, SCOTTY_ERR_UNSUPPORTED, "device results are provided by the exact engine only");
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "device results are provided by the exact engine and count path only");
   }
   return exact_watermark(op, wm, out, false);
 }
@@ -963,7 +1029,7 @@ int64_t scotty_key_count(scotty_op* op) { return (op && op->x) ? op->x->key_coun
 int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
   if (!op) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
-  if (op->mode == 2) return exact_watermark(op, wm, out, true);
+  if (op->mode == 2 || op->mode == 3) return exact_watermark(op, wm, out, true);
   if (op->keyed) {  // keyed op without any tuple yet: no per-key operators exist
     if (out) std::memset(out, 0, sizeof(*out));
     return SCOTTY_OK;
@@ -1087,6 +1153,7 @@ uint64_t scotty_dropped_count(scotty_op* op) { return op ? op->dropped : 0; }
 uint64_t scotty_processed_count(scotty_op* op) { return op ? op->processed : 0; }
 int64_t scotty_slice_count(scotty_op* op) {
   if (!op) return 0;
+  if (op->mode == 3) return op->c->slice_count();
   if (op->mode == 2) {
     if (op->keyed) return -1;
     int64_t c = 0;
@@ -1135,6 +1202,11 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (std::strcmp(key, "exact_serial") == 0) {
     if (op->mode != 0) return SCOTTY_ERR_ARG;
     op->x_serial = value != 0;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "count_path") == 0) {  // 0: count-window operators on the exact engine (A/B)
+    if (op->mode != 0) return SCOTTY_ERR_ARG;
+    op->x_count_off = value == 0;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_lane") == 0) {  // 0: wavefront-per-key replay even where the lane path applies

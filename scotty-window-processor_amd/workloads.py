@@ -49,6 +49,12 @@ def random_tumbling_sizes(n=1000, lo=1, hi=20, seed=10):
     return out
 
 
+def random_count_sizes(n=1000, lo=1, hi=20, seed=10):
+    """BenchmarkRunner.getAssigner("randomCount(n,lo,hi)"): TumblingWindow(Count, (int) size), Random(10)."""
+    r = JavaRandom(seed)
+    return [int(lo + r.nextDouble() * (hi - lo)) for _ in range(n)]
+
+
 def stream(n, rate_per_ms, t0=0, ooo_frac=0.0, max_delay=0, seed=0, value_type="i32", gaps=None):
     """Arrival-ordered (ts, value) columns.
 

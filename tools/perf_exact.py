@@ -20,7 +20,7 @@ import bench  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["c2s", "c3", "c4"])
+    ap.add_argument("which", choices=["c2s", "c3", "c4", "c5"])
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--keys", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=5)
@@ -32,6 +32,8 @@ def main():
     if args.which == "c2s":
         tune = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in args.tune}
         r = bench.extra_c2s(pkg, dev, args.batch or (1 << 27), args.steps, tune=tune, ooo=args.ooo)
+    elif args.which == "c5":
+        r = bench.extra_c5(pkg, dev, args.batch or (1 << 27), args.steps)
     elif args.which == "c3":
         r = bench.extra_c3(pkg, dev, args.batch or (1 << 26), args.steps)
     else:
