@@ -132,10 +132,17 @@ int scotty_process_watermark_device(scotty_op* op, int64_t watermark_ts, scotty_
  *   3. scotty_shard_commit(op, gathered, G): every rank decides the same slice edges (StreamSlicer rule from
  *      the global first crossings, S/StreamSlicer.java:55-116) and folds every rank's partials.
  * Watermarks then run unchanged (and identically) on every rank.  Context-free time windows only (the grid
- * path); other configurations return SCOTTY_ERR_UNSUPPORTED. */
+ * path) or count windows only (the count path, with scotty_shard_push_counted); other configurations return
+ * SCOTTY_ERR_UNSUPPORTED. */
 size_t scotty_shard_xbytes(scotty_op* op);
 int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0, void* d_xbuf);
 int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world);
+/* Step 1 for operators with count windows (also accepted by time-window operators, which ignore the counts):
+ * n_before = tuples of lower ranks in this micro-batch, n_total = the micro-batch's tuples over all ranks (the
+ * chunk's first tuple has count currentCount + n_before, S/WindowManager.java:196-198).  Count windows shard
+ * only in-order streams; the record holds per-rank count cells (count_common.h). */
+int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
+                              int64_t n_before, int64_t n_total, void* d_xbuf);
 
 /* Number of keys (operators) of a keyed op. */
 int64_t scotty_key_count(scotty_op* op);

@@ -145,6 +145,7 @@ def lib():
             "scotty_shard_xbytes": (ctypes.c_size_t, [P]),
             "scotty_shard_push": (ctypes.c_int, [P, P, P, ctypes.c_size_t, i64, P]),
             "scotty_shard_commit": (ctypes.c_int, [P, P, ctypes.c_int]),
+            "scotty_shard_push_counted": (ctypes.c_int, [P, P, P, ctypes.c_size_t, i64, i64, i64, P]),
             "scotty_dropped_count": (u64, [P]),
             "scotty_processed_count": (u64, [P]),
             "scotty_slice_count": (i64, [P]),
@@ -311,6 +312,10 @@ class SlicingWindowOperator:
         self._flush()
         self._check(self._l.scotty_shard_push(self._h, ts_ptr, val_ptr, n, ts0, xbuf_ptr))
 
+    def shardPushCounted(self, ts_ptr, val_ptr, n, ts0, n_before, n_total, xbuf_ptr):
+        self._flush()
+        self._check(self._l.scotty_shard_push_counted(self._h, ts_ptr, val_ptr, n, ts0, n_before, n_total, xbuf_ptr))
+
     def shardCommit(self, gathered_ptr, world):
         self._check(self._l.scotty_shard_commit(self._h, gathered_ptr, world))
 
@@ -409,7 +414,7 @@ class ShardedSlicingWindowOperator:
     every rank holds the same SlicingWindowOperator and feeds a contiguous arrival chunk of each global
     micro-batch; one all-gather of the per-rank exchange records (RCCL over xGMI for backend "nccl"; host
     staging for "gloo") joins them, and every rank then holds the identical slice store, so processWatermark
-    is purely local.  Context-free time windows only."""
+    is purely local.  Context-free time windows (the grid path) or count windows (the count path)."""
 
     def __init__(self, device=0, value_type=VALUE_I32, group=None):
         import torch
@@ -435,11 +440,20 @@ class ShardedSlicingWindowOperator:
                 self._hg = t.empty(words * self.world, dtype=t.int64)
         return self._xb, self._gb
 
-    def processChunk(self, ts_ptr, val_ptr, n, ts0=0):
+    def processChunk(self, ts_ptr, val_ptr, n, ts0=0, n_before=None, n_total=None):
         """This rank's arrival chunk of the next global micro-batch (device pointers); ts0 = the global first
-        tuple's timestamp (read on the very first batch only)."""
+        tuple's timestamp (read on the very first batch only).  n_before / n_total: tuples of the lower ranks /
+        of all ranks in this micro-batch (count windows number tuples globally); gathered when not given."""
+        if n_before is None or n_total is None:
+            t = self.torch
+            mine = t.tensor([n], dtype=t.int64, device=self.dev if not self.staged else "cpu")
+            allv = t.empty(self.world, dtype=t.int64, device=mine.device)
+            self.dist.all_gather_into_tensor(allv, mine, group=self.group)
+            sizes = allv.tolist()
+            r = self.dist.get_rank(self.group)
+            n_before, n_total = int(sum(sizes[:r])), int(sum(sizes))
         xb, gb = self._bufs()
-        self.op.shardPush(ts_ptr, val_ptr, n, ts0, xb.data_ptr())
+        self.op.shardPushCounted(ts_ptr, val_ptr, n, ts0, n_before, n_total, xb.data_ptr())
         if self.staged:
             self._hx.copy_(xb)
             self.dist.all_gather_into_tensor(self._hg, self._hx, group=self.group)

@@ -53,8 +53,19 @@ struct CMeta {
   int64_t oldest;          // tStart of the oldest retained slice
   int64_t r_lo, r_hi;      // aggregate scan range, absolute [r_lo, r_hi)
   int64_t range_err;       // startIndex == -1 with a non-empty loop (getSlice(-1))
-  int64_t pad[3];
+  uint64_t late_push;      // dropped tuples of the current push (folded into late_total by the commit)
+  int64_t pad[2];
 };
+
+// Time/arrival-range sharding of one count-window stream over G ranks (BASELINE configs[4]):
+// rank r ingests its arrival chunk at global count C + n_before_r into local cells and exports one record;
+// every rank commits the G records in rank order.  Record (int64 words):
+//   [0..15]  header: chunk max ts, dropped tuples, edges E_r, chunk size, count of the chunk's first tuple,
+//            overflow (E_r + 1 > cap)
+//   cells    cap x {cnt, tLast, tFirst, sum, min, max}   cell 0 = tuples before the chunk's first edge
+//   edges    cap x {global count of the edge, max ts before it within the chunk (INT64_MIN if none)}
+constexpr int CSHARD_HDR = 16;
+__host__ __device__ inline int64_t cshard_words(int64_t cap) { return CSHARD_HDR + 8 * cap; }
 
 struct CWin {  // one context-free count window, registration order
   int32_t kind;
@@ -82,6 +93,19 @@ struct CPushArgs {
   int64_t per_wave;      // steps per wave
   CCells cells;
   int64_t cell_cap;
+  CSlices sl;
+  CMeta* meta;
+  int32_t shard;         // ingest for a shard record: local prefix max only, no own-ts substitution
+  int64_t ts0;           // shard: timestamp of the stream's first tuple (first slice start)
+};
+
+struct CShardArgs {
+  const int64_t* gathered;  // world records
+  int32_t world;
+  int64_t cap;
+  int64_t ts0;
+  int32_t vt;
+  long long* plan;          // [2 * world] slice offset, prefix max before the rank
   CSlices sl;
   CMeta* meta;
 };

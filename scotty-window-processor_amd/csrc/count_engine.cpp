@@ -11,6 +11,8 @@ namespace scotty {
 hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, int64_t* scan_tmp,
                              long long* premax_tmp, hipStream_t st, hipEvent_t ingest_start, hipEvent_t ingest_end);
 hipError_t launch_count_wm_find(const CWmArgs& a, hipStream_t st);
+hipError_t launch_count_export(const CPushArgs& a, int64_t* rec, int64_t cap, hipStream_t st);
+hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hipStream_t st);
 hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st);
 hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st);
 
@@ -79,6 +81,7 @@ CEngine::~CEngine() {
   dfree(d_wstart); dfree(d_wend); dfree(d_meas); dfree(d_has);
   for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
   dfree(d_pre_cnt); dfree(d_pre_sum); dfree(d_bsum);
+  dfree(d_plan);
 }
 
 int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
@@ -179,18 +182,25 @@ int CEngine::grow_slices(int64_t need_more) {
   return SCOTTY_OK;
 }
 
-int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t ev0, hipEvent_t ev1) {
-  if (failed) return SCOTTY_ERR_STATE;
-  const size_t vb = vt == VT_I32 ? 4 : 8;
-  while (n > MAX_PUSH) {  // keep one launch chain within the step prefix-max depth
-    int rc = push(d_ts, d_val, MAX_PUSH, nullptr, nullptr);
-    if (rc) return rc;
-    d_ts += MAX_PUSH;
-    d_val = (const unsigned char*)d_val + MAX_PUSH * vb;
-    n -= MAX_PUSH;
+// edges of counts [lo_count, hi_count) of the stream: the pending edge and every union grid point after it
+int64_t CEngine::batch_edges_bound(int64_t lo_count, int64_t hi_count) const {
+  int64_t mark_from, b = 0;
+  if (pending == JMIN) {
+    if (count >= lo_count && count < hi_count) b = 1;
+    mark_from = next_point(count + 1);
+  } else {
+    mark_from = pending;
   }
-  if (n <= 0) return SCOTTY_OK;
-  // edges of this batch: the pending edge and every union grid point after it below count + n
+  const int64_t lo = std::max(lo_count, mark_from);
+  for (const CWin& w : wins) b += points_in(w, lo, hi_count);
+  return b;
+}
+
+// buffers and launch arguments for ingesting counts [C, C + n) (the whole stream's batch or a rank's chunk)
+int CEngine::prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, CPushArgs& a, int64_t& ebound,
+                     int64_t& maxp) {
+  (void)range_lo;
+  (void)range_hi;
   int64_t mark_from, extra = -1;
   if (pending == JMIN) {  // the stream's first tuple appends the first slice (S/StreamSlicer.java:37-43)
     extra = count;
@@ -198,8 +208,9 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
   } else {
     mark_from = pending;
   }
-  const int64_t lo = std::max(count, mark_from), hi = count + n;
-  int64_t ebound = extra >= 0 ? 1 : 0, maxp = 0;
+  const int64_t lo = std::max(C, mark_from), hi = C + n;
+  ebound = (extra >= C && extra < hi) ? 1 : 0;
+  maxp = 0;
   for (const CWin& w : wins) {
     const int64_t p = points_in(w, lo, hi);
     ebound += p;
@@ -207,7 +218,6 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
   }
   if (ebound > MAX_EDGES_PER_PUSH)
     return fail(SCOTTY_ERR_UNSUPPORTED, "count windows create more than 2^26 slices in one micro-batch");
-  // capacities
   const int64_t nwords = (n + 31) / 32, nsteps = (n + CSTEP - 1) / CSTEP;
   if (nwords > bcap) {
     dfree(d_bits);
@@ -235,18 +245,12 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
     CCHK(dalloc(&cells.e_ts, ccap));
     for (int k = 0; k < NPART; k++) CCHK(dalloc(&cells.p[k], ccap));
   }
-  if (tail_ub + ebound > scap) {
-    int rc = grow_slices(ebound);
-    if (rc) return rc;
-  }
   CCHK(hipMemsetAsync(d_bits, 0, nwords * 4, stream));
-  CPushArgs a{};
-  a.ts = d_ts;
-  a.val = d_val;
+  a = CPushArgs{};
   a.n = n;
   a.bits = d_bits;
   a.nwords = nwords;
-  a.C = count;
+  a.C = C;
   a.mark_from = mark_from;
   a.extra_point = extra;
   a.wins = d_wins;
@@ -263,10 +267,94 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
   a.cell_cap = ebound + 1;
   a.sl = sl;
   a.meta = d_meta;
+  return SCOTTY_OK;
+}
+
+int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t ev0, hipEvent_t ev1) {
+  if (failed) return SCOTTY_ERR_STATE;
+  const size_t vb = vt == VT_I32 ? 4 : 8;
+  while (n > MAX_PUSH) {  // keep one launch chain within the step prefix-max depth
+    int rc = push(d_ts, d_val, MAX_PUSH, nullptr, nullptr);
+    if (rc) return rc;
+    d_ts += MAX_PUSH;
+    d_val = (const unsigned char*)d_val + MAX_PUSH * vb;
+    n -= MAX_PUSH;
+  }
+  if (n <= 0) return SCOTTY_OK;
+  CPushArgs a;
+  int64_t ebound = 0, maxp = 0;
+  int rc = prepare(count, n, count, count + n, a, ebound, maxp);
+  if (rc) return rc;
+  if (tail_ub + ebound > scap) {
+    rc = grow_slices(ebound);
+    if (rc) return rc;
+    a.sl = sl;
+  }
+  a.ts = d_ts;
+  a.val = d_val;
   CCHK(launch_count_push(a, maxp, d_scan, d_premax, stream, ev0, ev1));
   count += n;
   pending = (pending != JMIN && pending >= count) ? pending : next_point(count);
   tail_ub += ebound;
+  started = true;
+  return SCOTTY_OK;
+}
+
+int CEngine::shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64_t ts0, int64_t n_before,
+                        int64_t n_total, int64_t* d_rec) {
+  if (failed) return SCOTTY_ERR_STATE;
+  if (n_total > MAX_PUSH || n < 0 || n_before < 0 || n_before + n > n_total)
+    return fail(SCOTTY_ERR_ARG, "shard chunk outside its micro-batch (or micro-batch above 2^28 tuples)");
+  shard_total = n_total;
+  if (pending == JMIN) shard_ts0 = ts0;
+  CPushArgs a;
+  int64_t ebound = 0, maxp = 0;
+  int rc = prepare(count + n_before, std::max<int64_t>(n, 1), count, count + n_total, a, ebound, maxp);
+  if (rc) return rc;
+  a.n = n;
+  a.ts = d_ts;
+  a.val = d_val;
+  a.shard = 1;
+  a.ts0 = shard_ts0;
+  if (n > 0) {
+    CCHK(launch_count_push(a, maxp, d_scan, d_premax, stream, nullptr, nullptr));
+    CCHK(launch_count_export(a, d_rec, shard_cap, stream));
+  } else {  // an empty chunk: no tuples, no edges, prefix max -inf
+    std::vector<int64_t> h(CSHARD_HDR, 0);
+    h[0] = JMIN;
+    h[4] = a.C;
+    CCHK(hipMemsetAsync(d_rec, 0, shard_words() * 8, stream));
+    CCHK(hipMemcpyAsync(d_rec, h.data(), CSHARD_HDR * 8, hipMemcpyHostToDevice, stream));
+  }
+  CCHK(hipStreamSynchronize(stream));  // the record is read by the collective on another stream
+  return SCOTTY_OK;
+}
+
+int CEngine::shard_commit(const int64_t* d_gathered, int world) {
+  if (failed) return SCOTTY_ERR_STATE;
+  const int64_t eb = batch_edges_bound(count, count + shard_total);
+  if (tail_ub + eb > scap) {
+    int rc = grow_slices(eb);
+    if (rc) return rc;
+  }
+  if (world > plan_cap) {
+    dfree(d_plan);
+    plan_cap = world;
+    CCHK(dalloc(&d_plan, 2 * (int64_t)world));
+  }
+  CShardArgs a{};
+  a.gathered = d_gathered;
+  a.world = world;
+  a.cap = shard_cap;
+  a.ts0 = shard_ts0;
+  a.vt = vt;
+  a.plan = d_plan;
+  a.sl = sl;
+  a.meta = d_meta;
+  CCHK(launch_count_shard_commit(a, std::min(eb, shard_cap), stream));
+  count += shard_total;
+  pending = (pending != JMIN && pending >= count) ? pending : next_point(count);
+  tail_ub += eb;
   started = true;
   return SCOTTY_OK;
 }
@@ -318,6 +406,8 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     return fail(SCOTTY_ERR_UNSUPPORTED,
                 "a tuple older than its count slice would be inserted into an earlier LazySlice and shift records "
                 "(S/SliceManager.java:64-85): not implemented on the MI355X count path");
+  if (h_meta->err & 4)
+    return fail(SCOTTY_ERR_NOMEM, "count-path shard record capacity exceeded (scotty_tune \"shard_count_cells\")");
   if (h_meta->err)
     return fail(SCOTTY_ERR_STATE, "internal: count path lost tuples");
   tail_ub = h_meta->tail;

@@ -18,6 +18,14 @@ class CEngine {
   // WindowManager.addWindowAssigner / addAggregation / setMaxLateness (S/WindowManager.java:121-202)
   int configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness);
   int push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t ev0, hipEvent_t ev1);
+  // sharding of one stream over G ranks (count_common.h CSHARD_HDR): every rank pushes its arrival chunk
+  // (n_before tuples of lower ranks precede it in a micro-batch of n_total), the caller all-gathers the
+  // records of shard_words() int64 each, every rank commits them
+  int64_t shard_words() const { return cshard_words(shard_cap); }
+  int shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64_t ts0, int64_t n_before, int64_t n_total,
+                 int64_t* d_rec);
+  int shard_commit(const int64_t* d_gathered, int world);
+  int64_t shard_cap = 1 << 16;  // cells per rank record (scotty_tune "shard_count_cells")
   int watermark(int64_t wm, XResult& r, bool to_host);
   int set_last_watermark(int64_t lw) {
     last_wm = lw;
@@ -37,6 +45,11 @@ class CEngine {
     return rc;
   }
   int64_t next_point(int64_t x) const;  // smallest union count-grid point >= x (x >= 1)
+  int prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, CPushArgs& a, int64_t& ebound, int64_t& maxp);
+  int64_t batch_edges_bound(int64_t lo_count, int64_t hi_count) const;
+  int64_t shard_ts0 = INT64_MIN, shard_total = 0;
+  long long* d_plan = nullptr;
+  int plan_cap = 0;
   void trigger(int64_t last_count, int64_t cend1);
 
   int device = 0;

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   }
   if (cur >= 0) flush();
   const uint32_t nl = wred(n_late, [](uint32_t p, uint32_t q) { return p + q; });
-  if (lane == 0 && nl) atomicAdd((unsigned long long*)&a.meta->late_total, (unsigned long long)nl);
+  if (lane == 0 && nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
 }
 
 // ---------------------------------------------------------------- 4. edge positions and slice starts
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(256) void count_edges_kernel(CPushArgs a) {
   if (s >= a.nsteps) return;
   if (a.stepc[s] == 0) return;
   const int64_t base = s * CSTEP;
-  const int64_t prev = a.meta->prev_max;
+  const int64_t prev = a.shard ? JMIN : a.meta->prev_max;  // shard records carry the chunk-local prefix
   long long before = s > 0 ? a.steppre[s - 1] : JMIN;
   before = max(before, (long long)prev);
   // lane l holds offsets 4l .. 4l+3
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void count_edges_kernel(CPushArgs a) {
       a.cells.e_pos[e] = base + o;
       // max ts of every tuple before the edge (StreamSlicer.maxEventTime); the stream's first tuple sets it to its
       // own ts first (S/StreamSlicer.java:39-40)
-      a.cells.e_ts[e] = run == JMIN ? t[j] : run;
+      a.cells.e_ts[e] = (run == JMIN && !a.shard) ? t[j] : run;
     }
     run = max(run, t[j]);
   }
@@ -409,13 +409,15 @@ __global__ void count_finish_kernel(CPushArgs a) {
   CMeta& m = *a.meta;
   m.tail += m.n_edges;
   m.prev_max = max(m.prev_max, (int64_t)a.steppre[a.nsteps - 1]);
+  m.late_total += m.late_push;
 }
 
 // first push of the stream: the oldest slice will be the one the first tuple opens (tStart = its ts)
 __global__ void count_first_start_kernel(CPushArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   CMeta& m = *a.meta;
-  m.first_start = m.tail > m.head ? a.sl.ts[m.head] : a.ts[0];
+  m.first_start = m.tail > m.head ? a.sl.ts[m.head] : (a.shard ? a.ts0 : a.ts[0]);
+  m.late_push = 0;
 }
 
 // ---------------------------------------------------------------- watermark
@@ -624,6 +626,118 @@ __global__ void count_gc_kernel(CWmArgs a) {
   if (idx > m.head) m.head = idx;
 }
 
+// ---------------------------------------------------------------- sharding (count_common.h, CSHARD_HDR)
+__global__ __launch_bounds__(256) void count_export_kernel(CPushArgs a, int64_t* rec, int64_t cap) {
+  const CMeta& m = *a.meta;
+  const int64_t E = m.n_edges;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) {
+    rec[0] = a.steppre[a.nsteps - 1];
+    rec[1] = (int64_t)m.late_push;
+    rec[2] = E;
+    rec[3] = a.n;
+    rec[4] = a.C;
+    rec[5] = E + 1 > cap ? 1 : 0;
+  }
+  int64_t* cells = rec + CSHARD_HDR;
+  int64_t* edges = cells + 6 * cap;
+  for (int64_t j = g; j < cap; j += (int64_t)gridDim.x * blockDim.x) {
+    if (j <= E) {
+      int64_t* c = cells + 6 * j;
+      c[0] = (int64_t)a.cells.cnt[j];
+      c[1] = a.cells.tl[j];
+      c[2] = a.cells.tf[j];
+      c[3] = (int64_t)a.cells.p[0][j];
+      c[4] = (int64_t)a.cells.p[1][j];
+      c[5] = (int64_t)a.cells.p[2][j];
+    }
+    if (j < E) {
+      edges[2 * j] = a.C + a.cells.e_pos[j];
+      edges[2 * j + 1] = a.cells.e_ts[j];
+    }
+  }
+}
+
+// rank offsets into the slice list and the stream's max ts before each rank's chunk
+__global__ void count_shard_plan_kernel(CShardArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  const int64_t words = cshard_words(a.cap);
+  int64_t off = m.tail;
+  long long pm = m.prev_max;
+  for (int r = 0; r < a.world; r++) {
+    const int64_t* h = a.gathered + r * words;
+    if (h[5]) atomicOr((unsigned long long*)&m.err, 4ull);  // exchange capacity exceeded
+    a.plan[2 * r] = off;
+    a.plan[2 * r + 1] = pm;
+    off += h[5] ? 0 : h[2];
+    pm = max(pm, (long long)h[0]);
+  }
+}
+
+__global__ __launch_bounds__(256) void count_shard_append_kernel(CShardArgs a) {
+  const int r = blockIdx.y;
+  const int64_t words = cshard_words(a.cap);
+  const int64_t* rec = a.gathered + r * words;
+  if (rec[5]) return;
+  const int64_t E = rec[2];
+  const int64_t* cells = rec + CSHARD_HDR;
+  const int64_t* edges = cells + 6 * a.cap;
+  const int64_t off = a.plan[2 * r];
+  const int64_t pm = a.plan[2 * r + 1];
+  for (int64_t j = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= E; j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t* c = cells + 6 * j;
+    int64_t st = max(pm, edges[2 * (j - 1) + 1]);
+    if (st == JMIN) st = a.ts0;  // the stream's first tuple sets maxEventTime to its own ts (S/StreamSlicer.java:39-40)
+    const int64_t k = off + j - 1;
+    if (c[0] != 0 && c[2] < st) atomicOr((unsigned long long*)&a.meta->err, 1ull);
+    a.sl.ts[k] = st;
+    a.sl.tl[k] = max(st, c[1]);
+    a.sl.cs[k] = edges[2 * (j - 1)];
+    a.sl.cnt[k] = (unsigned long long)c[0];
+    a.sl.p[0][k] = (unsigned long long)c[3];
+    a.sl.p[1][k] = (unsigned long long)c[4];
+    a.sl.p[2][k] = (unsigned long long)c[5];
+  }
+}
+
+// cell 0 of every rank folds into the slice open when its chunk began, in rank (= arrival) order
+__global__ void count_shard_merge_kernel(CShardArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CMeta& m = *a.meta;
+  const int64_t words = cshard_words(a.cap);
+  int64_t edges_total = 0;
+  long long pm = m.prev_max;
+  uint64_t late = 0;
+  for (int r = 0; r < a.world; r++) {
+    const int64_t* rec = a.gathered + r * words;
+    late += (uint64_t)rec[1];
+    pm = max(pm, (long long)rec[0]);
+    if (rec[5]) continue;
+    edges_total += rec[2];
+    const int64_t* c = rec + CSHARD_HDR;
+    if (c[0] == 0) continue;
+    const int64_t k = a.plan[2 * r] - 1;
+    if (k < m.head) {
+      atomicOr((unsigned long long*)&m.err, 2ull);
+      continue;
+    }
+    if (c[2] < a.sl.ts[k]) atomicOr((unsigned long long*)&m.err, 1ull);
+    a.sl.cnt[k] += (unsigned long long)c[0];
+    a.sl.tl[k] = max(a.sl.tl[k], c[1]);
+    if (a.vt == VT_F64)
+      a.sl.p[0][k] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)a.sl.p[0][k]) +
+                                                             __longlong_as_double((long long)c[3]));
+    else
+      a.sl.p[0][k] += (unsigned long long)c[3];
+    a.sl.p[1][k] = (unsigned long long)min((int64_t)a.sl.p[1][k], c[4]);
+    a.sl.p[2][k] = (unsigned long long)max((int64_t)a.sl.p[2][k], c[5]);
+  }
+  m.tail += edges_total;
+  m.prev_max = pm;
+  m.late_total += late;
+}
+
 }  // namespace ck
 
 // ---------------------------------------------------------------- launch wrappers
@@ -682,10 +796,25 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
                        premax_tmp);
   }
   hipLaunchKernelGGL(ck::count_edges_kernel, dim3((unsigned)((a.nsteps * 64 + 255) / 256)), dim3(256), 0, st, a);
+  if (a.shard) return hipGetLastError();  // the caller exports (launch_count_export) instead of appending
   const unsigned ab = (unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 8192);
   if (a.vt == VT_F64) hipLaunchKernelGGL(ck::count_append_kernel<VT_F64>, dim3(ab), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ck::count_append_kernel<VT_I32>, dim3(ab), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ck::count_finish_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_export(const CPushArgs& a, int64_t* rec, int64_t cap, hipStream_t st) {
+  hipLaunchKernelGGL(ck::count_export_kernel, dim3((unsigned)std::min<int64_t>((cap + 255) / 256, 4096)), dim3(256), 0,
+                     st, a, rec, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hipStream_t st) {
+  hipLaunchKernelGGL(ck::count_shard_plan_kernel, dim3(1), dim3(64), 0, st, a);
+  const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_edges + 255) / 256, 4096));
+  hipLaunchKernelGGL(ck::count_shard_append_kernel, dim3(bx, (unsigned)a.world), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ck::count_shard_merge_kernel, dim3(1), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

@@ -141,6 +141,8 @@ struct scotty_op {
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
   bool x_lane_off = false;
+  int64_t shard_count_total = 0;
+  int64_t count_shard_cap = 1 << 16;
   bool x_count_off = false;  // tuning: count-window operators on the exact engine instead of the count path
   uint64_t x_pushed = 0;
   std::vector<uint32_t> r_key;
@@ -757,6 +759,7 @@ static int decide_mode(scotty_op* op) {
     int rc = op->c->init(op->device, op->stream, op->vt, e);
     if (!rc) rc = op->c->configure(op->xwins, op->aggs, op->max_lateness);
     if (!rc && op->last_watermark != -1) rc = op->c->set_last_watermark(op->last_watermark);
+    op->c->shard_cap = op->count_shard_cap;
     if (rc) {
       op->failed = true;
       return fail(op, rc, e.empty() ? op->c->err : e);
@@ -952,7 +955,12 @@ int scotty_process_watermark_device(scotty_op* op, int64_t wm, scotty_windows* o
 
 static int64_t shard_words(const scotty_op* op) { return SHARD_HDR + 6 * op->shard_kc + 2 * op->shard_kg; }
 
-size_t scotty_shard_xbytes(scotty_op* op) { return op ? (size_t)shard_words(op) * 8 : 0; }
+size_t scotty_shard_xbytes(scotty_op* op) {
+  if (!op) return 0;
+  if (op->mode == 0 && !op->keyed && !op->xwins.empty()) (void)decide_mode(op);
+  if (op->mode == 3) return (size_t)op->c->shard_words() * 8;
+  return (size_t)shard_words(op) * 8;
+}
 
 static ShardArgs shard_args(scotty_op* op) {
   ShardArgs a{};
@@ -984,8 +992,10 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
   if (op->keyed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "keyed operators shard by key: no exchange needed");
   int rc = decide_mode(op);
   if (rc) return rc;
+  if (op->mode == 3)
+    return fail(op, SCOTTY_ERR_ARG, "count windows: use scotty_shard_push_counted (the chunk's count offset)");
   if (op->mode != 1)
-    return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs context-free time windows only (the grid path)");
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs context-free time windows or count windows only");
   if (!op->has_fixed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs at least one context-free window");
   if (!op->d_shrank) {
     HIPCHK(hipMalloc(&op->d_shrank, op->shard_kg * 4));
@@ -1013,9 +1023,31 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
   return SCOTTY_OK;
 }
 
+int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
+                              int64_t n_before, int64_t n_total, void* d_xbuf) {
+  if (!op || !d_xbuf || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
+  if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->keyed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "keyed operators shard by key: no exchange needed");
+  int rc = decide_mode(op);
+  if (rc) return rc;
+  if (op->mode != 3) return scotty_shard_push(op, d_ts, d_val, n, ts0, d_xbuf);
+  if (((uintptr_t)d_ts & 15) || ((uintptr_t)d_val & 15))
+    return fail(op, SCOTTY_ERR_ARG, "device buffers must be 16-byte aligned");
+  rc = op->c->shard_push(d_ts, d_val, (int64_t)n, ts0, n_before, n_total, (int64_t*)d_xbuf);
+  if (rc) return fail(op, rc, op->c->err);
+  op->shard_count_total = n_total;
+  return SCOTTY_OK;
+}
+
 int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world) {
   if (!op || !d_gathered || world < 1 || world > 64) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
+  if (op->mode == 3) {
+    int rc = op->c->shard_commit((const int64_t*)d_gathered, world);
+    if (rc) return fail(op, rc, op->c->err);
+    op->x_pushed += (uint64_t)op->shard_count_total;  // replicated state: every rank counts the whole batch
+    return SCOTTY_OK;
+  }
   if (op->mode != 1 || !op->d_shrank) return fail(op, SCOTTY_ERR_STATE, "scotty_shard_push must come first");
   ShardArgs a = shard_args(op);
   a.gathered = (const int64_t*)d_gathered;
@@ -1202,6 +1234,11 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (std::strcmp(key, "exact_serial") == 0) {
     if (op->mode != 0) return SCOTTY_ERR_ARG;
     op->x_serial = value != 0;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "shard_count_cells") == 0) {  // cells per rank record of the count path's exchange
+    if (op->mode != 0 || value < 16 || value > (1 << 24)) return SCOTTY_ERR_ARG;
+    op->count_shard_cap = value;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "count_path") == 0) {  // 0: count-window operators on the exact engine (A/B)

@@ -2,7 +2,7 @@
 import numpy as np
 
 from helpers import product, interval_schedule
-from specs import Tumbling, Sliding, FixedBand, Time, SUM, COUNT, MIN, MAX
+from specs import Tumbling, Sliding, FixedBand, Time, Count, SUM, COUNT, MIN, MAX
 
 
 def case(cid):
@@ -20,6 +20,24 @@ def case(cid):
         ts, vals = wl.stream(6000, 0.25, t0=1000, ooo_frac=0.1, max_delay=3, seed=cid)
         ts = ts + np.cumsum(rng.integers(0, 4, size=len(ts)))
         sched = interval_schedule(ts, 40, lag=5, pushes_per_interval=3)
+        return cfg, ts, vals, sched
+    elif cid == 4:  # C5-like: randomCount count windows, in-order with ties, a few too-late tuples (dropped)
+        sizes = wl.random_count_sizes(50, 100, 5000, seed=10)
+        cfg = dict(windows=[Tumbling(Count, s) for s in sizes], aggs=[SUM, COUNT, MIN, MAX], lateness=1)
+        n = 300_000
+        ts = 50 + np.arange(n, dtype=np.int64) // 30
+        vals = rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+        late = rng.choice(np.arange(n // 3, n), size=4, replace=False)
+        ts[late] = 10
+        sched = interval_schedule(ts, 7, lag=0, pushes_per_interval=2)
+        return cfg, ts, vals, sched
+    elif cid == 5:  # dense count edges (every few tuples): cells straddle chunk cuts, edge-heavy steps
+        cfg = dict(windows=[Sliding(Count, 9, 4), Tumbling(Count, 7), FixedBand(Count, 1000, 30_000)],
+                   aggs=[SUM, MAX], lateness=20)
+        n = 60_000
+        ts = 1000 + np.arange(n, dtype=np.int64) // 3
+        vals = rng.integers(-1000, 1000, size=n, dtype=np.int64).astype(np.int32)
+        sched = interval_schedule(ts, 9, lag=3, pushes_per_interval=3)
         return cfg, ts, vals, sched
     else:           # lateness edge skipping on jumps + fixed band
         cfg = dict(windows=[Tumbling(Time, 13), FixedBand(Time, 5000, 2000)], aggs=[SUM, MAX], lateness=3)

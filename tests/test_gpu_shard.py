@@ -1,7 +1,7 @@
 """Time/arrival-range sharding of one non-keyed stream: 2 ranks (one process each, both on
 cuda:0, exchange over gloo with host staging -- the protocol is identical to RCCL device all-gathers) must
 produce exactly the windows the single-stream oracle produces, out-of-order tuples across chunk boundaries
-included."""
+included; cases 4-5 are count windows (the count path's per-rank count cells, BASELINE configs[4])."""
 import json
 import os
 import subprocess
@@ -15,7 +15,7 @@ from shard_cases import case
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cid", [0, 1, 2, 3])
+@pytest.mark.parametrize("cid", [0, 1, 2, 3, 4, 5])
 def test_two_rank_sharded_stream_matches_oracle(tmp_path, cid):
     out = str(tmp_path / "w.json")
     port = str(29500 + cid + (os.getpid() % 400))
