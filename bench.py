@@ -164,37 +164,59 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
             "ingest": {"avg_launch_ms": avg_ms, "achieved_GBs": achieved, "frac": achieved / HBM_PEAK_GBS}}
 
 
-def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20_000_000):
-    """BASELINE configs[4] (C5), one GPU: count-based windows, BenchmarkRunner.randomCount(n, lo, hi)
-    (TumblingWindow(Count, size), java.util.Random(10)), SUM_I32 + COUNT, in-order non-keyed stream,
-    maxLateness 1.  Count windows make every slice a LazySlice (S/slice/SliceFactory.java:17-22)."""
+def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20_000_000, rank=0, world=1,
+              dist=None):
+    """BASELINE configs[4] (C5): count-based windows, BenchmarkRunner.randomCount(n, lo, hi) (TumblingWindow(Count,
+    size), java.util.Random(10)), SUM_I32 + COUNT, in-order non-keyed stream, maxLateness 1; count path (every slice
+    a LazySlice, S/slice/SliceFactory.java:17-22).  world > 1: time/arrival-range sharding -- rank r holds arrival
+    chunk r of every global micro-batch of world * batch tuples, one all-gather of count-cell records per batch
+    (RCCL over xGMI), every rank holds the same slices; weak scaling, max over ranks."""
     import torch
-    rate = max(1, batch // 1000)
+    G = world
+    rate = max(1, (batch * G) // 1000)
     g = torch.Generator(device=dev)
-    g.manual_seed(9)
-    op = pkg.SlicingWindowOperator(device=dev.index)
+    g.manual_seed(9 + rank)
+    if G > 1:
+        op = pkg.ShardedSlicingWindowOperator(device=dev.index)
+    else:
+        op = pkg.SlicingWindowOperator(device=dev.index)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.addWindowFunction(pkg.AGG_COUNT)
     op.setMaxLateness(1)
     for size in pkg.workloads.random_count_sizes(n_windows, lo, hi, seed=10):
         op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, size))
-    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    base = (torch.arange(batch, device=dev, dtype=torch.int64) + rank * batch) // rate
     times, rows = [], 0
     for s in range(warm + steps):
         ts = base + s * 1000
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         torch.cuda.synchronize(dev)
+        if dist is not None and s == warm:
+            dist.barrier()
         t0 = time.perf_counter()
-        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
-        n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
+        if G > 1:
+            op.processChunk(ts.data_ptr(), v.data_ptr(), batch, 0, n_before=rank * batch, n_total=G * batch)
+            n, _ = op.processWatermarkDevice(s * 1000 + (G * batch - 1) // rate)
+        else:
+            op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+            n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
         torch.cuda.synchronize(dev)
         if s >= warm:
             times.append(time.perf_counter() - t0)
             rows += n
-    return {"workload": "C5 (one GPU): %d tumbling count windows, sizes randomCount(%d,%d,%d) Random(10), "
-                        "SUM_I32+COUNT, in-order, maxLateness=1" % (n_windows, n_windows, lo, hi),
-            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
-            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
+    elapsed = sum(times)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    return {"workload": "C5: %d tumbling count windows, sizes randomCount(%d,%d,%d) Random(10), SUM_I32+COUNT, "
+                        "in-order, maxLateness=1%s" % (n_windows, n_windows, lo, hi,
+                                                       ", time-range sharded over %d GPUs (RCCL all-gather of count "
+                                                       "cells)" % G if G > 1 else ""),
+            "tuples_per_step": batch * G, "tuples_per_step_per_gpu": batch, "steps": steps,
+            "ms_per_step": 1e3 * elapsed / len(times), "value": batch * G * len(times) / elapsed, "unit": "tuples/s",
+            "scaling": "weak", "windows_emitted": rows}
 
 
 def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None):
@@ -233,7 +255,7 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
             rows += n
     elapsed = sum(times)
     if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
@@ -371,7 +393,8 @@ def main():
             extra = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
                      "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5), "c5": extra_c5(pkg, dev, 1 << 27, 5)}
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
-            extra = {"c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5, rank=rank, world=world, dist=dist)}
+            extra = {"c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5, rank=rank, world=world, dist=dist),
+                     "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist)}
         if rank == 0:
             res["extra"] = extra
     if rank == 0:
