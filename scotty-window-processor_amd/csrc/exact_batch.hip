@@ -174,13 +174,14 @@ __device__ __forceinline__ bool on_count_grid(const XCfg* c, int64_t cnt) {
   return false;
 }
 
-// Per-thread view of one tile: 16 contiguous tuples, their exclusive prefix max P, and the wave's grid bound.
+// Per-thread view of one tile: 16 contiguous tuples staged in LDS (row of this thread) and the exclusive prefix
+// max P before the first of them.  P and nextGrid(P) of later items are produced in order by TileWalk, so no
+// per-item arrays live in registers or scratch.
 struct TileItems {
-  int64_t t[XB_ITEMS];
-  int64_t p[XB_ITEMS];  // exclusive prefix max (incl. carry and p_start)
-  int64_t g[XB_ITEMS];  // nextGrid(p): the pending fixed edge once n0 was crossed
-  int64_t base;         // index of item 0
-  int cnt;              // valid items
+  const long long* row;  // tb + thread row: the thread's items in arrival order
+  int64_t pre;           // exclusive prefix max before item 0 (incl. carry and p_start)
+  int64_t base;          // index of item 0
+  int cnt;               // valid items
 };
 
 // per-lane nextGrid (serial over the windows): only recomputed when the running max reaches the cached edge
@@ -216,41 +217,35 @@ __device__ __forceinline__ void stage_tile(const int64_t* src, int64_t n, int64_
 }
 
 __device__ __forceinline__ void load_tile(const XBArgs& a, int64_t tile, TileItems& it, long long* wtot,
-                                          bool want_grid, long long* tb) {
+                                          long long* tb) {
   const XSnap& sn = *a.snap;
   it.base = tile * XB_TILE + (int64_t)threadIdx.x * XB_ITEMS;
   it.cnt = (int)max((int64_t)0, min((int64_t)XB_ITEMS, a.n - it.base));
   stage_tile(a.ts, a.n, tile, tb);
+  it.row = tb + threadIdx.x * (XB_ITEMS + 1);
   int64_t run = JMIN;
 #pragma unroll
-  for (int j = 0; j < XB_ITEMS; j++) {
-    it.t[j] = j < it.cnt ? (int64_t)tb[threadIdx.x * (XB_ITEMS + 1) + j] : JMIN;
-    it.p[j] = run;  // local exclusive
-    run = max(run, it.t[j]);
-  }
+  for (int j = 0; j < XB_ITEMS; j++) run = max(run, (int64_t)it.row[j]);  // padding items are JMIN
   const int64_t before = block_excl_max(run, wtot);
   const int64_t carry = max((int64_t)a.pcarry[tile], sn.p_start);
-  const int64_t pre = max(carry, before);
-#pragma unroll
-  for (int j = 0; j < XB_ITEMS; j++) it.p[j] = max(pre, it.p[j]);
-  // nextGrid(x) is constant on [x, nextGrid(x)) and P is non-decreasing along the thread's items
-  int64_t gcur = JMIN;
-  const bool grid = want_grid && a.cfg->has_fixed && a.cfg->has_time;
-#pragma unroll
-  for (int j = 0; j < XB_ITEMS; j++) {
-    if (!grid || j >= it.cnt) {
-      it.g[j] = JMAX;
-      continue;
-    }
-    const int64_t pj = it.p[j];
-    if (pj < 0) {  // assignNextWindowStart bounds the pending edge only for non-negative times (Java %)
-      it.g[j] = JMIN;
-      continue;
-    }
-    if (gcur == JMIN || pj >= gcur) gcur = next_grid_lane(a.cfg, pj);
-    it.g[j] = gcur;
-  }
+  it.pre = max(carry, before);
 }
+
+// walks a thread's items in order: t, its exclusive prefix max p, and the pending fixed edge g = nextGrid(p)
+// (nextGrid(x) is constant on [x, nextGrid(x)) and p is non-decreasing, so it is recomputed only on crossing)
+struct TileWalk {
+  int64_t p, gcur;
+  bool grid;
+  __device__ TileWalk(const XBArgs& a, const TileItems& it, bool want_grid)
+      : p(it.pre), gcur(JMIN), grid(want_grid && a.cfg->has_fixed && a.cfg->has_time) {}
+  __device__ __forceinline__ int64_t g(const XCfg* c) {
+    if (!grid) return JMAX;
+    if (p < 0) return JMIN;  // assignNextWindowStart bounds the pending edge only for non-negative times (Java %)
+    if (gcur == JMIN || p >= gcur) gcur = next_grid_lane(c, p);
+    return gcur;
+  }
+  __device__ __forceinline__ void next(int64_t t) { p = max(p, t); }
+};
 
 // in-order tuple t (t >= p): contexts in which it starts a new session (the chain of in-batch sessions), and
 // the end of the session before it
@@ -399,14 +394,19 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nscount_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
   TileItems it;
-  load_tile(a, blockIdx.x, it, wtot, false, tb);
+  load_tile(a, blockIdx.x, it, wtot, tb);
   int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
+  TileWalk w(a, it, false);
   for (int j = 0; j < it.cnt; j++) {
-    if (it.t[j] < it.p[j]) continue;
-    int64_t pb[XMAXCTX];
-    const int nsm = newsess_bits(a, it.t[j], it.p[j], pb);
-    for (int k = 0; k < a.cfg->n_ctx; k++)
-      if (nsm & (1 << k)) cnt[k]++;
+    const int64_t t = it.row[j];
+    if (t >= w.p) {
+      int64_t pb[XMAXCTX];
+      const int nsm = newsess_bits(a, t, w.p, pb);
+#pragma unroll
+      for (int k = 0; k < XMAXCTX; k++)
+        if (nsm & (1 << k)) cnt[k]++;
+    }
+    w.next(t);
   }
   for (int k = 0; k < a.cfg->n_ctx; k++) {
     int64_t tot;
@@ -449,29 +449,45 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nswrite_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
   TileItems it;
-  load_tile(a, blockIdx.x, it, wtot, false, tb);
+  load_tile(a, blockIdx.x, it, wtot, tb);
   int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
-  for (int j = 0; j < it.cnt; j++) {
-    if (it.t[j] < it.p[j]) continue;
-    int64_t pb[XMAXCTX];
-    const int nsm = newsess_bits(a, it.t[j], it.p[j], pb);
-    for (int k = 0; k < a.cfg->n_ctx; k++)
-      if (nsm & (1 << k)) cnt[k]++;
-  }
-  for (int k = 0; k < a.cfg->n_ctx; k++) {
-    int64_t off = block_excl_sum(cnt[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+  uint64_t nsm_all = 0;  // 4 bits per item
+  {
+    TileWalk w(a, it, false);
     for (int j = 0; j < it.cnt; j++) {
-      if (it.t[j] < it.p[j]) continue;
+      const int64_t t = it.row[j];
+      if (t >= w.p) {
+        int64_t pb[XMAXCTX];
+        const int nsm = newsess_bits(a, t, w.p, pb);
+        nsm_all |= (uint64_t)nsm << (4 * j);
+#pragma unroll
+        for (int k = 0; k < XMAXCTX; k++)
+          if (nsm & (1 << k)) cnt[k]++;
+      }
+      w.next(t);
+    }
+  }
+  int64_t off[XMAXCTX] = {0, 0, 0, 0};
+  for (int k = 0; k < a.cfg->n_ctx; k++)
+    off[k] = block_excl_sum(cnt[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+  if (nsm_all == 0) return;
+  TileWalk w(a, it, false);
+  for (int j = 0; j < it.cnt; j++) {
+    const int64_t t = it.row[j];
+    const int nsm = (int)((nsm_all >> (4 * j)) & 15u);
+    if (nsm) {
       int64_t pb[XMAXCTX];
-      const int nsm = newsess_bits(a, it.t[j], it.p[j], pb);
-      if (nsm & (1 << k)) {
-        if (off < a.ns_cap) {
-          a.ns_start[(int64_t)k * a.ns_cap + off] = it.t[j];
-          a.ns_pb[(int64_t)k * a.ns_cap + off] = pb[k];
+      (void)newsess_bits(a, t, w.p, pb);
+      for (int k = 0; k < a.cfg->n_ctx; k++) {
+        if (!(nsm & (1 << k))) continue;
+        if (off[k] < a.ns_cap) {
+          a.ns_start[(int64_t)k * a.ns_cap + off[k]] = t;
+          a.ns_pb[(int64_t)k * a.ns_cap + off[k]] = pb[k];
         }
-        off++;
+        off[k]++;
       }
     }
+    w.next(t);
   }
 }
 
@@ -532,20 +548,29 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
   TileItems it;
-  load_tile(a, blockIdx.x, it, wtot, true, tb);
+  load_tile(a, blockIdx.x, it, wtot, tb);
   const XCfg* c = a.cfg;
   // new sessions before each item: carry (exclusive offsets of the tile) + local exclusive count
   int64_t nsb[XMAXCTX] = {0, 0, 0, 0};
   int64_t loc[XMAXCTX] = {0, 0, 0, 0};
-  int nsm_item[XB_ITEMS];
-  uint32_t io_ev = 0;  // in-order events, evaluated once
-  for (int j = 0; j < it.cnt; j++) {
-    nsm_item[j] = 0;
-    if (it.t[j] >= it.p[j]) {
-      int64_t pb[XMAXCTX];
-      if (inorder_event(a, it.t[j], it.p[j], it.g[j], it.base + j, nsm_item[j], pb)) io_ev |= 1u << j;
-      for (int k = 0; k < c->n_ctx; k++)
-        if (nsm_item[j] & (1 << k)) loc[k]++;
+  uint64_t nsm_all = 0;  // 4 new-session bits per item
+  uint32_t io_ev = 0;    // in-order events, evaluated once
+  uint32_t io = 0;       // in-order items
+  {
+    TileWalk w(a, it, true);
+    for (int j = 0; j < it.cnt; j++) {
+      const int64_t t = it.row[j];
+      if (t >= w.p) {
+        io |= 1u << j;
+        int64_t pb[XMAXCTX];
+        int nsm = 0;
+        if (inorder_event(a, t, w.p, w.g(c), it.base + j, nsm, pb)) io_ev |= 1u << j;
+        nsm_all |= (uint64_t)nsm << (4 * j);
+#pragma unroll
+        for (int k = 0; k < XMAXCTX; k++)
+          if (nsm & (1 << k)) loc[k]++;
+      }
+      w.next(t);
     }
   }
   for (int k = 0; k < c->n_ctx; k++)
@@ -554,18 +579,23 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   int64_t nev = 0;
   int64_t tail_m = JMIN;  // max after this thread's last event
   bool has = false;
+  TileWalk w(a, it, false);
   for (int j = 0; j < it.cnt; j++) {
-    const bool ev = it.t[j] >= it.p[j] ? ((io_ev >> j) & 1) != 0 : classify(a, it.t[j], it.p[j], it.g[j], it.base + j, nsb);
-    for (int k = 0; k < c->n_ctx; k++)
-      if (nsm_item[j] & (1 << k)) nsb[k]++;
+    const int64_t t = it.row[j];
+    const bool ev = ((io >> j) & 1) ? ((io_ev >> j) & 1) != 0 : classify(a, t, w.p, JMAX, it.base + j, nsb);
+    const int nsm = (int)((nsm_all >> (4 * j)) & 15u);
+#pragma unroll
+    for (int k = 0; k < XMAXCTX; k++)
+      if (nsm & (1 << k)) nsb[k]++;
     if (ev) {
       bits |= 1u << j;
       nev++;
       has = true;
       tail_m = JMIN;
     } else {
-      tail_m = max(tail_m, it.t[j]);
+      tail_m = max(tail_m, t);
     }
+    w.next(t);
   }
   // bitmap: 16 bits per thread, two threads per word
   {
