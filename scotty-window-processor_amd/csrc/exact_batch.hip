@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "exact_op.h"
 
 namespace scotty {
@@ -605,26 +607,21 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   }
   int64_t tot;
   (void)block_excl_sum(nev, wtot, &tot);
-  // segmented max: the tile's "max after its last event" = fold over threads in order
-  __shared__ long long s_tail[XB_THREADS];
-  __shared__ int s_has[XB_THREADS];
-  s_tail[threadIdx.x] = tail_m;
-  s_has[threadIdx.x] = has;
+  // segmented max: the tile's "max after its last event" = max of the tails of the last thread with an event
+  // and of every thread after it (two block reductions instead of a serial fold)
+  __shared__ long long s_red[8];
+  int64_t last_ev = wmax(has ? (int64_t)threadIdx.x : (int64_t)-1);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = last_ev;
+  __syncthreads();
+  last_ev = max(max((int64_t)s_red[0], (int64_t)s_red[1]), max((int64_t)s_red[2], (int64_t)s_red[3]));
+  int64_t m = wmax((int64_t)threadIdx.x >= last_ev ? tail_m : JMIN);
+  if ((threadIdx.x & 63) == 0) s_red[4 + (threadIdx.x >> 6)] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int64_t m = JMIN;
-    int any = 0;
-    for (int i = 0; i < XB_THREADS; i++) {
-      if (s_has[i]) {
-        m = s_tail[i];
-        any = 1;
-      } else {
-        m = max(m, (int64_t)s_tail[i]);
-      }
-    }
+    m = max(max((int64_t)s_red[4], (int64_t)s_red[5]), max((int64_t)s_red[6], (int64_t)s_red[7]));
     a.ev_cnt[blockIdx.x] = tot;
     a.seg_tail[blockIdx.x] = m;
-    a.seg_has[blockIdx.x] = any;
+    a.seg_has[blockIdx.x] = last_ev >= 0 ? 1 : 0;
   }
 }
 
@@ -866,11 +863,21 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
   const int lane = threadIdx.x & 63;
   const XCfg* cfg = a.cfg;
   const int need = cfg->need;
+  const bool lazy = cfg->lazy != 0;
   const XState& st = *a.st;
   const int head = st.head;
   const int64_t nep = ctl.ep_count;
   const int wtop = a.ep_tail[nep - 1];
   const int wbase = max(head, wtop - XW);
+  const int64_t* sk = (st.unsorted & 1) ? a.sufmin : a.sl.ts;
+  // LDS copies of the search keys of the window's slices and of the epoch table (binary searches of every
+  // out-of-order tuple stay in LDS; only tuples older than the window search HBM)
+  constexpr int EPC = 512;
+  __shared__ long long w_key[XW];
+  __shared__ long long w_ts[XW];
+  __shared__ long long e_pos[EPC];
+  __shared__ int e_tail[EPC];
+  const bool ep_lds = nep <= EPC;
   for (int k = threadIdx.x; k < XW; k += 256) {
     w_cnt[k] = 0;
     w_tl[k] = JMIN;
@@ -878,34 +885,72 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
     w_p0[k] = 0;
     w_p1[k] = ID_MIN;
     w_p2[k] = ID_MAX;
+    w_key[k] = wbase + k < wtop ? sk[wbase + k] : JMAX;
+    w_ts[k] = wbase + k < wtop ? a.sl.ts[wbase + k] : JMAX;
   }
+  if (ep_lds)
+    for (int64_t k = threadIdx.x; k < nep; k += 256) {
+      e_pos[k] = a.ep_pos[k];
+      e_tail[k] = a.ep_tail[k];
+    }
   __syncthreads();
   const int64_t total = s1 - s0;
   int64_t chunk = (total + gridDim.x - 1) / gridDim.x;
   chunk = ((chunk + 255) / 256) * 256;
   const int64_t b0 = s0 + (int64_t)blockIdx.x * chunk;
   const int64_t b1 = min(s1, b0 + chunk);
-  const int64_t* sk = (st.unsorted & 1) ? a.sufmin : a.sl.ts;
-  for (int64_t i0 = b0; i0 < b1; i0 += 256) {
-    const int64_t i = i0 + threadIdx.x;
-    bool act = i < b1;
-    int64_t t = 0, vb = 0;
-    if (act) act = !((a.evbits[i >> 5] >> (i & 31)) & 1);
-    int si = -1;
-    if (act) {
+  // software pipelined: the next iteration's tuple and event word are in flight while this one is combined
+  auto ld = [&](int64_t i, int64_t& t, int64_t& vb, uint32_t& wd) {
+    if (i < b1) {
       t = a.ts[i];
       if constexpr (VT == VT_I32) vb = (int64_t)((const int32_t*)a.val)[i];
       else vb = ((const int64_t*)a.val)[i];
-      int64_t lo = 0, hi = nep;  // last epoch entry with pos < i: the last slice present at arrival
-      while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a.ep_pos[mid] < i) lo = mid; else hi = mid;
-      }
-      const int last = a.ep_tail[lo] - 1;
-      if (t >= a.sl.ts[last]) {
+      wd = a.evbits[i >> 5];
+    }
+  };
+  int64_t t_n = 0, v_n = 0;
+  uint32_t wd_n = 0;
+  ld(b0 + threadIdx.x, t_n, v_n, wd_n);
+  // epoch cursor of this wave (indices only increase): last epoch entry with pos < the wave's first index
+  auto epos = [&](int64_t k) -> int64_t { return ep_lds ? (int64_t)e_pos[k] : a.ep_pos[k]; };
+  auto etail = [&](int64_t k) -> int { return ep_lds ? e_tail[k] : a.ep_tail[k]; };
+  int64_t ecur = 0;
+  {
+    int64_t lo = 0, hi = nep;
+    const int64_t iw = b0 + (threadIdx.x & ~63);
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (epos(mid) < iw) lo = mid; else hi = mid;
+    }
+    ecur = lo;
+  }
+  for (int64_t i0 = b0; i0 < b1; i0 += 256) {
+    const int64_t i = i0 + threadIdx.x;
+    const int64_t t = t_n, vb = v_n;
+    const uint32_t wd = wd_n;
+    ld(i + 256, t_n, v_n, wd_n);
+    {
+      const int64_t iw = i0 + (threadIdx.x & ~63);
+      while (ecur + 1 < nep && epos(ecur + 1) < iw) ecur++;
+    }
+    bool act = i < b1 && !((wd >> (i & 31)) & 1);
+    int si = -1;
+    if (act) {
+      // last epoch entry with pos < i: the last slice present at arrival (a few steps from the wave cursor)
+      int64_t lo = ecur;
+      while (lo + 1 < nep && epos(lo + 1) < i) lo++;
+      const int last = etail(lo) - 1;
+      if (t >= (last >= wbase ? (int64_t)w_ts[last - wbase] : a.sl.ts[last])) {
         si = last;
+      } else if (last > wbase && t >= w_key[0]) {  // in the LDS window: last key <= t in [wbase, last)
+        int l = 0, h = last - wbase;
+        while (l < h) {
+          const int mid = (l + h) >> 1;
+          if (w_key[mid] <= t) l = mid + 1; else h = mid;
+        }
+        si = wbase + l - 1;
       } else {  // last slice in [head, last) with tStart <= t (suffix-min keys on an unsorted list)
-        int l = head, h = last;
+        int l = head, h = min(last, wbase);
         while (l < h) {
           const int mid = (l + h) >> 1;
           if (sk[mid] <= t) l = mid + 1; else h = mid;
@@ -920,33 +965,27 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
     const Lift lf = lift(VT, vb);
     const unsigned long long am = __ballot(act);
     if (!am) continue;
-    const int leader = __ffsll((long long)am) - 1;
-    const int s_lead = __builtin_amdgcn_readlane(si, leader);
-    const bool same = __ballot(act && si != s_lead) == 0;
-    int tgt = si;
-    unsigned int c_ = 1;
-    int64_t tmx = t, tmn = t, mn = lf.mn, mx = lf.mx;
-    uint64_t sw = lf.sum;
-    bool doit = act;
-    if (same) {
-      c_ = (unsigned int)__popcll(am);
-      tmx = wmax(act ? t : JMIN);
-      tmn = wmin(act ? t : JMAX);
-      if (need & NEED_SUM) {
-        if constexpr (VT == VT_F64) sw = (uint64_t)__double_as_longlong(wsumf(act ? __longlong_as_double(vb) : 0.0));
-        else sw = wsum(act ? lf.sum : 0);
-      }
-      if (need & NEED_MIN) mn = wmin(act ? lf.mn : ID_MIN);
-      if (need & NEED_MAX) mx = wmax(act ? lf.mx : ID_MAX);
-      tgt = s_lead;
-      doit = lane == leader;
+    // the slice of the wave's highest active lane (the open slice for in-order tuples) takes one combined
+    // update; lanes targeting other slices (out-of-order tuples) update theirs individually
+    const int ref = 63 - __clzll((long long)am);
+    const int s_ref = __builtin_amdgcn_readlane(si, ref);
+    const bool in_ref = act && si == s_ref;
+    const unsigned int c_ref = (unsigned int)__popcll(__ballot(in_ref));
+    const int64_t tmx_r = wmax(in_ref ? t : JMIN);
+    const int64_t tmn_r = wmin(in_ref ? t : JMAX);
+    uint64_t sw_r = 0;
+    if (need & NEED_SUM) {
+      if constexpr (VT == VT_F64) sw_r = (uint64_t)__double_as_longlong(wsumf(in_ref ? __longlong_as_double(vb) : 0.0));
+      else sw_r = wsum(in_ref ? lf.sum : 0);
     }
-    if (doit) {
+    const int64_t mn_r = (need & NEED_MIN) ? wmin(in_ref ? lf.mn : ID_MIN) : ID_MIN;
+    const int64_t mx_r = (need & NEED_MAX) ? wmax(in_ref ? lf.mx : ID_MAX) : ID_MAX;
+    auto update = [&](int tgt, unsigned int c_, int64_t tmx, int64_t tmn, uint64_t sw, int64_t mn, int64_t mx) {
       if (tgt >= wbase && tgt < wbase + XW) {
         const int k = tgt - wbase;
         atomicAdd(&w_cnt[k], c_);
         atomicMax(&w_tl[k], (long long)tmx);
-        atomicMin(&w_tf[k], (long long)tmn);
+        if (lazy) atomicMin(&w_tf[k], (long long)tmn);  // tFirst only feeds LazySlice record moves
         if (need & NEED_SUM) {
           if constexpr (VT == VT_F64) atomicAdd((double*)&w_p0[k], __longlong_as_double((long long)sw));
           else atomicAdd(&w_p0[k], (unsigned long long)sw);
@@ -957,7 +996,7 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
         atomicAdd(&a.sl.cnt[tgt], (unsigned long long)c_);
         atomicAdd((unsigned long long*)&a.sl.cl[tgt], (unsigned long long)c_);
         atomicMax((long long*)&a.sl.tl[tgt], (long long)tmx);
-        atomicMin((long long*)&a.sl.tf[tgt], (long long)tmn);
+        if (lazy) atomicMin((long long*)&a.sl.tf[tgt], (long long)tmn);
         if (need & NEED_SUM) {
           if constexpr (VT == VT_F64) atomicAdd((double*)&a.sl.p[0][tgt], __longlong_as_double((long long)sw));
           else atomicAdd(&a.sl.p[0][tgt], (unsigned long long)sw);
@@ -965,8 +1004,11 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
         if (need & NEED_MIN) atomicMin((long long*)&a.sl.p[1][tgt], (long long)mn);
         if (need & NEED_MAX) atomicMax((long long*)&a.sl.p[2][tgt], (long long)mx);
       }
-    }
+    };
+    if (lane == ref) update(s_ref, c_ref, tmx_r, tmn_r, sw_r, mn_r, mx_r);
+    if (act && !in_ref) update(si, 1u, t, t, lf.sum, lf.mn, lf.mx);
   }
+
   __syncthreads();
   for (int k = threadIdx.x; k < XW; k += 256) {
     const unsigned int c_ = w_cnt[k];
@@ -975,7 +1017,7 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
     atomicAdd(&a.sl.cnt[s_], (unsigned long long)c_);
     atomicAdd((unsigned long long*)&a.sl.cl[s_], (unsigned long long)c_);
     atomicMax((long long*)&a.sl.tl[s_], w_tl[k]);
-    atomicMin((long long*)&a.sl.tf[s_], w_tf[k]);
+    if (lazy) atomicMin((long long*)&a.sl.tf[s_], w_tf[k]);
     if (need & NEED_SUM) {
       if constexpr (VT == VT_F64) atomicAdd((double*)&a.sl.p[0][s_], __longlong_as_double((long long)w_p0[k]));
       else atomicAdd(&a.sl.p[0][s_], w_p0[k]);
@@ -1066,7 +1108,11 @@ hipError_t xb_events(XBArgs& a, hipStream_t st) {
 }
 hipError_t xb_apply(XBArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(xb::xb_sufmin_kernel, dim3(1), dim3(1024), 0, st, a);
-  const int64_t blocks = std::min<int64_t>((a.n + 4095) / 4096, 2048);
+  static const int64_t max_blocks = [] {
+    const char* e = getenv("SCOTTY_XB_APPLY_BLOCKS");  // A/B of the apply grid (flush contention vs occupancy)
+    return e ? std::max<int64_t>(64, atoll(e)) : (int64_t)4096;
+  }();
+  const int64_t blocks = std::min<int64_t>((a.n + 4095) / 4096, max_blocks);
   if (a.vt == VT_I32) hipLaunchKernelGGL(xb::xb_apply_kernel<VT_I32>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (a.vt == VT_I64) hipLaunchKernelGGL(xb::xb_apply_kernel<VT_I64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(xb::xb_apply_kernel<VT_F64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
