@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 METRIC = "tuples/sec (1/2/4/8 GPU) at 1000 concurrent windows; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_TUPLE = 12   # int64 ts + int32 value, read once
+C4_BATCH = 1 << 26     # GPU runs use N ~ 2^26 tuples per watermark batch (C4: per rank)
 
 
 def log(*a):
@@ -391,9 +392,9 @@ def main():
         torch.cuda.empty_cache()
         if world == 1:
             extra = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
-                     "c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5), "c5": extra_c5(pkg, dev, 1 << 27, 5)}
+                     "c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5), "c5": extra_c5(pkg, dev, 1 << 27, 5)}
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
-            extra = {"c4": extra_c4(pkg, dev, 1 << 24, 1 << 20, 5, rank=rank, world=world, dist=dist),
+            extra = {"c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, rank=rank, world=world, dist=dist),
                      "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist)}
         if rank == 0:
             res["extra"] = extra

@@ -1,0 +1,20 @@
+"""C4 (keyed, 1M keys) at several per-step batch sizes: prints one JSON line per size (GPU box tool)."""
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+pkg = importlib.import_module("scotty-window-processor_amd")
+dev = torch.device("cuda", 0)
+for lg in [int(x) for x in (sys.argv[1:] or ["24", "25", "26"])]:
+    r = bench.extra_c4(pkg, dev, 1 << lg, 1 << 20, 5)
+    r["log2_batch"] = lg
+    print(json.dumps(r), flush=True)
+    torch.cuda.empty_cache()
