@@ -219,8 +219,20 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
   L.dropped = 0;
   L.hang = false;
   // capacity pre-check (same bound as the wavefront replay): defer the key, the host grows and retries
+  // the lane's run is read 4 records per round so 4 scattered loads are in flight at once (the kernel waits on
+  // memory, not ALU: SQ_WAIT_ANY is ~80% of its wave cycles)
   int64_t tmin = JMAX, tmax = JMIN;
-  for (int64_t i = b0; i < b1; i++) {
+  int64_t i = b0;
+  for (; i + 4 <= b1; i += 4) {
+    int64_t t0, t1, t2, t3, v_;
+    load(i, t0, v_);
+    load(i + 1, t1, v_);
+    load(i + 2, t2, v_);
+    load(i + 3, t3, v_);
+    tmin = min(tmin, min(min(t0, t1), min(t2, t3)));
+    tmax = max(tmax, max(max(t0, t1), max(t2, t3)));
+  }
+  for (; i < b1; i++) {
     int64_t t, vb;
     load(i, t, vb);
     tmin = min(tmin, t);
@@ -255,9 +267,12 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
     L.tail = n;
   }
   L.load_cur();
-  for (int64_t i = b0; i < b1 && !L.hang; i++) {
-    int64_t t, vb;
-    load(i, t, vb);
+  // replay with the next record's load issued before the current record is processed
+  int64_t t_nx, v_nx;
+  load(b0, t_nx, v_nx);
+  for (int64_t j = b0; j < b1 && !L.hang; j++) {
+    const int64_t t = t_nx, vb = v_nx;
+    if (j + 1 < b1) load(j + 1, t_nx, v_nx);
     L.process(t, vb);
   }
   L.flush_cur();
