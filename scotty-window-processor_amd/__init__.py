@@ -326,6 +326,22 @@ class SlicingWindowOperator:
         st = self._check(self._l.scotty_process_watermark_device(self._h, watermark_ts, ctypes.byref(out)))
         return out.n_windows, st
 
+    def processWatermarkArrays(self, watermark_ts):
+        """processWatermark as numpy columns (no per-window objects, for million-window results): a dict with
+        start, end, measure, has_value, values (one column per aggregation, registration order) and, on a keyed
+        operator, key."""
+        self._flush()
+        out = scotty_windows()
+        self.last_status = self._check(self._l.scotty_process_watermark(self._h, watermark_ts, ctypes.byref(out)))
+        n = out.n_windows
+        col = lambda p, dt: np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, dt)
+        res = {"start": col(out.start, np.int64), "end": col(out.end, np.int64),
+               "measure": col(out.measure, np.int32), "has_value": col(out.has_value, np.uint8).astype(bool),
+               "values": [col(out.values[k], np.int64) for k in range(len(self._aggs))]}
+        if self._flags & FLAG_KEYED:
+            res["key"] = col(out.key, np.uint32)
+        return res
+
     def processWatermarkRaw(self, watermark_ts):
         """processWatermark without building Python objects: returns (n_windows, status)."""
         self._flush()

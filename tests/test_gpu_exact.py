@@ -277,6 +277,35 @@ def test_keyed_config4_reduced(pkg):
     assert _keyed_run(pkg, cfg, keys, ts, vals, sched) > 20_000
 
 
+def test_keyed_config4_full_size_per_key_totals(pkg):
+    """C4 at the bench's full size: 2^26 tuples over 2^20 keys in one push (ts in [0, 1000) ms), SlidingWindow
+    (60 s, 1 s), maxLateness 1.  At wm = 59999 every key's operator emits exactly [0, 60000) (SlidingWindow.
+    triggerWindows, C/windowType/SlidingWindow.java:50-57: ws >= 0 and ws + size <= wm + 1), so its COUNT is
+    the key's tuple count and its SUM the key's int32-wrapped value sum (SumAggregation.java:16-18)."""
+    n, nk = 1 << 26, 1 << 20
+    rng = np.random.default_rng(26)
+    keys = rng.integers(0, nk, size=n, dtype=np.uint32)
+    ts = np.arange(n, dtype=np.int64) // (n // 1000)
+    vals = rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    op = pkg.KeyedSlicingWindowOperator()
+    op.addWindowFunction(SUM)
+    op.addWindowFunction(COUNT)
+    op.setMaxLateness(1)
+    op.addWindowAssigner(Sliding(Time, 60_000, 1_000))
+    op.processElements(keys, ts, vals)
+    r = op.processWatermarkArrays(59_999)
+    present = np.bincount(keys, minlength=nk)
+    assert op.keyCount() == int((present > 0).sum())
+    assert len(r["key"]) == op.keyCount()
+    assert (r["start"] == 0).all() and (r["end"] == 60_000).all() and r["has_value"].all()
+    k = r["key"].astype(np.int64)
+    assert np.array_equal(np.sort(k), np.nonzero(present)[0])
+    assert np.array_equal(r["values"][1], present[k])
+    s = np.bincount(keys, weights=vals.astype(np.float64), minlength=nk)  # |sum| < 2^53: exact
+    wrapped = ((s.astype(np.int64) + 2**31) % 2**32) - 2**31
+    assert np.array_equal(r["values"][0], wrapped[k])
+
+
 def test_keyed_large_batch_count_property(pkg):
     """2^24 tuples over 100k keys in one push: tumbling windows partition each key's in-order stream, so
     the COUNTs of all emitted windows add up to the tuple count."""
