@@ -4,20 +4,26 @@ Workload (N=1): 1000 concurrent tumbling windows with sizes from BenchmarkRunner
 (java.util.Random(10)), SUM_I32 + COUNT, in-order synthetic stream, maxLateness 1 (Flink connector default).
 One step = one watermark interval: a micro-batch of --batch tuples per GPU covering 1 s of event time,
 resident in HBM before the timed region, pushed through the C-ABI (ingest + edge commit kernels) followed by
-processWatermark (window assembly + GC + results to host).  N>1: one process per GPU; the ONE non-keyed C2
-stream is sharded by arrival (= time) range -- rank r holds chunk r of every global micro-batch of N*batch
-tuples -- and one RCCL all-gather over xGMI per micro-batch exchanges the ranks' first-crossing records and
-slice partials; every rank then holds the same slice store and emits the same windows.
-Weak scaling: tuples per GPU fixed; value = all ranks' tuples / max-over-ranks time.
+processWatermark (triggers, window assembly, GC, one packed transfer of the results to the host).  N>1: one
+process per GPU; the ONE non-keyed C2 stream is sharded by arrival (= time) range -- rank r holds chunk r of every
+global micro-batch of N*batch tuples -- and one RCCL all-gather over xGMI per micro-batch exchanges the ranks'
+first-crossing records and slice partials; every rank then holds the same slice store and emits
+the same windows.  Weak scaling: tuples per GPU fixed; value = all ranks' tuples / max-over-ranks time.
 
-Prints ONE JSON line (rank 0).  cpu_baseline = the CPU restatement of SlicingWindowOperator (oracle/),
-single thread, on a bounded sample of the same workload.
+`python bench.py --gpus N` without a launcher starts N ranks itself (torch.distributed.run, before any GPU call)
+and every rank asserts WORLD_SIZE == N, so an N-GPU run can never silently measure one GPU.
+
+Prints ONE JSON line (rank 0).  roofline: the ingest kernel (frac) and ALL device work of a step (frac_step), from
+HIP events on the operator's stream.  extra: the other BASELINE configs (C2s = the north_star target: 1000 sliding
+windows, 20 % out-of-order; C3, C4, C5), each with its own CPU baseline (oracle/, the C++ restatement of the
+reference operator; keyed: T threads) on a bounded sample of the same stream.
 """
 import argparse
 import ctypes
 import importlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -28,43 +34,199 @@ sys.path.insert(0, ROOT)
 METRIC = "tuples/sec (1/2/4/8 GPU) at 1000 concurrent windows; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_TUPLE = 12   # int64 ts + int32 value, read once
+KEYED_BYTES_PER_TUPLE = 16  # + uint32 key
 C4_BATCH = 1 << 26     # GPU runs use N ~ 2^26 tuples per watermark batch (C4: per rank)
+CPU_BUDGET_S = float(os.environ.get("SCOTTY_CPU_BUDGET_S", "12"))
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(sizes, rate_per_ms, budget_s=12.0):
-    """Oracle (C++ restatement of the reference operator, 1 thread) on a bounded prefix of the same stream."""
+def device_roofline(op, steps, batch, bytes_per_tuple, kernel):
+    """Roofline of the dominant kernel (ingest) and of the whole step (every timed launch/transfer class)."""
+    t = op.deviceTiming()
+    ing_ms, ing_n = t["ingest"]
+    step_ms = sum(v[0] for v in t.values()) / max(1, steps)
+    avg = ing_ms / max(1, ing_n)
+    algo = batch * bytes_per_tuple
+    ach = algo / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
+    ach_step = algo / (step_ms * 1e-3) / 1e9 if step_ms > 0 else 0.0
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "kernel": kernel, "algorithmic_bytes_per_launch": algo, "avg_launch_ms": avg, "launches": ing_n,
+            "achieved_step": ach_step, "frac_step": ach_step / HBM_PEAK_GBS, "device_ms_per_step": step_ms,
+            "device_ms_per_step_by_class": {k: v[0] / max(1, steps) for k, v in t.items()}}
+
+
+# ----------------------------------------------------------------------------------------------- CPU baselines
+def _cpu_nonkeyed(setup, gen_step, wm_of, steps_range, budget_s, chunk, warm=None, sample=""):
+    """Oracle (C++ restatement of SlicingWindowOperator, 1 thread) on the same stream: an untimed sparse warm-up
+    (warm: list of (ts, vals, wm)), then the full-rate steps of the GPU leg in chunks of `chunk` tuples, a watermark
+    at the end of every step (the GPU cadence), until the budget is spent; a watermark closes the sample."""
     from oracle.oracle import OracleOperator
     op = OracleOperator()
-    op.addWindowFunction(0)  # SUM_I32
-    op.addWindowFunction(1)  # COUNT
-    op.setMaxLateness(1)
-    for s in sizes:
-        op.addWindowAssigner(0, 0, s, 0)
-    chunk = 1 << 21
-    rng = np.random.default_rng(11)
-    done, t_proc, ms_per_chunk = 0, 0.0, chunk / rate_per_ms
-    t_start = time.time()
-    k = 0
-    while time.time() - t_start < budget_s:
-        idx = np.arange(done, done + chunk, dtype=np.int64)
-        ts = (idx // rate_per_ms).astype(np.int64)
-        vals = rng.integers(-2**31, 2**31, size=chunk, dtype=np.int64).astype(np.int32).astype(np.int64)
-        t0 = time.perf_counter()
+    setup(op)
+    for ts, vals, wm in (warm or []):
         op.processElements(ts, vals)
-        op.processWatermark(int(ts[-1]))
+        if wm is not None:
+            op.processWatermark(wm)
+    done, t_proc, n_wm, last_ts = 0, 0.0, 0, None
+    for s in steps_range:
+        ts, vals = gen_step(s)
+        for c0 in range(0, len(ts), chunk):
+            t0 = time.perf_counter()
+            op.processElements(ts[c0:c0 + chunk], vals[c0:c0 + chunk])
+            t_proc += time.perf_counter() - t0
+            done += min(chunk, len(ts) - c0)
+            last_ts = int(ts[min(len(ts), c0 + chunk) - 1])
+            if t_proc > budget_s:
+                break
+        t0 = time.perf_counter()
+        op.processWatermark(wm_of(s, last_ts) if t_proc <= budget_s else wm_of(s, last_ts, partial=True))
         t_proc += time.perf_counter() - t0
-        done += chunk
-        k += 1
+        n_wm += 1
+        if t_proc > budget_s:
+            break
     return {"value": done / t_proc, "unit": "tuples/s", "cores": 1, "kind": "port",
-            "sample": "%d tuples (%.0f ms of event time at %d tuples/ms, %d watermarks) of the same C2 stream, "
-                      "oracle/ C++ restatement of SlicingWindowOperator, 1 thread" % (done, done / rate_per_ms,
-                                                                                    rate_per_ms, k)}
+            "sample": "%d tuples, %d watermarks of the same stream; %s; oracle/ C++ restatement of "
+                      "SlicingWindowOperator, 1 thread" % (done, n_wm, sample)}
 
 
+def cpu_c2(sizes, rate):
+    def setup(op):
+        op.addWindowFunction(0)
+        op.addWindowFunction(1)
+        op.setMaxLateness(1)
+        for s in sizes:
+            op.addWindowAssigner(0, 0, s, 0)
+    rng = np.random.default_rng(11)
+    warm_ts = np.arange(0, 21000, dtype=np.int64)
+    warm = [(warm_ts, np.zeros(len(warm_ts), np.int64), 20999)]
+
+    def gen(s):
+        ts = 21000 + s * 1000 + np.arange(rate * 1000, dtype=np.int64) // rate
+        return ts, rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64)
+    return _cpu_nonkeyed(setup, gen, lambda s, lt, partial=False: lt, range(1000), CPU_BUDGET_S, 1 << 22, warm,
+                         "C2 at %d tuples/ms after a 21 s sparse warm-up (1 tuple/ms)" % rate)
+
+
+def c2s_windows(pkg):
+    """1000 concurrent sliding windows: sizes BenchmarkRunner.randomTumbling(1000,1,20) (java.util.Random(10)),
+    slide = size/20 (50..1000 ms; a power-of-two slide is bumped by 1 ms, as the reference would hang on it)."""
+    out = []
+    for size in pkg.workloads.random_tumbling_sizes(1000, 1, 20, seed=10):
+        slide = max(1, size // 20)
+        if slide & (slide - 1) == 0:
+            slide += 1
+        out.append((size, slide))
+    return out
+
+
+def cpu_c2s(pkg, rate):
+    wins = c2s_windows(pkg)
+
+    def setup(op):
+        op.addWindowFunction(0)
+        op.addWindowFunction(1)
+        op.setMaxLateness(1000)
+        for size, slide in wins:
+            op.addWindowAssigner(1, 0, size, slide)
+    rng = np.random.default_rng(12)
+    warm_ts = np.arange(1, 21000, dtype=np.int64)
+    warm = [(warm_ts, np.zeros(len(warm_ts), np.int64), 20499)]
+
+    def gen(s):
+        ts = 21000 + s * 1000 + np.arange(rate * 1000, dtype=np.int64) // rate
+        late = rng.random(len(ts)) < 0.2
+        d = rng.integers(1, 501, size=len(ts))
+        ts = np.where(late, np.maximum(ts - d, 1), ts)
+        return ts, rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64)
+    return _cpu_nonkeyed(setup, gen, lambda s, lt, partial=False: 21000 + s * 1000 + 999 - 500, range(1000),
+                         CPU_BUDGET_S, 1 << 20, warm,
+                         "C2s at %d tuples/ms, 20%% late by U[1,500] ms, after a 21 s sparse warm-up" % rate)
+
+
+def cpu_c3(rate):
+    def setup(op):
+        op.addWindowFunction(2)
+        op.addWindowFunction(3)
+        op.setMaxLateness(1000)
+        op.addWindowAssigner(1, 0, 60_000, 60)
+        op.addWindowAssigner(2, 0, 1000, 0)
+    rng = np.random.default_rng(13)
+    warm = []
+    for s in range(61):  # sparse warm-up with the same session pauses
+        t_begin = s * 1000 + 1000 + (s // 10) * 1500
+        ts = t_begin + np.arange(0, 1000, dtype=np.int64)
+        warm.append((ts, np.zeros(len(ts), np.int64), t_begin + 999 - 500 if s % 10 == 9 or s == 60 else None))
+
+    def gen(s):
+        t_begin = s * 1000 + 1000 + (s // 10) * 1500
+        ts = t_begin + np.arange(rate * 1000, dtype=np.int64) // rate
+        late = rng.random(len(ts)) < 0.2
+        d = rng.integers(1, 501, size=len(ts))
+        ts = np.where(late, np.maximum(ts - d, t_begin - 500), ts)
+        return ts, rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64)
+
+    def wm(s, lt, partial=False):
+        return s * 1000 + 1000 + (s // 10) * 1500 + 999 - 500 if not partial else lt - 500
+    return _cpu_nonkeyed(setup, gen, wm, range(61, 2000), CPU_BUDGET_S, 1 << 20, warm,
+                         "C3 at %d tuples/ms, 20%% late, after a 61 s sparse warm-up with the session pauses" % rate)
+
+
+def cpu_c5(pkg, rate):
+    sizes = pkg.workloads.random_count_sizes(1000, 1_000_000, 20_000_000, seed=10)
+
+    def setup(op):
+        op.addWindowFunction(0)
+        op.addWindowFunction(1)
+        op.setMaxLateness(1)
+        for size in sizes:
+            op.addWindowAssigner(0, 1, size, 0)
+    rng = np.random.default_rng(14)
+
+    def gen(s):
+        ts = s * 1000 + np.arange(rate * 1000, dtype=np.int64) // rate
+        return ts, rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64)
+    return _cpu_nonkeyed(setup, gen, lambda s, lt, partial=False: lt, range(1000), CPU_BUDGET_S, 1 << 22, None,
+                         "C5 from the stream start at %d tuples/ms (count windows fire every 1M-20M tuples)" % rate)
+
+
+def cpu_c4(keys, batch, threads):
+    """KeyedScottyWindowOperator on T threads (key % T partitions): sparse warm-up (2^20 tuples per second for
+    60 s, so every key's operator holds its sliding-window slices), then full-rate steps of the GPU leg."""
+    from oracle.oracle import KeyedOracleThreads
+    op = KeyedOracleThreads(threads)
+    op.addWindowFunction(0)
+    op.setMaxLateness(1)
+    op.addWindowAssigner(1, 0, 60_000, 1_000)
+    rng = np.random.default_rng(15)
+    warm_n = 1 << 20
+    for s in range(60):
+        k = rng.integers(0, keys, size=warm_n).astype(np.uint32)
+        ts = s * 1000 + np.arange(warm_n, dtype=np.int64) // (warm_n // 1000)
+        op.process(op.partition(k, ts, np.zeros(warm_n, np.int64)), s * 1000 + 999)
+    rate = batch // 1000
+    done, t_proc, rows, steps = 0, 0.0, 0, 0
+    for s in range(60, 1000):
+        k = rng.integers(0, keys, size=batch).astype(np.uint32)
+        ts = s * 1000 + np.arange(batch, dtype=np.int64) // rate
+        v = rng.integers(-2**31, 2**31, size=batch, dtype=np.int64)
+        p = op.partition(k, ts, v)
+        t0 = time.perf_counter()
+        rows += op.process(p, s * 1000 + (batch - 1) // rate)
+        t_proc += time.perf_counter() - t0
+        done += batch
+        steps += 1
+        if t_proc > CPU_BUDGET_S:
+            break
+    return {"value": done / t_proc, "unit": "tuples/s", "cores": threads, "kind": "port",
+            "sample": "%d steps of %d tuples (%d uniform keys, 1 s of event time each, one watermark per step) after a "
+                      "60 s sparse warm-up; oracle/ KeyedScottyWindowOperator restatement, %d threads (key %% %d "
+                      "partitions)" % (steps, batch, keys, threads, threads)}
+
+
+# ----------------------------------------------------------------------------------------------- GPU legs
 def extra_c3(pkg, dev, batch, steps, warm=61):
     """BASELINE configs[2] (C3): SlidingWindow(60 s, 60 ms) + SessionWindow(1 s gap), MIN_I32 + MAX_I32, 20 %
     out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; exact engine
@@ -82,7 +244,7 @@ def extra_c3(pkg, dev, batch, steps, warm=61):
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 60))
     op.addWindowAssigner(pkg.SessionWindow(pkg.WindowMeasure.Time, 1000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
-    times, rows, events = [], 0, 0
+    times, rows = [], 0
     for s in range(warm + steps):
         t_begin = s * 1000 + 1000 + (s // 10) * 1500
         ts = base + t_begin
@@ -101,25 +263,16 @@ def extra_c3(pkg, dev, batch, steps, warm=61):
     return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
                         "(delay U[1,500] ms), lag 500 ms, 1.5 s pause every 10 s, non-keyed, exact engine",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
-            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows}
-
-
-def c2s_windows(pkg):
-    """1000 concurrent sliding windows: sizes BenchmarkRunner.randomTumbling(1000,1,20) (java.util.Random(10)),
-    slide = size/20 (50..1000 ms; a power-of-two slide is bumped by 1 ms, as the reference would hang on it)."""
-    out = []
-    for size in pkg.workloads.random_tumbling_sizes(1000, 1, 20, seed=10):
-        slide = max(1, size // 20)
-        if slide & (slide - 1) == 0:
-            slide += 1
-        out.append((size, slide))
-    return out
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
+            "roofline_wall": {"achieved": batch * BYTES_PER_TUPLE * len(times) / sum(times) / 1e9,
+                              "frac": batch * BYTES_PER_TUPLE * len(times) / sum(times) / 1e9 / HBM_PEAK_GBS}}
 
 
 def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
     """north_star target workload: 1000 concurrent sliding windows (c2s_windows), SUM_I32 + COUNT, 20 %
     out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; grid path.  Warm-up until the
-    largest window (20 s) has been emitted, so every timed step assembles a full set of windows."""
+    largest window (20 s) has been emitted, so every timed step assembles a full set of windows.  Inputs are
+    generated for every step before the timed region starts (resident in HBM)."""
     import torch
     rate = max(1, batch // 1000)
     g = torch.Generator(device=dev)
@@ -133,40 +286,42 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
     for size, slide in c2s_windows(pkg):
         op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, size, slide))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
-    times, rows = [], 0
-    op.enableTiming(True)
-    for s in range(warm + steps):
+
+    def gen(s):
         ts = base + s * 1000 + 1000
         late = torch.rand(batch, device=dev, generator=g) < ooo
         d = torch.randint(1, 501, (batch,), device=dev, generator=g)
         ts = torch.where(late, torch.clamp(ts - d, min=1), ts).contiguous()
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
-        if s == warm:
-            op.enableTiming(False)
-            op.enableTiming(True)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
+        return ts, v
+    for s in range(warm):
+        ts, v = gen(s)
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
+    timed = [gen(s) for s in range(warm, warm + steps)]
+    torch.cuda.synchronize(dev)
+    rows = 0
+    op.enableTiming(True)
+    t0 = time.perf_counter()
+    for i, s in enumerate(range(warm, warm + steps)):
+        ts, v = timed[i]
         op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
         n, _ = op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
-        torch.cuda.synchronize(dev)
-        if s >= warm:
-            times.append(time.perf_counter() - t0)
-            rows += n
-    ingest_ms, launches, _ = op.ingestTiming()
-    avg_ms = ingest_ms / max(1, launches)
-    achieved = batch * BYTES_PER_TUPLE / (avg_ms * 1e-3) / 1e9
+        rows += n
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
     f = op._l.scotty_debug_grid_stat
     f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int]
     log("c2s: tuples added with global atomics since creation:", f(op._h, 0))
     return {"workload": "C2s: 1000 concurrent sliding windows, sizes randomTumbling(1000,1,20) Random(10), slide "
                         "size/20, SUM_I32+COUNT, 20% out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000",
-            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
-            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
-            "ingest": {"avg_launch_ms": avg_ms, "achieved_GBs": achieved, "frac": achieved / HBM_PEAK_GBS}}
+            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * elapsed / steps,
+            "value": batch * steps / elapsed, "unit": "tuples/s", "windows_emitted": rows,
+            "roofline": device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")}
 
 
 def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20_000_000, rank=0, world=1,
-              dist=None):
+             dist=None):
     """BASELINE configs[4] (C5): count-based windows, BenchmarkRunner.randomCount(n, lo, hi) (TumblingWindow(Count,
     size), java.util.Random(10)), SUM_I32 + COUNT, in-order non-keyed stream, maxLateness 1; count path (every slice
     a LazySlice, S/slice/SliceFactory.java:17-22).  world > 1: time/arrival-range sharding -- rank r holds arrival
@@ -217,7 +372,9 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
                                                        "cells)" % G if G > 1 else ""),
             "tuples_per_step": batch * G, "tuples_per_step_per_gpu": batch, "steps": steps,
             "ms_per_step": 1e3 * elapsed / len(times), "value": batch * G * len(times) / elapsed, "unit": "tuples/s",
-            "scaling": "weak", "windows_emitted": rows}
+            "scaling": "weak", "windows_emitted": rows,
+            "roofline_wall": {"achieved": batch * BYTES_PER_TUPLE * len(times) / (elapsed / G * G) / 1e9,
+                              "frac": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9 / HBM_PEAK_GBS}}
 
 
 def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None):
@@ -260,12 +417,28 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
+    per_gpu = batch * len(times) / elapsed
     return {"workload": "C4: keyed SlidingWindow(60s,1s) SUM_I32, %d uniform keys%s, maxLateness=1, results left "
                         "in HBM" % (keys, " key-hash sharded over %d GPUs (no collective)" % world if world > 1 else ""),
             "tuples_per_step": batch * world, "tuples_per_step_per_gpu": batch, "steps": steps,
             "keys_per_gpu": op.keyCount(), "ms_per_step": 1e3 * elapsed / len(times),
             "value": batch * world * len(times) / elapsed, "unit": "tuples/s", "scaling": "weak",
-            "windows_emitted_rank0": rows}
+            "windows_emitted_rank0": rows,
+            "roofline_wall": {"achieved": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9,
+                              "frac": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9 / HBM_PEAK_GBS}}
+
+
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: run N ranks through torch.distributed.run as a child (no GPU touched here)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench: launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd)
 
 
 def main():
@@ -275,14 +448,23 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C4 secondary measurements")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5); default all")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d: refusing to report a run on a different GPU count"
+                         % (args.gpus, world))
     import torch
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        raise SystemExit("bench: rank %d needs GPU %d but only %d GPU(s) are visible" % (rank, local, ndev))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -346,13 +528,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    ingest_ms, launches, tuples = op.ingestTiming()
     assert op.processedCount() >= B * nsteps - 1, op.processedCount()
+    log("bench: C2 done, %.3f ms/step" % (elapsed * 1e3 / args.steps))
 
+    res = None
     if rank == 0:
         total = B * args.steps * world
-        avg_ms = ingest_ms / max(1, launches)
-        achieved = (B * BYTES_PER_TUPLE) / (avg_ms * 1e-3) / 1e9
+        roof = device_roofline(op, args.steps, B, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "ingest_traffic.json")
         if os.path.exists(tfile):
@@ -362,6 +544,7 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        roof["traffic"] = traffic
         res = {
             "metric": METRIC,
             "value": total / elapsed,
@@ -381,26 +564,44 @@ def main():
                        "windows_emitted": n_windows,
                        "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch"
                                        % world) if sharded else "single GPU"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "ingest_kernel<VT_I32,NEED_SUM>", "algorithmic_bytes_per_launch":
-                             B * BYTES_PER_TUPLE, "avg_launch_ms": avg_ms, "launches": launches},
+            "roofline": roof,
         }
+    legs = set(x for x in args.only.split(",") if x) or {"c2s", "c3", "c4", "c5"}
+    extra = {}
     if not args.no_extra:
         del batches
         del op
         torch.cuda.empty_cache()
         if world == 1:
-            extra = {"c2s": extra_c2s(pkg, dev, 1 << 27, 5), "c3": extra_c3(pkg, dev, 1 << 26, 5),
-                     "c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5), "c5": extra_c5(pkg, dev, 1 << 27, 5)}
+            if "c2s" in legs:
+                extra["c2s"] = extra_c2s(pkg, dev, 1 << 27, 5)
+                log("bench: C2s done")
+            if "c3" in legs:
+                extra["c3"] = extra_c3(pkg, dev, 1 << 26, 5)
+                log("bench: C3 done")
+            if "c4" in legs:
+                extra["c4"] = extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5)
+                log("bench: C4 done")
+            if "c5" in legs:
+                extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)
+                log("bench: C5 done")
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
             extra = {"c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, rank=rank, world=world, dist=dist),
                      "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist)}
-        if rank == 0:
-            res["extra"] = extra
     if rank == 0:
+        if extra:
+            res["extra"] = extra
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(sizes, rate)
+            # CPU baselines on this box's host cores, rank 0, N=1 only (bounded samples of the same streams)
+            res["cpu_baseline"] = cpu_c2(sizes, rate)
+            log("bench: CPU C2 done")
+            threads = min(16, os.cpu_count() or 1)  # the box's CPU share for one GPU
+            cb = {"c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
+                  "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000)}
+            for name, fn in cb.items():
+                if name in extra:
+                    extra[name]["cpu_baseline"] = fn()
+                    log("bench: CPU %s done" % name)
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -158,12 +158,22 @@ int64_t scotty_slice_count(scotty_op* op);
  * milliseconds and launch count since the last reset. */
 int scotty_enable_timing(scotty_op* op, int on);
 int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, uint64_t* tuples);
+/* Device time per class since scotty_enable_timing, from HIP events around each launch group on the op's stream
+ * (grid path: every launch and transfer of a micro-batch and a watermark is in exactly one class, so the sum over
+ * the classes is the device time of the step; count path: ingest only).  Resolved at each watermark. */
+#define SCOTTY_TIME_INGEST 0      /* the ingest kernel (the HBM-bound pass over the tuples) */
+#define SCOTTY_TIME_PUSH_OTHER 1  /* the other kernels of a micro-batch (cell index, edge commit) */
+#define SCOTTY_TIME_WATERMARK 2   /* triggers, window assembly, GC */
+#define SCOTTY_TIME_RESULT_COPY 3 /* the packed result transfer to the host */
+int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* intervals);
 
 /* Tuning knobs (not semantics): "slice_capacity" / "session_capacity" per operator of the exact engine
  * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only), "exact_serial"
  * (non-keyed: single-wavefront replay, A/B only), "keyed_lane" 0 (keyed: wavefront-per-key replay instead of
  * the lane-per-key path for context-free time windows, A/B only), "count_path" 0 (count-window operators on the
- * exact engine instead of the count path, A/B only), "ingest_blocks", "shard_cells" / "shard_cands". */
+ * exact engine instead of the count path, A/B only), "ingest_blocks", "shard_cells" / "shard_cands" (cells /
+ * edge candidates per rank record of the time-window exchange), "shard_count_cells" (count cells per rank record
+ * of the count-window exchange). */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */

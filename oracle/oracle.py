@@ -90,6 +90,13 @@ def lib():
             "orc_manager_flags": (ctypes.c_int, [P]),
             "orc_max_lateness": (i64, [P]),
             "orc_current_count": (i64, [P]),
+            "orc_keyed_create": (P, [ctypes.c_int]),
+            "orc_keyed_destroy": (None, [P]),
+            "orc_keyed_add_window": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_int, i64, i64]),
+            "orc_keyed_add_aggregation": (ctypes.c_int, [P, ctypes.c_int]),
+            "orc_keyed_set_max_lateness": (ctypes.c_int, [P, i64]),
+            "orc_keyed_num_keys": (i64, [P]),
+            "orc_keyed_process": (i64, [P, P, P, P, P, i64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -251,3 +258,51 @@ class OracleOperator:
 
     def max_lateness(self):
         return self._l.orc_max_lateness(self._h)
+
+
+class KeyedOracleThreads:
+    """KeyedScottyWindowOperator (flink-connector/.../KeyedScottyWindowOperator.java:41-86) restated on the CPU with
+    the key space split over T threads (partition = key % T, as an upstream keyBy of parallelism T delivers).
+    CPU baseline of the keyed configuration; process() returns the forwarded (hasValue) window count."""
+
+    def __init__(self, threads):
+        self._l = lib()
+        self.threads = int(threads)
+        self._h = self._l.orc_keyed_create(self.threads)
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._l.orc_keyed_destroy(self._h)
+        except Exception:
+            pass
+
+    def addWindowAssigner(self, kind, measure, a=0, b=0):
+        self._l.orc_keyed_add_window(self._h, kind, measure, a, b)
+
+    def addWindowFunction(self, kind):
+        self._l.orc_keyed_add_aggregation(self._h, kind)
+
+    def setMaxLateness(self, l):
+        self._l.orc_keyed_set_max_lateness(self._h, l)
+
+    def partition(self, keys, ts, values):
+        """Rows grouped by partition (stable: arrival order kept inside each partition) + offsets."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        part = (keys % self.threads).astype(np.uint8)
+        order = np.argsort(part, kind="stable")
+        off = np.zeros(self.threads + 1, dtype=np.int64)
+        off[1:] = np.cumsum(np.bincount(part, minlength=self.threads))
+        return (off, np.ascontiguousarray(keys[order]), np.ascontiguousarray(np.asarray(ts, dtype=np.int64)[order]),
+                np.ascontiguousarray(np.asarray(values, dtype=np.int64)[order]))
+
+    def process(self, parted, watermark):
+        off, k, t, v = parted
+        n = self._l.orc_keyed_process(self._h, off.ctypes.data, k.ctypes.data, t.ctypes.data, v.ctypes.data,
+                                      int(watermark))
+        if n < 0:
+            raise JavaError(n, "keyed oracle error %d" % n)
+        return n
+
+    def numKeys(self):
+        return self._l.orc_keyed_num_keys(self._h)

@@ -22,6 +22,8 @@
 #include <random>
 #include <set>
 #include <string>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -1051,5 +1053,97 @@ int orc_manager_flags(orc_op* o) {
 }
 int64_t orc_max_lateness(orc_op* o) { return o->op.maxLateness; }
 int64_t orc_current_count(orc_op* o) { return o->op.currentCount; }
+
+// ---- keyed connector (flink-connector/.../KeyedScottyWindowOperator.java:41-86): one operator per key, created on
+//      first sight (:56-62); a watermark is processed by every key's operator (:72-86), which forwards only hasValue()
+//      windows (:80).  The CPU baseline runs T partitions of the key space on T threads (what an upstream keyBy with
+//      parallelism T delivers): partition t owns rows [off[t], off[t+1]) of the arrays.
+struct orc_keyed {
+  struct WinSpec {
+    int kind, measure;
+    int64_t a, b;
+  };
+  std::vector<WinSpec> wins;
+  std::vector<int> aggs;
+  int64_t lateness = 1000;
+  int threads = 1;
+  std::vector<std::unordered_map<uint32_t, orc_op*>> maps;
+};
+
+orc_keyed* orc_keyed_create(int threads) {
+  orc_keyed* k = new orc_keyed();
+  k->threads = threads < 1 ? 1 : threads;
+  k->maps.resize(k->threads);
+  return k;
+}
+void orc_keyed_destroy(orc_keyed* k) {
+  if (!k) return;
+  for (auto& m : k->maps)
+    for (auto& kv : m) delete kv.second;
+  delete k;
+}
+int orc_keyed_add_window(orc_keyed* k, int kind, int measure, int64_t a, int64_t b) {
+  k->wins.push_back({kind, measure, a, b});
+  return ORC_OK;
+}
+int orc_keyed_add_aggregation(orc_keyed* k, int kind) {
+  k->aggs.push_back(kind);
+  return ORC_OK;
+}
+int orc_keyed_set_max_lateness(orc_keyed* k, int64_t l) {
+  k->lateness = l;
+  return ORC_OK;
+}
+int64_t orc_keyed_num_keys(orc_keyed* k) {
+  int64_t n = 0;
+  for (auto& m : k->maps) n += (int64_t)m.size();
+  return n;
+}
+// processElement of every row (arrival order within each partition), then processWatermark(wm) of every key's
+// operator.  Returns the number of forwarded (hasValue) windows, or a negative Java error code.
+int64_t orc_keyed_process(orc_keyed* k, const int64_t* off, const uint32_t* keys, const int64_t* ts,
+                          const int64_t* vi, int64_t wm) {
+  std::vector<int64_t> emitted(k->threads, 0);
+  std::vector<int> errs(k->threads, ORC_OK);
+  auto work = [&](int t) {
+    auto& mp = k->maps[t];
+    for (int64_t r = off[t]; r < off[t + 1]; r++) {
+      auto it = mp.find(keys[r]);
+      orc_op* o;
+      if (it == mp.end()) {  // initWindowOperator() (:57-60)
+        o = orc_create(ORC_STATE_MEMORY);
+        for (auto& w : k->wins) orc_add_window(o, w.kind, w.measure, w.a, w.b);
+        for (int a : k->aggs) orc_add_aggregation(o, a);
+        orc_set_max_lateness(o, k->lateness);
+        mp.emplace(keys[r], o);
+      } else {
+        o = it->second;
+      }
+      Elem e{vi[r], (double)vi[r]};
+      const int rc = guarded(o, [&] { o->op.processElement(e, ts[r]); });
+      if (rc != ORC_OK && errs[t] == ORC_OK) errs[t] = rc;
+    }
+    for (auto& kv : mp) {
+      orc_op* o = kv.second;
+      const int rc = guarded(o, [&] { o->op.processWatermark(wm); });
+      if (rc != ORC_OK) {
+        if (errs[t] == ORC_OK) errs[t] = rc;
+        continue;
+      }
+      for (auto& w : o->op.result)
+        if (w.st.hasValues()) emitted[t]++;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < k->threads; t++) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  int64_t tot = 0;
+  for (int t = 0; t < k->threads; t++) {
+    if (errs[t] != ORC_OK) return errs[t];
+    tot += emitted[t];
+  }
+  return tot;
+}
 
 }  // extern "C"

@@ -112,6 +112,18 @@ int orc_manager_flags(orc_op*);
 int64_t orc_max_lateness(orc_op*);
 int64_t orc_current_count(orc_op*);
 
+/* --- keyed connector (KeyedScottyWindowOperator.java:41-86) on T threads: CPU baseline of the keyed config --- */
+typedef struct orc_keyed orc_keyed;
+orc_keyed* orc_keyed_create(int threads);
+void orc_keyed_destroy(orc_keyed*);
+int orc_keyed_add_window(orc_keyed*, int kind, int measure, int64_t a, int64_t b);
+int orc_keyed_add_aggregation(orc_keyed*, int kind);
+int orc_keyed_set_max_lateness(orc_keyed*, int64_t);
+int64_t orc_keyed_num_keys(orc_keyed*);
+/* partition t = rows [off[t], off[t+1]); returns forwarded (hasValue) windows or a negative error */
+int64_t orc_keyed_process(orc_keyed*, const int64_t* off, const uint32_t* keys, const int64_t* ts,
+                          const int64_t* value_i, int64_t watermark);
+
 #ifdef __cplusplus
 }
 #endif

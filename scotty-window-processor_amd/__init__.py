@@ -152,6 +152,8 @@ def lib():
             "scotty_enable_timing": (ctypes.c_int, [P, ctypes.c_int]),
             "scotty_ingest_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
                                                     ctypes.POINTER(u64)]),
+            "scotty_device_timing": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                    ctypes.POINTER(u64)]),
             "scotty_sync": (ctypes.c_int, [P]),
         }
         for name, (res, args) in sig.items():
@@ -337,7 +339,8 @@ class SlicingWindowOperator:
         col = lambda p, dt: np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, dt)
         res = {"start": col(out.start, np.int64), "end": col(out.end, np.int64),
                "measure": col(out.measure, np.int32), "has_value": col(out.has_value, np.uint8).astype(bool),
-               "values": [col(out.values[k], np.int64) for k in range(len(self._aggs))]}
+               "values": [col(out.values[k], np.int64).view(np.float64) if kind in F64_AGGS
+                          else col(out.values[k], np.int64) for k, kind in enumerate(self._aggs)]}
         if self._flags & FLAG_KEYED:
             res["key"] = col(out.key, np.uint32)
         return res
@@ -367,6 +370,16 @@ class SlicingWindowOperator:
         self._check(self._l.scotty_ingest_timing(self._h, ctypes.byref(ms), ctypes.byref(launches),
                                                  ctypes.byref(tuples)))
         return ms.value, launches.value, tuples.value
+
+    def deviceTiming(self):
+        """Device milliseconds per class since enableTiming (include/scotty_mi355x.h SCOTTY_TIME_*): a dict
+        {ingest, push_other, watermark, result_copy: (ms, intervals)}."""
+        out = {}
+        for cls, name in enumerate(("ingest", "push_other", "watermark", "result_copy")):
+            ms, n = ctypes.c_double(), ctypes.c_uint64()
+            self._check(self._l.scotty_device_timing(self._h, cls, ctypes.byref(ms), ctypes.byref(n)))
+            out[name] = (ms.value, n.value)
+        return out
 
     def sync(self):
         self._check(self._l.scotty_sync(self._h))

@@ -7,6 +7,7 @@
 //   tilemax  [TCAP]  max ts of each 4096-tuple arrival tile                    -- edge first-crossing lookups
 //   meta             DevMeta (device-resident slicer / store scalars)
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace scotty {
@@ -37,6 +38,8 @@ struct DevMeta {
   uint64_t late_push, overflow_push;   // per-push counters (reset by the commit kernel)
   uint64_t late_total, processed_total;
   uint64_t glb_slow;          // statistics: tuples the ingest kernel added with global atomics (outside the LDS window)
+  int64_t dirty_from;         // lowest slice index whose partials changed since the last watermark (block summaries)
+  int64_t whead;              // head before the last watermark's GC (window assembly reads [whead, tail))
 };
 
 struct IngestArgs {
@@ -85,21 +88,53 @@ struct CommitArgs {
   int64_t push_seq;
 };
 
-struct WindowArgs {
-  const int64_t* w_start;
-  const int64_t* w_end;
-  int64_t n_windows;
+// ---- watermark of the grid path (window_kernels.hip): window assembly over slice-block summaries.
+// Slices are grouped in blocks of SBLK consecutive slice-array entries.  Per block: count, sum, min, max; an
+// inclusive prefix over the blocks of count and (integer) sum -- int wrap arithmetic is exactly invertible, so
+// a run of whole blocks is P[last] - P[first-1]; a sparse table over block minima / maxima (level k covers 2^k
+// blocks) answers min / max of a run of whole blocks with two lookups.  A window [sa, sb) of slices is the
+// partial head block + the run of whole blocks + the partial tail block.
+constexpr int SBLK = 64;
+constexpr int ST_LEVELS = 15;      // 2^14 blocks * 64 = 2^20 slices (the slice capacity)
+constexpr int WM_HDR = 512;        // packed watermark output: header bytes (DevMeta snapshot + counts)
+constexpr int WM_HDR_N = 448;      // offset of the device's window count in the header
+
+struct WmArgs {
+  DevMeta* meta;
   const int64_t* s_tstart;
   const int64_t* s_tlast;
   const unsigned long long* s_cnt;
   const unsigned long long* s_part[NPART];
-  DevMeta* meta;
-  // outputs
-  uint8_t* has_value;
-  unsigned long long* o_cnt;
-  unsigned long long* o_part[NPART];
+  // block summaries (index = slice index / SBLK)
+  unsigned long long* b_cnt;
+  unsigned long long* b_part[NPART];
+  unsigned long long* p_cnt;       // inclusive prefix of b_cnt
+  unsigned long long* p_sum;       // inclusive prefix of b_part[0] (integer value types)
+  long long* st_min;               // [ST_LEVELS][nbcap], level 0 = b_part[1]
+  long long* st_max;
+  int64_t nbcap;
+  // window definitions (registration order): kind, a, b per definition
+  const int64_t* wdef;
+  int32_t n_defs;
+  int64_t last_wm, wm, remove_from;
+  int64_t n_windows;               // the host's count of triggered windows (layout of the packed output)
+  unsigned char* out;              // packed output (device): header, start[n], end[n], values[n_aggs][n], has[n]
+  int32_t n_aggs;
+  int32_t agg_kind[8];
   int need;
   int vt;
+};
+
+// byte offsets of the packed watermark output's columns for n windows and n_aggs aggregations
+struct WmLayout {
+  int64_t start, end, vals, has, total;
+  __host__ __device__ WmLayout(int64_t n, int n_aggs) {
+    start = WM_HDR;
+    end = start + 8 * n;
+    vals = end + 8 * n;
+    has = vals + 8 * n * n_aggs;
+    total = has + ((n + 7) / 8) * 8;
+  }
 };
 
 // Time/arrival-range sharding of one non-keyed micro-batch over G ranks: rank r ingests

@@ -23,7 +23,7 @@ hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long
                              hipStream_t st);
 hipError_t launch_key_assign(unsigned long long* table, const uint32_t* new_pos, int64_t n_new, int64_t base,
                              uint32_t* slot_key, hipStream_t st);
-hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask,
+hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask, int drop_new,
                          hipStream_t st);
 hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
                        uint32_t* slot, bool fixup, hipStream_t st);
@@ -383,7 +383,7 @@ int XEngine::ensure_batch(int64_t n) {
   return SCOTTY_OK;
 }
 
-int XEngine::ensure_table(int64_t keys_needed) {
+int XEngine::ensure_table(int64_t keys_needed, bool drop_new) {
   uint64_t want = 1024;
   while ((int64_t)want < 2 * keys_needed) want <<= 1;
   if (want <= tcap) return SCOTTY_OK;
@@ -391,7 +391,7 @@ int XEngine::ensure_table(int64_t keys_needed) {
   XCHK(dalloc(&nt, want));
   XCHK(hipMemsetAsync(nt, 0, want * 8, stream));
   if (d_table) {
-    XCHK(launch_rehash(d_table, tcap, nt, want - 1, stream));
+    XCHK(launch_rehash(d_table, tcap, nt, want - 1, drop_new ? 1 : 0, stream));
     XCHK(hipStreamSynchronize(stream));
     dfree(d_table);
   }
@@ -579,19 +579,25 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
   if (rc) return rc;
   rc = ensure_table(n_ops + std::min<int64_t>(n, 1 << 24));
   if (rc) return rc;
-  // 1. new keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator()))
-  XCHK(hipMemsetAsync(d_newcnt, 0, 8, stream));
-  XCHK(hipMemsetAsync(d_full, 0, 4, stream));
-  XCHK(launch_key_insert(d_key, n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, d_slot, stream));
-  XCHK(hipMemcpyAsync(h_misc, d_newcnt, 8, hipMemcpyDeviceToHost, stream));
-  XCHK(hipMemcpyAsync(h_misc + 1, d_full, 4, hipMemcpyDeviceToHost, stream));
-  XCHK(hipStreamSynchronize(stream));
-  const int64_t n_new = h_misc[0];
-  if ((int32_t)h_misc[1] != 0) {
-    err = "key hash table full";
-    failed = true;
-    return SCOTTY_ERR_NOMEM;
+  // 1. new keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator())).
+  //    A table that fills up mid-pass is grown (the pass's unassigned insertions dropped) and the pass re-run.
+  for (int attempt = 0;; attempt++) {
+    XCHK(hipMemsetAsync(d_newcnt, 0, 8, stream));
+    XCHK(hipMemsetAsync(d_full, 0, 4, stream));
+    XCHK(launch_key_insert(d_key, n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, d_slot, stream));
+    XCHK(hipMemcpyAsync(h_misc, d_newcnt, 8, hipMemcpyDeviceToHost, stream));
+    XCHK(hipMemcpyAsync(h_misc + 1, d_full, 4, hipMemcpyDeviceToHost, stream));
+    XCHK(hipStreamSynchronize(stream));
+    if ((int32_t)h_misc[1] == 0) break;
+    if (attempt >= 8 || (int64_t)tcap >= ((int64_t)1 << 33)) {
+      err = "key hash table full";
+      failed = true;
+      return SCOTTY_ERR_NOMEM;
+    }
+    rc = ensure_table((int64_t)tcap, true);  // 2x the slots
+    if (rc) return rc;
   }
+  const int64_t n_new = h_misc[0];
   if (n_new > 0) {
     rc = grow_ops(n_ops + n_new);
     if (rc) return rc;

@@ -63,7 +63,7 @@ class XEngine {
   int grow_ops(int64_t need);
   int grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx);
   int ensure_batch(int64_t n);
-  int ensure_table(int64_t keys);
+  int ensure_table(int64_t keys, bool drop_new = false);
   int ensure_rows(int64_t rows);
   int check_ready();
   XBatchArgs batch_args() const;

@@ -77,11 +77,15 @@ __global__ void key_assign_kernel(unsigned long long* table, const uint32_t* new
   }
 }
 
-__global__ void rehash_kernel(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask) {
+// drop_new: leave out keys inserted by an unfinished key_insert pass (slot placeholder 0xFFFFFFFF), so that pass
+// can be re-run from scratch on the grown table
+__global__ void rehash_kernel(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask,
+                              int drop_new) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)old_n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long e = old_t[i];
     if (e == 0) continue;
+    if (drop_new && (uint32_t)e == 0xFFFFFFFFu) continue;
     uint64_t h = hash32((uint32_t)((e >> 32) - 1)) & mask;
     while (atomicCAS(&nt[h], 0ull, e) != 0ull) h = (h + 1) & mask;
   }
@@ -347,8 +351,9 @@ hipError_t launch_key_assign(unsigned long long* table, const uint32_t* new_pos,
   return hipGetLastError();
 }
 hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsigned long long* nt, uint64_t mask,
-                         hipStream_t st) {
-  hipLaunchKernelGGL(k::rehash_kernel, dim3(grid_for((int64_t)old_n)), dim3(256), 0, st, old_t, old_n, nt, mask);
+                         int drop_new, hipStream_t st) {
+  hipLaunchKernelGGL(k::rehash_kernel, dim3(grid_for((int64_t)old_n)), dim3(256), 0, st, old_t, old_n, nt, mask,
+                     drop_new);
   return hipGetLastError();
 }
 hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,

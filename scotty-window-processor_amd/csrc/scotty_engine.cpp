@@ -24,8 +24,7 @@ namespace scotty {
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
-hipError_t launch_windows(const WindowArgs& a, hipStream_t st);
-hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st);
+hipError_t launch_wm(const WmArgs& a, hipStream_t st);
 hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
 hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st);
 hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st);
@@ -55,10 +54,8 @@ struct CFWin {  // context-free window (C/windowType/ContextFreeWindow.java)
   int64_t clear_delay() const { return kind == SCOTTY_WIN_FIXED_BAND ? b : a; }
 };
 
-struct TrigWin {
-  int64_t start, end;
-  int32_t measure;
-};
+// Device-time classes of scotty_device_timing (include/scotty_mi355x.h)
+constexpr int NTCLS = 4;
 
 }  // namespace
 
@@ -88,9 +85,8 @@ struct scotty_op {
   bool grid_complete = false;
 
   // ---- device buffers
-  int64_t scap = 0, gcap = 0, ccap = 0, tcap = 0, wcap = 0;
+  int64_t scap = 0, gcap = 0, ccap = 0, tcap = 0;
   DevMeta* d_meta = nullptr;
-  DevMeta* d_snap = nullptr;
   DevMeta* h_snap = nullptr;  // pinned
   int64_t* d_tstart = nullptr;
   int64_t* d_tlast = nullptr;
@@ -107,14 +103,21 @@ struct scotty_op {
   int32_t* d_rank = nullptr;
   int32_t* d_flag = nullptr;
   unsigned long long* d_scratch = nullptr;
-  // windows
-  int64_t* d_wstart = nullptr;
-  int64_t* d_wend = nullptr;
-  uint8_t* d_has = nullptr;
-  unsigned long long* d_ocnt = nullptr;
-  unsigned long long* d_opart[NPART] = {};
-  int64_t* h_wbuf = nullptr;        // pinned [2*wcap]
-  unsigned char* h_obuf = nullptr;  // pinned results
+  // watermark (window_kernels.hip): slice-block summaries, prefix sums, sparse tables, window definitions, and the
+  // packed result buffer (device + pinned host copy, one transfer per watermark)
+  int64_t nbcap = 0;
+  unsigned long long* d_bcnt = nullptr;
+  unsigned long long* d_bpart[NPART] = {};
+  unsigned long long* d_pcnt = nullptr;
+  unsigned long long* d_psum = nullptr;
+  long long* d_stmin = nullptr;
+  long long* d_stmax = nullptr;
+  int64_t* d_wdef = nullptr;
+  int64_t wdef_cap = 0;
+  bool wdef_dirty = true;
+  unsigned char* d_out = nullptr;
+  unsigned char* h_out = nullptr;  // pinned
+  int64_t out_cap = 0;
 
   // ---- pushes of the current watermark interval (replayed after a horizon overflow)
   struct Push {
@@ -153,18 +156,21 @@ struct scotty_op {
   int64_t shard_tile = TILE_MIN, shard_n = 0;
   XResult xr;
 
-  // ---- timing
+  // ---- timing: HIP events around every launch group on the op's stream, per device-time class
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;  // ingest launches (class 0)
+  struct TEv {
+    int cls;
+    hipEvent_t a, b;
+  };
+  std::vector<TEv> tev_pending;
   double t_ms = 0.0;
   uint64_t t_launches = 0, t_tuples = 0;
+  double t_cls_ms[NTCLS] = {};
+  uint64_t t_cls_n[NTCLS] = {};
 
   // ---- results
-  std::vector<TrigWin> trig;
-  std::vector<int64_t> r_start, r_end;
-  std::vector<int32_t> r_measure;
-  std::vector<uint8_t> r_has;
-  std::vector<std::vector<int64_t>> r_vals;
+  std::vector<int32_t> r_measure;  // grid path: every window is a time window (SCOTTY_MEASURE_TIME == 0)
 };
 
 namespace {
@@ -183,6 +189,41 @@ int fail(scotty_op* op, int code, const std::string& m) {
     }                                                                                 \
   } while (0)
 
+// Timed section of one device-time class: events recorded on the op's stream around a launch group.
+int tbegin(scotty_op* op, scotty_op::TEv& e, int cls) {
+  e.cls = cls;
+  e.a = e.b = nullptr;
+  if (!op->timing) return SCOTTY_OK;
+  if (!op->ev_pool.empty()) {
+    e.a = op->ev_pool.back().first;
+    e.b = op->ev_pool.back().second;
+    op->ev_pool.pop_back();
+  } else {
+    HIPCHK(hipEventCreate(&e.a));
+    HIPCHK(hipEventCreate(&e.b));
+  }
+  HIPCHK(hipEventRecord(e.a, op->stream));
+  return SCOTTY_OK;
+}
+int tend(scotty_op* op, scotty_op::TEv& e) {
+  if (!op->timing || !e.a) return SCOTTY_OK;
+  HIPCHK(hipEventRecord(e.b, op->stream));
+  op->tev_pending.push_back(e);
+  return SCOTTY_OK;
+}
+// after a stream synchronisation: fold every recorded interval into its class
+void tresolve(scotty_op* op) {
+  for (auto& e : op->tev_pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+      op->t_cls_ms[e.cls] += ms;
+      op->t_cls_n[e.cls]++;
+    }
+    op->ev_pool.push_back({e.a, e.b});
+  }
+  op->tev_pending.clear();
+}
+
 int agg_value_type(int kind) {
   switch (kind) {
     case SCOTTY_AGG_SUM_I32: case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MAX_I32: return VT_I32;
@@ -199,38 +240,6 @@ int agg_need(int kind) {
     case SCOTTY_AGG_MAX_I32: case SCOTTY_AGG_MAX_I64: case SCOTTY_AGG_MAX_F64: return NEED_MAX;
     default: return 0;
   }
-}
-
-double key_to_f64(int64_t k) {  // inverse of f64_key (slicing_kernels.hip)
-  int64_t b = k ^ ((k >> 63) & 0x7FFFFFFFFFFFFFFFLL);
-  double d;
-  std::memcpy(&d, &b, 8);
-  return d;
-}
-
-// lowered value of aggregation kind from (cnt, sum word, min word, max word)
-int64_t lower_value(int kind, uint64_t cnt, uint64_t sw, int64_t mn, int64_t mx) {
-  switch (kind) {
-    case SCOTTY_AGG_SUM_I32: return (int64_t)(int32_t)(uint32_t)sw;
-    case SCOTTY_AGG_COUNT: return (int64_t)(int32_t)(uint32_t)cnt;
-    case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MIN_I64: return mn;
-    case SCOTTY_AGG_MAX_I32: case SCOTTY_AGG_MAX_I64: return mx;
-    case SCOTTY_AGG_SUM_I64: return (int64_t)sw;
-    case SCOTTY_AGG_SUM_F64: return (int64_t)sw;  // already double bits
-    case SCOTTY_AGG_MIN_F64: {
-      double d = mn == INT64_MIN ? __builtin_nan("") : key_to_f64(mn);
-      int64_t b;
-      std::memcpy(&b, &d, 8);
-      return b;
-    }
-    case SCOTTY_AGG_MAX_F64: {
-      double d = mx == INT64_MAX ? __builtin_nan("") : key_to_f64(mx);
-      int64_t b;
-      std::memcpy(&b, &d, 8);
-      return b;
-    }
-  }
-  return 0;
 }
 
 // min over context-free time windows of assignNextWindowStart (StreamSlicer.calculateNextFixedEdge's loop,
@@ -304,11 +313,9 @@ int alloc_all(scotty_op* op) {
   op->gcap = 1 << 20;
   op->ccap = op->scap + op->gcap;
   op->tcap = 0;
-  op->wcap = 0;
   HIPCHK(hipSetDevice(op->device));
   HIPCHK(hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking));
   HIPCHK(hipMalloc(&op->d_meta, sizeof(DevMeta)));
-  HIPCHK(hipMalloc(&op->d_snap, sizeof(DevMeta)));
   HIPCHK(hipHostMalloc(&op->h_snap, sizeof(DevMeta), hipHostMallocDefault));
   HIPCHK(hipMemset(op->d_meta, 0, sizeof(DevMeta)));
   HIPCHK(hipMalloc(&op->d_tstart, op->scap * 8));
@@ -343,22 +350,54 @@ int ensure_tiles(scotty_op* op, int64_t n) {
   return SCOTTY_OK;
 }
 
-int ensure_windows(scotty_op* op, int64_t nw) {
-  if (nw <= op->wcap) return SCOTTY_OK;
+// Slice-block summaries of the watermark path (window_kernels.hip), sized for the slice capacity.
+int alloc_blocks(scotty_op* op) {
+  if (op->d_bcnt) return SCOTTY_OK;
+  op->nbcap = op->scap / SBLK + 1;
+  HIPCHK(hipMalloc(&op->d_bcnt, op->nbcap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_bpart[k], op->nbcap * 8));
+  HIPCHK(hipMalloc(&op->d_pcnt, op->nbcap * 8));
+  HIPCHK(hipMalloc(&op->d_psum, op->nbcap * 8));
+  HIPCHK(hipMalloc(&op->d_stmin, (size_t)ST_LEVELS * op->nbcap * 8));
+  HIPCHK(hipMalloc(&op->d_stmax, (size_t)ST_LEVELS * op->nbcap * 8));
+  return SCOTTY_OK;
+}
+
+// Packed watermark output (device + pinned host) of at least `bytes`.
+int ensure_wm_out(scotty_op* op, int64_t bytes) {
+  if (bytes <= op->out_cap) return SCOTTY_OK;
   HIPCHK(hipStreamSynchronize(op->stream));
-  auto F = [&](void* p) { if (p) (void)hipFree(p); };
-  F(op->d_wstart); F(op->d_wend); F(op->d_has); F(op->d_ocnt);
-  for (int k = 0; k < NPART; k++) F(op->d_opart[k]);
-  if (op->h_wbuf) (void)hipHostFree(op->h_wbuf);
-  if (op->h_obuf) (void)hipHostFree(op->h_obuf);
-  op->wcap = ((std::max(nw, (int64_t)1024) + 63) / 64) * 64;
-  HIPCHK(hipMalloc(&op->d_wstart, op->wcap * 8));
-  HIPCHK(hipMalloc(&op->d_wend, op->wcap * 8));
-  HIPCHK(hipMalloc(&op->d_has, op->wcap));
-  HIPCHK(hipMalloc(&op->d_ocnt, op->wcap * 8));
-  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_opart[k], op->wcap * 8));
-  HIPCHK(hipHostMalloc(&op->h_wbuf, op->wcap * 16, hipHostMallocDefault));
-  HIPCHK(hipHostMalloc(&op->h_obuf, op->wcap * (1 + 8 * (1 + NPART)), hipHostMallocDefault));
+  if (op->d_out) HIPCHK(hipFree(op->d_out));
+  if (op->h_out) HIPCHK(hipHostFree(op->h_out));
+  op->d_out = nullptr;
+  op->h_out = nullptr;
+  op->out_cap = std::max<int64_t>(bytes + bytes / 2, 1 << 16);
+  HIPCHK(hipMalloc(&op->d_out, op->out_cap));
+  HIPCHK(hipHostMalloc(&op->h_out, op->out_cap, hipHostMallocDefault));
+  return SCOTTY_OK;
+}
+
+// Window definitions (registration order) for the device triggers: kind, a, b.
+int upload_wdefs(scotty_op* op) {
+  if (!op->wdef_dirty) return SCOTTY_OK;
+  const int64_t n = (int64_t)op->windows.size();
+  if (n > op->wdef_cap) {
+    HIPCHK(hipStreamSynchronize(op->stream));
+    if (op->d_wdef) HIPCHK(hipFree(op->d_wdef));
+    op->wdef_cap = std::max<int64_t>(n, 64);
+    HIPCHK(hipMalloc(&op->d_wdef, op->wdef_cap * 3 * 8));
+  }
+  std::vector<int64_t> v;
+  for (const CFWin& w : op->windows) {
+    v.push_back(w.kind);
+    v.push_back(w.a);
+    v.push_back(w.b);
+  }
+  if (n > 0) {
+    HIPCHK(hipMemcpyAsync(op->d_wdef, v.data(), v.size() * 8, hipMemcpyHostToDevice, op->stream));
+    HIPCHK(hipStreamSynchronize(op->stream));  // v is pageable and local
+  }
+  op->wdef_dirty = false;
   return SCOTTY_OK;
 }
 
@@ -401,10 +440,13 @@ int compact_if_needed(scotty_op* op) {
   }
   int64_t ht[2] = {0, live};
   HIPCHK(hipMemcpyAsync(&op->d_meta->head, ht, 16, hipMemcpyHostToDevice, op->stream));
+  const int64_t zero = 0;  // block summaries follow slice indices: all of them are recomputed
+  HIPCHK(hipMemcpyAsync(&op->d_meta->dirty_from, &zero, 8, hipMemcpyHostToDevice, op->stream));
   HIPCHK(hipStreamSynchronize(op->stream));
   HIPCHK(hipFree(tmp));
   m.head = 0;
   m.tail = live;
+  m.dirty_from = 0;
   return SCOTTY_OK;
 }
 
@@ -435,7 +477,12 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   }
   ia.cix = op->d_cix;
   ia.cix_meta = op->d_cixmeta;
+  scotty_op::TEv tx;
+  rc = tbegin(op, tx, SCOTTY_TIME_PUSH_OTHER);
+  if (rc) return rc;
   HIPCHK(launch_cix_build(ia, op->stream));
+  rc = tend(op, tx);
+  if (rc) return rc;
   // tile: power of two >= TILE_MIN with at most NT_MAX tiles (the commit kernel keeps them in LDS)
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
@@ -495,8 +542,11 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
   ca.need = op->need;
   ca.vt = op->vt;
   ca.push_seq = seq;
+  scotty_op::TEv tc;
+  rc = tbegin(op, tc, SCOTTY_TIME_PUSH_OTHER);
+  if (rc) return rc;
   HIPCHK(launch_commit(ca, op->stream));
-  return SCOTTY_OK;
+  return tend(op, tc);
 }
 
 // First tuple of the operator's life: StreamSlicer + SliceManager for tuple 0 (the store is empty).
@@ -582,25 +632,32 @@ int replay_after_overflow(scotty_op* op) {
   return fail(op, SCOTTY_ERR_UNSUPPORTED, "edge-grid horizon overflow could not be resolved");
 }
 
-void trigger_windows(scotty_op* op, int64_t last_wm, int64_t wm) {
-  // WindowManager.assignContextFreeWindows (S/WindowManager.java:104-118) in registration order
-  op->trig.clear();
+// Number of windows WindowManager.assignContextFreeWindows triggers (S/WindowManager.java:104-118): the same loops as
+// TumblingWindow / SlidingWindow / FixedBandWindow.triggerWindows, which the device runs again to emit them (the
+// count only sizes the packed result transfer).  -1: more windows than any result buffer could hold.
+int64_t count_triggers(const scotty_op* op, int64_t last_wm, int64_t wm) {
+  int64_t n = 0;
+  const int64_t limit = (int64_t)1 << 31;
   for (const CFWin& w : op->windows) {
     if (w.kind == SCOTTY_WIN_TUMBLING) {  // TumblingWindow.triggerWindows :34-39
       const int64_t size = w.a;
       const int64_t last_start = jsub(last_wm, jmod(jadd(last_wm, size), size));
       for (int64_t ws = last_start; jadd(ws, size) <= wm; ws = jadd(ws, size))
-        op->trig.push_back({ws, jadd(ws, size), SCOTTY_MEASURE_TIME});
+        if (++n > limit) return -1;
     } else if (w.kind == SCOTTY_WIN_SLIDING) {  // SlidingWindow.triggerWindows :50-57
       const int64_t size = w.a, slide = w.b;
       const int64_t last_start = jsub(wm, jmod(jadd(wm, slide), slide));
-      for (int64_t ws = last_start; jadd(ws, size) > last_wm; ws = jsub(ws, slide))
-        if (ws >= 0 && jadd(ws, size) <= jadd(wm, 1)) op->trig.push_back({ws, jadd(ws, size), SCOTTY_MEASURE_TIME});
+      int64_t it = 0;
+      for (int64_t ws = last_start; jadd(ws, size) > last_wm; ws = jsub(ws, slide)) {
+        if (ws >= 0 && jadd(ws, size) <= jadd(wm, 1)) n++;
+        if (++it > limit || n > limit) return -1;
+      }
     } else {  // FixedBandWindow.triggerWindows :51-57
       const int64_t e = jadd(w.a, w.b);
-      if (last_wm <= e && e <= wm) op->trig.push_back({w.a, e, SCOTTY_MEASURE_TIME});
+      if (last_wm <= e && e <= wm) n++;
     }
   }
+  return n;
 }
 
 }  // namespace
@@ -633,14 +690,15 @@ void scotty_destroy(scotty_op* op) {
   (void)hipSetDevice(op->device);
   if (op->stream) (void)hipStreamSynchronize(op->stream);
   auto F = [](void* p) { if (p) (void)hipFree(p); };
-  F(op->d_meta); F(op->d_snap); F(op->d_tstart); F(op->d_tlast); F(op->d_scnt); F(op->d_grid);
+  F(op->d_meta); F(op->d_tstart); F(op->d_tlast); F(op->d_scnt); F(op->d_grid);
   F(op->d_ccnt); F(op->d_ctmax); F(op->d_tilemax); F(op->d_pmax); F(op->d_rank); F(op->d_flag);
-  F(op->d_scratch); F(op->d_wstart); F(op->d_wend); F(op->d_has); F(op->d_ocnt);
-  for (int k = 0; k < NPART; k++) { F(op->d_spart[k]); F(op->d_cpart[k]); F(op->d_opart[k]); }
+  F(op->d_scratch); F(op->d_bcnt); F(op->d_pcnt); F(op->d_psum); F(op->d_stmin); F(op->d_stmax); F(op->d_wdef);
+  F(op->d_out);
+  for (int k = 0; k < NPART; k++) { F(op->d_spart[k]); F(op->d_cpart[k]); F(op->d_bpart[k]); }
   for (void* p : op->owned) F(p);
   if (op->h_snap) (void)hipHostFree(op->h_snap);
-  if (op->h_wbuf) (void)hipHostFree(op->h_wbuf);
-  if (op->h_obuf) (void)hipHostFree(op->h_obuf);
+  if (op->h_out) (void)hipHostFree(op->h_out);
+  for (auto& e : op->tev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
@@ -990,6 +1048,8 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
   if (!op || !d_xbuf || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
   if (op->keyed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "keyed operators shard by key: no exchange needed");
+  if (((uintptr_t)d_ts & 15) || ((uintptr_t)d_val & 15))  // the ingest kernels load 16 B per lane
+    return fail(op, SCOTTY_ERR_ARG, "device buffers must be 16-byte aligned");
   int rc = decide_mode(op);
   if (rc) return rc;
   if (op->mode == 3)
@@ -1028,11 +1088,11 @@ int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_
   if (!op || !d_xbuf || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
   if (op->keyed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "keyed operators shard by key: no exchange needed");
+  if (((uintptr_t)d_ts & 15) || ((uintptr_t)d_val & 15))
+    return fail(op, SCOTTY_ERR_ARG, "device buffers must be 16-byte aligned");
   int rc = decide_mode(op);
   if (rc) return rc;
   if (op->mode != 3) return scotty_shard_push(op, d_ts, d_val, n, ts0, d_xbuf);
-  if (((uintptr_t)d_ts & 15) || ((uintptr_t)d_val & 15))
-    return fail(op, SCOTTY_ERR_ARG, "device buffers must be 16-byte aligned");
   rc = op->c->shard_push(d_ts, d_val, (int64_t)n, ts0, n_before, n_total, (int64_t*)d_xbuf);
   if (rc) return fail(op, rc, op->c->err);
   op->shard_count_total = n_total;
@@ -1070,51 +1130,60 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
   const uint64_t dropped_before = op->dropped;
   // WindowManager.processWatermark (S/WindowManager.java:41-80)
   if (op->last_watermark == -1) op->last_watermark = std::max((int64_t)0, jsub(wm, op->max_lateness));
-  op->r_start.clear(); op->r_end.clear(); op->r_measure.clear(); op->r_has.clear();
-  op->r_vals.assign(op->aggs.size(), {});
+  int64_t nw = 0;
+  const unsigned char* res = nullptr;
   if (!op->started) {
     op->last_watermark = wm;
   } else {
+    // lastWatermark is raised to the oldest slice's start (S/WindowManager.java:51-55)
     int64_t last_wm = op->last_watermark;
     if (last_wm < op->h_oldest) last_wm = op->h_oldest;
-    trigger_windows(op, last_wm, wm);
-    const int64_t nw = (int64_t)op->trig.size();
-    rc = ensure_windows(op, nw);
+    nw = count_triggers(op, last_wm, wm);
+    if (nw < 0) return fail(op, SCOTTY_ERR_NOMEM, "watermark triggers more than 2^31 windows");
+    const WmLayout L(nw, (int)op->aggs.size());
+    rc = alloc_blocks(op);
+    if (!rc) rc = ensure_wm_out(op, L.total);
+    if (!rc) rc = upload_wdefs(op);
     if (rc) return rc;
     const int64_t remove_from = jsub(jsub(wm, op->max_lateness), op->max_fixed_window_size);
+    WmArgs wa{};
+    wa.meta = op->d_meta;
+    wa.s_tstart = op->d_tstart;
+    wa.s_tlast = op->d_tlast;
+    wa.s_cnt = op->d_scnt;
+    for (int k = 0; k < NPART; k++) wa.s_part[k] = op->d_spart[k];
+    wa.b_cnt = op->d_bcnt;
+    for (int k = 0; k < NPART; k++) wa.b_part[k] = op->d_bpart[k];
+    wa.p_cnt = op->d_pcnt;
+    wa.p_sum = op->d_psum;
+    wa.st_min = op->d_stmin;
+    wa.st_max = op->d_stmax;
+    wa.nbcap = op->nbcap;
+    wa.wdef = op->d_wdef;
+    wa.n_defs = (int32_t)op->windows.size();
+    wa.last_wm = last_wm;
+    wa.wm = wm;
+    wa.remove_from = remove_from;
+    wa.n_windows = nw;
+    wa.out = op->d_out;
+    wa.n_aggs = (int32_t)op->aggs.size();
+    for (size_t k = 0; k < op->aggs.size(); k++) wa.agg_kind[k] = op->aggs[k];
+    wa.need = op->need;
+    wa.vt = op->vt;
     for (int attempt = 0; attempt < 2; attempt++) {
-      if (nw > 0) {
-        for (int64_t i = 0; i < nw; i++) {
-          op->h_wbuf[i] = op->trig[i].start;
-          op->h_wbuf[op->wcap + i] = op->trig[i].end;
-        }
-        HIPCHK(hipMemcpyAsync(op->d_wstart, op->h_wbuf, nw * 8, hipMemcpyHostToDevice, op->stream));
-        HIPCHK(hipMemcpyAsync(op->d_wend, op->h_wbuf + op->wcap, nw * 8, hipMemcpyHostToDevice, op->stream));
-        WindowArgs wa{};
-        wa.w_start = op->d_wstart;
-        wa.w_end = op->d_wend;
-        wa.n_windows = nw;
-        wa.s_tstart = op->d_tstart;
-        wa.s_tlast = op->d_tlast;
-        wa.s_cnt = op->d_scnt;
-        for (int k = 0; k < NPART; k++) wa.s_part[k] = op->d_spart[k];
-        wa.meta = op->d_meta;
-        wa.has_value = op->d_has;
-        wa.o_cnt = op->d_ocnt;
-        for (int k = 0; k < NPART; k++) wa.o_part[k] = op->d_opart[k];
-        wa.need = op->need;
-        wa.vt = op->vt;
-        HIPCHK(launch_windows(wa, op->stream));
-        unsigned char* hb = op->h_obuf;
-        HIPCHK(hipMemcpyAsync(hb, op->d_has, nw, hipMemcpyDeviceToHost, op->stream));
-        HIPCHK(hipMemcpyAsync(hb + op->wcap, op->d_ocnt, nw * 8, hipMemcpyDeviceToHost, op->stream));
-        for (int k = 0; k < NPART; k++)
-          HIPCHK(hipMemcpyAsync(hb + op->wcap * (1 + 8 * (1 + k)), op->d_opart[k], nw * 8, hipMemcpyDeviceToHost,
-                                op->stream));
-      }
-      HIPCHK(launch_gc(op->d_meta, op->d_tstart, remove_from, op->d_snap, op->stream));
-      HIPCHK(hipMemcpyAsync(op->h_snap, op->d_snap, sizeof(DevMeta), hipMemcpyDeviceToHost, op->stream));
+      // triggers + window assembly + GC (window_kernels.hip), then ONE transfer of the packed result
+      scotty_op::TEv tw, tc;
+      rc = tbegin(op, tw, SCOTTY_TIME_WATERMARK);
+      if (rc) return rc;
+      HIPCHK(launch_wm(wa, op->stream));
+      rc = tend(op, tw);
+      if (!rc) rc = tbegin(op, tc, SCOTTY_TIME_RESULT_COPY);
+      if (rc) return rc;
+      HIPCHK(hipMemcpyAsync(op->h_out, op->d_out, L.total, hipMemcpyDeviceToHost, op->stream));
+      rc = tend(op, tc);
+      if (rc) return rc;
       HIPCHK(hipStreamSynchronize(op->stream));
+      std::memcpy(op->h_snap, op->h_out, sizeof(DevMeta));
       if (!op->h_snap->overflow) break;
       rc = replay_after_overflow(op);
       if (rc) {
@@ -1126,20 +1195,14 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
       op->failed = true;
       return fail(op, SCOTTY_ERR_UNSUPPORTED, "edge-grid horizon overflow");
     }
-    // results (AggregateWindowState.getAggValues / hasValue, S/state/AggregateWindowState.java:41-49)
-    const unsigned char* hb = op->h_obuf;
-    const uint64_t* ocnt = (const uint64_t*)(hb + op->wcap);
-    const uint64_t* op0 = (const uint64_t*)(hb + op->wcap * (1 + 8));
-    const int64_t* op1 = (const int64_t*)(hb + op->wcap * (1 + 16));
-    const int64_t* op2 = (const int64_t*)(hb + op->wcap * (1 + 24));
-    for (int64_t i = 0; i < nw; i++) {
-      op->r_start.push_back(op->trig[i].start);
-      op->r_end.push_back(op->trig[i].end);
-      op->r_measure.push_back(op->trig[i].measure);
-      op->r_has.push_back(hb[i]);
-      for (size_t k = 0; k < op->aggs.size(); k++)
-        op->r_vals[k].push_back(hb[i] ? lower_value(op->aggs[k], ocnt[i], op0[i], op1[i], op2[i]) : 0);
+    int64_t n_dev;
+    std::memcpy(&n_dev, op->h_out + WM_HDR_N, 8);
+    if (n_dev != nw) {
+      op->failed = true;
+      return fail(op, SCOTTY_ERR_STATE, "internal: device triggered " + std::to_string(n_dev) + " windows, host counted " +
+                                            std::to_string(nw));
     }
+    res = op->h_out;
     op->last_watermark = wm;
     // bookkeeping at the synchronisation point
     const DevMeta& m = *op->h_snap;
@@ -1153,26 +1216,37 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     rc = compact_if_needed(op);
     if (rc) return rc;
   }
-  // timing of the ingest launches of this interval
+  // timing of the launches of this interval
   for (auto& e : op->ev_pending) {
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) op->t_ms += ms;
+    if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+      op->t_ms += ms;
+      op->t_cls_ms[SCOTTY_TIME_INGEST] += ms;
+    }
     op->t_launches++;
+    op->t_cls_n[SCOTTY_TIME_INGEST]++;
     op->ev_pool.push_back(e);
   }
   op->ev_pending.clear();
+  tresolve(op);
   for (void* p : op->owned) (void)hipFree(p);
   op->owned.clear();
   op->pending.clear();
   if (out) {
+    // results: AggregateWindowState.getAggValues / hasValue (S/state/AggregateWindowState.java:41-49), lowered on
+    // the device; the columns point into the pinned result buffer (valid until the next call on the op)
     std::memset(out, 0, sizeof(*out));
-    out->n_windows = op->r_start.size();
+    out->n_windows = (size_t)nw;
     out->n_aggs = (int32_t)op->aggs.size();
-    out->start = op->r_start.data();
-    out->end = op->r_end.data();
-    out->measure = op->r_measure.data();
-    out->has_value = op->r_has.data();
-    for (size_t k = 0; k < op->aggs.size(); k++) out->values[k] = op->r_vals[k].data();
+    if (nw > 0) {
+      const WmLayout L(nw, (int)op->aggs.size());
+      if ((int64_t)op->r_measure.size() < nw) op->r_measure.assign(nw, SCOTTY_MEASURE_TIME);
+      out->start = (const int64_t*)(res + L.start);
+      out->end = (const int64_t*)(res + L.end);
+      out->measure = op->r_measure.data();
+      out->has_value = (const uint8_t*)(res + L.has);
+      for (size_t k = 0; k < op->aggs.size(); k++) out->values[k] = (const int64_t*)(res + L.vals + 8 * nw * k);
+    }
   }
   if (op->dropped > dropped_before) {
     op->err = "tuples older than the oldest retained slice were dropped (reference: IndexOutOfBoundsException)";
@@ -1203,6 +1277,17 @@ int scotty_enable_timing(scotty_op* op, int on) {
   op->t_ms = 0.0;
   op->t_launches = 0;
   op->t_tuples = 0;
+  for (int k = 0; k < NTCLS; k++) {
+    op->t_cls_ms[k] = 0.0;
+    op->t_cls_n[k] = 0;
+  }
+  return SCOTTY_OK;
+}
+
+int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* intervals) {
+  if (!op || cls < 0 || cls >= NTCLS) return SCOTTY_ERR_ARG;
+  if (total_ms) *total_ms = op->t_cls_ms[cls];
+  if (intervals) *intervals = op->t_cls_n[cls];
   return SCOTTY_OK;
 }
 

@@ -18,10 +18,7 @@
 //      decides which grid points become slice edges with the reference's rule, evaluated for every
 //      candidate in parallel from first-crossing lookups (prefix max over tile maxima + an exact
 //      in-tile scan for the rare ambiguous case), appends the new slices and folds cells into slices.
-//   3. window_kernel + gc_kernel at a watermark (replace LazyAggregateStore.aggregate,
-//      S/aggregationstore/LazyAggregateStore.java:83-111, AggregateWindowState.containsSlice/addState,
-//      S/state/AggregateWindowState.java:25-53, and WindowManager.clearAfterWatermark /
-//      LazyAggregateStore.removeSlices, S/WindowManager.java:82-95, LazyAggregateStore.java:138-146).
+//   3. at a watermark: window_kernels.hip (triggers, window assembly from slice-block summaries, GC).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -583,7 +580,9 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __shared__ long long s_p[NT_MAX];   // tile maxima -> prefix maxima (arrival order)
   __shared__ long long s_w[32];
   __shared__ int64_t sc[16];
+  __shared__ long long s_dirty;       // lowest slice whose partials change (watermark block summaries)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_dirty = INT64_MAX;
   if (tid == 0) {
     const DevMeta& m = *a.meta;
     sc[0] = m.overflow; sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount; sc[5] = m.prev_max;
@@ -739,6 +738,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
         const int32_t r = a.rank[c - c_old];
         s = r > 0 ? tail + r - 1 : tail - 1;
       }
+      atomicMin(&s_dirty, (long long)s);
       atomicAdd(&a.s_cnt[s], cnt);
       atomicMax((long long*)&a.s_tlast[s], a.c_tmax[c]);
       if (a.need & NEED_SUM) {
@@ -774,6 +774,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       m.j0 = j0 + ncand;
       m.prev_max = batch_max;
       m.n_emitted = n_emit;
+      m.dirty_from = min(m.dirty_from, min((int64_t)s_dirty, tail));
       m.late_total += m.late_push;
       m.processed_total += (uint64_t)a.n - m.late_push;
     } else {
@@ -783,76 +784,6 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     m.late_push = 0;
     m.overflow_push = 0;
   }
-}
-
-// ================================================================ 3. windows + GC
-// One wave per window: contained slices are the contiguous range [first tStart >= start, first tLast >= end)
-// (AggregateWindowState.containsSlice: start <= tStart && end > tLast, S/state/AggregateWindowState.java:25-31).
-__global__ __launch_bounds__(256) void window_kernel(WindowArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (wi >= a.n_windows) return;
-  if (a.meta->overflow) return;
-  const int64_t head = a.meta->head, tail = a.meta->tail;
-  const int64_t ws = a.w_start[wi], we = a.w_end[wi];
-  int64_t lo = head, hi = tail;
-  while (lo < hi) {  // first tStart >= ws
-    int64_t mid = (lo + hi) >> 1;
-    if (a.s_tstart[mid] < ws) lo = mid + 1; else hi = mid;
-  }
-  const int64_t sa = lo;
-  lo = head; hi = tail;
-  while (lo < hi) {  // first tLast >= we
-    int64_t mid = (lo + hi) >> 1;
-    if (a.s_tlast[mid] < we) lo = mid + 1; else hi = mid;
-  }
-  const int64_t sb = lo;
-  uint64_t cnt = 0, sw = 0;
-  double sf = 0.0;
-  int64_t mn = PART_ID_MIN, mx = PART_ID_MAX;
-  for (int64_t s = sa + lane; s < sb; s += 64) {
-    const uint64_t c = a.s_cnt[s];
-    if (c == 0) continue;
-    cnt += c;
-    if (a.need & NEED_SUM) {
-      if (a.vt == VT_F64) sf += __longlong_as_double((long long)a.s_part[0][s]);
-      else sw += a.s_part[0][s];
-    }
-    if (a.need & NEED_MIN) mn = min(mn, (int64_t)a.s_part[1][s]);
-    if (a.need & NEED_MAX) mx = max(mx, (int64_t)a.s_part[2][s]);
-  }
-  cnt = wsum64(cnt);
-  if (a.need & NEED_SUM) {
-    if (a.vt == VT_F64) sf = wsumf(sf);
-    else sw = wsum64(sw);
-  }
-  if (a.need & NEED_MIN) mn = wmin64(mn);
-  if (a.need & NEED_MAX) mx = wmax64(mx);
-  if (lane == 0) {
-    a.has_value[wi] = cnt ? 1 : 0;
-    a.o_cnt[wi] = cnt;
-    a.o_part[0][wi] = a.vt == VT_F64 ? (unsigned long long)__double_as_longlong(sf) : sw;
-    a.o_part[1][wi] = (unsigned long long)mn;
-    a.o_part[2][wi] = (unsigned long long)mx;
-  }
-}
-
-// WindowManager.clearAfterWatermark -> LazyAggregateStore.removeSlices(t): drop [0, idx) with idx the
-// last slice whose tStart <= t (S/aggregationstore/LazyAggregateStore.java:138-146).
-__global__ void gc_kernel(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  DevMeta& m = *meta;
-  if (!m.overflow && m.tail > m.head) {
-    int64_t lo = m.head, hi = m.tail;  // count of tStart <= t -> idx = that - 1
-    while (lo < hi) {
-      int64_t mid = (lo + hi) >> 1;
-      if (s_tstart[mid] <= remove_from) lo = mid + 1; else hi = mid;
-    }
-    const int64_t idx = lo - 1;
-    if (idx > m.head) m.head = idx;
-    m.oldest_start = s_tstart[m.head];
-  }
-  *snapshot = m;
 }
 
 __global__ void fill_u64_kernel(unsigned long long* p, int64_t n, unsigned long long v) {
@@ -1023,7 +954,9 @@ __global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
   __shared__ long long s_pre[64];  // pre_r = max(prev_max, chunk max of ranks < r)
   __shared__ int64_t sc[16];
   __shared__ long long s_w[32];
+  __shared__ long long s_dirty;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_dirty = INT64_MAX;
   const int64_t xw = SHARD_HDR + 6 * a.kc_cap + 2 * a.kg_cap;
   if (tid == 0) {
     DevMeta& m = *a.meta;
@@ -1127,6 +1060,7 @@ __global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
           const int32_t rk = a.rank_buf[c - c_old];
           s = rk > 0 ? tail + rk - 1 : tail - 1;
         }
+        atomicMin(&s_dirty, (long long)s);
         atomicAdd(&a.s_cnt[s], (unsigned long long)rec[1]);
         atomicMax((long long*)&a.s_tlast[s], (long long)rec[2]);
         if (a.need & NEED_SUM) {
@@ -1147,6 +1081,7 @@ __global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
       m.j0 = j0 + ncand;
       m.prev_max = batch_max;
       m.n_emitted = n_emit;
+      m.dirty_from = min(m.dirty_from, min((int64_t)s_dirty, tail));
       m.late_total += (uint64_t)sc[7];
       m.processed_total += (uint64_t)(sc[10] - sc[7]);
     } else {
@@ -1212,17 +1147,6 @@ hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st) {
 }
 hipError_t launch_shard_commit(const ShardArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(shard_commit_kernel, dim3(1), dim3(1024), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_windows(const WindowArgs& a, hipStream_t st) {
-  if (a.n_windows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(window_kernel, dim3((unsigned)((a.n_windows + 3) / 4)), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_gc(DevMeta* meta, const int64_t* s_tstart, int64_t remove_from, DevMeta* snapshot, hipStream_t st) {
-  hipLaunchKernelGGL(gc_kernel, dim3(1), dim3(64), 0, st, meta, s_tstart, remove_from, snapshot);
   return hipGetLastError();
 }
 

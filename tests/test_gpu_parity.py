@@ -198,3 +198,70 @@ def test_large_batch_tumbling_partition_property(pkg):
     tot = sum(w.getAggValues()[0] for w in ws if w.hasValue())
     assert cnt == n
     assert (tot - int(vals.astype(np.int64).sum())) % (1 << 32) == 0
+
+
+# ---------------------------------------------------------------- watermark path: block summaries / sparse table
+@pytest.mark.parametrize("vt", ["i32", "i64", "f64"])
+def test_windows_over_many_slice_blocks(vt):
+    """Windows spanning thousands of slices (= many 64-slice blocks): prefix-sum differences, sparse-table levels
+    and partial head/tail blocks (window_kernels.hip) against the oracle's O(S*W) assembly
+    (S/aggregationstore/LazyAggregateStore.java:83-111), out-of-order tuples touching old blocks."""
+    aggs = {"i32": [SUM, COUNT, MIN, MAX], "i64": [SUM_I64, COUNT, MIN_I64, MAX_I64],
+            "f64": [SUM_F64, COUNT, MIN_F64, MAX_F64]}[vt]
+    cfg = dict(windows=[Tumbling(Time, 3), Sliding(Time, 5003, 997), Sliding(Time, 20011, 3001),
+                        FixedBand(Time, 1234, 40000)], aggs=aggs, lateness=300)
+    ts, vals = product().workloads.stream(400_000, 5, t0=11, ooo_frac=0.1, max_delay=250, seed=21, value_type=vt)
+    gpu, ora = build_ops(cfg, vt)
+    sched = interval_schedule(ts, 12, lag=200, pushes_per_interval=2)
+    f64_cols = [0] if vt == "f64" else []
+    assert run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols) > 20000
+
+
+def test_slice_compaction_keeps_window_assembly_exact():
+    """More than 2^19 slices over the operator's life: the slice arrays are compacted at a watermark (head moves
+    to 0), which re-bases every block summary; windows before and after must stay bit-exact."""
+    n = 600_000
+    ts = np.arange(n, dtype=np.int64) * 3 + 1
+    vals = np.random.default_rng(8).integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    cfg = dict(windows=[Tumbling(Time, 3), Sliding(Time, 9001, 3001)], aggs=[SUM, COUNT, MAX], lateness=10)
+    gpu, ora = build_ops(cfg)
+    sched = interval_schedule(ts, 14, lag=5)
+    assert run_schedule(gpu, ora, ts, vals, sched) > n // 2
+
+
+def test_watermark_arrays_f64_columns(pkg):
+    """processWatermarkArrays returns F64 aggregations as doubles, equal to processWatermark's values."""
+    cfg = dict(windows=[Tumbling(Time, 50), Sliding(Time, 200, 70)], aggs=[SUM_F64, MIN_F64, MAX_F64, COUNT],
+               lateness=20)
+    ts, vals = product().workloads.stream(20_000, 4, t0=3, seed=9, value_type="f64")
+    a, _ = build_ops(cfg, "f64")
+    b, _ = build_ops(cfg, "f64")
+    for op in (a, b):
+        op.processElements(ts, vals)
+    rows = a.processWatermark(int(ts.max()) + 500)
+    arr = b.processWatermarkArrays(int(ts.max()) + 500)
+    assert len(rows) == len(arr["start"]) > 0
+    for k in range(3):
+        assert arr["values"][k].dtype == np.float64
+    for i, w in enumerate(rows):
+        assert (w.getStart(), w.getEnd(), w.hasValue()) == (arr["start"][i], arr["end"][i], arr["has_value"][i])
+        if w.hasValue():
+            assert w.getAggValues()[:3] == [arr["values"][k][i] for k in range(3)]
+            assert w.getAggValues()[3] == arr["values"][3][i]
+
+
+def test_device_timing_classes(pkg):
+    """scotty_device_timing: every launch group of a grid-path step lands in one class."""
+    ts, vals = product().workloads.stream(200_000, 50, t0=0, seed=2)
+    op = pkg.SlicingWindowOperator()
+    op.addWindowFunction(SUM)
+    op.addWindowAssigner(Tumbling(Time, 100))
+    op.setMaxLateness(1)
+    op.enableTiming(True)
+    for lo in range(0, len(ts), 50_000):
+        op.processElements(ts[lo:lo + 50_000], vals[lo:lo + 50_000])
+        op.processWatermark(int(ts[lo + 49_999]))
+    t = op.deviceTiming()
+    assert t["ingest"][1] == 4 and t["watermark"][1] == 4 and t["result_copy"][1] == 4
+    assert t["push_other"][1] == 8
+    assert all(v[0] > 0 for v in t.values()), t
