@@ -753,6 +753,7 @@ int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b
                 "first context-free window added after elements were processed (edge walk would append "
                 "slices out of order)");
   op->windows.push_back(w);
+  op->wdef_dirty = true;
   op->max_fixed_window_size = std::max(op->max_fixed_window_size, w.clear_delay());  // S/WindowManager.java:124
   op->has_fixed = true;
   if (op->started) {
