@@ -18,6 +18,8 @@ constexpr int WCAP = 1024;        // cells in a workgroup's LDS window
 constexpr int64_t CIX_CAP = 1 << 20;  // entries of the cell index (ts bucket -> first cell), see cix_build_kernel
 constexpr int LCIX = 2048;        // cell-index entries staged in LDS for a workgroup's window
 constexpr int NPART = 3;          // partial slots per slice/cell: 0 sum, 1 min, 2 max
+constexpr int ING_SC = 24;        // block scalars of the ingest kernel (int64)
+constexpr int DEFER_CAP = 320;    // per-wave deferred out-of-order queue of the ingest kernel (entries)
 
 enum : int { VT_I32 = 0, VT_I64 = 1, VT_F64 = 2 };
 enum : int { NEED_SUM = 1, NEED_MIN = 2, NEED_MAX = 4 };
@@ -38,6 +40,7 @@ struct DevMeta {
   uint64_t late_push, overflow_push;   // per-push counters (reset by the commit kernel)
   uint64_t late_total, processed_total;
   uint64_t glb_slow;          // statistics: tuples the ingest kernel added with global atomics (outside the LDS window)
+  int64_t cmin;               // lowest cell index the current push's ingest added to (commit folds from there)
   int64_t dirty_from;         // lowest slice index whose partials changed since the last watermark (block summaries)
   int64_t whead;              // head before the last watermark's GC (window assembly reads [whead, tail))
 };
@@ -61,7 +64,8 @@ struct IngestArgs {
   int64_t tile;              // tuples per tile (power of two >= TILE_MIN, nT <= NT_MAX)
   // cell index (built per push by cix_build_kernel): cix[k] = cell of ts cix_meta[0] + (k << cix_meta[1])
   uint32_t* cix;
-  int64_t* cix_meta;         // [base, shift, n]
+  int64_t* cix_meta;         // [base, shift, n, cells indexed, ts end of the indexed range]
+  int64_t cix_margin;        // ms past the stream front (prev_max) the index covers
 };
 
 struct CommitArgs {

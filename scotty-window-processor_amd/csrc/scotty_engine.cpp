@@ -473,10 +473,11 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   ia.meta = op->d_meta;
   if (!op->d_cix) {
     HIPCHK(hipMalloc(&op->d_cix, CIX_CAP * 4));
-    HIPCHK(hipMalloc(&op->d_cixmeta, 4 * 8));
+    HIPCHK(hipMalloc(&op->d_cixmeta, 8 * 8));
   }
   ia.cix = op->d_cix;
   ia.cix_meta = op->d_cixmeta;
+  ia.cix_margin = std::max<int64_t>(4 * op->last_span, 4000);
   scotty_op::TEv tx;
   rc = tbegin(op, tx, SCOTTY_TIME_PUSH_OTHER);
   if (rc) return rc;

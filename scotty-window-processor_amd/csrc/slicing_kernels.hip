@@ -103,19 +103,21 @@ struct CellView {
   }
 };
 
-// Cell index: cix[k] = last cell with start <= base + (k << shift), built once per push over the whole cell
-// range [first cell start, horizon end) (cix_build_kernel).  A lookup is one load plus at most one compare when
-// shift == 0 (cell starts are distinct integers), instead of a ~16-step binary search through HBM / L2.
+// Cell index: cix[k] = last cell with start <= base + (k << shift), built once per push (cix_build_kernel) over
+// the cells a push can reach in practice: [first cell start, span_end) with span_end = min(horizon end, stream
+// front + margin).  A lookup is one load plus at most one compare when shift == 0 (cell starts are distinct
+// integers), instead of a ~16-step binary search through HBM / L2; a tuple beyond span_end (a stream jump) takes
+// the binary search over the whole cell view.
 struct CellIndex {
   const uint32_t* cix;
-  int64_t base, n, ctot;
+  int64_t base, n, ctot, c_hi, span_end;
   int shift;
   // largest c with start(c) <= t; requires start(0) <= t (and t < h_end when the horizon is finite)
   __device__ __forceinline__ int64_t find(const CellView& cv, int64_t t) const {
+    if (t >= span_end) return c_hi == ctot ? ctot - 1 : cv.find(t);
     const uint64_t k = (uint64_t)(t - base) >> shift;
-    if (k >= (uint64_t)n) return ctot - 1;
     int64_t lo = cix[k];
-    int64_t hi = k + 1 < (uint64_t)n ? (int64_t)cix[k + 1] + 1 : ctot;
+    int64_t hi = k + 1 < (uint64_t)n ? (int64_t)cix[k + 1] + 1 : c_hi;
     while (hi - lo > 1) {
       const int64_t mid = (lo + hi) >> 1;
       if (cv.start(mid) <= t) lo = mid; else hi = mid;
@@ -135,11 +137,16 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
   const int64_t ctot = cv.c_old + kc;
   if (ctot <= 0) return;
   const int64_t first = cv.start(0);
-  const int64_t span_end = h_end != INT64_MAX ? h_end : cv.start(ctot - 1) + 1;
+  const int64_t full_end = h_end != INT64_MAX ? h_end : cv.start(ctot - 1) + 1;
+  // the index stops `margin` ms past the stream front (prev_max): the cells of a far horizon cost a pass each
+  const int64_t front = m.prev_max > first ? m.prev_max : first;
+  const int64_t reach = front > INT64_MAX - a.cix_margin ? INT64_MAX : front + a.cix_margin;
+  const int64_t span_end = reach < full_end ? reach : full_end;
+  const int64_t c_hi = span_end < full_end ? cv.find(span_end - 1) + 1 : ctot;
   const uint64_t span = (uint64_t)(span_end - first);
   // about four buckets per cell: dense enough that a lookup rarely needs more than one compare, sparse enough
   // that building it is O(cells) even when a few cells span most of the range
-  const uint64_t target = (uint64_t)min(CIX_CAP, max((int64_t)4096, 4 * ctot));
+  const uint64_t target = (uint64_t)min(CIX_CAP, max((int64_t)4096, 4 * c_hi));
   int shift = 0;
   while ((span >> shift) >= target) shift++;
   const int64_t n = (int64_t)(span >> shift) + 1;
@@ -148,12 +155,14 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
     a.cix_meta[0] = first;
     a.cix_meta[1] = shift;
     a.cix_meta[2] = n;
+    a.cix_meta[3] = c_hi;
+    a.cix_meta[4] = span_end;
   }
   // thread per cell: cell c owns the buckets whose point first + (k << shift) lies in [start(c), start(c+1))
   const uint64_t round = ((uint64_t)1 << shift) - 1;
-  for (int64_t c = g; c < ctot; c += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t c = g; c < c_hi; c += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k0 = c == 0 ? 0 : (int64_t)(((uint64_t)(cv.start(c) - first) + round) >> shift);
-    const int64_t k1 = c + 1 == ctot ? n : min(n, (int64_t)(((uint64_t)(cv.start(c + 1) - first) + round) >> shift));
+    const int64_t k1 = c + 1 == c_hi ? n : min(n, (int64_t)(((uint64_t)(cv.start(c + 1) - first) + round) >> shift));
     for (int64_t k = k0; k < k1; k++) a.cix[k] = (uint32_t)c;
   }
 }
@@ -202,26 +211,36 @@ struct Acc {
   }
 };
 
+// LDS sum word of a cell: int32 values need the sum mod 2^32 only (Java int wrap, SumAggregation.java:16-18), so
+// the LDS window keeps 4-byte sums for them; int64 / double keep 8 bytes
+template <int VT>
+struct LdsSum {
+  using T = typename std::conditional<VT == VT_I32, uint32_t, unsigned long long>::type;
+};
 
 // LDS cell window of a workgroup
+template <int VT>
 struct LdsWin {
   int64_t* tw;                // [WCAP+1] cell starts
   uint32_t* cnt;              // [WCAP]
   long long* tmax;            // [WCAP]
-  unsigned long long* part[NPART];
+  typename LdsSum<VT>::T* sum;  // [WCAP] (NEED_SUM)
+  long long* mn;              // [WCAP] (NEED_MIN)
+  long long* mx;              // [WCAP] (NEED_MAX)
 };
 
 template <int VT, int NEED>
-__device__ __forceinline__ void lds_add(const LdsWin& w, int64_t i, uint32_t cnt, int64_t tmax, uint64_t sumw,
+__device__ __forceinline__ void lds_add(const LdsWin<VT>& w, int64_t i, uint32_t cnt, int64_t tmax, uint64_t sumw,
                                         double sumf, int64_t mn, int64_t mx) {
   atomicAdd(&w.cnt[i], cnt);
   atomicMax(&w.tmax[i], (long long)tmax);
   if constexpr ((NEED & NEED_SUM) != 0) {
-    if constexpr (VT == VT_F64) atomicAdd((double*)&w.part[0][i], sumf);
-    else atomicAdd(&w.part[0][i], (unsigned long long)sumw);
+    if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[i], sumf);
+    else if constexpr (VT == VT_I32) atomicAdd(&w.sum[i], (uint32_t)sumw);
+    else atomicAdd(&w.sum[i], (unsigned long long)sumw);
   }
-  if constexpr ((NEED & NEED_MIN) != 0) atomicMin((long long*)&w.part[1][i], (long long)mn);
-  if constexpr ((NEED & NEED_MAX) != 0) atomicMax((long long*)&w.part[2][i], (long long)mx);
+  if constexpr ((NEED & NEED_MIN) != 0) atomicMin(&w.mn[i], (long long)mn);
+  if constexpr ((NEED & NEED_MAX) != 0) atomicMax(&w.mx[i], (long long)mx);
 }
 
 template <int VT, int NEED>
@@ -237,33 +256,63 @@ __device__ __forceinline__ void glb_add(const IngestArgs& a, int64_t c, uint64_t
   if constexpr ((NEED & NEED_MAX) != 0) atomicMax((long long*)&a.c_part[2][c], (long long)mx);
 }
 
+// LDS bytes of one ingest workgroup (host launch and kernel carve the same layout)
+template <int VT, int NEED, int MODE>
+__host__ __device__ constexpr size_t ingest_lds_bytes() {
+  size_t b = 8 * ING_SC + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP;
+  if (NEED & NEED_SUM) b += (VT == VT_I32 ? 4 : 8) * WCAP;
+  if (NEED & NEED_MIN) b += 8 * WCAP;
+  if (NEED & NEED_MAX) b += 8 * WCAP;
+  b += 2 * LCIX;
+  if (MODE & 4) b += 4 * DEFER_CAP * (4 + (VT == VT_I32 ? 4 : 8));
+  return (b + 15) & ~(size_t)15;
+}
+
 // ================================================================ 1. ingest
 // MODE bit0: software-pipelined (next step's loads in flight while the current step is combined)
 // MODE bit1: non-temporal loads for the once-read tuple columns
+// MODE bit2: deferred slow path -- tuples outside the wave's current cell but inside the workgroup's LDS window
+//            (out-of-order tuples) are appended to a per-wave LDS queue (ballot + mbcnt, no dependent loads) and
+//            folded 64 at a time with every lane busy, instead of a per-lane loop of dependent lookups whose
+//            iterations run with a fraction of the lanes active
 template <int VT, int NEED, int MODE>
 __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   using V = typename ValT<VT>::T;
+  constexpr bool DEFER = (MODE & 4) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int64_t* sc = (int64_t*)smem;  // block scalars [16]
-  LdsWin w;
-  w.tw = (int64_t*)(smem + 128);
-  w.cnt = (uint32_t*)(smem + 128 + 8 * (WCAP + 2));
-  w.tmax = (long long*)((unsigned char*)w.cnt + 4 * WCAP);
-  unsigned char* p = (unsigned char*)(w.tmax + WCAP);
-#pragma unroll
-  for (int k = 0; k < NPART; k++) {
-    if (NEED & (1 << k)) {
-      w.part[k] = (unsigned long long*)p;
-      p += 8 * WCAP;
-    } else {
-      w.part[k] = nullptr;
-    }
+  int64_t* sc = (int64_t*)smem;  // block scalars [ING_SC]
+  LdsWin<VT> w;
+  unsigned char* p = smem + 8 * ING_SC;
+  w.tw = (int64_t*)p;
+  p += 8 * (WCAP + 2);
+  w.tmax = (long long*)p;
+  p += 8 * WCAP;
+  w.mn = nullptr;
+  w.mx = nullptr;
+  if (NEED & NEED_MIN) {
+    w.mn = (long long*)p;
+    p += 8 * WCAP;
   }
+  if (NEED & NEED_MAX) {
+    w.mx = (long long*)p;
+    p += 8 * WCAP;
+  }
+  w.sum = nullptr;
+  if (NEED & NEED_SUM) {
+    w.sum = (typename LdsSum<VT>::T*)p;
+    p += sizeof(typename LdsSum<VT>::T) * WCAP;
+  }
+  w.cnt = (uint32_t*)p;
+  p += 4 * WCAP;
   uint16_t* lcix = (uint16_t*)p;  // [LCIX] cell index entries of the window, relative to wbase
+  p += 2 * LCIX;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  // per-wave deferred queue: time offsets from the window's first cell start + values
+  uint32_t* q_t = DEFER ? (uint32_t*)p + wid * DEFER_CAP : nullptr;
+  V* q_v = DEFER ? (V*)((uint32_t*)p + 4 * DEFER_CAP) + wid * DEFER_CAP : nullptr;
   const int64_t per_block = a.per_wave * 4;
   const int64_t b0 = (int64_t)blockIdx.x * per_block;
   const int64_t b1 = min(a.n, b0 + per_block);
@@ -286,25 +335,34 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
     int64_t ctot = cv.c_old + kc;
     int64_t first_start = cv.start(0);
+    const int64_t cbase = a.cix_meta[0], cshift = a.cix_meta[1], cn = a.cix_meta[2];
+    const int64_t c_hi = a.cix_meta[3], span_end = a.cix_meta[4];
+    const CellIndex cx0{a.cix, cbase, cn, ctot, c_hi, span_end, (int)cshift};
     int64_t x = sc[15];
     int64_t chi;
     if (x < first_start) chi = 0;
     else if (x >= h_end) chi = ctot - 1;
-    else chi = cv.find(x);
+    else chi = cx0.find(cv, x);
     int64_t wbase = max((int64_t)0, chi + 16 - WCAP);
     int64_t wn = min((int64_t)WCAP, ctot - wbase);
     sc[0] = m.overflow;
     sc[1] = head; sc[2] = tail; sc[3] = j0; sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
     sc[7] = wbase; sc[8] = wn;
-    const int64_t cbase = a.cix_meta[0], cshift = a.cix_meta[1], cn = a.cix_meta[2];
     const int64_t twa = cv.start(wbase), twb = cv.start(wbase + wn);
     // stage the cell index for the most recent part of the window (out-of-order tuples are mostly recent)
     int64_t k0 = (int64_t)((uint64_t)(twa - cbase) >> cshift);
     const int64_t kl = (int64_t)((uint64_t)(twb - 1 - cbase) >> cshift);
     if (twb != INT64_MAX && kl + 2 - k0 > LCIX) k0 = kl + 2 - LCIX;
+    int64_t lcn = (twb != INT64_MAX && twb > twa) ? kl - k0 + 2 : 0;  // staged entries (0: LDS binary search)
+    if (lcn > cn - k0) lcn = max((int64_t)0, cn - k0);                 // only entries of the built index
+    if (twb > span_end && lcn > 0) lcn = max((int64_t)0, min(lcn, ((span_end - 1 - cbase) >> cshift) - k0));
     sc[9] = cbase; sc[10] = cshift; sc[11] = cn; sc[12] = k0;
-    sc[13] = (twb != INT64_MAX && twb > twa) ? kl - k0 + 2 : 0;  // staged entries (0: LDS binary search)
+    sc[13] = lcn;
     sc[14] = ctot;
+    sc[16] = c_hi;
+    sc[17] = span_end;
+    // deferred queue: time offsets from the window's first start must fit 32 bits
+    sc[18] = (DEFER && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
   }
   __syncthreads();
   if (sc[0] != 0) return;  // an earlier push of this interval overflowed: nothing is committed until replay
@@ -313,21 +371,23 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   const int64_t h_end = uni64(sc[5]), first_start = uni64(sc[6]);
   const int64_t wbase = uni64(sc[7]), wn = uni64(sc[8]);
   const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
-  const CellIndex cx{a.cix, uni64(sc[9]), uni64(sc[11]), uni64(sc[14]), (int)uni64(sc[10])};
+  const CellIndex cx{a.cix, uni64(sc[9]), uni64(sc[11]), uni64(sc[14]), uni64(sc[16]), uni64(sc[17]),
+                     (int)uni64(sc[10])};
   const int64_t lk0 = uni64(sc[12]), lcn = uni64(sc[13]);
+  const bool qok = uni64(sc[18]) != 0;
   for (int64_t i = tid; i <= wn; i += 256) w.tw[i] = cv.start(wbase + i);
   for (int64_t i = tid; i < lcn; i += 256) {
     const int64_t kk = lk0 + i;
-    int64_t v = kk < cx.n ? (int64_t)cx.cix[kk] : cx.ctot - 1;
+    int64_t v = (int64_t)cx.cix[kk];
     v = min(max(v - wbase, (int64_t)0), wn - 1);
     lcix[i] = (uint16_t)v;
   }
   for (int64_t i = tid; i < wn; i += 256) {
     w.cnt[i] = 0;
     w.tmax[i] = INT64_MIN;
-    if (NEED & NEED_SUM) w.part[0][i] = 0;
-    if (NEED & NEED_MIN) w.part[1][i] = (unsigned long long)PART_ID_MIN;
-    if (NEED & NEED_MAX) w.part[2][i] = (unsigned long long)PART_ID_MAX;
+    if (NEED & NEED_SUM) w.sum[i] = 0;
+    if (NEED & NEED_MIN) w.mn[i] = PART_ID_MIN;
+    if (NEED & NEED_MAX) w.mx[i] = PART_ID_MAX;
   }
   __syncthreads();
   const int64_t tw0 = uni64(w.tw[0]), twn = uni64(w.tw[wn]);
@@ -354,6 +414,8 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
   uint32_t n_late = 0, n_ovf = 0, n_glb = 0;
   int64_t tile_max = INT64_MIN;
+  int64_t cmin = INT64_MAX;  // lowest cell this wave added to outside the LDS window (commit folds from there)
+  int qn = 0;                // deferred queue fill (wave-uniform)
 
   auto flush = [&]() {
     uint32_t c = wsum32(acc.cnt);
@@ -367,12 +429,21 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       }
       int64_t mn = (NEED & NEED_MIN) ? wmin64(acc.mn) : 0;
       int64_t mx = (NEED & NEED_MAX) ? wmax64(acc.mx) : 0;
-      if (lane == 0) {
-        if (cstar >= wbase && cstar < wbase + wn) lds_add<VT, NEED>(w, cstar - wbase, c, tm, sw, sf, mn, mx);
-        else glb_add<VT, NEED>(a, cstar, c, tm, sw, sf, mn, mx);
+      if (cstar >= wbase && cstar < wbase + wn) {
+        if (lane == 0) lds_add<VT, NEED>(w, cstar - wbase, c, tm, sw, sf, mn, mx);
+      } else {
+        if (lane == 0) glb_add<VT, NEED>(a, cstar, c, tm, sw, sf, mn, mx);
+        cmin = min(cmin, cstar);
       }
     }
     acc.reset();
+  };
+
+  auto lds_one = [&](int64_t l, int64_t t, V v) {
+    Acc<VT, NEED> one;
+    one.reset();
+    one.add(t, v);
+    lds_add<VT, NEED>(w, l, 1u, t, one.sum_word(), one.sum_f(), one.mn, one.mx);
   };
 
   auto slow = [&](int64_t t, V v) {
@@ -381,23 +452,28 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     } else if (t >= h_end && h_end != INT64_MAX) {
       n_ovf++;
     } else if (t >= tw0 && t < twn) {
-      const int64_t l = wfind(t);
-      Acc<VT, NEED> one;
-      one.reset();
-      one.add(t, v);
-      const uint64_t sw = one.sum_word();
-      const double sf = one.sum_f();
-      lds_add<VT, NEED>(w, l, 1u, t, sw, sf, one.mn, one.mx);
+      lds_one(wfind(t), t, v);
     } else {
       n_glb++;
       const int64_t c = cx.find(cv, t);
+      cmin = min(cmin, c);
       Acc<VT, NEED> one;
       one.reset();
       one.add(t, v);
-      const uint64_t sw = one.sum_word();
-      const double sf = one.sum_f();
-      glb_add<VT, NEED>(a, c, 1u, t, sw, sf, one.mn, one.mx);
+      glb_add<VT, NEED>(a, c, 1u, t, one.sum_word(), one.sum_f(), one.mn, one.mx);
     }
+  };
+
+  // fold the deferred queue: 64 entries per pass, every lane one lookup + one set of LDS atomics
+  auto drain = [&]() {
+    for (int b = 0; b < qn; b += 64) {
+      const int e = b + lane;
+      if (e < qn) {
+        const int64_t t = tw0 + (int64_t)q_t[e];
+        lds_one(wfind(t), t, q_v[e]);
+      }
+    }
+    qn = 0;
   };
 
   constexpr bool PIPE = (MODE & 1) != 0;
@@ -466,6 +542,23 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
       else sm |= 1u << j;
     }
+    if constexpr (DEFER) {
+      if (qok) {
+        if (qn > DEFER_CAP - 256) drain();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const bool q = ((sm >> j) & 1) && t[j] >= tw0 && t[j] < twn;
+          const unsigned long long bal = __ballot(q);
+          if (q) {
+            const int pos = qn + (int)__popcll(bal & ((1ull << lane) - 1));
+            q_t[pos] = (uint32_t)(t[j] - tw0);
+            q_v[pos] = v[j];
+            sm &= ~(1u << j);
+          }
+          qn += (int)__popcll(bal);
+        }
+      }
+    }
     while (sm) {
       const int j = __builtin_ctz(sm);
       sm &= sm - 1;
@@ -506,6 +599,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       tile_done(s);
     }
   }
+  if constexpr (DEFER) drain();
   if (w1_full < w1) {  // ragged tail of the wave's range
     const int64_t s = w1_full;
     const int64_t i0 = s + 2 * lane, i1 = s + 128 + 2 * lane;
@@ -525,22 +619,29 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   flush();
   {
     uint32_t nl = wsum32(n_late), no = wsum32(n_ovf), ng = wsum32(n_glb);
+    const int64_t cm = wmin64(cmin);
     if (lane == 0 && ng) atomicAdd((unsigned long long*)&a.meta->glb_slow, (unsigned long long)ng);
+    if (lane == 0 && cm != INT64_MAX) atomicMin((long long*)&a.meta->cmin, (long long)cm);
     if (lane == 0 && (nl | no)) {
       if (nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
       if (no) atomicAdd((unsigned long long*)&a.meta->overflow_push, (unsigned long long)no);
     }
   }
   __syncthreads();
+  // the window's partials to the global cells; the lowest touched cell bounds the commit's fold
+  int64_t bmin = INT64_MAX;
   for (int64_t i = tid; i < wn; i += 256) {
     uint32_t c = w.cnt[i];
     if (c) {
-      uint64_t sw = (NEED & NEED_SUM) ? w.part[0][i] : 0;
+      uint64_t sw = (NEED & NEED_SUM) ? (uint64_t)w.sum[i] : 0;
       double sf = (NEED & NEED_SUM) ? __longlong_as_double((long long)sw) : 0.0;
-      glb_add<VT, NEED>(a, wbase + i, c, w.tmax[i], sw, sf, (NEED & NEED_MIN) ? (int64_t)w.part[1][i] : 0,
-                        (NEED & NEED_MAX) ? (int64_t)w.part[2][i] : 0);
+      glb_add<VT, NEED>(a, wbase + i, c, w.tmax[i], sw, sf, (NEED & NEED_MIN) ? (int64_t)w.mn[i] : 0,
+                        (NEED & NEED_MAX) ? (int64_t)w.mx[i] : 0);
+      bmin = min(bmin, wbase + i);
     }
   }
+  bmin = wmin64(bmin);
+  if (lane == 0 && bmin != INT64_MAX) atomicMin((long long*)&a.meta->cmin, (long long)bmin);
 }
 
 // ================================================================ 2. commit (single workgroup)
@@ -586,6 +687,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   if (tid == 0) {
     const DevMeta& m = *a.meta;
     sc[0] = m.overflow; sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount; sc[5] = m.prev_max;
+    sc[10] = m.cmin;
   }
   __syncthreads();
   if (sc[0] != 0) return;
@@ -726,9 +828,11 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       }
     }
     __syncthreads();
-    // ---- (f) fold cells into slices (AbstractSlice.addElement + AggregateState.merge semantics)
+    // ---- (f) fold cells into slices (AbstractSlice.addElement + AggregateState.merge semantics); cells below
+    //      the lowest cell the ingest touched (DevMeta.cmin) are untouched
     const int64_t ncell = c_old + ncand;
-    for (int64_t c = tid; c < ncell; c += 1024) {
+    const int64_t cfirst = min(max(sc[10], (int64_t)0), ncell);
+    for (int64_t c = cfirst + tid; c < ncell; c += 1024) {
       const unsigned long long cnt = a.c_cnt[c];
       if (cnt == 0) continue;
       int64_t s;
@@ -783,6 +887,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     }
     m.late_push = 0;
     m.overflow_push = 0;
+    m.cmin = INT64_MAX;
   }
 }
 
@@ -946,6 +1051,7 @@ __global__ __launch_bounds__(1024) void shard_export_kernel(ShardArgs a) {
     DevMeta& m = *a.meta;
     m.late_push = 0;
     m.overflow_push = 0;
+    m.cmin = INT64_MAX;
   }
 }
 
@@ -1093,14 +1199,14 @@ __global__ __launch_bounds__(1024) void shard_commit_kernel(ShardArgs a) {
 // ---------------------------------------------------------------- host-side launch wrappers
 template <int VT, int NEED, int MODE>
 static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStream_t st) {
-  size_t lds = 128 + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP + 2 * LCIX;
-  for (int k = 0; k < NPART; k++)
-    if (NEED & (1 << k)) lds += 8 * WCAP;
+  constexpr size_t lds = ingest_lds_bytes<VT, NEED, MODE>();
   hipLaunchKernelGGL((ingest_kernel<VT, NEED, MODE>), dim3((unsigned)nblocks), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
-constexpr int DEFAULT_MODE = 2;  // non-temporal loads, no software pipelining (A/B: profiles/r01/ab_ingest_modes.json)
+// non-temporal loads + deferred out-of-order queue, no software pipelining (A/B: profiles/r01/ab_ingest_modes.json,
+// profiles/r02/)
+constexpr int DEFAULT_MODE = 6;
 
 template <int VT>
 static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
@@ -1128,7 +1234,8 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
       case 0: return launch_ingest_t<VT_I32, NEED_SUM, 0>(a, nblocks, st);
       case 1: return launch_ingest_t<VT_I32, NEED_SUM, 1>(a, nblocks, st);
       case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
-      default: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
+      case 3: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
+      default: return launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st);
     }
   }
   if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);
