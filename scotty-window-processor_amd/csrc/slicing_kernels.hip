@@ -110,14 +110,14 @@ struct CellView {
 // the binary search over the whole cell view.
 struct CellIndex {
   const uint32_t* cix;
-  int64_t base, n, ctot, c_hi, span_end;
+  int64_t base, n, ctot, full, span_end;  // full: the index reaches the cell view's end
   int shift;
   // largest c with start(c) <= t; requires start(0) <= t (and t < h_end when the horizon is finite)
   __device__ __forceinline__ int64_t find(const CellView& cv, int64_t t) const {
-    if (t >= span_end) return c_hi == ctot ? ctot - 1 : cv.find(t);
+    if (t >= span_end) return full ? ctot - 1 : cv.find(t);
     const uint64_t k = (uint64_t)(t - base) >> shift;
     int64_t lo = cix[k];
-    int64_t hi = k + 1 < (uint64_t)n ? (int64_t)cix[k + 1] + 1 : c_hi;
+    int64_t hi = k + 1 < (uint64_t)n ? (int64_t)cix[k + 1] + 1 : ctot;
     while (hi - lo > 1) {
       const int64_t mid = (lo + hi) >> 1;
       if (cv.start(mid) <= t) lo = mid; else hi = mid;
@@ -142,11 +142,11 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
   const int64_t front = m.prev_max > first ? m.prev_max : first;
   const int64_t reach = front > INT64_MAX - a.cix_margin ? INT64_MAX : front + a.cix_margin;
   const int64_t span_end = reach < full_end ? reach : full_end;
-  const int64_t c_hi = span_end < full_end ? cv.find(span_end - 1) + 1 : ctot;
   const uint64_t span = (uint64_t)(span_end - first);
-  // about four buckets per cell: dense enough that a lookup rarely needs more than one compare, sparse enough
-  // that building it is O(cells) even when a few cells span most of the range
-  const uint64_t target = (uint64_t)min(CIX_CAP, max((int64_t)4096, 4 * c_hi));
+  // one bucket per ms up to CIX_CAP buckets (coarser only for very long retained spans): a lookup rarely needs
+  // more than one compare, and building it is O(cells + buckets).  (No per-thread search for the cell at
+  // span_end: 65k threads bisecting the same addresses serialise on one L2 channel.)
+  const uint64_t target = (uint64_t)CIX_CAP;
   int shift = 0;
   while ((span >> shift) >= target) shift++;
   const int64_t n = (int64_t)(span >> shift) + 1;
@@ -155,14 +155,18 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
     a.cix_meta[0] = first;
     a.cix_meta[1] = shift;
     a.cix_meta[2] = n;
-    a.cix_meta[3] = c_hi;
+    a.cix_meta[3] = span_end == full_end ? 1 : 0;
     a.cix_meta[4] = span_end;
   }
-  // thread per cell: cell c owns the buckets whose point first + (k << shift) lies in [start(c), start(c+1))
+  // thread per cell: cell c owns the buckets whose point first + (k << shift) lies in [start(c), start(c+1));
+  // cells are sorted, so a thread stops at its first cell starting at or beyond span_end
   const uint64_t round = ((uint64_t)1 << shift) - 1;
-  for (int64_t c = g; c < c_hi; c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k0 = c == 0 ? 0 : (int64_t)(((uint64_t)(cv.start(c) - first) + round) >> shift);
-    const int64_t k1 = c + 1 == c_hi ? n : min(n, (int64_t)(((uint64_t)(cv.start(c + 1) - first) + round) >> shift));
+  for (int64_t c = g; c < ctot; c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t sc0 = cv.start(c);
+    if (c > 0 && sc0 >= span_end) break;
+    const int64_t sc1 = c + 1 < ctot ? cv.start(c + 1) : INT64_MAX;
+    const int64_t k0 = c == 0 ? 0 : (int64_t)(((uint64_t)(sc0 - first) + round) >> shift);
+    const int64_t k1 = sc1 >= span_end ? n : min(n, (int64_t)(((uint64_t)(sc1 - first) + round) >> shift));
     for (int64_t k = k0; k < k1; k++) a.cix[k] = (uint32_t)c;
   }
 }
@@ -336,8 +340,8 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     int64_t ctot = cv.c_old + kc;
     int64_t first_start = cv.start(0);
     const int64_t cbase = a.cix_meta[0], cshift = a.cix_meta[1], cn = a.cix_meta[2];
-    const int64_t c_hi = a.cix_meta[3], span_end = a.cix_meta[4];
-    const CellIndex cx0{a.cix, cbase, cn, ctot, c_hi, span_end, (int)cshift};
+    const int64_t c_full = a.cix_meta[3], span_end = a.cix_meta[4];
+    const CellIndex cx0{a.cix, cbase, cn, ctot, c_full, span_end, (int)cshift};
     int64_t x = sc[15];
     int64_t chi;
     if (x < first_start) chi = 0;
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     sc[9] = cbase; sc[10] = cshift; sc[11] = cn; sc[12] = k0;
     sc[13] = lcn;
     sc[14] = ctot;
-    sc[16] = c_hi;
+    sc[16] = c_full;
     sc[17] = span_end;
     // deferred queue: time offsets from the window's first start must fit 32 bits
     sc[18] = (DEFER && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
@@ -721,15 +725,36 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __syncthreads();
   const int64_t batch_max = max(prev_max, nT > 0 ? (int64_t)s_p[nT - 1] : INT64_MIN);
 
-  // ---- (b) candidates: grid points g[k] <= batch_max (k < kc)
-  if (tid == 0) {
-    int64_t lo = 0, hi = kc;
-    while (lo < hi) {
-      int64_t mid = (lo + hi) >> 1;
-      if (g[mid] <= batch_max) lo = mid + 1; else hi = mid;
+  // ---- (b) candidates: grid points g[k] <= batch_max (k < kc): wavefront-cooperative search (64 probes per
+  //      round) instead of a 20-step chain of dependent loads on one thread
+  if (wid == 0) {
+    int64_t lo = 0, hi = kc;  // first k with g[k] > batch_max
+    while (hi - lo > 64) {
+      const int64_t stride = (hi - lo + 63) >> 6;
+      const int64_t p = lo + (int64_t)lane * stride;
+      const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
+      if (bal == 0) {
+        lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
+      } else {
+        const int f = __ffsll((long long)bal) - 1;
+        if (f == 0) {
+          hi = lo;
+          break;
+        }
+        const int64_t pf = lo + (int64_t)f * stride;
+        lo = pf - stride + 1;
+        hi = pf;
+      }
     }
-    sc[8] = lo;
-    sc[9] = (h_end != INT64_MAX && batch_max >= h_end) ? 1 : 0;
+    if (hi > lo) {
+      const int64_t p = lo + lane;
+      const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
+      lo = bal ? lo + __ffsll((long long)bal) - 1 : hi;
+    }
+    if (lane == 0) {
+      sc[8] = lo;
+      sc[9] = (h_end != INT64_MAX && batch_max >= h_end) ? 1 : 0;
+    }
   }
   __syncthreads();
   const int64_t ncand = sc[8];
