@@ -336,6 +336,7 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
         op = pkg.ShardedSlicingWindowOperator(device=dev.index)
     else:
         op = pkg.SlicingWindowOperator(device=dev.index)
+        op.tune("count_path", 1)  # the C5 stream is in timestamp order: no LazySlice record sets needed
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.addWindowFunction(pkg.AGG_COUNT)
     op.setMaxLateness(1)

@@ -57,6 +57,10 @@ extern "C" {
 #define SCOTTY_AGG_SUM_F64 7 /* within 1e-6 relative of the reference's arrival-order fold */
 #define SCOTTY_AGG_MIN_F64 8
 #define SCOTTY_AGG_MAX_F64 9
+/* OR-able flag: the function is an InvertibleAggregateFunction (C/windowFunction/InvertibleAggregateFunction.java):
+ * a record leaving a LazySlice is removed by liftAndInvert instead of recomputing the slice from its record set
+ * (S/state/AggregateValueState.java:33-41).  Sums and counts only. */
+#define SCOTTY_AGG_INVERTIBLE 0x10000
 #define SCOTTY_MAX_AGGS 8
 
 /* ---- create flags */
@@ -93,7 +97,8 @@ const char* scotty_last_error(scotty_op* op);
  * a,b = size,0 | size,slide | gap,0 | start,size */
 int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b);
 /* WindowOperator.addAggregation / SlicingWindowOperator.addWindowFunction (C/WindowOperator.java:30,
- * S/SlicingWindowOperator.java:57-63).  Returns the aggregation index (>=0) or an error. */
+ * S/SlicingWindowOperator.java:57-63).  agg_kind: SCOTTY_AGG_* [| SCOTTY_AGG_INVERTIBLE].  Returns the aggregation
+ * index (>=0) or an error. */
 int scotty_add_aggregation(scotty_op* op, int agg_kind);
 /* WindowOperator.setMaxLateness (C/WindowOperator.java:37; default 1000, S/WindowManager.java:24) */
 int scotty_set_max_lateness(scotty_op* op, int64_t max_lateness);
@@ -170,8 +175,10 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
 /* Tuning knobs (not semantics): "slice_capacity" / "session_capacity" per operator of the exact engine
  * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only), "exact_serial"
  * (non-keyed: single-wavefront replay, A/B only), "keyed_lane" 0 (keyed: wavefront-per-key replay instead of
- * the lane-per-key path for context-free time windows, A/B only), "count_path" 0 (count-window operators on the
- * exact engine instead of the count path, A/B only), "ingest_blocks", "shard_cells" / "shard_cands" (cells /
+ * the lane-per-key path for context-free time windows, A/B only), "count_path" 1 (a promise that the stream is in
+ * timestamp order: non-keyed operators with count windows only keep no LazySlice record sets and run on the
+ * segmented-reduction count path; an out-of-order tuple that would move records then fails loudly -- without the
+ * promise they run on the exact engine, which keeps the record sets), "ingest_blocks", "shard_cells" / "shard_cands" (cells /
  * edge candidates per rank record of the time-window exchange), "shard_count_cells" (count cells per rank record
  * of the count-window exchange). */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);

@@ -33,6 +33,7 @@ AGG_SUM_I32, AGG_COUNT, AGG_MIN_I32, AGG_MAX_I32 = 0, 1, 2, 3
 AGG_SUM_I64, AGG_MIN_I64, AGG_MAX_I64 = 4, 5, 6
 AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64 = 7, 8, 9
 F64_AGGS = (AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64)
+AGG_INVERTIBLE = 0x10000  # OR-able: the function is an InvertibleAggregateFunction (include/scotty_mi355x.h)
 MAX_AGGS = 8
 
 
@@ -100,6 +101,9 @@ MinAggregateFunction = _agg(AGG_MIN_I32, "MinAggregateFunction")
 MaxAggregateFunction = _agg(AGG_MAX_I32, "MaxAggregateFunction")
 LongSumAggregateFunction = _agg(AGG_SUM_I64, "LongSumAggregateFunction")
 DoubleSumAggregateFunction = _agg(AGG_SUM_F64, "DoubleSumAggregateFunction")
+# InvertibleReduceAggregateFunction variants (C/windowFunction/InvertibleReduceAggregateFunction.java)
+InvertibleSumAggregateFunction = _agg(AGG_SUM_I32 | AGG_INVERTIBLE, "InvertibleSumAggregateFunction")
+InvertibleCountAggregateFunction = _agg(AGG_COUNT | AGG_INVERTIBLE, "InvertibleCountAggregateFunction")
 
 
 class scotty_windows(ctypes.Structure):
@@ -247,7 +251,7 @@ class SlicingWindowOperator:
         self._flush()
         kind = _kind_of(fn)
         idx = self._check(self._l.scotty_add_aggregation(self._h, kind))
-        self._aggs.append(kind)
+        self._aggs.append(kind & 0xFFFF)
         return idx
 
     addWindowFunction = addAggregation
@@ -450,6 +454,9 @@ class ShardedSlicingWindowOperator:
         import torch.distributed as dist
         self.dist, self.torch, self.group = dist, torch, group
         self.op = SlicingWindowOperator(device=device, value_type=value_type)
+        # sharding count windows by arrival is exact for in-order streams only: the promise lets
+        # count-only operators run on the count path, which exports per-rank count cells
+        self.op.tune("count_path", 1)
         self.world = dist.get_world_size(group)
         self.dev = torch.device("cuda", device)
         self.staged = dist.get_backend(group) != "nccl"

@@ -812,7 +812,7 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
     o.exc = 0;
     o.determine_slices(t);
     if (!o.exc) o.manager_process(t, vb);
-    if (o.exc == XERR_INDEX) {
+    if (xerr_tuple_failed(o.exc)) {
       o.s.dropped++;
       o.exc = 0;
     } else if (o.exc) {

@@ -40,12 +40,22 @@ enum : int32_t {
   XERR_SESS_CAP = 4,     // per-context session capacity exceeded -- fatal
   XERR_HANG = 5,         // reference would loop forever in StreamSlicer (power-of-two size/slide) -- fatal
   XERR_WM_INDEX = 6,     // processWatermark threw (empty session context / count trigger) -- fatal for the call
+  XERR_NPE = 7,          // NullPointerException: a LazySlice ran out of records while records move (tuple failed,
+                         // counted; the state keeps the reference's partial changes)
+  XERR_NOELEM = 8,       // NoSuchElementException (TreeSet.first() on an emptied record set; same handling)
+  XERR_REC_CAP = 9,      // per-operator record capacity exceeded (internal; the pre-check prevents it) -- fatal
 };
+// a tuple whose processing threw one of these is counted as failed, like the reference's per-tuple exception
+__host__ __device__ inline bool xerr_tuple_failed(int32_t e) { return e == XERR_INDEX || e == XERR_NPE || e == XERR_NOELEM; }
 
 struct XCfg {
   int32_t n_cf;           // context-free windows (registration order)
   int32_t n_ctx;          // context-aware (session) windows (registration order)
   int32_t has_fixed, has_ctx, has_count, has_time, session_case, lazy;
+  // LazySlice record sets (S/slice/LazySlice.java:14-54, ST/memory/MemorySetState.java): kept when slices are Lazy;
+  // invertible: every function is an InvertibleAggregateFunction (removal = liftAndInvert), else recompute()
+  int32_t records, invertible;
+  int64_t rcap;           // records per operator (arena capacity)
   int32_t need, vt;
   int32_t sc;             // slice capacity per operator
   int32_t sesscap;        // session capacity per context per operator
@@ -72,6 +82,7 @@ struct XState {          // 128 B
   uint64_t dropped;                                                 // tuples whose processing threw
   int64_t wlo, whi;                                                 // watermark: slice scan range
   int32_t pending, pad;                                             // batch deferred: capacity too small
+  int64_t rend;                                                     // records: end of the live arena range
 };
 
 struct XSlices {
@@ -79,6 +90,13 @@ struct XSlices {
   int32_t* ty;
   unsigned long long* cnt;
   unsigned long long* p[NPART];
+  // records mode (XCfg.records): slice s owns arena records [rlo[s], rhi[s]) of its op (rhi[s] == rlo[s+1]: the
+  // slices' record sets lie in slice order, each sorted by ts, no duplicate ts -- the TreeSet<StreamRecord>
+  // ordered by ts only, S/slice/StreamRecord.java:25-27); nn[s]: the partial is non-null (AggregateValueState
+  // keeps a value after liftAndInvert even at count 0)
+  int64_t *rlo, *rhi;
+  int32_t* nn;
+  int64_t *rts, *rv;      // arena [n_ops * rcap]: record ts, value bits
 };
 
 struct XSess {
@@ -100,7 +118,7 @@ struct XBatchArgs {
   XSess ss;
   int32_t rec_stride;       // keyed: tuples are AoS records (ts at +0, value at +8, op at +rec_stride-4)
   int32_t retry;            // process only ops marked pending by an earlier launch
-  unsigned long long* need; // [2] capacity pre-check: max slices / sessions an op may need (atomicMax)
+  unsigned long long* need; // [3] capacity pre-check: max slices / sessions / records an op may need (atomicMax)
 };
 
 struct XWmArgs {

@@ -126,6 +126,7 @@ void XEngine::release() {
   dfree(d_st);
   dfree(sl.ts); dfree(sl.te); dfree(sl.tl); dfree(sl.tf); dfree(sl.cs); dfree(sl.cl); dfree(sl.ty); dfree(sl.cnt);
   for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  dfree(sl.rlo); dfree(sl.rhi); dfree(sl.nn); dfree(sl.rts); dfree(sl.rv);
   dfree(ss.start); dfree(ss.end);
   dfree(d_need); dfree(d_table); dfree(d_newpos); dfree(d_newcnt); dfree(d_full); dfree(d_slot_key);
   dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32); dfree(d_seg_b); dfree(d_seg_e);
@@ -153,12 +154,13 @@ int XEngine::init(int dev, hipStream_t st, int value_type, bool is_keyed, std::s
   XCHK(hipHostMalloc((void**)&h_misc, 8 * sizeof(int64_t), hipHostMallocDefault));
   XCHK(dalloc(&d_newcnt, 1));
   XCHK(dalloc(&d_full, 1));
-  XCHK(dalloc(&d_need, 2));
+  XCHK(dalloc(&d_need, 4));
   return SCOTTY_OK;
 }
 
 // WindowManager.addWindowAssigner / addAggregation / setMaxLateness (S/WindowManager.java:121-202)
-int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness) {
+int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness,
+                       const std::vector<int>& agg_inv) {
   XCfg c{};
   std::vector<int32_t> kind, meas;
   std::vector<int64_t> a, b;
@@ -195,6 +197,17 @@ int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>&
   c.max_fixed = max_fixed;
   // SliceFactory.createSlice (S/slice/SliceFactory.java:17-22)
   c.lazy = !(!c.has_count && (!has_ctx || session_case) && max_lateness > 0);
+  // LazySlice record sets, kept from the first configuration with Lazy slices on (a later lateness change keeps them)
+  records = records || c.lazy;
+  c.records = records ? 1 : 0;
+  int n_inv = 0;
+  for (size_t i = 0; i < aggs.size(); i++) n_inv += (i < agg_inv.size() && agg_inv[i]) ? 1 : 0;
+  c.invertible = (!aggs.empty() && n_inv == (int)aggs.size()) ? 1 : 0;
+  if (records && n_inv != 0 && n_inv != (int)aggs.size()) {
+    err = "LazySlice record removal with both invertible and non-invertible functions on one operator (each keeps "
+          "its own partial in the reference) is not supported on the MI355X path";
+    return SCOTTY_ERR_UNSUPPORTED;
+  }
   c.vt = vt;
   c.need = 0;
   c.n_aggs = (int32_t)aggs.size();
@@ -223,9 +236,11 @@ int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>&
     }
   }
   if (sesscap == 0) sesscap = sess_override > 0 ? sess_override : (keyed ? 64 : 4096);
+  if (records && rcap_ == 0) rcap_ = keyed ? 256 : (1 << 20);
   c.sc = sc;
   c.sesscap = sesscap;
   c.ctx_alloc = ctx_alloc;
+  c.rcap = rcap_;
   // context-free window table
   dfree(d_cf_kind); dfree(d_cf_meas); dfree(d_cf_a); dfree(d_cf_b);
   d_cf_kind = nullptr; d_cf_meas = nullptr; d_cf_a = nullptr; d_cf_b = nullptr;
@@ -247,6 +262,10 @@ int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>&
   XCHK(hipMemcpyAsync(d_cfg, &cfg, sizeof(XCfg), hipMemcpyHostToDevice, stream));
   if (nctx > ctx_alloc) {  // session windows registered (possibly mid-stream): widen the per-op session table
     int rc = grow_caps(sc, sesscap, nctx);
+    if (rc) return rc;
+  }
+  if (records && !sl.rts && ops_cap > 0) {  // records switched on mid-stream: every existing set is empty
+    int rc = alloc_records();
     if (rc) return rc;
   }
   XCHK(hipStreamSynchronize(stream));
@@ -289,16 +308,41 @@ int XEngine::grow_ops(int64_t need) {
     XCHK(grow(&ss.end, (int64_t)ctx_alloc * sesscap));
   }
   if (keyed) XCHK(grow(&d_slot_key, 1));
+  if (records) {
+    XCHK(grow(&sl.rlo, sc)); XCHK(grow(&sl.rhi, sc)); XCHK(grow(&sl.nn, sc));
+    XCHK(grow(&sl.rts, rcap_)); XCHK(grow(&sl.rv, rcap_));
+  }
   XCHK(hipStreamSynchronize(stream));
   ops_cap = cap;
   return SCOTTY_OK;
 }
 
+// Record arrays for every allocated op (records enabled after slices existed: every record range is [0, 0)).
+int XEngine::alloc_records() {
+  XCHK(hipStreamSynchronize(stream));
+  const int64_t rows = std::max<int64_t>(ops_cap, 1);
+  XCHK(dalloc(&sl.rlo, rows * sc)); XCHK(dalloc(&sl.rhi, rows * sc)); XCHK(dalloc(&sl.nn, rows * sc));
+  XCHK(dalloc(&sl.rts, rows * rcap_)); XCHK(dalloc(&sl.rv, rows * rcap_));
+  XCHK(hipMemsetAsync(sl.rlo, 0, rows * sc * 8, stream));
+  XCHK(hipMemsetAsync(sl.rhi, 0, rows * sc * 8, stream));
+  // existing slices got nn from their counts: conservatively non-null iff they hold tuples (set by the kernels
+  // on the next add); a zero fill is exact for slices created from now on
+  XCHK(hipMemsetAsync(sl.nn, 0, rows * sc * 4, stream));
+  XCHK(hipStreamSynchronize(stream));
+  return SCOTTY_OK;
+}
+
 // Re-lay out the per-op slice / session tables with larger capacities (row = one op, 2-D copies).
-int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx) {
-  int64_t nsc = sc, nss = sesscap;
+int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx, int64_t need_rec) {
+  int64_t nsc = sc, nss = sesscap, nrc = rcap_;
   while (nsc < need_sc) nsc *= 2;
   while (nss < need_sess) nss *= 2;
+  while (records && nrc < need_rec) nrc *= 2;
+  if (nrc > ((int64_t)1 << 34)) {
+    err = "per-operator LazySlice record capacity would exceed the supported maximum";
+    failed = true;
+    return SCOTTY_ERR_NOMEM;
+  }
   const int32_t nctx = std::max(ctx_alloc, need_ctx);
   if (nsc > (1 << 26) || nss > (1 << 24)) {
     err = "per-operator slice / session capacity would exceed the supported maximum";
@@ -330,6 +374,13 @@ int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx) {
     XCHK(relayout(&sl.cs, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.cl, sc, nsc, rows, n_ops));
     XCHK(relayout(&sl.ty, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.cnt, sc, nsc, rows, n_ops));
     for (int k = 0; k < NPART; k++) XCHK(relayout(&sl.p[k], sc, nsc, rows, n_ops));
+    if (records && sl.rlo) {
+      XCHK(relayout(&sl.rlo, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.rhi, sc, nsc, rows, n_ops));
+      XCHK(relayout(&sl.nn, sc, nsc, rows, n_ops));
+    }
+  }
+  if (records && nrc != rcap_ && sl.rts) {
+    XCHK(relayout(&sl.rts, rcap_, nrc, rows, n_ops)); XCHK(relayout(&sl.rv, rcap_, nrc, rows, n_ops));
   }
   if (nss != sesscap || nctx != ctx_alloc) {
     // row = one op: ctx_alloc contexts x sesscap sessions; re-pitch contexts first, then widen each context
@@ -358,9 +409,11 @@ int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx) {
   sc = (int32_t)nsc;
   sesscap = (int32_t)nss;
   ctx_alloc = nctx;
+  rcap_ = nrc;
   cfg.sc = sc;
   cfg.sesscap = sesscap;
   cfg.ctx_alloc = ctx_alloc;
+  cfg.rcap = rcap_;
   XCHK(hipMemcpyAsync(d_cfg, &cfg, sizeof(XCfg), hipMemcpyHostToDevice, stream));
   XCHK(hipStreamSynchronize(stream));
   return SCOTTY_OK;
@@ -422,8 +475,28 @@ int XEngine::push(const int64_t* d_ts, const void* d_val, int64_t n) {
   a.val = d_val;
   a.n = n;
   a.rec_stride = 0;
-  XCHK(launch_replay(a, vt, stream));
-  return SCOTTY_OK;
+  if (!records) {
+    XCHK(launch_replay(a, vt, stream));
+    return SCOTTY_OK;
+  }
+  // records mode: capacity pre-check (slices, sessions, records); a deferred op is grown and relaunched
+  a.need = d_need;
+  for (int attempt = 0; attempt < 8; attempt++) {
+    XCHK(hipMemsetAsync(d_need, 0, 32, stream));
+    a.retry = attempt > 0;
+    a.sl = sl;
+    a.ss = ss;
+    XCHK(launch_replay(a, vt, stream));
+    XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));
+    XCHK(hipStreamSynchronize(stream));
+    if (h_misc[0] == 0 && h_misc[1] == 0 && h_misc[2] == 0) return SCOTTY_OK;
+    int rc = grow_caps(std::max<int64_t>(h_misc[0], sc), std::max<int64_t>(h_misc[1], sesscap), ctx_alloc,
+                       std::max<int64_t>(h_misc[2], rcap_));
+    if (rc) return rc;
+  }
+  err = "capacity growth did not converge";
+  failed = true;
+  return SCOTTY_ERR_NOMEM;
 }
 
 // Non-keyed micro-batch: classify (all CUs) -> compacted events (one wave, exact) -> apply (all CUs).  A
@@ -638,15 +711,16 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
   a.rec_stride = rec;
   a.need = d_need;
   for (int attempt = 0; attempt < 6; attempt++) {
-    XCHK(hipMemsetAsync(d_need, 0, 16, stream));
+    XCHK(hipMemsetAsync(d_need, 0, 32, stream));
     a.retry = attempt > 0;
     a.sl = sl;
     a.ss = ss;
     XCHK(lane_mode() ? launch_lane_replay(a, cfg, stream) : launch_replay(a, vt, stream));
-    XCHK(hipMemcpyAsync(h_misc, d_need, 16, hipMemcpyDeviceToHost, stream));
+    XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
-    if (h_misc[0] == 0 && h_misc[1] == 0) return SCOTTY_OK;
-    rc = grow_caps(std::max<int64_t>(h_misc[0], sc), std::max<int64_t>(h_misc[1], sesscap), ctx_alloc);
+    if (h_misc[0] == 0 && h_misc[1] == 0 && h_misc[2] == 0) return SCOTTY_OK;
+    rc = grow_caps(std::max<int64_t>(h_misc[0], sc), std::max<int64_t>(h_misc[1], sesscap), ctx_alloc,
+                   std::max<int64_t>(h_misc[2], rcap_));
     if (rc) return rc;
   }
   err = "capacity growth did not converge";
@@ -710,11 +784,13 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   XCHK(hipStreamSynchronize(stream));
   r.dropped = (uint64_t)h_misc[1];
   const int32_t op_err = (int32_t)h_misc[2];
-  if (op_err & ~(1 << XERR_INDEX)) {
+  if (op_err & ~((1 << XERR_INDEX) | (1 << XERR_NPE) | (1 << XERR_NOELEM))) {
     failed = true;
     if (op_err & (1 << XERR_UNSUPPORTED))
-      err = "a LazySlice (count windows / maxLateness<=0 / non-session context windows) would move records "
-            "(out-of-order tuple): not implemented on the MI355X path yet";
+      err = "an EagerSlice would have to move LazySlice records (slices created before the operator's slices "
+            "became Lazy): not supported on the MI355X path";
+    else if (op_err & (1 << XERR_REC_CAP))
+      err = "internal: LazySlice record capacity exceeded after the pre-check";
     else if (op_err & (1 << XERR_SLICE_CAP))
       err = "per-operator slice capacity exceeded (scotty_tune \"slice_capacity\")";
     else if (op_err & (1 << XERR_SESS_CAP))

@@ -36,7 +36,9 @@ class XEngine {
  public:
   ~XEngine();
   int init(int device, hipStream_t stream, int vt, bool keyed, std::string& err);
-  int configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness);
+  // agg_inv[i]: function i is an InvertibleAggregateFunction (C/windowFunction/InvertibleAggregateFunction.java)
+  int configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness,
+                const std::vector<int>& agg_inv = {});
   int push(const int64_t* d_ts, const void* d_val, int64_t n);
   int push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n);
   int push_batch(const int64_t* d_ts, const void* d_val, int64_t n);  // non-keyed, batch-parallel
@@ -55,13 +57,17 @@ class XEngine {
   bool serial = false;  // non-keyed: single-wavefront replay instead of the batch-parallel path (A/B)
   bool lane_off = false;  // keyed: force the wavefront-per-key replay even where the lane path applies (A/B)
   bool lane_mode() const {  // keyed_lane.hip: context-free time windows on Eager slices only
-    return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && cfg.n_cf > 0;
+    return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && !records && cfg.n_cf > 0;
   }
+  // non-keyed: the single-wavefront replay (LazySlice record sets live only there)
+  bool use_serial() const { return serial || records; }
+  bool records = false;   // LazySlice record sets kept (XCfg.records)
 
  private:
   void release();
   int grow_ops(int64_t need);
-  int grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx);
+  int grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx, int64_t need_rec = 0);
+  int alloc_records();
   int ensure_batch(int64_t n);
   int ensure_table(int64_t keys, bool drop_new = false);
   int ensure_rows(int64_t rows);
@@ -77,6 +83,7 @@ class XEngine {
   int32_t *d_cf_kind = nullptr, *d_cf_meas = nullptr;
   int64_t *d_cf_a = nullptr, *d_cf_b = nullptr;
   int32_t sc = 0, sesscap = 0, ctx_alloc = 0;
+  int64_t rcap_ = 0;  // records per op (records mode)
   unsigned long long* d_need = nullptr;
   int64_t n_ops = 0, ops_cap = 0;
   XState* d_st = nullptr;

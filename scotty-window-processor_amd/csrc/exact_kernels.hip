@@ -85,15 +85,25 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
       int need_x = 0;
       for (int c = 0; c < cfg->n_ctx; c++) need_x = max(need_x, o.s.nsess[c]);
       const int64_t need_ss = cfg->n_ctx > 0 ? (int64_t)need_x + seglen + 1 : 0;
-      if (need_s > (double)cfg->sc || need_ss > cfg->sesscap) {
+      // records: every tuple adds at most one record; the live arena range is compacted first when needed
+      int64_t need_r = 0;
+      if (cfg->records) {
+        const int64_t live = o.s.tail > o.s.head ? o.s.rend - o.rlo[o.s.head] : 0;
+        need_r = live + seglen + 64;
+      }
+      if (need_s > (double)cfg->sc || need_ss > cfg->sesscap || need_r > cfg->rcap) {
         if (lane == 0) {
           atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
           atomicMax(&a.need[1], (unsigned long long)need_ss);
+          atomicMax(&a.need[2], (unsigned long long)need_r);
           o.s.pending = 1;
           a.st[op] = o.s;
         }
         continue;
       }
+      if (cfg->records && o.s.rend + seglen + 64 > cfg->rcap) o.rec_compact();
+    } else if (cfg->records && o.s.rend + (b1 - b0) + 64 > cfg->rcap) {
+      o.rec_compact();
     }
     for (int64_t c0 = b0; c0 < b1 && !o.s.err; c0 += 64) {
       const int n = (int)min((int64_t)64, b1 - c0);
@@ -164,6 +174,8 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
           if (t < cur_start) {
             if (cfg->has_count || (o.s.unsorted & 1) || t < o.ts[o.s.head]) simple = false;
           }
+          // records: a tuple inside the current slice but not after its last record takes a sorted insert
+          if (cfg->records) simple = false;
         }
         const unsigned long long ev = __ballot(mine && !simple);
         const int jstar = ev ? (__ffsll((long long)ev) - 1) : n;
@@ -215,6 +227,24 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
             if (cfg->need & NEED_MAX) o.p2[si] = (unsigned long long)max((int64_t)o.p2[si], mx);
             pend &= ~m;
           }
+          if (cfg->records) {
+            // every simple lane landed in the current slice in ts order: append its record unless an earlier
+            // record of the slice has the same ts (TreeSet.add, S/slice/LazySlice.java:23-27)
+            o.nn[cur] = 1;
+            if (ty_lazy(o.ty[cur])) {
+              const int64_t lastrec = o.rhi[cur] > o.rlo[cur] ? o.rts[o.rhi[cur] - 1] : JMIN;
+              const bool nr = act && t > max(lastrec, q);
+              const unsigned long long m = __ballot(nr);
+              if (nr) {
+                const int64_t pos = o.s.rend + __popcll(m & ((1ull << lane) - 1));
+                o.rts[pos] = t;
+                o.rv[pos] = vb;
+              }
+              const int64_t k = __popcll(m);
+              o.rhi[cur] += k;
+              o.s.rend += k;
+            }
+          }
           const int64_t pmax = wmax(act ? t : JMIN);
           o.s.maxEventTime = max(o.s.maxEventTime, pmax);
           o.s.currentCount = jadd(o.s.currentCount, jstar - j0);
@@ -232,7 +262,7 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
           o.exc = 0;
           o.determine_slices(et);
           if (!o.exc) o.manager_process(et, ev_b);
-          if (o.exc == XERR_INDEX) {
+          if (xerr_tuple_failed(o.exc)) {
             o.s.dropped++;
             o.exc = 0;
           } else if (o.exc) {
@@ -447,7 +477,8 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
     hi = l;
   }
   const int need = a.cfg->need, vt = a.cfg->vt;
-  uint64_t cnt = 0, sw = 0;
+  const bool recs = a.cfg->records != 0;
+  uint64_t cnt = 0, sw = 0, present = 0;
   double sf = 0.0;
   int64_t mn = ID_MIN, mx = ID_MAX;
   for (int64_t i = lo + lane; i < hi; i += G) {
@@ -455,7 +486,9 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
     const bool contains = tmeas ? (ws <= a.sl.ts[s] && we > a.sl.tl[s]) : (ws <= a.sl.cs[s] && we >= a.sl.cl[s]);
     if (!contains) continue;
     const uint64_t c = a.sl.cnt[s];
-    if (c == 0) continue;
+    // a partial is present when non-null: count > 0, or (records mode) kept after liftAndInvert
+    if (recs ? a.sl.nn[s] == 0 : c == 0) continue;
+    present = 1;
     cnt += c;
     if (need & NEED_SUM) {
       if (vt == VT_F64) sf += __longlong_as_double((long long)a.sl.p[0][s]);
@@ -468,6 +501,7 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   auto min_i = [](long long x, long long y) { return x < y ? x : y; };
   auto max_i = [](long long x, long long y) { return x > y ? x : y; };
   cnt = greduce<G>((unsigned long long)cnt, add_u);
+  present = greduce<G>((unsigned long long)present, add_u);
   if (need & NEED_SUM) {
     if (vt == VT_F64) sf = greduce<G>(sf, [](double x, double y) { return x + y; });
     else sw = greduce<G>((unsigned long long)sw, add_u);
@@ -475,11 +509,11 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   if (need & NEED_MIN) mn = greduce<G>((long long)mn, min_i);
   if (need & NEED_MAX) mx = greduce<G>((long long)mx, max_i);
   if (lane == 0) {
-    a.has_value[wi] = cnt ? 1 : 0;
+    a.has_value[wi] = present ? 1 : 0;
     if (a.w_key) a.w_key[wi] = a.slot_key ? a.slot_key[op] : (uint32_t)op;
     const uint64_t sword = vt == VT_F64 ? (uint64_t)__double_as_longlong(sf) : sw;
     for (int k = 0; k < a.cfg->n_aggs; k++)
-      a.values[k][wi] = cnt ? lower_value(a.cfg->agg_kind[k], cnt, sword, mn, mx) : 0;
+      a.values[k][wi] = present ? lower_value(a.cfg->agg_kind[k], cnt, sword, mn, mx) : 0;
   }
 }
 

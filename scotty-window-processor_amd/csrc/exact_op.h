@@ -118,6 +118,9 @@ struct Op {
   unsigned long long *cnt, *p0, *p1, *p2;
   int64_t* ss[XMAXCTX];
   int64_t* se[XMAXCTX];
+  // records mode: per-slice record ranges, non-null flags, the op's record arena
+  int64_t *rlo, *rhi, *rts, *rv;
+  int32_t* nn;
   XState s;
   int32_t exc;
   int lane;
@@ -127,6 +130,13 @@ struct Op {
     const int64_t b = op * (int64_t)c->sc;
     ts = sl.ts + b; te = sl.te + b; tl = sl.tl + b; tf = sl.tf + b; cs = sl.cs + b; cl = sl.cl + b;
     ty = sl.ty + b; cnt = sl.cnt + b; p0 = sl.p[0] + b; p1 = sl.p[1] + b; p2 = sl.p[2] + b;
+    if (c->records) {
+      rlo = sl.rlo + b; rhi = sl.rhi + b; nn = sl.nn + b;
+      rts = sl.rts + op * c->rcap; rv = sl.rv + op * c->rcap;
+    } else {
+      rlo = rhi = rts = rv = nullptr;
+      nn = nullptr;
+    }
     for (int c2 = 0; c2 < XMAXCTX; c2++) {
       const int64_t sb = (op * c->ctx_alloc + min(c2, max(c->ctx_alloc - 1, 0))) * (int64_t)c->sesscap;
       ss[c2] = sx.start + sb;
@@ -141,45 +151,53 @@ struct Op {
     ts[dst] = ts[src]; te[dst] = te[src]; tl[dst] = tl[src]; tf[dst] = tf[src];
     cs[dst] = cs[src]; cl[dst] = cl[src]; ty[dst] = ty[src];
     cnt[dst] = cnt[src]; p0[dst] = p0[src]; p1[dst] = p1[src]; p2[dst] = p2[src];
+    if (cfg->records) {
+      rlo[dst] = rlo[src]; rhi[dst] = rhi[src]; nn[dst] = nn[src];
+    }
   }
   // lane-parallel move of n slices from src to dst (dst < src: forward chunks; dst > src: backward chunks)
   __device__ void move_range(int dst, int src, int n) {
     if (n <= 0 || dst == src) return;
+    const bool rec = cfg->records != 0;
     if (dst < src) {
       for (int b = 0; b < n; b += 64) {
         const int i = b + lane;
-        int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0;
-        int32_t a6 = 0;
+        int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, r0 = 0, r1 = 0;
+        int32_t a6 = 0, r2 = 0;
         unsigned long long a7 = 0, a8 = 0, a9 = 0, a10 = 0;
         if (i < n) {
           a0 = ts[src + i]; a1 = te[src + i]; a2 = tl[src + i]; a3 = tf[src + i]; a4 = cs[src + i];
           a5 = cl[src + i]; a6 = ty[src + i]; a7 = cnt[src + i]; a8 = p0[src + i]; a9 = p1[src + i];
           a10 = p2[src + i];
+          if (rec) { r0 = rlo[src + i]; r1 = rhi[src + i]; r2 = nn[src + i]; }
         }
         __builtin_amdgcn_wave_barrier();
         if (i < n) {
           ts[dst + i] = a0; te[dst + i] = a1; tl[dst + i] = a2; tf[dst + i] = a3; cs[dst + i] = a4;
           cl[dst + i] = a5; ty[dst + i] = a6; cnt[dst + i] = a7; p0[dst + i] = a8; p1[dst + i] = a9;
           p2[dst + i] = a10;
+          if (rec) { rlo[dst + i] = r0; rhi[dst + i] = r1; nn[dst + i] = r2; }
         }
         __builtin_amdgcn_wave_barrier();
       }
     } else {
       for (int b = n; b > 0; b -= 64) {
         const int i = b - 1 - lane;
-        int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0;
-        int32_t a6 = 0;
+        int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, r0 = 0, r1 = 0;
+        int32_t a6 = 0, r2 = 0;
         unsigned long long a7 = 0, a8 = 0, a9 = 0, a10 = 0;
         if (i >= 0) {
           a0 = ts[src + i]; a1 = te[src + i]; a2 = tl[src + i]; a3 = tf[src + i]; a4 = cs[src + i];
           a5 = cl[src + i]; a6 = ty[src + i]; a7 = cnt[src + i]; a8 = p0[src + i]; a9 = p1[src + i];
           a10 = p2[src + i];
+          if (rec) { r0 = rlo[src + i]; r1 = rhi[src + i]; r2 = nn[src + i]; }
         }
         __builtin_amdgcn_wave_barrier();
         if (i >= 0) {
           ts[dst + i] = a0; te[dst + i] = a1; tl[dst + i] = a2; tf[dst + i] = a3; cs[dst + i] = a4;
           cl[dst + i] = a5; ty[dst + i] = a6; cnt[dst + i] = a7; p0[dst + i] = a8; p1[dst + i] = a9;
           p2[dst + i] = a10;
+          if (rec) { rlo[dst + i] = r0; rhi[dst + i] = r1; nn[dst + i] = r2; }
         }
         __builtin_amdgcn_wave_barrier();
       }
@@ -198,9 +216,14 @@ struct Op {
     s.head = 0;
     return true;
   }
-  __device__ void init_slice(int i, int64_t start, int64_t end, int64_t c_s, int64_t c_l, int32_t type) {
+  // rpos: where the slice's (empty) record range starts (records mode)
+  __device__ void init_slice(int i, int64_t start, int64_t end, int64_t c_s, int64_t c_l, int32_t type,
+                             int64_t rpos = 0) {
     ts[i] = start; te[i] = end; tl[i] = start; tf[i] = JMAX; cs[i] = c_s; cl[i] = c_l; ty[i] = type;
     cnt[i] = 0; p0[i] = 0; p1[i] = (unsigned long long)ID_MIN; p2[i] = (unsigned long long)ID_MAX;
+    if (cfg->records) {
+      rlo[i] = rpos; rhi[i] = rpos; nn[i] = 0;
+    }
   }
   __device__ int32_t new_lazy_bit() const { return cfg->lazy ? XTYPE_LAZY : 0; }
   __device__ void note_order(int i) {
@@ -284,6 +307,271 @@ struct Op {
     }
     if (cfg->need & NEED_MIN) p1[i] = (unsigned long long)min((int64_t)p1[i], l.mn);
     if (cfg->need & NEED_MAX) p2[i] = (unsigned long long)max((int64_t)p2[i], l.mx);
+    if (cfg->records) {
+      nn[i] = 1;
+      if (ty_lazy(ty[i])) rec_insert(i, t, vbits);  // LazySlice.addElement: records.add (:23-27)
+    }
+  }
+
+  // ---------------------------------------------------------------- LazySlice record sets (records mode)
+  // lane-parallel move of n records from src to dst in the op's arena (either direction, overlap-safe)
+  __device__ void rec_move(int64_t dst, int64_t src, int64_t n) {
+    if (n <= 0 || dst == src) return;
+    if (dst < src) {
+      for (int64_t b = 0; b < n; b += 64) {
+        const int64_t i = b + lane;
+        int64_t a = 0, v = 0;
+        if (i < n) { a = rts[src + i]; v = rv[src + i]; }
+        __builtin_amdgcn_wave_barrier();
+        if (i < n) { rts[dst + i] = a; rv[dst + i] = v; }
+        __builtin_amdgcn_wave_barrier();
+      }
+    } else {
+      for (int64_t b = n; b > 0; b -= 64) {
+        const int64_t i = b - 1 - lane;
+        int64_t a = 0, v = 0;
+        if (i >= 0) { a = rts[src + i]; v = rv[src + i]; }
+        __builtin_amdgcn_wave_barrier();
+        if (i >= 0) { rts[dst + i] = a; rv[dst + i] = v; }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __threadfence_block();
+  }
+  // record ranges of slices [from, tail) move by d
+  __device__ void rec_adjust(int from, int64_t d) {
+    for (int i = from + lane; i < s.tail; i += 64) {
+      rlo[i] += d;
+      rhi[i] += d;
+    }
+    __threadfence_block();
+  }
+  // first p in [lo, hi) with rts[p] >= t (hi if none): wavefront-cooperative, 64 probes per round
+  __device__ int64_t rec_lb(int64_t lo, int64_t hi, int64_t t) {
+    while (hi - lo > 64) {
+      const int64_t stride = (hi - lo + 63) >> 6;
+      const int64_t p = lo + (int64_t)lane * stride;
+      const unsigned long long bal = __ballot(p < hi && rts[p] >= t);
+      if (bal == 0) {
+        lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
+      } else {
+        const int f = __ffsll((long long)bal) - 1;
+        if (f == 0) return lo;
+        const int64_t pf = lo + (int64_t)f * stride;
+        lo = pf - stride + 1;
+        hi = pf;
+      }
+    }
+    const int64_t p = lo + lane;
+    const unsigned long long bal = __ballot(p < hi && rts[p] >= t);
+    return bal ? lo + __ffsll((long long)bal) - 1 : hi;
+  }
+  // TreeSet.add: insert (t, v) into slice i's sorted set unless a record with ts t exists (S/slice/StreamRecord.java:25-27)
+  __device__ void rec_insert(int i, int64_t t, int64_t vbits) {
+    const int64_t p = rec_lb(rlo[i], rhi[i], t);
+    if (p < rhi[i] && rts[p] == t) return;
+    if (s.rend >= cfg->rcap) {
+      exc = XERR_REC_CAP;
+      return;
+    }
+    rec_move(p + 1, p, s.rend - p);
+    rts[p] = t;
+    rv[p] = vbits;
+    rhi[i] += 1;
+    rec_adjust(i + 1, 1);
+    s.rend++;
+  }
+  // remove the arena record at p owned by slice i
+  __device__ void rec_delete(int i, int64_t p) {
+    rec_move(p, p + 1, s.rend - p - 1);
+    rhi[i] -= 1;
+    rec_adjust(i + 1, -1);
+    s.rend--;
+  }
+  // AggregateValueState.recompute over the slice's record set (S/state/AggregateValueState.java:43-49)
+  __device__ void rec_recompute(int i) {
+    uint64_t c = 0, sw = 0;
+    double sf = 0.0;
+    int64_t mn = ID_MIN, mx = ID_MAX;
+    for (int64_t p = rlo[i] + lane; p < rhi[i]; p += 64) {
+      const Lift l = lift(cfg->vt, rv[p]);
+      c++;
+      if (cfg->vt == VT_F64) sf += __longlong_as_double((long long)l.sum);
+      else sw += l.sum;
+      mn = min(mn, l.mn);
+      mx = max(mx, l.mx);
+    }
+    c = wsum(c);
+    if (cfg->vt == VT_F64) sw = (uint64_t)__double_as_longlong(wsumf(sf));
+    else sw = wsum(sw);
+    mn = wmin(mn);
+    mx = wmax(mx);
+    cnt[i] = c;
+    p0[i] = sw;
+    p1[i] = (unsigned long long)mn;
+    p2[i] = (unsigned long long)mx;
+    nn[i] = c != 0;  // clear() then addElement per record: null when the set is empty
+  }
+  // AggregateState.removeElement (S/state/AggregateValueState.java:33-41): liftAndInvert of every (invertible)
+  // function, else recompute from the records.  have == false: the record is Java null.
+  __device__ void part_remove(int i, bool have, int64_t vbits) {
+    if (cfg->invertible) {
+      if (!have) {  // liftAndInvert(partial, null.record)
+        exc = XERR_NPE;
+        return;
+      }
+      const Lift l = lift(cfg->vt, vbits);
+      cnt[i] = cnt[i] - 1;
+      if (cfg->vt == VT_F64)
+        p0[i] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)p0[i]) -
+                                                         __longlong_as_double((long long)l.sum));
+      else
+        p0[i] = p0[i] - l.sum;
+    } else {
+      rec_recompute(i);
+    }
+  }
+  // AbstractSlice.addElement + AggregateState.addElement of a moved record (LazySlice.prependElement :29-33), the
+  // record itself placed by the caller
+  __device__ void part_add(int i, int64_t t, int64_t vbits) {
+    tl[i] = max(tl[i], t);
+    tf[i] = min(tf[i], t);
+    cl[i] = jadd(cl[i], 1);
+    cnt[i] = cnt[i] + 1;
+    nn[i] = 1;
+    const Lift l = lift(cfg->vt, vbits);
+    if (cfg->vt == VT_F64)
+      p0[i] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)p0[i]) +
+                                                       __longlong_as_double((long long)l.sum));
+    else
+      p0[i] = p0[i] + l.sum;
+    p1[i] = (unsigned long long)min((int64_t)p1[i], l.mn);
+    p2[i] = (unsigned long long)max((int64_t)p2[i], l.mx);
+  }
+  // slice(i).dropLastElement() -> slice(i+1).prependElement(record) (LazySlice.java:29-44).  The two record sets
+  // are adjacent in the arena: the record changes owner by moving the boundary, then takes its sorted place in
+  // slice i+1 (a rotation; a duplicate ts is dropped -- TreeSet.add of an equal element).
+  __device__ void move_last_to_next(int i) {
+    const int j = i + 1;
+    const bool have = rhi[i] > rlo[i];
+    int64_t t = 0, v = 0;
+    if (have) {
+      t = rts[rhi[i] - 1];
+      v = rv[rhi[i] - 1];
+      rhi[i] -= 1;
+      rlo[j] -= 1;
+    }
+    cl[i] = jsub(cl[i], 1);
+    if (rhi[i] > rlo[i]) tl[i] = rts[rhi[i] - 1];
+    part_remove(i, have, v);
+    if (exc) {  // the record left slice i but never reached slice i+1
+      if (have) rec_delete(j, rlo[j]);
+      return;
+    }
+    if (!have) {  // prependElement(null)
+      exc = XERR_NPE;
+      return;
+    }
+    part_add(j, t, v);
+    const int64_t p = rec_lb(rlo[j] + 1, rhi[j], t);
+    if (p < rhi[j] && rts[p] == t) {
+      rec_delete(j, rlo[j]);
+    } else if (p > rlo[j] + 1) {
+      rec_move(rlo[j], rlo[j] + 1, p - 1 - rlo[j]);
+      rts[p - 1] = t;
+      rv[p - 1] = v;
+      __threadfence_block();
+    }
+  }
+  // slice(j).dropFirstElement() -> slice(j-1).prependElement(record) (LazySlice.java:29-33, :46-53)
+  __device__ void move_first_to_prev(int j) {
+    const int i = j - 1;
+    const bool have = rhi[j] > rlo[j];
+    int64_t t = 0, v = 0;
+    if (have) {
+      t = rts[rlo[j]];
+      v = rv[rlo[j]];
+      rlo[j] += 1;
+      rhi[i] += 1;
+    }
+    if (rhi[j] <= rlo[j]) {  // records.getFirst() on the emptied set
+      if (have) rec_delete(i, rhi[i] - 1);
+      exc = XERR_NOELEM;
+      return;
+    }
+    cl[j] = jsub(cl[j], 1);
+    tf[j] = rts[rlo[j]];
+    part_remove(j, have, v);
+    if (exc) {
+      if (have) rec_delete(i, rhi[i] - 1);
+      return;
+    }
+    part_add(i, t, v);
+    const int64_t e = rhi[i] - 1;  // the new record, last in slice i's range
+    const int64_t p = rec_lb(rlo[i], e, t);
+    if (p < e && rts[p] == t) {
+      rec_delete(i, e);
+    } else if (p < e) {
+      rec_move(p + 1, p, e - p);
+      rts[p] = t;
+      rv[p] = v;
+      __threadfence_block();
+    }
+  }
+  // slice(j).dropLastElement() -> slice(j-1).prependElement(record) (DeleteModification, S/SliceManager.java:141-146):
+  // slice j's last record is rotated to the front of j's range, then moved like move_first_to_prev
+  __device__ void move_last_of_next_to_prev(int j) {
+    const int i = j - 1;
+    const bool have = rhi[j] > rlo[j];
+    int64_t t = 0, v = 0;
+    if (have) {
+      t = rts[rhi[j] - 1];
+      v = rv[rhi[j] - 1];
+      rec_move(rlo[j] + 1, rlo[j], rhi[j] - 1 - rlo[j]);
+      rts[rlo[j]] = t;
+      rv[rlo[j]] = v;
+      __threadfence_block();
+      rlo[j] += 1;
+      rhi[i] += 1;
+    }
+    cl[j] = jsub(cl[j], 1);
+    if (rhi[j] > rlo[j]) tl[j] = rts[rhi[j] - 1];
+    part_remove(j, have, v);
+    if (exc) {
+      if (have) rec_delete(i, rhi[i] - 1);
+      return;
+    }
+    if (!have) {
+      exc = XERR_NPE;
+      return;
+    }
+    part_add(i, t, v);
+    const int64_t e = rhi[i] - 1;
+    const int64_t p = rec_lb(rlo[i], e, t);
+    if (p < e && rts[p] == t) {
+      rec_delete(i, e);
+    } else if (p < e) {
+      rec_move(p + 1, p, e - p);
+      rts[p] = t;
+      rv[p] = v;
+      __threadfence_block();
+    }
+  }
+  // arena compaction: live records [rlo[head], rend) move to the arena start
+  __device__ void rec_compact() {
+    if (!cfg->records || s.tail <= s.head) {
+      if (cfg->records && s.tail <= s.head) s.rend = 0;
+      return;
+    }
+    const int64_t base = rlo[s.head];
+    if (base <= 0) return;
+    rec_move(0, base, s.rend - base);
+    for (int i = s.head + lane; i < s.tail; i += 64) {
+      rlo[i] -= base;
+      rhi[i] -= base;
+    }
+    __threadfence_block();
+    s.rend -= base;
   }
 
   // SliceManager.appendSlice (S/SliceManager.java:27-38)
@@ -295,7 +583,7 @@ struct Op {
     }
     if (!ensure_room()) return;
     const int i = s.tail;
-    init_slice(i, start, JMAX, s.currentCount, s.currentCount, 1 | new_lazy_bit());
+    init_slice(i, start, JMAX, s.currentCount, s.currentCount, 1 | new_lazy_bit(), s.rend);
     s.tail++;
     if (i > s.head && ts[i - 1] > start) s.unsorted |= 1;
   }
@@ -319,11 +607,17 @@ struct Op {
     bpos = insert_at(bpos);
     if (bpos < 0) return;
     a = s.head + rel_a;
-    init_slice(bpos, timestamp, a_end, a_cs, a_cl, ty_kind(a_ty) | new_lazy_bit());
+    init_slice(bpos, timestamp, a_end, a_cs, a_cl, ty_kind(a_ty) | new_lazy_bit(), cfg->records ? rhi[a] : 0);
     te[a] = timestamp;
     ty[a] = 1 | (a_ty & XTYPE_LAZY);
     note_order(bpos);
-    if (ty_lazy(a_ty) && tl[a] >= timestamp) exc = XERR_UNSUPPORTED;  // LazySlice record movement
+    if (ty_lazy(a_ty) && tl[a] >= timestamp) {  // move records to the new slice (:186-191)
+      if (!cfg->records || !ty_lazy(ty[bpos])) {
+        exc = XERR_UNSUPPORTED;
+        return;
+      }
+      while (!exc && tl[a] >= timestamp) move_last_to_next(a);
+    }
   }
 
   // AbstractSlice.merge + LazyAggregateStore.mergeSlice (:119-124)
@@ -341,6 +635,11 @@ struct Op {
       p0[idx] = p0[idx] + p0[b];
     p1[idx] = (unsigned long long)min((int64_t)p1[idx], (int64_t)p1[b]);
     p2[idx] = (unsigned long long)max((int64_t)p2[idx], (int64_t)p2[b]);
+    if (cfg->records) {
+      nn[idx] = nn[idx] | nn[b];
+      // AbstractSlice.merge does not move records: slice b's remaining set is dropped with the slice
+      while (rhi[b] > rlo[b]) rec_delete(b, rhi[b] - 1);
+    }
     remove_at(b);
   }
 
@@ -359,11 +658,17 @@ struct Op {
           ts[nx] = m.post;
           s.unsorted |= 2;
           note_order(nx);
-          if (ty_lazy(st)) {
+          if (ty_lazy(st)) {  // move tuples across the moved edge (:106-125)
             if (m.post < m.pre) {
-              if (tf[si] < tl[si] && tl[si] >= m.post) exc = XERR_UNSUPPORTED;
+              if (tf[si] < tl[si] && tl[si] >= m.post) {
+                if (!cfg->records) exc = XERR_UNSUPPORTED;
+                while (!exc && tf[si] < tl[si] && tl[si] >= m.post) move_last_to_next(si);
+              }
             } else {
-              if (tf[nx] < tl[nx] && tf[nx] < m.post) exc = XERR_UNSUPPORTED;
+              if (tf[nx] < tl[nx] && tf[nx] < m.post) {
+                if (!cfg->records) exc = XERR_UNSUPPORTED;
+                while (!exc && tf[nx] < tl[nx] && tf[nx] < m.post) move_first_to_prev(nx);
+              }
             }
           }
         } else {
@@ -376,9 +681,13 @@ struct Op {
           const int32_t st = ty[si];
           if (ty_movable(st)) {
             if (!valid(si + 1)) return;
-            if (ty_lazy(ty[si + 1]) && cl[si + 1] > 0) {
-              exc = XERR_UNSUPPORTED;
-              return;
+            if (ty_lazy(ty[si + 1]) && cl[si + 1] > 0) {  // move records to the new slice (:141-146)
+              if (!cfg->records) {
+                exc = XERR_UNSUPPORTED;
+                return;
+              }
+              while (!exc && cl[si + 1] > 0) move_last_of_next_to_prev(si + 1);
+              if (exc) return;
             }
             merge_slice(si);
           } else if (!ty_fixed(st)) {
@@ -586,7 +895,20 @@ struct Op {
     const int idx = find_ts(t);
     if (!valid(idx)) return;
     add_element(idx, t, vbits);
-    if (cfg->has_count && idx <= s.tail - 2) exc = XERR_UNSUPPORTED;  // LazySlice count shift (:77-85)
+    if (exc) return;
+    if (cfg->has_count && idx <= s.tail - 2) {  // shift count in slices: each later slice's last record (:77-85)
+      if (!cfg->records) {
+        exc = XERR_UNSUPPORTED;
+        return;
+      }
+      for (int i = idx; i <= s.tail - 2 && !exc; i++) {
+        if (!ty_lazy(ty[i]) || !ty_lazy(ty[i + 1])) {  // (LazySlice) cast of an EagerSlice
+          exc = XERR_UNSUPPORTED;
+          return;
+        }
+        move_last_to_next(i);
+      }
+    }
   }
 };
 

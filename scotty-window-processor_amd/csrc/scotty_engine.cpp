@@ -68,7 +68,8 @@ struct scotty_op {
 
   // ---- WindowManager / StreamSlicer scalars
   std::vector<CFWin> windows;
-  std::vector<int> aggs;
+  std::vector<int> aggs;      // SCOTTY_AGG_* kinds (without SCOTTY_AGG_INVERTIBLE)
+  std::vector<int> agg_inv;   // 1: the function is an InvertibleAggregateFunction
   int need = 0;
   int64_t max_lateness = 1000;
   int64_t max_fixed_window_size = 0;
@@ -146,7 +147,8 @@ struct scotty_op {
   bool x_lane_off = false;
   int64_t shard_count_total = 0;
   int64_t count_shard_cap = 1 << 16;
-  bool x_count_off = false;  // tuning: count-window operators on the exact engine instead of the count path
+  bool x_count_on = false;   // "count_path" 1: the stream is in timestamp order -> count-only operators keep no
+                             // LazySlice records and run on the count path (count_engine.cpp)
   uint64_t x_pushed = 0;
   std::vector<uint32_t> r_key;
   // sharded grid path (scotty_shard_*)
@@ -735,7 +737,7 @@ int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b
   }
   if (op->mode == 2) {  // exact engine: reconfigure (windows may be added mid-stream, S/WindowManager.java:121-147)
     op->xwins.push_back({kind, measure, a, b});
-    int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
+    int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness, op->agg_inv);
     if (rc) {
       op->xwins.pop_back();
       return fail(op, rc, op->x->err);
@@ -772,8 +774,13 @@ int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b
   return SCOTTY_OK;
 }
 
-int scotty_add_aggregation(scotty_op* op, int kind) {
+int scotty_add_aggregation(scotty_op* op, int kind_flags) {
   if (!op) return SCOTTY_ERR_ARG;
+  const int kind = kind_flags & 0xFFFF;
+  const bool inv = (kind_flags & SCOTTY_AGG_INVERTIBLE) != 0;
+  if ((kind_flags & ~(0xFFFF | SCOTTY_AGG_INVERTIBLE)) != 0) return fail(op, SCOTTY_ERR_ARG, "unknown aggregation flags");
+  if (inv && agg_need(kind) != NEED_SUM && kind != SCOTTY_AGG_COUNT)
+    return fail(op, SCOTTY_ERR_ARG, "only sums and counts have an inverse (InvertibleAggregateFunction)");
   const int vt = agg_value_type(kind);
   if (vt == -2) return fail(op, SCOTTY_ERR_ARG, "unknown aggregation kind");
   if (vt >= 0 && vt != op->vt) return fail(op, SCOTTY_ERR_ARG, "aggregation kind does not match the value type");
@@ -781,6 +788,7 @@ int scotty_add_aggregation(scotty_op* op, int kind) {
   if (op->mode != 0)  // existing slices would lack the new function's state (S/state/AggregateState.java:44-50)
     return fail(op, SCOTTY_ERR_UNSUPPORTED, "aggregation added after elements were processed");
   op->aggs.push_back(kind);
+  op->agg_inv.push_back(inv ? 1 : 0);
   op->need |= agg_need(kind);
   return (int)op->aggs.size() - 1;
 }
@@ -793,7 +801,7 @@ int scotty_set_max_lateness(scotty_op* op, int64_t l) {
     if (rc) return fail(op, rc, op->c->err);
   }
   if (op->mode == 2) {
-    int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
+    int rc = op->x->configure(op->xwins, op->aggs, op->max_lateness, op->agg_inv);
     if (rc) return fail(op, rc, op->x->err);
   }
   return SCOTTY_OK;
@@ -810,7 +818,7 @@ static int decide_mode(scotty_op* op) {
     op->mode = 1;
     return SCOTTY_OK;
   }
-  bool count_only = !op->keyed && !op->xwins.empty() && !op->x_count_off;
+  bool count_only = !op->keyed && !op->xwins.empty() && op->x_count_on;
   for (const XWinDef& w : op->xwins)
     if (w.kind == SCOTTY_WIN_SESSION || w.measure != SCOTTY_MEASURE_COUNT) count_only = false;
   if (count_only) {  // count_common.h: edges are a function of counts, one micro-batch = segmented reduction
@@ -834,7 +842,7 @@ static int decide_mode(scotty_op* op) {
   op->x->lane_off = op->x_lane_off;
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
-  if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness);
+  if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness, op->agg_inv);
   if (!rc && !op->keyed && op->last_watermark != -1) rc = op->x->set_last_watermark(op->last_watermark);
   if (rc) {
     op->failed = true;
@@ -872,7 +880,7 @@ static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int6
   if (op->mode == 2) {
     op->pending.push_back({d_ts, d_val, n, op->push_seq++});
     op->x_pushed += (uint64_t)n;
-    rc = op->x->serial ? op->x->push(d_ts, d_val, n) : op->x->push_batch(d_ts, d_val, n);
+    rc = op->x->use_serial() ? op->x->push(d_ts, d_val, n) : op->x->push_batch(d_ts, d_val, n);
     if (rc) return fail(op, rc, op->x->err);
     return SCOTTY_OK;
   }
@@ -1328,9 +1336,9 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     op->count_shard_cap = value;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "count_path") == 0) {  // 0: count-window operators on the exact engine (A/B)
+  if (std::strcmp(key, "count_path") == 0) {  // 1: in-order stream promised -> count path (no LazySlice records)
     if (op->mode != 0) return SCOTTY_ERR_ARG;
-    op->x_count_off = value == 0;
+    op->x_count_on = value != 0;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_lane") == 0) {  // 0: wavefront-per-key replay even where the lane path applies

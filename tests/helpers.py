@@ -40,13 +40,15 @@ def same_windows(a, b, f64_cols=(), rel=1e-6):
                 assert p == q, (i, j, p, q, x, y)
 
 
-def build_ops(cfg, value_type="i32", device=0):
+def build_ops(cfg, value_type="i32", device=0, tune=None):
     """Create (product, oracle) operators with the same windows / functions / lateness.
-    cfg: dict(windows=[spec...], aggs=[kind...], lateness=int|None)."""
+    cfg: dict(windows=[spec...], aggs=[kind...], lateness=int|None); tune: scotty_tune knobs of the product."""
     from oracle.oracle import OracleOperator
     pkg = product()
     vt = {"i32": pkg.VALUE_I32, "i64": pkg.VALUE_I64, "f64": pkg.VALUE_F64}[value_type]
     gpu = pkg.SlicingWindowOperator(device=device, value_type=vt)
+    for k, v in (tune or {}).items():
+        gpu.tune(k, v)
     ora = OracleOperator()
     for op in (gpu, ora):
         for a in cfg["aggs"]:

@@ -1,5 +1,6 @@
 """Parity of the count-window path (count_common.h / count_kernels.hip: non-keyed operators whose windows are
-all context-free COUNT windows, BASELINE configs[4]) against the oracle, and against the exact engine."""
+all context-free COUNT windows, BASELINE configs[4]; chosen with the in-order promise scotty_tune("count_path", 1))
+against the oracle, and against the exact engine (the default, which keeps LazySlice record sets)."""
 import numpy as np
 import pytest
 
@@ -55,7 +56,7 @@ def test_count_path_matches_oracle(seed):
     n = int(rng.integers(1000, 60_000))
     ts, vals = _in_order_stream(rng, n, [0.3, 2, 25][seed % 3], int(rng.integers(0, 5000)), vt,
                                 n_late=int(rng.integers(0, 5)))
-    gpu, ora = build_ops(cfg, vt)
+    gpu, ora = build_ops(cfg, vt, tune={"count_path": 1})
     sched = interval_schedule(ts, int(rng.integers(1, 12)), lag=int(rng.integers(0, 50)),
                               pushes_per_interval=int(rng.integers(1, 4)))
     f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
@@ -71,12 +72,15 @@ def test_count_path_out_of_order_never_silently_wrong(pkg, seed):
     n = 20_000
     ts, vals = product().workloads.stream(n, 2, t0=1000, ooo_frac=[0.001, 0.05][seed % 2],
                                           max_delay=int(rng.integers(1, 30)), seed=seed)
-    gpu, ora = build_ops(cfg)
+    gpu, ora = build_ops(cfg, tune={"count_path": 1})
     sched = interval_schedule(ts, 6, lag=40)
     try:
         run_schedule(gpu, ora, ts, vals, sched)
     except pkg.ScottyError as e:
         assert e.code == -2, e  # SCOTTY_ERR_UNSUPPORTED
+    # without the in-order promise the operator keeps LazySlice record sets and matches exactly
+    gpu, ora = build_ops(cfg)
+    run_schedule(gpu, ora, ts, vals, sched)
 
 
 def test_count_path_equals_exact_engine(pkg):
@@ -116,8 +120,9 @@ def test_count_config5_reduced():
     n = 400_000
     rng = np.random.default_rng(5)
     ts, vals = _in_order_stream(rng, n, 50, 0, "i32")
-    gpu, ora = build_ops(cfg)
-    assert run_schedule(gpu, ora, ts, vals, interval_schedule(ts, 16, lag=0, pushes_per_interval=2)) > 1000
+    for tune in ({"count_path": 1}, None):
+        gpu, ora = build_ops(cfg, tune=tune)
+        assert run_schedule(gpu, ora, ts, vals, interval_schedule(ts, 16, lag=0, pushes_per_interval=2)) > 1000
 
 
 @pytest.fixture(scope="module")

@@ -11,7 +11,7 @@ import pytest
 import junit_cases
 from helpers import product, build_ops, run_schedule, interval_schedule, KeyedOracle, same_keyed_windows
 from specs import Tumbling, Sliding, Session, FixedBand, Time, Count, SUM, COUNT, MIN, MAX, SUM_I64, \
-    MIN_I64, MAX_I64, SUM_F64, MIN_F64, MAX_F64
+    MIN_I64, MAX_I64, SUM_F64, MIN_F64, MAX_F64, INVERTIBLE
 
 pytestmark = pytest.mark.gpu
 
@@ -28,13 +28,77 @@ def test_junit_session_and_count_golden_values_on_gpu(pkg, case):
     case(lambda: pkg.SlicingWindowOperator(device=0))
 
 
-@pytest.mark.parametrize("case", [c for c in junit_cases.TUMBLING_COUNT if c is not junit_cases.tumbling_inOrderTestCount],
-                         ids=lambda c: c.__name__)
-def test_junit_lazy_count_out_of_order_fails_loudly(pkg, case):
-    """Out-of-order tuples with count windows move LazySlice records (S/SliceManager.java:77-85), and the
-    test-only (a,b)->a-b function has no GPU kind: both raise instead of falling back to the CPU."""
+@pytest.mark.parametrize("case", [junit_cases.tumbling_outOfOrderOrderTestCount,
+                                  junit_cases.tumbling_outOfOrderOrderTestCount3], ids=lambda c: c.__name__)
+def test_junit_lazy_count_out_of_order_on_gpu(pkg, case):
+    """Out-of-order tuples with count windows move LazySlice records (the count-shift loop, S/SliceManager.java:
+    77-85; LazySlice.dropLastElement / prependElement, S/slice/LazySlice.java:29-44) -- on the GPU."""
+    case(lambda: pkg.SlicingWindowOperator(device=0))
+
+
+def test_junit_lambda_without_gpu_kind_fails_loudly(pkg):
+    """The test-only (a,b)->a-b function (TumblingWindowOperatorTest.java:212) has no GPU kind: loud, no CPU
+    fallback."""
     with pytest.raises(pkg.ScottyError):
-        case(lambda: pkg.SlicingWindowOperator(device=0))
+        junit_cases.tumbling_outOfOrderOrderTestCount2(lambda: pkg.SlicingWindowOperator(device=0))
+
+
+# ---------------------------------------------------------------- LazySlice record sets (out-of-order, Lazy slices)
+def _lazy_aggs(rng, vt, invertible):
+    if invertible:  # InvertibleAggregateFunction sums / counts (removal by liftAndInvert)
+        base = {"i32": [SUM, COUNT], "i64": [SUM_I64, COUNT], "f64": [SUM_F64, COUNT]}[vt]
+        return [a | INVERTIBLE for a in base if rng.random() < 0.8] or [base[0] | INVERTIBLE]
+    return _aggs(rng, vt)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_out_of_order_count_windows_match_oracle(seed):
+    """Random count-window operators (plus time / session windows) on out-of-order streams with duplicate
+    timestamps: every out-of-order tuple shifts the last record of each later LazySlice, the TreeSet drops records
+    of equal ts, non-invertible functions recompute from the record set (S/state/AggregateValueState.java:33-49)."""
+    rng = np.random.default_rng(9700 + seed)
+    vt = ["i32", "i32", "i64", "f64"][seed % 4]
+    wins = [Tumbling(Count, int(rng.integers(1, 40)))]
+    if rng.random() < 0.5:
+        size = int(rng.integers(2, 60))
+        wins.append(Sliding(Count, size, int(rng.integers(1, size + 1))))
+    if rng.random() < 0.4:
+        wins.append(Tumbling(Time, _nz(int(rng.integers(5, 100)))))
+    if rng.random() < 0.25:
+        wins.append(Session(Time, int(rng.integers(5, 100))))
+    rng.shuffle(wins)
+    aggs = _lazy_aggs(rng, vt, invertible=seed % 3 == 2)
+    cfg = dict(windows=wins, aggs=aggs, lateness=int(rng.choice([10, 100, 1000])))
+    n = int(rng.integers(200, 6000))
+    ts, vals = product().workloads.stream(n, [0.5, 1, 3, 8][seed % 4], t0=int(rng.integers(0, 500)),
+                                          ooo_frac=[0.02, 0.1, 0.3][seed % 3], max_delay=int(rng.integers(1, 60)),
+                                          seed=seed, value_type=vt, gaps=_gaps(rng, n, 400, 10, 150))
+    gpu, ora = build_ops(cfg, vt)
+    sched = interval_schedule(ts, int(rng.integers(1, 6)), lag=int(rng.integers(0, 60)),
+                              pushes_per_interval=int(rng.integers(1, 3)))
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a & 0xFFFF == SUM_F64]
+    run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_lazy_session_slices_match_oracle(seed):
+    """maxLateness <= 0 makes every slice a LazySlice (S/slice/SliceFactory.java:17-22): out-of-order session
+    tuples split / shift / merge slices and move records across the edges (S/SliceManager.java:89-192)."""
+    rng = np.random.default_rng(9900 + seed)
+    vt = ["i32", "i64", "i32", "f64"][seed % 4]
+    cfg = _session_cfg(rng, vt)
+    cfg["lateness"] = int(rng.choice([0, -5]))
+    cfg["aggs"] = _lazy_aggs(rng, vt, invertible=seed % 4 == 3)
+    n = int(rng.integers(100, 5000))
+    gaps = _gaps(rng, n, int(rng.integers(50, 800)), 50, 600)
+    ts, vals = product().workloads.stream(n, [0.2, 1, 4][seed % 3], t0=int(rng.integers(0, 3000)),
+                                          ooo_frac=[0.05, 0.2][seed % 2], max_delay=int(rng.integers(1, 200)),
+                                          seed=seed, value_type=vt, gaps=gaps)
+    gpu, ora = build_ops(cfg, vt)
+    sched = interval_schedule(ts, int(rng.integers(1, 6)), lag=int(rng.integers(0, 200)),
+                              pushes_per_interval=int(rng.integers(1, 3)))
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a & 0xFFFF == SUM_F64]
+    run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols)
 
 
 def _nz(x):  # a power-of-two size/slide makes the reference loop forever; avoid it in random configs
@@ -371,3 +435,29 @@ def test_keyed_hash_sharding_equals_single_operator(pkg):
     assert sum(p.keyCount() for p in parts) == whole.keyCount()
     assert sum(p.droppedCount() for p in parts) == whole.droppedCount()
     assert total > 0
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_keyed_out_of_order_count_windows_match_per_key_oracles(pkg, seed):
+    """Keyed operators with count windows on out-of-order streams: every key's operator keeps its own LazySlice
+    record sets (per-key record arenas, grown on demand) -- KeyedScottyWindowOperator.java:56-86 per key."""
+    rng = np.random.default_rng(9500 + seed)
+    vt = ["i32", "i64", "i32", "f64"][seed % 4]
+    wins = [Tumbling(Count, int(rng.integers(1, 20)))]
+    if rng.random() < 0.5:
+        size = int(rng.integers(2, 30))
+        wins.append(Sliding(Count, size, int(rng.integers(1, size + 1))))
+    if rng.random() < 0.3:
+        wins.append(Tumbling(Time, _nz(int(rng.integers(5, 100)))))
+    cfg = dict(windows=wins, aggs=_lazy_aggs(rng, vt, invertible=seed % 4 == 1),
+               lateness=int(rng.choice([10, 100, 1000])))
+    nkeys = int(rng.choice([1, 7, 60, 400]))
+    n = int(rng.integers(1000, 12_000))
+    ts, vals = product().workloads.stream(n, [0.5, 2, 6][seed % 3], t0=int(rng.integers(0, 500)),
+                                          ooo_frac=[0.05, 0.2][seed % 2], max_delay=int(rng.integers(1, 80)),
+                                          seed=seed, value_type=vt)
+    keys = (rng.integers(0, nkeys, size=n) * 2654435761 % (2**32)).astype(np.uint32)
+    sched = interval_schedule(ts, int(rng.integers(1, 5)), lag=int(rng.integers(0, 60)),
+                              pushes_per_interval=int(rng.integers(1, 3)))
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a & 0xFFFF == SUM_F64]
+    _keyed_run(pkg, cfg, keys, ts, vals, sched, vt=vt, f64_cols=f64_cols)
