@@ -899,6 +899,18 @@ int XEngine::debug_dump(int64_t op, std::vector<int64_t>& out) {
   }
   out.push_back(s.maxEventTime); out.push_back(s.nextEdgeTs); out.push_back(s.currentCount);
   out.push_back(s.unsorted); out.push_back(s.head); out.push_back(s.tail);
+  if (records && S > 0) {  // record ranges, non-null flags, then the records themselves (ts, value)
+    if (col(sl.rlo) || col(sl.rhi)) return SCOTTY_ERR_HIP;
+    XCHK(hipMemcpy(ty.data(), sl.nn + b, S * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < S; i++) out.push_back(ty[i]);
+    out.push_back(s.rend);
+    std::vector<int64_t> rt(std::max<int64_t>(s.rend, 1)), rvv(std::max<int64_t>(s.rend, 1));
+    if (s.rend > 0) {
+      XCHK(hipMemcpy(rt.data(), sl.rts + op * rcap_, s.rend * 8, hipMemcpyDeviceToHost));
+      XCHK(hipMemcpy(rvv.data(), sl.rv + op * rcap_, s.rend * 8, hipMemcpyDeviceToHost));
+    }
+    for (int64_t i = 0; i < s.rend; i++) { out.push_back(rt[i]); out.push_back(rvv[i]); }
+  }
   return SCOTTY_OK;
 }
 
