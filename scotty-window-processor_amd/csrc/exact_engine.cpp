@@ -899,6 +899,7 @@ int XEngine::debug_dump(int64_t op, std::vector<int64_t>& out) {
   }
   out.push_back(s.maxEventTime); out.push_back(s.nextEdgeTs); out.push_back(s.currentCount);
   out.push_back(s.unsorted); out.push_back(s.head); out.push_back(s.tail);
+  out.push_back(s.wlo); out.push_back(s.whi); out.push_back(s.lastWatermark); out.push_back(s.lastCount);
   if (records && S > 0) {  // record ranges, non-null flags, then the records themselves (ts, value)
     if (col(sl.rlo) || col(sl.rhi)) return SCOTTY_ERR_HIP;
     XCHK(hipMemcpy(ty.data(), sl.nn + b, S * 4, hipMemcpyDeviceToHost));

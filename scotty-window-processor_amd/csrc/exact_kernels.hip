@@ -469,12 +469,16 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
     }
     const int64_t nlo = l;
     l = nlo; h = hi;
-    while (l < h) {
-      int64_t m = (l + h) >> 1;
-      if (key[m] <= we) l = m + 1; else h = m;
+    // contained slices start no later than the window's end -- except with LazySlice record moves, which can
+    // leave a slice's tLast (cLast) below its tStart (cStart): then only the lower bound narrows
+    if (!a.cfg->records) {
+      while (l < h) {
+        int64_t m = (l + h) >> 1;
+        if (key[m] <= we) l = m + 1; else h = m;
+      }
+      hi = l;
     }
     lo = nlo;
-    hi = l;
   }
   const int need = a.cfg->need, vt = a.cfg->vt;
   const bool recs = a.cfg->records != 0;

@@ -33,7 +33,9 @@ def gpu_slices(op):
     nctx = v[p]; p += 1
     for _ in range(nctx):
         ns = v[p]; p += 1 + 2 * ns
-    p += 6
+    meta = v[p:p + 10]
+    p += 10
+    gpu_slices.meta = meta
     rlo, rhi, nn = v[p:p + S], v[p + S:p + 2 * S], v[p + 2 * S:p + 3 * S]
     p += 3 * S
     rend = v[p]; p += 1
@@ -77,22 +79,47 @@ def main():
                                     ooo_frac=[0.02, 0.1, 0.3][seed % 3], max_delay=int(rng.integers(1, 60)),
                                     seed=seed, value_type=vt, gaps=T._gaps(rng, n, 400, 10, 150))
     print("cfg", cfg, "n", n)
+    from helpers import interval_schedule, same_windows
+    sched = interval_schedule(ts, int(rng.integers(1, 6)), lag=int(rng.integers(0, 60)),
+                              pushes_per_interval=int(rng.integers(1, 3)))
+    chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     gpu, ora = build_ops(cfg, vt)
-    for i in range(n):
-        gpu.processElements(ts[i:i + 1], vals[i:i + 1])
-        ora.processElements(ts[i:i + 1], vals[i:i + 1])
-        if i % 1 == 0:
-            g = [x[:5] + x[6:] for x in gpu_slices(gpu)]
-            o = [x[:5] + x[6:] for x in ora_slices(ora)]
-            if g != o:
-                print("DIVERGED after tuple", i, "ts", ts[i], "prev", ts[max(0, i - 5):i + 1])
-                for k in range(max(len(g), len(o))):
-                    a = g[k] if k < len(g) else None
-                    b = o[k] if k < len(o) else None
-                    if a != b:
-                        print("  slice", k, "\n   gpu", a, "\n   ora", b)
+    for st in sched:
+        if st[0] == "push":
+            lo, hi = st[1], st[2]
+            step = chunk or (hi - lo)
+            for a in range(lo, hi, step):
+                b = min(hi, a + step)
+                gpu.processElements(ts[a:b], vals[a:b])
+                ora.processElements(ts[a:b], vals[a:b])
+                g = [x[:5] + x[6:] for x in gpu_slices(gpu)]
+                o = [x[:5] + x[6:] for x in ora_slices(ora)]
+                if g != o:
+                    print("DIVERGED after push [%d,%d)" % (a, b), "ts", ts[a:b][:80].tolist())
+                    shown = 0
+                    for k in range(max(len(g), len(o))):
+                        x = g[k] if k < len(g) else None
+                        y = o[k] if k < len(o) else None
+                        if x != y and shown < 6:
+                            print("  slice", k, "\n   gpu", x, "\n   ora", y)
+                            shown += 1
+                    return
+        else:
+            before = gpu_slices(gpu)
+            wa = gpu.processWatermark(st[1])
+            wb = ora.processWatermark(st[1])
+            try:
+                same_windows(wa, wb)
+            except AssertionError as e:
+                print("WINDOWS DIVERGED at wm", st[1], str(e)[:300])
+                gpu_slices(gpu)
+                print("meta after wm (maxEventTime nextEdgeTs currentCount unsorted head tail wlo whi lastWm lastCount)",
+                      gpu_slices.meta)
+                for k, x in enumerate(before):
+                    if x[0] >= 1100 and x[0] <= 1200:
+                        print("  slice", k, x[:7], "nrec", len(x[7]), x[7][:8])
                 return
-    print("no divergence in", n, "tuples")
+    print("no divergence")
 
 
 if __name__ == "__main__":
