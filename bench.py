@@ -294,10 +294,16 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
         ts = torch.where(late, torch.clamp(ts - d, min=1), ts).contiguous()
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         return ts, v
+    f = op._l.scotty_debug_grid_stat
+    f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int]
+    glb = []
     for s in range(warm):
         ts, v = gen(s)
+        torch.cuda.synchronize(dev)  # the C-ABI reads the buffers on its own stream
         op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
         op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
+        glb.append(f(op._h, 0))
+    log("c2s: global-atomic tuples after each warm-up step:", glb)
     timed = [gen(s) for s in range(warm, warm + steps)]
     torch.cuda.synchronize(dev)
     rows = 0
@@ -310,9 +316,9 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
         rows += n
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    f = op._l.scotty_debug_grid_stat
-    f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int]
     log("c2s: tuples added with global atomics since creation:", f(op._h, 0))
+    log("c2s: cell index base %d shift %d buckets %d full %d span_end %d; slices %d, grid ahead %d, prev_max %d"
+        % tuple(f(op._h, k) for k in range(1, 9)))
     return {"workload": "C2s: 1000 concurrent sliding windows, sizes randomTumbling(1000,1,20) Random(10), slide "
                         "size/20, SUM_I32+COUNT, 20% out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * elapsed / steps,

@@ -1359,7 +1359,16 @@ int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
   if (!op || op->mode != 1 || !op->d_meta) return -1;
   DevMeta m;
   if (hipMemcpy(&m, op->d_meta, sizeof(DevMeta), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return which == 0 ? (int64_t)m.glb_slow : -1;
+  if (which == 0) return (int64_t)m.glb_slow;
+  if (which >= 1 && which <= 5 && op->d_cixmeta) {  // cell index: base, shift, buckets, full, span end
+    int64_t cm[8];
+    if (hipMemcpy(cm, op->d_cixmeta, sizeof(cm), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return cm[which - 1];
+  }
+  if (which == 6) return m.tail - m.head;
+  if (which == 7) return m.gcount - m.j0;
+  if (which == 8) return m.prev_max;
+  return -1;
 }
 
 // Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds).
