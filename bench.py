@@ -304,10 +304,10 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
         op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
         glb.append(f(op._h, 0))
     log("c2s: global-atomic tuples after each warm-up step:", glb)
-    timed = [gen(s) for s in range(warm, warm + steps)]
+    # wall-clock steps (no instrumentation), then as many steps with HIP events around every launch group (roofline)
+    timed = [gen(s) for s in range(warm, warm + 2 * steps)]
     torch.cuda.synchronize(dev)
     rows = 0
-    op.enableTiming(True)
     t0 = time.perf_counter()
     for i, s in enumerate(range(warm, warm + steps)):
         ts, v = timed[i]
@@ -316,6 +316,12 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
         rows += n
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    op.enableTiming(True)
+    for i, s in enumerate(range(warm + steps, warm + 2 * steps)):
+        ts, v = timed[steps + i]
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
+    torch.cuda.synchronize(dev)
     log("c2s: tuples added with global atomics since creation:", f(op._h, 0))
     log("c2s: cell index base %d shift %d buckets %d full %d span_end %d; slices %d, grid ahead %d, prev_max %d"
         % tuple(f(op._h, k) for k in range(1, 9)))
@@ -458,6 +464,7 @@ def main():
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
     ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5); default all")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
+    ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -489,7 +496,8 @@ def main():
                                 rank=0, world_size=1)
     G = world
     rate = max(1, (B * G) // 1000)  # tuples per ms of event time of the global stream
-    nsteps = args.steps + args.warmup
+    nroof = max(1, args.roof_steps)
+    nsteps = args.steps + args.warmup + nroof
 
     # ---- inputs resident in HBM before the timed region: this rank's arrival chunk of every global batch
     gen = torch.Generator(device=dev)
@@ -521,15 +529,20 @@ def main():
 
     for i in range(args.warmup):
         step(i)
-    op.enableTiming(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.warmup, nsteps):
+    for i in range(args.warmup, args.warmup + args.steps):
         n_windows += step(i)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    # roofline: the same step with HIP events around every launch group (after the wall-clock region, so the
+    # instrumentation does not count in `value`)
+    op.enableTiming(True)
+    for i in range(args.warmup + args.steps, nsteps):
+        step(i)
+    torch.cuda.synchronize(dev)
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -541,7 +554,7 @@ def main():
     res = None
     if rank == 0:
         total = B * args.steps * world
-        roof = device_roofline(op, args.steps, B, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")
+        roof = device_roofline(op, nroof, B, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "ingest_traffic.json")
         if os.path.exists(tfile):

@@ -121,7 +121,8 @@ struct WmArgs {
   const int64_t* wdef;
   int32_t n_defs;
   int64_t last_wm, wm, remove_from;
-  int64_t n_windows;               // the host's count of triggered windows (layout of the packed output)
+  int64_t n_windows;               // row capacity of the packed output (an upper bound of the triggered windows,
+                                   // computed on the host in O(#definitions)); the device writes the true count
   unsigned char* out;              // packed output (device): header, start[n], end[n], values[n_aggs][n], has[n]
   int32_t n_aggs;
   int32_t agg_kind[8];

@@ -638,6 +638,29 @@ int replay_after_overflow(scotty_op* op) {
 // Number of windows WindowManager.assignContextFreeWindows triggers (S/WindowManager.java:104-118): the same loops as
 // TumblingWindow / SlidingWindow / FixedBandWindow.triggerWindows, which the device runs again to emit them (the
 // count only sizes the packed result transfer).  -1: more windows than any result buffer could hold.
+// Upper bound of count_triggers in O(#definitions): triggered tumbling windows start in (last_wm - size, wm - size],
+// sliding windows end in (last_wm, wm + 1] (one per slide), a fixed band emits at most once.  -1 when the values
+// are too large for the bound to be exact arithmetic (the exact loops run instead).
+int64_t bound_triggers(const scotty_op* op, int64_t last_wm, int64_t wm) {
+  const int64_t LIM = (int64_t)1 << 61;
+  if (wm > LIM || wm < -LIM || last_wm > LIM || last_wm < -LIM) return -1;
+  const int64_t span = std::max<int64_t>(0, wm - last_wm + 1);
+  int64_t n = 0;
+  for (const CFWin& w : op->windows) {
+    if (w.kind == SCOTTY_WIN_TUMBLING) {
+      if (w.a > LIM) return -1;
+      n += span / w.a + 2;
+    } else if (w.kind == SCOTTY_WIN_SLIDING) {
+      if (w.a > LIM || w.b > LIM) return -1;
+      n += span / w.b + 2;
+    } else {
+      n += 1;
+    }
+    if (n > ((int64_t)1 << 31)) return -1;
+  }
+  return n;
+}
+
 int64_t count_triggers(const scotty_op* op, int64_t last_wm, int64_t wm) {
   int64_t n = 0;
   const int64_t limit = (int64_t)1 << 31;
@@ -1140,7 +1163,7 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
   const uint64_t dropped_before = op->dropped;
   // WindowManager.processWatermark (S/WindowManager.java:41-80)
   if (op->last_watermark == -1) op->last_watermark = std::max((int64_t)0, jsub(wm, op->max_lateness));
-  int64_t nw = 0;
+  int64_t nw = 0, res_cap = 0;
   const unsigned char* res = nullptr;
   if (!op->started) {
     op->last_watermark = wm;
@@ -1148,9 +1171,10 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     // lastWatermark is raised to the oldest slice's start (S/WindowManager.java:51-55)
     int64_t last_wm = op->last_watermark;
     if (last_wm < op->h_oldest) last_wm = op->h_oldest;
-    nw = count_triggers(op, last_wm, wm);
-    if (nw < 0) return fail(op, SCOTTY_ERR_NOMEM, "watermark triggers more than 2^31 windows");
-    const WmLayout L(nw, (int)op->aggs.size());
+    int64_t cap = bound_triggers(op, last_wm, wm);  // row capacity; the device writes the true count
+    if (cap < 0) cap = count_triggers(op, last_wm, wm);
+    if (cap < 0) return fail(op, SCOTTY_ERR_NOMEM, "watermark triggers more than 2^31 windows");
+    const WmLayout L(cap, (int)op->aggs.size());
     rc = alloc_blocks(op);
     if (!rc) rc = ensure_wm_out(op, L.total);
     if (!rc) rc = upload_wdefs(op);
@@ -1174,7 +1198,7 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     wa.last_wm = last_wm;
     wa.wm = wm;
     wa.remove_from = remove_from;
-    wa.n_windows = nw;
+    wa.n_windows = cap;
     wa.out = op->d_out;
     wa.n_aggs = (int32_t)op->aggs.size();
     for (size_t k = 0; k < op->aggs.size(); k++) wa.agg_kind[k] = op->aggs[k];
@@ -1205,13 +1229,13 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
       op->failed = true;
       return fail(op, SCOTTY_ERR_UNSUPPORTED, "edge-grid horizon overflow");
     }
-    int64_t n_dev;
-    std::memcpy(&n_dev, op->h_out + WM_HDR_N, 8);
-    if (n_dev != nw) {
+    std::memcpy(&nw, op->h_out + WM_HDR_N, 8);
+    if (nw < 0 || nw > cap) {
       op->failed = true;
-      return fail(op, SCOTTY_ERR_STATE, "internal: device triggered " + std::to_string(n_dev) + " windows, host counted " +
-                                            std::to_string(nw));
+      return fail(op, SCOTTY_ERR_STATE, "internal: device triggered " + std::to_string(nw) + " windows, capacity " +
+                                            std::to_string(cap));
     }
+    res_cap = cap;
     res = op->h_out;
     op->last_watermark = wm;
     // bookkeeping at the synchronisation point
@@ -1249,13 +1273,13 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     out->n_windows = (size_t)nw;
     out->n_aggs = (int32_t)op->aggs.size();
     if (nw > 0) {
-      const WmLayout L(nw, (int)op->aggs.size());
+      const WmLayout L(res_cap, (int)op->aggs.size());  // columns are res_cap rows apart
       if ((int64_t)op->r_measure.size() < nw) op->r_measure.assign(nw, SCOTTY_MEASURE_TIME);
       out->start = (const int64_t*)(res + L.start);
       out->end = (const int64_t*)(res + L.end);
       out->measure = op->r_measure.data();
       out->has_value = (const uint8_t*)(res + L.has);
-      for (size_t k = 0; k < op->aggs.size(); k++) out->values[k] = (const int64_t*)(res + L.vals + 8 * nw * k);
+      for (size_t k = 0; k < op->aggs.size(); k++) out->values[k] = (const int64_t*)(res + L.vals + 8 * res_cap * k);
     }
   }
   if (op->dropped > dropped_before) {

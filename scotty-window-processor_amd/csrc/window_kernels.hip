@@ -315,6 +315,7 @@ __global__ __launch_bounds__(256) void wm_windows_kernel(WmArgs a) {
   if (wi >= a.n_windows) return;
   const DevMeta* meta = a.meta;
   if (meta->overflow) return;
+  if (wi >= *(const int64_t*)(a.out + WM_HDR_N)) return;  // rows the triggers actually produced
   const WmLayout L(a.n_windows, a.n_aggs);
   const int64_t head = meta->whead, tail = meta->tail;
   const int64_t ws = ((const int64_t*)(a.out + L.start))[wi];
