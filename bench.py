@@ -390,7 +390,7 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
                               "frac": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9 / HBM_PEAK_GBS}}
 
 
-def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None):
+def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None):
     """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
     connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
     with no collective -- rank r owns the keys k with k mod world == r (what an upstream keyBy delivers), `keys`
@@ -403,6 +403,8 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
     op = pkg.KeyedSlicingWindowOperator(device=dev.index)
     if not lane:
         op.tune("keyed_lane", 0)
+    for k, v in (tune or {}).items():
+        op.tune(k, v)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.setMaxLateness(1)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))

@@ -175,7 +175,9 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
 /* Tuning knobs (not semantics): "slice_capacity" / "session_capacity" per operator of the exact engine
  * (set before the first push), "ingest_mode" (grid-path ingest kernel variant, A/B only), "exact_serial"
  * (non-keyed: single-wavefront replay, A/B only), "keyed_lane" 0 (keyed: wavefront-per-key replay instead of
- * the lane-per-key path for context-free time windows, A/B only), "count_path" 1 (a promise that the stream is in
+ * the lane-per-key path for context-free time windows, A/B only), "keyed_grid" 0 (keyed: every batch sorted by
+ * key and replayed, instead of the sort-free path for in-order batches of context-free time windows, A/B only),
+ * "count_path" 1 (a promise that the stream is in
  * timestamp order: non-keyed operators with count windows only keep no LazySlice record sets and run on the
  * segmented-reduction count path; an out-of-order tuple that would move records then fails loudly -- without the
  * promise they run on the exact engine, which keeps the record sets), "ingest_blocks", "shard_cells" / "shard_cands" (cells /

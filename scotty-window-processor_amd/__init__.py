@@ -242,6 +242,15 @@ class SlicingWindowOperator:
         """Capacity knobs of the exact engine ("slice_capacity", "session_capacity"), before the first push."""
         self._check(self._l.scotty_tune(self._h, key.encode(), int(value)))
 
+    def _debug_stat(self, which):
+        """Internal statistics of the last push (scotty_debug_stat in scotty_engine.cpp); tests and tools only.
+        Keyed: 2 path of the last push (0 replay, 1 sort-free, 2 sort-free + replay of deferred keys), 3 deferred
+        tuples, 4 keys committed on the sort-free path."""
+        f = self._l.scotty_debug_stat
+        f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int]
+        self._flush()
+        return int(f(self._h, which))
+
     # ---- WindowOperator API
     def addWindowAssigner(self, window):
         self._flush()

@@ -16,6 +16,7 @@
 //                               Flink connector builds every per-key operator identically,
 //                               flink-connector/.../KeyedScottyWindowOperator.java:41-49)
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include "device_common.h"
@@ -81,7 +82,8 @@ struct XState {          // 128 B
   int32_t nsess[XMAXCTX];
   uint64_t dropped;                                                 // tuples whose processing threw
   int64_t wlo, whi;                                                 // watermark: slice scan range
-  int32_t pending, pad;                                             // batch deferred: capacity too small
+  int32_t pending;                                                  // batch deferred: capacity too small
+  int32_t pvalid;                                                   // lane path: slice prefixes valid below this
   int64_t rend;                                                     // records: end of the live arena range
 };
 
@@ -97,7 +99,67 @@ struct XSlices {
   int64_t *rlo, *rhi;
   int32_t* nn;
   int64_t *rts, *rv;      // arena [n_ops * rcap]: record ts, value bits
+  // lane path (keyed_lane.hip, keyed_grid.hip): running prefixes of cnt and of the wrapping integer sum over the
+  // op's slice positions 0..i (positions below head keep their values until a compaction), valid for positions
+  // below XState.pvalid -- a window's COUNT / SUM is then two reads instead of a scan of its slices
+  unsigned long long *pc, *ps;
+  // lane path for COUNT / integer SUM functions: the store kept as records instead (XSliceRec, the columns above
+  // unused) -- a key's commit or watermark then touches a few 128-B lines, not one line per column
+  struct XSliceRec* rec;
 };
+
+// One slice of the lane path's record store: every field of one slice in one 128-B line.
+struct XSliceRec {
+  int64_t ts, te, tl, tf, cs, cl;
+  unsigned long long cnt, p[NPART];
+  unsigned long long pc, ps;
+  int32_t ty, pad0;
+  int64_t pad1[3];
+};
+static_assert(sizeof(XSliceRec) == 128 && offsetof(XSliceRec, p) == 56 && offsetof(XSliceRec, pc) == 80 &&
+                  offsetof(XSliceRec, ty) == 96,
+              "one cache line per slice; XRecView offsets");
+
+// Column views of the record store with the syntax of XSlices' columns (q.ts[j], q.p[k][j], q.ts + base), so one
+// kernel body serves both layouts (template parameter V = XSlices or XRecView).
+template <typename T, int OFF>
+struct XRecCol {
+  XSliceRec* r;
+  __host__ __device__ T& operator[](int64_t j) const { return *(T*)((unsigned char*)(r + j) + OFF); }
+  __host__ __device__ XRecCol operator+(int64_t j) const { return XRecCol{r + j}; }
+};
+struct XRecPart {
+  XSliceRec* r;
+  int k;
+  __host__ __device__ unsigned long long& operator[](int64_t j) const { return r[j].p[k]; }
+  __host__ __device__ XRecPart operator+(int64_t j) const { return XRecPart{r + j, k}; }
+};
+struct XRecParts {
+  XSliceRec* r;
+  __host__ __device__ XRecPart operator[](int k) const { return XRecPart{r, k}; }
+};
+struct XRecView {
+  XRecCol<int64_t, 0> ts;
+  XRecCol<int64_t, 8> te;
+  XRecCol<int64_t, 16> tl;
+  XRecCol<int64_t, 24> tf;
+  XRecCol<int64_t, 32> cs;
+  XRecCol<int64_t, 40> cl;
+  XRecCol<unsigned long long, 48> cnt;
+  XRecParts p;
+  XRecCol<unsigned long long, 80> pc;
+  XRecCol<unsigned long long, 88> ps;
+  XRecCol<int32_t, 96> ty;
+  __host__ __device__ XRecView() : XRecView(nullptr) {}
+  __host__ __device__ explicit XRecView(XSliceRec* r)
+      : ts{r}, te{r}, tl{r}, tf{r}, cs{r}, cl{r}, cnt{r}, p{r}, pc{r}, ps{r}, ty{r} {}
+};
+template <typename V>
+__host__ __device__ inline V xview(const XSlices& s);
+template <>
+__host__ __device__ inline XSlices xview<XSlices>(const XSlices& s) { return s; }
+template <>
+__host__ __device__ inline XRecView xview<XRecView>(const XSlices& s) { return XRecView(s.rec); }
 
 struct XSess {
   int64_t *start, *end;
@@ -145,6 +207,8 @@ struct XWmArgs {
   uint32_t* w_key;                      // key of the row's op (keyed)
   const uint32_t* slot_key;            // nullable
   int64_t n_rows;
+  int32_t prefix_reset;                // lane path: recompute every op's slice prefixes from position 0
+  unsigned long long* row_count;       // lane path: rows reserved by the emit kernel itself (n_rows = capacity)
 };
 
 }  // namespace scotty

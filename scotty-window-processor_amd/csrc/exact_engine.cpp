@@ -3,8 +3,10 @@
 // the host sequences launches on the op's stream and owns the window/function configuration, like the
 // reference's WindowManager registration (S/WindowManager.java:121-151).
 #include "exact_engine.h"
+#include "keyed_grid.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstddef>
 #include <cstring>
 
@@ -15,7 +17,7 @@ hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group);
 hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st);
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
-hipError_t launch_lane_wm_emit(const XWmArgs& a, hipStream_t st);
+hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st);
 hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
 hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
 hipError_t launch_key_insert(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
@@ -32,6 +34,21 @@ hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, cons
                                void** result, hipStream_t st);
 hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end, hipStream_t st);
 int64_t sort_tile();
+hipError_t launch_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t st);
+hipError_t launch_kg_build(const uint32_t* slot_key, int64_t n_ops, unsigned long long* tab, uint64_t mask,
+                           hipStream_t st);
+hipError_t launch_kg_partition(const KgArgs& a, int vt, hipStream_t st);
+hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st);
+hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hipStream_t st);
+hipError_t launch_kg_mark_deferred(const KgArgs& a, hipStream_t st);
+int kg_tile(int vt, int64_t nbk, int variant);
+int kg_cells(bool mm);
+hipError_t launch_kg_bounds(const int64_t* ts, int64_t n, const XCfg* cfg, int kmax, int64_t* gpts, int64_t* out,
+                            hipStream_t st);
+hipError_t launch_kg_dcount(const uint8_t* mark, int64_t n, int32_t* blk, hipStream_t st);
+hipError_t launch_kg_dgather(const uint32_t* key, const int64_t* ts, const void* val, uint8_t* mark, int64_t n,
+                             const int32_t* blk_off, uint32_t* okey, int64_t* ots, void* oval, int vt,
+                             hipStream_t st);
 }  // namespace scotty
 
 // batch-parallel path (exact_batch.hip): the argument block mirrors XBArgs there
@@ -125,6 +142,7 @@ void XEngine::release() {
   dfree(d_cfg); dfree(d_cf_kind); dfree(d_cf_meas); dfree(d_cf_a); dfree(d_cf_b);
   dfree(d_st);
   dfree(sl.ts); dfree(sl.te); dfree(sl.tl); dfree(sl.tf); dfree(sl.cs); dfree(sl.cl); dfree(sl.ty); dfree(sl.cnt);
+  dfree(sl.pc); dfree(sl.ps); dfree(sl.rec);
   for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
   dfree(sl.rlo); dfree(sl.rhi); dfree(sl.nn); dfree(sl.rts); dfree(sl.rv);
   dfree(ss.start); dfree(ss.end);
@@ -138,6 +156,10 @@ void XEngine::release() {
   dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
   dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
   dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
+  dfree(d_kgtab); dfree(d_kghist); dfree(d_kgscan); dfree(d_kgblk); dfree(d_kgrec); dfree(d_kgmark); dfree(d_kgctl);
+  dfree(d_kgkey); dfree(d_kgts); dfree(d_kgval); dfree(d_kggpts); dfree(d_kgpos); dfree(d_kgpart); dfree(d_kgdflag);
+  if (h_kgctl) (void)hipHostFree(h_kgctl);
+  h_kgctl = nullptr;
   d_cfg = nullptr;
   d_st = nullptr;
   h_misc = nullptr;
@@ -161,6 +183,7 @@ int XEngine::init(int dev, hipStream_t st, int value_type, bool is_keyed, std::s
 // WindowManager.addWindowAssigner / addAggregation / setMaxLateness (S/WindowManager.java:121-202)
 int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>& aggs, int64_t max_lateness,
                        const std::vector<int>& agg_inv) {
+  h_wins = wins;
   XCfg c{};
   std::vector<int32_t> kind, meas;
   std::vector<int64_t> a, b;
@@ -299,10 +322,17 @@ int XEngine::grow_ops(int64_t need) {
     *p = np;
     return hipSuccess;
   };
+  if (ops_cap == 0)  // the store's layout is fixed with the first allocation
+    aos = keyed && lane_mode() && vt != VT_F64 && !(cfg.need & (NEED_MIN | NEED_MAX));
   XCHK(grow(&d_st, 1));
-  XCHK(grow(&sl.ts, sc)); XCHK(grow(&sl.te, sc)); XCHK(grow(&sl.tl, sc)); XCHK(grow(&sl.tf, sc));
-  XCHK(grow(&sl.cs, sc)); XCHK(grow(&sl.cl, sc)); XCHK(grow(&sl.ty, sc)); XCHK(grow(&sl.cnt, sc));
-  for (int k = 0; k < NPART; k++) XCHK(grow(&sl.p[k], sc));
+  if (aos) {
+    XCHK(grow(&sl.rec, sc));
+  } else {
+    XCHK(grow(&sl.ts, sc)); XCHK(grow(&sl.te, sc)); XCHK(grow(&sl.tl, sc)); XCHK(grow(&sl.tf, sc));
+    XCHK(grow(&sl.cs, sc)); XCHK(grow(&sl.cl, sc)); XCHK(grow(&sl.ty, sc)); XCHK(grow(&sl.cnt, sc));
+    for (int k = 0; k < NPART; k++) XCHK(grow(&sl.p[k], sc));
+    XCHK(grow(&sl.pc, sc)); XCHK(grow(&sl.ps, sc));
+  }
   if (ctx_alloc > 0) {
     XCHK(grow(&ss.start, (int64_t)ctx_alloc * sesscap));
     XCHK(grow(&ss.end, (int64_t)ctx_alloc * sesscap));
@@ -368,12 +398,14 @@ int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx, int
     *p = np;
     return hipSuccess;
   };
+  if (nsc != sc && sl.rec) XCHK(relayout(&sl.rec, sc, nsc, rows, n_ops));
   if (nsc != sc && sl.ts) {
     XCHK(relayout(&sl.ts, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.te, sc, nsc, rows, n_ops));
     XCHK(relayout(&sl.tl, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.tf, sc, nsc, rows, n_ops));
     XCHK(relayout(&sl.cs, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.cl, sc, nsc, rows, n_ops));
     XCHK(relayout(&sl.ty, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.cnt, sc, nsc, rows, n_ops));
     for (int k = 0; k < NPART; k++) XCHK(relayout(&sl.p[k], sc, nsc, rows, n_ops));
+    XCHK(relayout(&sl.pc, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.ps, sc, nsc, rows, n_ops));
     if (records && sl.rlo) {
       XCHK(relayout(&sl.rlo, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.rhi, sc, nsc, rows, n_ops));
       XCHK(relayout(&sl.nn, sc, nsc, rows, n_ops));
@@ -646,7 +678,195 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
   return SCOTTY_OK;
 }
 
+// Sort-free path (keyed_grid.hip) for one batch.  *deferred: -1 the batch did not qualify (nothing changed),
+// else the number of tuples left marked for the replay path (keys new or not eligible in this batch).
+int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n, int64_t* deferred,
+                     int32_t* flag_out) {
+  *deferred = -1;
+  *flag_out = -1;
+  // compact key table over the known keys (<= 50 % load), rebuilt when keys were added
+  uint64_t want = 2048;
+  while ((int64_t)want < 2 * n_ops) want <<= 1;
+  if ((want >> KG_RB) > (uint64_t)KG_NB_MAX) return SCOTTY_OK;  // > 2^21 keys: replay path
+  if (want != kgcap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_kgtab);
+    XCHK(dalloc(&d_kgtab, want));
+    kgcap = want;
+    kg_built = -1;
+  }
+  if (kg_built != n_ops) {
+    XCHK(hipMemsetAsync(d_kgtab, 0, kgcap * 8, stream));
+    XCHK(launch_kg_build(d_slot_key, n_ops, d_kgtab, kgcap - 1, stream));
+    kg_built = n_ops;
+  }
+  const int vb = vt == VT_I32 ? 4 : 8;
+  const int rec = vt == VT_I32 ? 16 : 24;
+  const int64_t nbk = (int64_t)(kgcap >> KG_RB);
+  const int tile = kg_tile(vt, nbk, kg_variant);
+  const int64_t ntiles = (n + tile - 1) / tile;
+  const bool mm = (cfg.need & (NEED_MIN | NEED_MAX)) != 0;
+  const int cm = kg_cells(mm);
+  if (n_ops * cm > kg_pcap) {  // per-(key, cell) partials and deferral flags, zero between batches
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_kgpart); dfree(d_kgdflag);
+    kg_pcap = std::max<int64_t>(ops_cap * cm, 4096);
+    XCHK(dalloc(&d_kgpart, kg_pcap));
+    XCHK(dalloc(&d_kgdflag, kg_pcap));
+    XCHK(hipMemsetAsync(d_kgpart, 0, kg_pcap * sizeof(KPart), stream));
+    XCHK(hipMemsetAsync(d_kgdflag, 0, kg_pcap, stream));
+  }
+  if (n > kg_ncap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_kgrec); dfree(d_kgmark); dfree(d_kgblk);
+    kg_ncap = std::max<int64_t>(n, 1 << 16);
+    XCHK(dalloc((unsigned char**)&d_kgrec, (size_t)kg_ncap * rec));
+    XCHK(dalloc(&d_kgmark, kg_ncap));
+    XCHK(hipMemsetAsync(d_kgmark, 0, kg_ncap, stream));  // marks are reset by the gather that consumes them
+    XCHK(dalloc(&d_kgblk, kg_ncap / 1024 + 64));
+  }
+  if (nbk * ntiles > kg_hcap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_kghist); dfree(d_kgscan);
+    kg_hcap = std::max<int64_t>(nbk * ntiles, 1 << 16);
+    XCHK(dalloc(&d_kghist, kg_hcap));
+    XCHK(dalloc(&d_kgscan, kg_hcap / 512 + 64));
+  }
+  if (!d_kgctl) {
+    XCHK(dalloc((unsigned char**)&d_kgctl, sizeof(KgCtl)));
+    XCHK(hipHostMalloc(&h_kgctl, sizeof(KgCtl), hipHostMallocDefault));
+  }
+  KgArgs a{};
+  a.key = d_key;
+  a.ts = d_ts;
+  a.val = d_val;
+  a.n = n;
+  a.ktab = d_kgtab;
+  a.kmask = kgcap - 1;
+  a.nbk = (int32_t)nbk;
+  a.ntiles = (int32_t)ntiles;
+  a.cmax = cm;
+  a.tile = tile;
+  a.variant = kg_variant;
+  a.part = d_kgpart;
+  a.dflag = d_kgdflag;
+  a.hist = d_kghist;
+  a.rec = d_kgrec;
+  a.mark = d_kgmark;
+  a.ctl = (KgCtl*)d_kgctl;
+  a.cfg = d_cfg;
+  a.st = d_st;
+  a.sl = sl;
+  XCHK(launch_kg_partition(a, vt, stream));
+  XCHK(launch_scan_i32(d_kghist, d_kghist, nbk * ntiles, d_kgscan, stream));
+  XCHK(launch_kg_scatter(a, vt, stream));
+  XCHK(launch_kg_bucket(a, vt, mm, n_ops, stream));
+  KgCtl* hc = (KgCtl*)h_kgctl;
+  XCHK(hipMemcpyAsync(hc, d_kgctl, sizeof(KgCtl), hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  (void)vb;
+  *flag_out = hc->flag;
+  if (hc->flag) return SCOTTY_OK;
+  *deferred = (int64_t)hc->deferred;
+  for (int i = 0; i < KG_SHARDS; i++) last_kg_keys += (int64_t)hc->keys_shard[i];
+  if (hc->defer_keys > 0) {  // known keys the commit deferred: mark their tuples, clear the flags
+    XCHK(launch_kg_mark_deferred(a, stream));
+    XCHK(hipMemsetAsync(d_kgdflag, 0, n_ops, stream));
+  }
+  return SCOTTY_OK;
+}
+
 int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n) {
+  if (n <= 0) return SCOTTY_OK;
+  last_kg = 0;
+  last_kg_deferred = 0;
+  last_kg_keys = 0;
+  kg_used = kg_replayed = 0;
+  int rc;
+  if (lane_mode() && !kg_off && n < ((int64_t)1 << 31)) rc = push_keyed_kg(d_key, d_ts, d_val, n, true);
+  else rc = push_keyed_replay(d_key, d_ts, d_val, n);
+  last_kg = kg_used ? (kg_replayed ? 2 : 1) : 0;
+  return rc;
+}
+
+// One in-order range through the sort-free path: deferred keys' tuples replayed after it; a range over more grid
+// cells than a bucket pass keeps cut into chunks of consecutive cells (split), each run the same way in order
+// (a chunk's replay precedes the next chunk, so a key deferred in one chunk is current in the next); a range the
+// path cannot take replayed whole.  Every tuple is processed once, in an order that keeps each key's arrival order.
+int XEngine::push_keyed_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n, bool split) {
+  if (n <= 0) return SCOTTY_OK;
+  if (n_ops == 0) {  // no key known yet: every key is new
+    kg_replayed = 1;
+    return push_keyed_replay(d_key, d_ts, d_val, n);
+  }
+  int64_t deferred = -1;
+  int32_t flag = 0;
+  int rc = push_kg(d_key, d_ts, d_val, n, &deferred, &flag);
+  if (rc) return rc;
+  if (flag == 0) {
+    kg_used = 1;
+    if (deferred == 0) return SCOTTY_OK;
+    // gather the deferred keys' tuples in arrival order, replay them
+    kg_replayed = 1;
+    last_kg_deferred += deferred;
+    const int64_t nblk = (n + 1023) / 1024;
+    XCHK(launch_kg_dcount(d_kgmark, n, d_kgblk, stream));
+    XCHK(launch_scan_i32(d_kgblk, d_kgblk, nblk, d_kgscan, stream));
+    if (deferred > kg_gcap) {
+      XCHK(hipStreamSynchronize(stream));
+      dfree(d_kgkey); dfree(d_kgts); dfree(d_kgval);
+      kg_gcap = std::max<int64_t>(deferred, 1 << 16);
+      XCHK(dalloc(&d_kgkey, kg_gcap));
+      XCHK(dalloc(&d_kgts, kg_gcap));
+      XCHK(dalloc((unsigned char**)&d_kgval, (size_t)kg_gcap * (vt == VT_I32 ? 4 : 8)));
+    }
+    XCHK(launch_kg_dgather(d_key, d_ts, d_val, d_kgmark, n, d_kgblk, d_kgkey, d_kgts, d_kgval, vt, stream));
+    return push_keyed_replay(d_kgkey, d_kgts, d_kgval, deferred);
+  }
+  const int cm = kg_cells((cfg.need & (NEED_MIN | NEED_MAX)) != 0);
+  if (split && flag == KG_CELLS) {
+    constexpr int KMAX = 4096;
+    if (!d_kggpts) {
+      XCHK(dalloc(&d_kggpts, KMAX));
+      XCHK(dalloc(&d_kgpos, KMAX + 1));
+    }
+    XCHK(launch_kg_bounds(d_ts, n, d_cfg, KMAX, d_kggpts, d_kgpos, stream));
+    h_kgpos.resize(KMAX + 1);
+    XCHK(hipMemcpyAsync(h_kgpos.data(), d_kgpos, 8, hipMemcpyDeviceToHost, stream));
+    XCHK(hipStreamSynchronize(stream));
+    const int64_t k = h_kgpos[0];
+    const bool more = k == KMAX;  // the walk stopped at KMAX grid points: whole chunks now, the rest after
+    const int64_t chunks = k < 0 ? 0 : (more ? k / cm : k / cm + 1);
+    if (k > 0 && n / chunks >= kg_min_chunk) {
+      XCHK(hipMemcpy(h_kgpos.data() + 1, d_kgpos + 1, k * 8, hipMemcpyDeviceToHost));
+      bool mono = true;
+      for (int64_t j = 1; j < k; j++) mono = mono && h_kgpos[1 + j] >= h_kgpos[j];
+      if (mono) {
+        // chunk c: cells [c*cm, (c+1)*cm), i.e. tuples from the first >= g_{c*cm} (cell 0: from 0)
+        const int vb = vt == VT_I32 ? 4 : 8;
+        int64_t p0 = 0;
+        for (int64_t c = 0; c < chunks; c++) {
+          const int64_t j = (c + 1) * cm;  // grid point g_j starts the next chunk (1-based)
+          const int64_t p1 = j <= k ? h_kgpos[j] : n;
+          if (p1 > p0) {
+            rc = push_keyed_kg(d_key + p0, d_ts + p0, (const unsigned char*)d_val + p0 * vb, p1 - p0, false);
+            if (rc) return rc;
+          }
+          p0 = p1;
+        }
+        if (p0 < n) {  // the rest of a walk cut at KMAX grid points, in order
+          rc = push_keyed_kg(d_key + p0, d_ts + p0, (const unsigned char*)d_val + p0 * vb, n - p0, true);
+          if (rc) return rc;
+        }
+        return SCOTTY_OK;
+      }
+    }
+  }
+  kg_replayed = 1;
+  return push_keyed_replay(d_key, d_ts, d_val, n);
+}
+
+int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n) {
   if (n <= 0) return SCOTTY_OK;
   int rc = ensure_batch(n);
   if (rc) return rc;
@@ -715,6 +935,7 @@ int XEngine::push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* 
     a.retry = attempt > 0;
     a.sl = sl;
     a.ss = ss;
+    if (!lane_mode()) prefix_stale = true;  // the wavefront replay does not track the lane path's slice prefixes
     XCHK(lane_mode() ? launch_lane_replay(a, cfg, stream) : launch_replay(a, vt, stream));
     XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
@@ -775,6 +996,41 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.dropped_total = (unsigned long long*)(d_misc + 1);
   a.op_err = (int32_t*)(d_misc + 2);
   a.slot_key = keyed ? d_slot_key : nullptr;
+  // lane path: COUNT / integer SUM windows straight from the slice prefixes in the emit kernel; MIN / MAX / f64
+  // sums scan the slices (wm_agg)
+  const bool prefix_agg = lane_mode() && !(cfg.need & (NEED_MIN | NEED_MAX)) &&
+                          !((cfg.need & NEED_SUM) && vt == VT_F64);
+  a.prefix_reset = prefix_stale ? 1 : 0;
+  const int64_t bound = prefix_agg ? lane_row_bound(wm) : -1;
+  if (bound >= 0) {  // one kernel: count, reserve, emit, aggregate, GC -- rows sized from the bound
+    int rc = ensure_rows(std::max<int64_t>(bound, 1));
+    if (rc) return rc;
+    XCHK(hipMemsetAsync(d_misc, 0, 4 * 8, stream));
+    a.row_count = (unsigned long long*)(d_misc + 3);
+    a.n_rows = rcap;
+    a.w_start = d_w_start;
+    a.w_end = d_w_end;
+    a.w_meas = d_w_meas;
+    a.w_op = d_w_op;
+    a.has_value = d_has;
+    for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
+    a.w_key = d_w_key;
+    XCHK(launch_lane_wm_emit(a, true, stream));
+    XCHK(hipMemcpyAsync(h_misc, d_misc, 4 * 8, hipMemcpyDeviceToHost, stream));
+    XCHK(hipStreamSynchronize(stream));
+    prefix_stale = false;
+    have_wm = true;
+    last_wm = wm;
+    r.dropped = (uint64_t)h_misc[1];
+    rc = op_error((int32_t)h_misc[2]);
+    if (rc) return rc;
+    if ((int32_t)h_misc[0] & 4) {
+      err = "internal: watermark rows exceeded the host bound";
+      failed = true;
+      return SCOTTY_ERR_STATE;
+    }
+    return finish_rows((int64_t)h_misc[3], r, to_host, false);
+  }
   XCHK(hipMemsetAsync(d_misc, 0, 3 * 8, stream));
   XCHK(lane_mode() ? launch_lane_wm_count(a, stream) : launch_wm_count(a, stream));
   XCHK(launch_scan_i64(d_wcount, d_woff, n_ops, d_scan64, stream));
@@ -783,7 +1039,38 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   XCHK(hipMemcpyAsync(h_misc + 4, d_wcount + n_ops - 1, 8, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
   r.dropped = (uint64_t)h_misc[1];
-  const int32_t op_err = (int32_t)h_misc[2];
+  int rc = op_error((int32_t)h_misc[2]);
+  if (rc) return rc;
+  if ((int32_t)h_misc[0] & 1) {
+    err = "processWatermark threw IndexOutOfBoundsException (empty session context / count trigger before the "
+          "oldest slice, S/WindowManager.java:98-118)";
+    return SCOTTY_ERR_INDEX;
+  }
+  const int64_t rows = h_misc[3] + h_misc[4];
+  rc = ensure_rows(rows);
+  if (rc) return rc;
+  a.w_start = d_w_start;
+  a.w_end = d_w_end;
+  a.w_meas = d_w_meas;
+  a.w_op = d_w_op;
+  a.has_value = d_has;
+  for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
+  a.w_key = d_w_key;
+  a.n_rows = rows;
+  if (lane_mode()) {
+    XCHK(launch_lane_wm_emit(a, prefix_agg, stream));
+    if (prefix_agg) prefix_stale = false;
+  } else {
+    XCHK(launch_wm_emit(a, stream));
+  }
+  if (!prefix_agg) XCHK(launch_wm_agg(a, stream, keyed ? 16 : 64));
+  have_wm = true;
+  last_wm = wm;
+  return finish_rows(rows, r, to_host, true);
+}
+
+// Fatal per-operator errors recorded by the kernels (OR of 1 << XState.err over the ops).
+int XEngine::op_error(int32_t op_err) {
   if (op_err & ~((1 << XERR_INDEX) | (1 << XERR_NPE) | (1 << XERR_NOELEM))) {
     failed = true;
     if (op_err & (1 << XERR_UNSUPPORTED))
@@ -803,24 +1090,29 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     return (op_err & (1 << XERR_HANG)) || (op_err & (1 << XERR_UNSUPPORTED)) ? SCOTTY_ERR_UNSUPPORTED
                                                                                : SCOTTY_ERR_NOMEM;
   }
-  if ((int32_t)h_misc[0] & 1) {
-    err = "processWatermark threw IndexOutOfBoundsException (empty session context / count trigger before the "
-          "oldest slice, S/WindowManager.java:98-118)";
-    return SCOTTY_ERR_INDEX;
+  return SCOTTY_OK;
+}
+
+// Upper bound of the rows one lane-path watermark can emit (LaneWindows: every key's last watermark is the
+// engine's previous one, or -- keys created since -- max(0, wm - maxLateness), WindowManager.java:43-44; a
+// window is emitted once its end passes it).  -1: no useful bound, use the count pass.
+int64_t XEngine::lane_row_bound(int64_t wm) const {
+  const double lo = std::max(0.0, (double)wm - (double)cfg.max_lateness);
+  const double l0 = have_wm ? std::min(lo, (double)last_wm) : lo;
+  const double span = std::max(0.0, (double)wm + 1.0 - l0);
+  double per = 0;
+  for (const XWinDef& w : h_wins) {
+    if (w.kind == SCOTTY_WIN_TUMBLING && w.a > 0) per += std::floor(span / (double)w.a) + 2;
+    else if (w.kind == SCOTTY_WIN_SLIDING && w.b > 0) per += std::floor(span / (double)w.b) + 2;
+    else if (w.kind == SCOTTY_WIN_FIXED_BAND) per += 1;
+    else return -1;
   }
-  const int64_t rows = h_misc[3] + h_misc[4];
-  int rc = ensure_rows(rows);
-  if (rc) return rc;
-  a.w_start = d_w_start;
-  a.w_end = d_w_end;
-  a.w_meas = d_w_meas;
-  a.w_op = d_w_op;
-  a.has_value = d_has;
-  for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
-  a.w_key = d_w_key;
-  a.n_rows = rows;
-  XCHK(lane_mode() ? launch_lane_wm_emit(a, stream) : launch_wm_emit(a, stream));
-  XCHK(launch_wm_agg(a, stream, keyed ? 16 : 64));
+  const double rows = per * (double)n_ops;
+  return rows > 2e9 ? -1 : (int64_t)rows;
+}
+
+// check: a kernel may have flagged LazyAggregateStore.aggregate's getSlice(-1) (err_flag bit 1)
+int XEngine::finish_rows(int64_t rows, XResult& r, bool to_host, bool check) {
   r.n = rows;
   r.d_start = d_w_start;
   r.d_end = d_w_end;
@@ -838,6 +1130,10 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     XCHK(hipMemcpyAsync(r.key.data(), d_w_key, rows * 4, hipMemcpyDeviceToHost, stream));
     for (int k = 0; k < cfg.n_aggs; k++)
       XCHK(hipMemcpyAsync(r.vals[k].data(), d_vals[k], rows * 8, hipMemcpyDeviceToHost, stream));
+  }
+  if (!check) {
+    if (to_host && rows > 0) XCHK(hipStreamSynchronize(stream));
+    return SCOTTY_OK;
   }
   XCHK(hipMemcpyAsync(h_misc, d_misc, 8, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
@@ -880,7 +1176,16 @@ int XEngine::debug_dump(int64_t op, std::vector<int64_t>& out) {
     out.insert(out.end(), tmp.begin(), tmp.begin() + S);
     return SCOTTY_OK;
   };
-  if (S > 0) {
+  if (S > 0 && sl.rec) {  // record store: the same columns, unpacked
+    std::vector<XSliceRec> rr(S);
+    XCHK(hipMemcpy(rr.data(), sl.rec + b, S * sizeof(XSliceRec), hipMemcpyDeviceToHost));
+    for (auto f : {&XSliceRec::ts, &XSliceRec::te, &XSliceRec::tl})
+      for (int64_t i = 0; i < S; i++) out.push_back(rr[i].*f);
+    for (int64_t i = 0; i < S; i++) out.push_back((int64_t)rr[i].cnt);
+    for (auto f : {&XSliceRec::cs, &XSliceRec::cl})
+      for (int64_t i = 0; i < S; i++) out.push_back(rr[i].*f);
+    for (int64_t i = 0; i < S; i++) out.push_back(rr[i].ty);
+  } else if (S > 0) {
     if (col(sl.ts) || col(sl.te) || col(sl.tl) || col(sl.cnt) || col(sl.cs) || col(sl.cl)) return SCOTTY_ERR_HIP;
     XCHK(hipMemcpy(ty.data(), sl.ty + b, S * 4, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < S; i++) out.push_back(ty[i]);

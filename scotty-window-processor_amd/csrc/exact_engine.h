@@ -7,6 +7,7 @@
 
 #include "../../include/scotty_mi355x.h"
 #include "exact_common.h"
+#include "keyed_grid.h"
 
 namespace scotty {
 
@@ -56,12 +57,24 @@ class XEngine {
   int32_t sc_override = 0, sess_override = 0;
   bool serial = false;  // non-keyed: single-wavefront replay instead of the batch-parallel path (A/B)
   bool lane_off = false;  // keyed: force the wavefront-per-key replay even where the lane path applies (A/B)
+  bool kg_off = false;    // keyed: no sort-free path (keyed_grid.hip), every batch sorted + replayed (A/B)
+  // a batch over more grid cells than one bucket pass keeps is cut into chunks of consecutive cells when they
+  // average at least this many tuples (below, the sort + replay path is cheaper than a pass per chunk)
+  int64_t kg_min_chunk = 1 << 19;
+  int32_t kg_variant = 1;   // sort-free path kernel variant (A/B)
+  // last keyed push: 0 replay path only, 1 sort-free path only, 2 both (deferred keys / chunks replayed)
+  int32_t last_kg = 0;
+  int64_t last_kg_deferred = 0, last_kg_keys = 0;
   bool lane_mode() const {  // keyed_lane.hip: context-free time windows on Eager slices only
     return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && !records && cfg.n_cf > 0;
   }
   // non-keyed: the single-wavefront replay (LazySlice record sets live only there)
   bool use_serial() const { return serial || records; }
   bool records = false;   // LazySlice record sets kept (XCfg.records)
+  // lane path with COUNT / integer SUM functions only: the slice store is kept as records (XSlices.rec), fixed with
+  // the first allocation -- the lane path cannot be switched off afterwards
+  bool aos = false;
+  bool layout_fixed() const { return aos; }
 
  private:
   void release();
@@ -71,6 +84,18 @@ class XEngine {
   int ensure_batch(int64_t n);
   int ensure_table(int64_t keys, bool drop_new = false);
   int ensure_rows(int64_t rows);
+  int op_error(int32_t op_err);
+  int64_t lane_row_bound(int64_t wm) const;
+  int finish_rows(int64_t rows, XResult& r, bool to_host, bool check);
+  int push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n);
+  int push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n, int64_t* deferred,
+              int32_t* flag);
+  int push_keyed_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n, bool split);
+  int kg_used = 0, kg_replayed = 0;
+  bool prefix_stale = false;
+  std::vector<XWinDef> h_wins;
+  bool have_wm = false;   // a watermark was processed (last_wm: its value)
+  int64_t last_wm = 0;  // ops were replayed without prefix tracking: the next lane watermark rebuilds them
   int check_ready();
   XBatchArgs batch_args() const;
 
@@ -97,6 +122,24 @@ class XEngine {
   int32_t* d_full = nullptr;
   uint32_t* d_slot_key = nullptr;
   std::vector<uint32_t> h_slot_key;
+  // sort-free keyed path (keyed_grid.hip): compact key table, partition scratch, deferred-tuple gather
+  unsigned long long* d_kgtab = nullptr;
+  uint64_t kgcap = 0;
+  int64_t kg_built = -1;
+  int64_t kg_ncap = 0, kg_hcap = 0, kg_gcap = 0;
+  int32_t *d_kghist = nullptr, *d_kgscan = nullptr, *d_kgblk = nullptr;
+  void* d_kgrec = nullptr;
+  uint8_t* d_kgmark = nullptr;
+  void* d_kgctl = nullptr;
+  void* h_kgctl = nullptr;   // pinned copy of the control block
+  uint32_t* d_kgkey = nullptr;
+  int64_t* d_kgts = nullptr;
+  void* d_kgval = nullptr;
+  int64_t *d_kggpts = nullptr, *d_kgpos = nullptr;
+  KPart* d_kgpart = nullptr;
+  uint8_t* d_kgdflag = nullptr;
+  int64_t kg_pcap = 0;
+  std::vector<int64_t> h_kgpos;
   // batch scratch
   int64_t bcap = 0;
   uint32_t* d_slot = nullptr;

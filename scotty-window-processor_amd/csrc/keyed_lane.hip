@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "exact_common.h"
+#include "exact_op.h"
 
 namespace scotty {
 namespace ln {
@@ -41,15 +42,16 @@ __device__ __forceinline__ int64_t assign_next(const XCfg* c, int w, int64_t t) 
 // key's base offset, the StreamSlicer / store scalars it changes, and the current slice's aggregation fields
 // (VGPR budget: the kernel is latency bound, occupancy is what hides the per-key record and slice loads).
 // MM: the operator has a MIN or MAX aggregation (partials p[1] / p[2] live).
-template <int VT, bool MM>
+template <int VT, bool MM, class V>
 struct Lane {
   const XCfg* c;
-  XSlices sl;
+  V sl;
   int64_t b;  // op * sc
   // XState fields the per-tuple path changes
   int64_t maxEventTime, nextEdgeTs, currentCount;
   int32_t head, tail, started;
   uint32_t dropped;
+  int32_t minmod;  // lowest slice position whose cnt / sum changed (slice prefixes above it go stale)
   // register copy of the current (last) slice
   int32_t ci;
   int64_t c_tl, c_tf, c_cl;
@@ -136,6 +138,7 @@ struct Lane {
   // ... on an older slice (out-of-order tuple), in HBM
   __device__ void add_mem(int i, int64_t t, int64_t vb) {
     const int64_t j = b + i;
+    minmod = min(minmod, i);
     sl.tl[j] = max(sl.tl[j], t);
     sl.tf[j] = min(sl.tf[j], t);
     sl.cl[j] = jadd(sl.cl[j], 1);
@@ -189,7 +192,7 @@ struct Lane {
   }
 };
 
-template <int VT, bool MM>
+template <int VT, bool MM, class V>
 __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
   const XCfg* cfg = a.cfg;
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -206,9 +209,9 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
     if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
     else vb = *(const int64_t*)(r + 8);
   };
-  Lane<VT, MM> L;
+  Lane<VT, MM, V> L{};
   L.c = cfg;
-  L.sl = a.sl;
+  L.sl = xview<V>(a.sl);
   L.b = op * (int64_t)cfg->sc;
   L.maxEventTime = sp->maxEventTime;
   L.nextEdgeTs = sp->nextEdgeTs;
@@ -218,6 +221,7 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
   L.started = sp->started;
   L.dropped = 0;
   L.hang = false;
+  int32_t pvalid = sp->pvalid;
   // capacity pre-check (same bound as the wavefront replay): defer the key, the host grows and retries
   // the lane's run is read 4 records per round so 4 scattered loads are in flight at once (the kernel waits on
   // memory, not ALU: SQ_WAIT_ANY is ~80% of its wave cycles)
@@ -256,7 +260,7 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
   if ((double)L.tail + bound > (double)cfg->sc && L.head > 0) {  // compact [head, tail) to the front
     const int n = L.tail - L.head;
     const int64_t h = L.b + L.head, d = L.b;
-    const XSlices& q = a.sl;
+    const V q = xview<V>(a.sl);
     for (int i = 0; i < n; i++) {
       q.ts[d + i] = q.ts[h + i]; q.te[d + i] = q.te[h + i]; q.tl[d + i] = q.tl[h + i]; q.tf[d + i] = q.tf[h + i];
       q.cs[d + i] = q.cs[h + i]; q.cl[d + i] = q.cl[h + i]; q.ty[d + i] = q.ty[h + i];
@@ -265,7 +269,9 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
     }
     L.head = 0;
     L.tail = n;
+    pvalid = 0;
   }
+  L.minmod = max(L.tail - 1, 0);  // the current slice takes the in-order tuples, appended slices follow it
   L.load_cur();
   // replay with the next record's load issued before the current record is processed
   int64_t t_nx, v_nx;
@@ -284,6 +290,7 @@ __global__ __launch_bounds__(256) void lane_replay_kernel(XBatchArgs a) {
   sp->started = L.started;
   if (L.dropped) sp->dropped += L.dropped;
   if (L.hang) sp->err = XERR_HANG;
+  sp->pvalid = min(pvalid, L.minmod);
 }
 
 // ---------------------------------------------------------------- watermark, one lane per key
@@ -322,6 +329,7 @@ __device__ int64_t lane_triggers(const XCfg* c, int64_t last, int64_t wm, int64_
   return k;
 }
 
+template <class V>
 __global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (op >= a.n_ops) return;
@@ -331,7 +339,7 @@ __global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
   int64_t k = 0;
   if (!s.err && s.tail > s.head) {
     int64_t last = s.lastWatermark == -1 ? max((int64_t)0, jsub(a.wm, a.cfg->max_lateness)) : s.lastWatermark;
-    const int64_t oldest = a.sl.ts[op * (int64_t)a.cfg->sc + s.head];
+    const int64_t oldest = xview<V>(a.sl).ts[op * (int64_t)a.cfg->sc + s.head];
     if (last < oldest) last = oldest;
     int64_t mn = JMAX, mx = 0;
     k = lane_triggers<false>(a.cfg, last, a.wm, nullptr, nullptr, nullptr, nullptr, 0, 0, mn, mx);
@@ -339,61 +347,199 @@ __global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
   a.wcount[op] = k;
 }
 
-__global__ __launch_bounds__(256) void lane_wm_emit_kernel(XWmArgs a) {
-  const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (op >= a.n_ops) return;
-  XState s = a.st[op];
-  if (s.err) return;
-  const XCfg* c = a.cfg;
-  if (s.lastWatermark == -1) s.lastWatermark = max((int64_t)0, jsub(a.wm, c->max_lateness));  // :43-44
-  if (s.tail <= s.head) {
-    s.lastWatermark = a.wm;
-    a.st[op] = s;
-    return;
+// first position in [lo, hi) where the monotone predicate p turns true (hi if never), probing from lo upward
+// (galloping: a target near lo costs a few loads, not a full bisection's chain of dependent ones)
+template <typename P>
+__device__ __forceinline__ int first_true_up(int lo, int hi, P p) {
+  if (lo >= hi || p(lo)) return lo;
+  int a = lo, step = 1;  // !p(a)
+  while (a + step < hi && !p(a + step)) {
+    a += step;
+    step <<= 1;
   }
+  int c = min(a + step, hi);  // p(c) or c == hi
+  while (c - a > 1) {
+    const int m = (a + c) >> 1;
+    if (p(m)) c = m; else a = m;
+  }
+  return c;
+}
+// the same position, probing from hi - 1 downward
+template <typename P>
+__device__ __forceinline__ int first_true_down(int lo, int hi, P p) {
+  if (lo >= hi || !p(hi - 1)) return hi;
+  int c = hi - 1, step = 1;  // p(c)
+  while (c - step >= lo && p(c - step)) {
+    c -= step;
+    step <<= 1;
+  }
+  int a = max(c - step, lo - 1);  // !p(a) or a == lo - 1
+  while (c - a > 1) {
+    const int m = (a + c) >> 1;
+    if (p(m)) c = m; else a = m;
+  }
+  return c;
+}
+
+// WindowManager.processWatermark for one key (S/WindowManager.java:38-61): triggered windows, the
+// LazyAggregateStore.aggregate scan range (:83-90, its getSlice(-1) exception included), clearAfterWatermark
+// (:82-95).  AGG: also the windows' values -- COUNT and integer SUM from the slice prefixes (extended from
+// XState.pvalid to tail first), so a window costs two gallops and two reads instead of a scan of its slices
+// (S/slice/SliceManager... AggregateWindowState over the contained slices, S/state/AggregateWindowState.java);
+// without AGG the host runs wm_agg_kernel over [wlo, whi) (MIN / MAX / f64 sums).
+//
+// Rows: with a.row_count the kernel also counts (no separate count pass): each wavefront reserves its keys' rows
+// with one atomic, the host having sized the row columns from a bound (lane_row_bound); else at a.woff[op].
+constexpr int EMIT_T = 1024;
+template <bool AGG, class V>
+__global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
+  const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const XCfg* c = a.cfg;
+  const V q = xview<V>(a.sl);
   const int64_t base = op * (int64_t)c->sc;
-  const int64_t* ts = a.sl.ts + base;
-  const int64_t* cs = a.sl.cs + base;
-  if (s.lastWatermark < ts[s.head]) s.lastWatermark = ts[s.head];
+  const auto ts = q.ts + base;
+  XState s{};
+  bool live = op < a.n_ops;
+  int64_t k = 0;
+  if (live) {
+    s = a.st[op];
+    if (a.row_count) {  // what the count pass accumulates
+      if (s.dropped) atomicAdd(a.dropped_total, (unsigned long long)s.dropped);
+      if (s.err) atomicOr(a.op_err, 1 << s.err);
+    }
+    if (s.err) {
+      live = false;
+    } else {
+      if (s.lastWatermark == -1) s.lastWatermark = max((int64_t)0, jsub(a.wm, c->max_lateness));  // :43-44
+      if (s.tail <= s.head) {
+        s.lastWatermark = a.wm;
+        a.st[op] = s;
+        live = false;
+      } else {
+        if (s.lastWatermark < ts[s.head]) s.lastWatermark = ts[s.head];
+        if (a.row_count) {
+          int64_t mn = JMAX, mx = 0;
+          k = lane_triggers<false>(c, s.lastWatermark, a.wm, nullptr, nullptr, nullptr, nullptr, 0, 0, mn, mx);
+        }
+      }
+    }
+  }
+  int64_t off = 0;
+  if (a.row_count) {  // workgroup-aggregated row reservation: one atomic per workgroup (one counter word takes
+                      // only ~90 atomics per us, a per-wavefront reservation would serialise on it)
+    __shared__ long long s_w[EMIT_T / 64 + 1];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t inc = k;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) s_w[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long run = 0;
+      for (int w = 0; w < EMIT_T / 64; w++) {
+        const long long v = s_w[w];
+        s_w[w] = run;
+        run += v;
+      }
+      s_w[EMIT_T / 64] = run > 0 ? (long long)atomicAdd(a.row_count, (unsigned long long)run) : 0;
+    }
+    __syncthreads();
+    off = (int64_t)s_w[EMIT_T / 64] + (int64_t)s_w[wid] + inc - k;
+    if (live && off + k > a.n_rows) {  // the host bound was wrong: nothing is written, the call fails
+      atomicOr(a.err_flag, 4);
+      return;
+    }
+  } else if (live) {
+    off = a.woff[op];
+  }
+  if (!live) return;
+  const auto tl = q.tl + base;
+  const auto cs = q.cs + base;
   int64_t minTs = JMAX, maxTs = 0;
-  const int64_t k = lane_triggers<true>(c, s.lastWatermark, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, a.woff[op],
-                                        (int32_t)op, minTs, maxTs);
-  auto find_ts = [&](int64_t t) {
-    int lo = s.head, hi = s.tail;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (ts[mid] <= t) lo = mid + 1; else hi = mid;
-    }
-    return lo - 1 >= s.head ? lo - 1 : -1;
-  };
-  auto find_count = [&](int64_t cc) {
-    int lo = s.head, hi = s.tail;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (cs[mid] <= cc) lo = mid + 1; else hi = mid;
-    }
-    return lo - 1 >= s.head ? lo - 1 : -1;
-  };
-  if (k > 0) {  // LazyAggregateStore.aggregate scan range (:83-90); no count windows: minCount = currentCount
-    const int S = s.tail - s.head;
-    auto rel = [&](int i) { return i < 0 ? -1 : i - s.head; };
-    int si = max(rel(find_ts(minTs)), 0);
-    si = min(si, rel(find_count(s.currentCount)));
-    int ei = min(S - 1, rel(find_ts(maxTs)));
-    ei = max(ei, rel(find_count(0)));
+  k = lane_triggers<true>(c, s.lastWatermark, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, off, (int32_t)op, minTs,
+                          maxTs);
+  const int h = s.head, t = s.tail;
+  // find_ts / find_count: last slice with key <= x (LazyAggregateStore.findSliceIndexBy*, :29-50), -1 if none
+  auto last_ts_le_up = [&](int64_t x) { return first_true_up(h, t, [&](int i) { return ts[i] > x; }) - 1; };
+  auto last_ts_le_dn = [&](int64_t x) { return first_true_down(h, t, [&](int i) { return ts[i] > x; }) - 1; };
+  auto last_cs_le_up = [&](int64_t x) { return first_true_up(h, t, [&](int i) { return cs[i] > x; }) - 1; };
+  auto last_cs_le_dn = [&](int64_t x) { return first_true_down(h, t, [&](int i) { return cs[i] > x; }) - 1; };
+  auto fix = [&](int i) { return i < h ? -1 : i; };
+  if (AGG) {
+    // the scan range only bounds the contained slices, which the prefix lookup finds directly; its getSlice(-1)
+    // exception needs cStart[head] > currentCount, impossible here (cStart is the count at append time)
+    s.wlo = h;
+    s.whi = t;
+  } else if (k > 0) {  // LazyAggregateStore.aggregate scan range (:83-90); no count windows: minCount = currentCount
+    const int S = t - h;
+    auto rel = [&](int i) { return i < 0 ? -1 : i - h; };
+    int si = max(rel(fix(last_ts_le_up(minTs))), 0);
+    si = min(si, rel(fix(last_cs_le_dn(s.currentCount))));
+    int ei = min(S - 1, rel(fix(last_ts_le_dn(maxTs))));
+    ei = max(ei, rel(fix(last_cs_le_up(0))));
     if (si < 0 && si <= ei) {
       atomicOr(a.err_flag, 2);
       si = 0;
     }
-    s.wlo = s.head + si;
-    s.whi = s.head + ei + 1;
+    s.wlo = h + si;
+    s.whi = h + ei + 1;
   } else {
-    s.wlo = s.whi = s.head;
+    s.wlo = s.whi = h;
+  }
+  if (AGG && k > 0) {
+    const bool sums = (c->need & NEED_SUM) != 0;
+    const auto pc = q.pc + base;
+    const auto ps = q.ps + base;
+    const auto cnt = q.cnt + base;
+    const auto p0 = q.p[0] + base;
+    int pv = a.prefix_reset ? 0 : s.pvalid;
+    if (pv < t) {  // extend the prefixes over the slices changed since the last watermark
+      unsigned long long rc = pv > 0 ? pc[pv - 1] : 0, rs = pv > 0 && sums ? ps[pv - 1] : 0;
+      for (int i = pv; i < t; i++) {
+        rc += cnt[i];
+        pc[i] = rc;
+        if (sums) {
+          rs += p0[i];
+          ps[i] = rs;
+        }
+      }
+      pv = t;
+    }
+    s.pvalid = pv;
+    const bool sorted = !(s.unsorted & 3);
+    const int lo0 = (int)s.wlo, hi0 = (int)s.whi;
+    const uint32_t key = a.slot_key ? a.slot_key[op] : (uint32_t)op;
+    for (int64_t r = off; r < off + k; r++) {
+      const int64_t ws = a.w_start[r], we = a.w_end[r];
+      uint64_t cn = 0, sw = 0;
+      if (sorted) {  // the contained slices (ws <= tStart, tLast < we) are the run [lo, hi): tLast increases
+        const int lo = first_true_up(lo0, hi0, [&](int i) { return ts[i] >= ws; });
+        const int hi = first_true_down(lo, hi0, [&](int i) { return tl[i] >= we; });
+        if (hi > lo) {
+          cn = pc[hi - 1] - (lo > 0 ? pc[lo - 1] : 0ull);
+          if (sums) sw = ps[hi - 1] - (lo > 0 ? ps[lo - 1] : 0ull);
+        }
+      } else {
+        for (int i = lo0; i < hi0; i++) {
+          if (!(ws <= ts[i] && we > tl[i])) continue;
+          cn += cnt[i];
+          if (sums) sw += p0[i];
+        }
+      }
+      const bool present = cn != 0;
+      a.has_value[r] = present ? 1 : 0;
+      if (a.w_key) a.w_key[r] = key;
+      for (int q = 0; q < c->n_aggs; q++)
+        a.values[q][r] = present ? x::lower_value(c->agg_kind[q], cn, sw, ID_MIN, ID_MAX) : 0;
+    }
   }
   s.lastWatermark = a.wm;
   s.lastCount = s.currentCount;
-  const int64_t t = jsub(jsub(a.wm, c->max_lateness), c->max_fixed);  // clearAfterWatermark (:82-95)
-  const int idx = find_ts(t);
+  const int64_t gt = jsub(jsub(a.wm, c->max_lateness), c->max_fixed);  // clearAfterWatermark (:82-95)
+  const int idx = fix(last_ts_le_up(gt));
   if (idx > s.head) s.head = idx;
   a.st[op] = s;
 }
@@ -405,7 +551,12 @@ hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStre
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
   const bool mm = (host_cfg.need & (NEED_MIN | NEED_MAX)) != 0;
   const int vt = host_cfg.vt;
-#define SCOTTY_LANE(V, M) hipLaunchKernelGGL((ln::lane_replay_kernel<V, M>), grid, block, 0, st, a)
+  if (a.sl.rec) {  // record store: COUNT / integer SUM only (no MIN / MAX, no f64)
+    if (vt == VT_I32) hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I32, false, XRecView>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I64, false, XRecView>), grid, block, 0, st, a);
+    return hipGetLastError();
+  }
+#define SCOTTY_LANE(V, M) hipLaunchKernelGGL((ln::lane_replay_kernel<V, M, XSlices>), grid, block, 0, st, a)
   if (vt == VT_I32) { if (mm) SCOTTY_LANE(VT_I32, true); else SCOTTY_LANE(VT_I32, false); }
   else if (vt == VT_I64) { if (mm) SCOTTY_LANE(VT_I64, true); else SCOTTY_LANE(VT_I64, false); }
   else { if (mm) SCOTTY_LANE(VT_F64, true); else SCOTTY_LANE(VT_F64, false); }
@@ -414,12 +565,17 @@ hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStre
 }
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ln::lane_wm_count_kernel, dim3((unsigned)((a.n_ops + 255) / 256)), dim3(256), 0, st, a);
+  const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
+  if (a.sl.rec) hipLaunchKernelGGL(ln::lane_wm_count_kernel<XRecView>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(ln::lane_wm_count_kernel<XSlices>, grid, block, 0, st, a);
   return hipGetLastError();
 }
-hipError_t launch_lane_wm_emit(const XWmArgs& a, hipStream_t st) {
+hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ln::lane_wm_emit_kernel, dim3((unsigned)((a.n_ops + 255) / 256)), dim3(256), 0, st, a);
+  const dim3 grid((unsigned)((a.n_ops + ln::EMIT_T - 1) / ln::EMIT_T)), block(ln::EMIT_T);
+  if (a.sl.rec) hipLaunchKernelGGL((ln::lane_wm_emit_kernel<true, XRecView>), grid, block, 0, st, a);
+  else if (agg) hipLaunchKernelGGL((ln::lane_wm_emit_kernel<true, XSlices>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((ln::lane_wm_emit_kernel<false, XSlices>), grid, block, 0, st, a);
   return hipGetLastError();
 }
 

@@ -145,6 +145,9 @@ struct scotty_op {
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
   bool x_lane_off = false;
+  bool x_kg_off = false;
+  int64_t x_kg_chunk = -1;
+  int32_t x_kg_variant = -1;
   int64_t shard_count_total = 0;
   int64_t count_shard_cap = 1 << 16;
   bool x_count_on = false;   // "count_path" 1: the stream is in timestamp order -> count-only operators keep no
@@ -863,6 +866,9 @@ static int decide_mode(scotty_op* op) {
   op->x->sess_override = op->x_sess;
   op->x->serial = op->x_serial;
   op->x->lane_off = op->x_lane_off;
+  op->x->kg_off = op->x_kg_off;
+  if (op->x_kg_chunk >= 0) op->x->kg_min_chunk = op->x_kg_chunk;
+  if (op->x_kg_variant >= 0) op->x->kg_variant = op->x_kg_variant;
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
   if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness, op->agg_inv);
@@ -1365,9 +1371,29 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     op->x_count_on = value != 0;
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "keyed_grid") == 0) {  // 0: keyed batches always sorted + replayed (no sort-free path)
+    if (op->mode != 0) return SCOTTY_ERR_ARG;
+    op->x_kg_off = value == 0;
+    if (op->x) op->x->kg_off = op->x_kg_off;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only)
+    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;
+    op->x_kg_variant = (int32_t)value;
+    if (op->x) op->x->kg_variant = op->x_kg_variant;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "keyed_grid_chunk") == 0) {  // min average tuples per chunk of a many-cell batch
+    if (op->mode != 0 || value < 0) return SCOTTY_ERR_ARG;
+    op->x_kg_chunk = value;
+    if (op->x) op->x->kg_min_chunk = value;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "keyed_lane") == 0) {  // 0: wavefront-per-key replay even where the lane path applies
     if (op->mode != 0) return SCOTTY_ERR_ARG;
+    if (op->x && op->x->layout_fixed() && value == 0) return SCOTTY_ERR_ARG;  // the record store needs the lane path
     op->x_lane_off = value == 0;
+    if (op->x) op->x->lane_off = op->x_lane_off;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "slice_capacity") == 0 || std::strcmp(key, "session_capacity") == 0) {
@@ -1395,10 +1421,19 @@ int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
   return -1;
 }
 
-// Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds).
+// Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds; keyed:
+// 2 path of the last push (0 replay, 1 sort-free, 2 sort-free + replay of deferred keys), 3 deferred tuples,
+// 4 keys committed on the sort-free path).
 int64_t scotty_debug_stat(scotty_op* op, int which) {
   if (!op || !op->x) return -1;
-  return which == 0 ? op->x->last_events : op->x->last_segments;
+  switch (which) {
+    case 0: return op->x->last_events;
+    case 1: return op->x->last_segments;
+    case 2: return op->x->last_kg;
+    case 3: return op->x->last_kg_deferred;
+    case 4: return op->x->last_kg_keys;
+    default: return -1;
+  }
 }
 
 // Internal (not in the header): state of one operator of the exact engine, for tests and debugging.
