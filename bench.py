@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 METRIC = "tuples/sec (1/2/4/8 GPU) at 1000 concurrent windows; % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_TUPLE = 12   # int64 ts + int32 value, read once
+PCIE_GBS = 64.0        # host link, PCIe Gen5 x16 (32 GT/s x 16 lanes): the bound of host-buffer ingest
 KEYED_BYTES_PER_TUPLE = 16  # + uint32 key
 C4_BATCH = 1 << 26     # GPU runs use N ~ 2^26 tuples per watermark batch (C4: per rank)
 CPU_BUDGET_S = float(os.environ.get("SCOTTY_CPU_BUDGET_S", "12"))
@@ -443,6 +444,44 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
                               "frac": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9 / HBM_PEAK_GBS}}
 
 
+def extra_pcie(pkg, sizes, batch, steps):
+    """PCIe-inclusive C2: the same operator fed from HOST memory through scotty_process_elements --
+    (a) the op's pinned staging slots (scotty_host_buffers: DMA in place, double-buffered), (b) pageable numpy
+    arrays (chunked through pinned staging).  Timed: push + watermark calls per step, each step ending with its
+    results on the host; the producer's writes of the next batch (ts column) are outside the timed calls."""
+    import numpy as np
+    rate = max(1, batch // 1000)
+    out = {"tuples_per_step": batch, "steps": steps, "bytes_per_tuple": BYTES_PER_TUPLE,
+           "pcie_bound_tuples_per_s": PCIE_GBS * 1e9 / BYTES_PER_TUPLE}
+    rng = np.random.default_rng(77)
+    base = np.arange(batch, dtype=np.int64) // rate
+    vals0 = rng.integers(-2**31, 2**31, size=batch, dtype=np.int64).astype(np.int32)
+    for mode in ("pinned", "pageable"):
+        op = pkg.SlicingWindowOperator()
+        op.addWindowFunction(pkg.AGG_SUM_I32)
+        op.addWindowFunction(pkg.AGG_COUNT)
+        op.setMaxLateness(1)
+        for sz in sizes:
+            op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Time, sz))
+        timed = 0.0
+        for s in range(steps + 2):
+            if mode == "pinned":
+                ts, vals = op.hostBuffers(batch)
+                np.add(base, s * 1000, out=ts)
+                vals[:] = vals0
+            else:
+                ts, vals = base + s * 1000, vals0
+            t0 = time.perf_counter()
+            op.processElements(ts, vals)
+            op.processWatermarkRaw(s * 1000 + (batch - 1) // rate)
+            if s >= 2:
+                timed += time.perf_counter() - t0
+        out[mode] = {"value": batch * steps / timed, "unit": "tuples/s", "ms_per_step": 1e3 * timed / steps,
+                     "frac_of_pcie_bound": batch * steps / timed / out["pcie_bound_tuples_per_s"]}
+        op.close()
+    return out
+
+
 def spawn_ranks(args):
     """`--gpus N` without a launcher: run N ranks through torch.distributed.run as a child (no GPU touched here)."""
     import socket
@@ -464,7 +503,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
-    ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5); default all")
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5,pcie); default all")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
@@ -588,7 +627,7 @@ def main():
                                        % world) if sharded else "single GPU"},
             "roofline": roof,
         }
-    legs = set(x for x in args.only.split(",") if x) or {"c2s", "c3", "c4", "c5"}
+    legs = set(x for x in args.only.split(",") if x) or {"c2s", "c3", "c4", "c5", "pcie"}
     extra = {}
     if not args.no_extra:
         del batches
@@ -607,6 +646,9 @@ def main():
             if "c5" in legs:
                 extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)
                 log("bench: C5 done")
+            if "pcie" in legs:
+                extra["pcie_inclusive"] = extra_pcie(pkg, sizes, 1 << 26, 5)
+                log("bench: PCIe-inclusive C2 done")
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
             extra = {"c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, rank=rank, world=world, dist=dist),
                      "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist)}

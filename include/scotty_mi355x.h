@@ -104,9 +104,16 @@ int scotty_add_aggregation(scotty_op* op, int agg_kind);
 int scotty_set_max_lateness(scotty_op* op, int64_t max_lateness);
 
 /* A micro-batch of WindowOperator.processElement(element, ts) calls (C/WindowOperator.java:14) in
- * arrival order.  Host memory, caller-owned, consumed (copied) before return.  val points to n
- * values of the op's value type. */
+ * arrival order.  Host memory, caller-owned, consumed before return (pageable input is copied through the op's
+ * pinned staging while earlier chunks are DMA'd; memory from scotty_host_buffers is DMA'd in place).  val points to
+ * n values of the op's value type.  The transfer overlaps the op's queued device work; no device synchronisation. */
 int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, size_t n);
+/* Pinned host staging owned by the op, for up to n tuples: the caller fills ts / val (/ key, keyed ops) -- the
+ * off-heap buffer of the Java shim's processElement -- and passes the same pointers to scotty_process_elements /
+ * scotty_process_keyed_elements, which DMA them without a CPU copy (PCIe-bound ingest).  Two slots alternate
+ * between calls: a slot handed out again is reusable once its previous DMA has finished (the call waits for
+ * that), so the caller fills one slot while the other is in flight. */
+int scotty_host_buffers(scotty_op* op, size_t n, int64_t** ts, void** val, uint32_t** key);
 /* Same, with device pointers already resident in HBM (device `device` of the op).  The buffers must
  * stay valid and unmodified until the next scotty_process_watermark() returns. */
 int scotty_process_elements_device(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n);

@@ -283,6 +283,25 @@ class SlicingWindowOperator:
         if len(ts):
             self._check(self._l.scotty_process_elements(self._h, ts.ctypes.data, v.ctypes.data, len(ts)))
 
+    def hostBuffers(self, n):
+        """(ts, values) numpy views of one of the op's two pinned staging slots (scotty_host_buffers) for n tuples:
+        fill them and pass them to processElements, which DMAs them in place (no CPU copy).  Slots alternate between
+        calls; a slot is handed out again once its previous transfer has finished."""
+        self._flush()
+        f = self._l.scotty_host_buffers
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]
+        pts, pval, pkey = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(f(self._h, n, ctypes.byref(pts), ctypes.byref(pval), ctypes.byref(pkey)))
+        dt = {VALUE_I32: np.int32, VALUE_I64: np.int64, VALUE_F64: np.float64}[self.value_type]
+        ts = np.ctypeslib.as_array(ctypes.cast(pts, ctypes.POINTER(ctypes.c_int64)), shape=(n,))
+        vals = np.frombuffer((ctypes.c_char * (n * np.dtype(dt).itemsize)).from_address(pval.value), dtype=dt)
+        if pkey.value:
+            keys = np.ctypeslib.as_array(ctypes.cast(pkey, ctypes.POINTER(ctypes.c_uint32)), shape=(n,))
+            return ts, vals, keys
+        return ts, vals
+
     def processElementsDevice(self, ts_ptr, val_ptr, n):
         """A micro-batch already resident in HBM (e.g. torch tensors' data_ptr()); buffers must stay valid
         until the next processWatermark returns."""

@@ -400,8 +400,19 @@ __device__ __forceinline__ unsigned long long add_sum(unsigned long long acc, un
 // per-(key, cell) partials with LDS atomics, write the partials of every touched key to its slot (KPart).
 // Records whose key is not in the table (new keys, or probed past the spill) are marked for the replay path.
 template <int VT, bool MM>
-__global__ __launch_bounds__(1024) void kg_bucket_kernel(KgArgs a) {
-  constexpr int CM = MM ? 2 : 4;
+__device__ __forceinline__ void kg_bucket_body(const KgArgs& a);
+// COUNT / SUM: 74 KB of LDS and <= 64 VGPRs, two workgroups per CU; MIN / MAX: one (87 KB)
+template <int VT, bool MM>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void kg_bucket_kernel(KgArgs a) {
+  kg_bucket_body<VT, MM>(a);
+}
+template <int VT, bool MM>
+__global__ __launch_bounds__(1024) void kg_bucket_mm_kernel(KgArgs a) {
+  kg_bucket_body<VT, MM>(a);
+}
+template <int VT, bool MM>
+__device__ __forceinline__ void kg_bucket_body(const KgArgs& a) {
+  constexpr int CM = MM ? 2 : 3;
   constexpr int VB = VT == VT_I32 ? 4 : 8;
   __shared__ KgLds<CM, MM> L;
   __shared__ unsigned long long s_miss;
@@ -455,7 +466,7 @@ __global__ __launch_bounds__(1024) void kg_bucket_kernel(KgArgs a) {
       atomicMax(&L.vmax[q], (long long)mx);
     }
   };
-  constexpr int U = 4;  // records loaded per round before they are folded: 4 loads in flight per lane
+  constexpr int U = 2;  // records loaded per round before they are folded: 2 loads in flight per lane
   int64_t r = r0 + tid;
   for (; r + (U - 1) * nt < r1; r += U * nt) {
     KRec<VB> rc[U];
@@ -648,7 +659,7 @@ __device__ bool kg_commit_key(const KgArgs& a, const KPart* kp, uint32_t slot, i
 
 template <int VT, bool MM, class V>
 __global__ __launch_bounds__(256) void kg_commit_kernel(KgArgs a, int64_t n_ops) {
-  constexpr int CM = MM ? 2 : 4;
+  constexpr int CM = MM ? 2 : 3;
   __shared__ unsigned long long s_def_t, s_def_k, s_keys;
   const int tid = threadIdx.x;
   if (tid == 0) s_def_t = s_def_k = s_keys = 0;
@@ -820,14 +831,19 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
     }
     return hipGetLastError();
   }
-#define SCOTTY_KG(V, M)                                                                      \
-  do {                                                                                       \
-    hipLaunchKernelGGL((kg::kg_bucket_kernel<V, M>), grid, block, 0, st, a);                 \
-    hipLaunchKernelGGL((kg::kg_commit_kernel<V, M, XSlices>), cgrid, cblock, 0, st, a, n_ops); \
+#define SCOTTY_KG(V)                                                                              \
+  do {                                                                                            \
+    if (mm) {                                                                                     \
+      hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<V, true>), grid, block, 0, st, a);             \
+      hipLaunchKernelGGL((kg::kg_commit_kernel<V, true, XSlices>), cgrid, cblock, 0, st, a, n_ops);  \
+    } else {                                                                                      \
+      hipLaunchKernelGGL((kg::kg_bucket_kernel<V, false>), grid, block, 0, st, a);               \
+      hipLaunchKernelGGL((kg::kg_commit_kernel<V, false, XSlices>), cgrid, cblock, 0, st, a, n_ops); \
+    }                                                                                             \
   } while (0)
-  if (vt == VT_I32) { if (mm) SCOTTY_KG(VT_I32, true); else SCOTTY_KG(VT_I32, false); }
-  else if (vt == VT_I64) { if (mm) SCOTTY_KG(VT_I64, true); else SCOTTY_KG(VT_I64, false); }
-  else { if (mm) SCOTTY_KG(VT_F64, true); else SCOTTY_KG(VT_F64, false); }
+  if (vt == VT_I32) SCOTTY_KG(VT_I32);
+  else if (vt == VT_I64) SCOTTY_KG(VT_I64);
+  else SCOTTY_KG(VT_F64);
 #undef SCOTTY_KG
   return hipGetLastError();
 }
@@ -838,7 +854,7 @@ hipError_t launch_kg_mark_deferred(const KgArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-int kg_cells(bool mm) { return mm ? 2 : 4; }
+int kg_cells(bool mm) { return mm ? 2 : 3; }
 
 hipError_t launch_kg_bounds(const int64_t* ts, int64_t n, const XCfg* cfg, int kmax, int64_t* gpts, int64_t* out,
                             hipStream_t st) {

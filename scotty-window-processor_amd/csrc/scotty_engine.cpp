@@ -19,6 +19,7 @@
 #include "device_common.h"
 #include "count_engine.h"
 #include "exact_engine.h"
+#include "host_ingest.h"
 
 namespace scotty {
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
@@ -128,7 +129,8 @@ struct scotty_op {
     int64_t seq;
   };
   std::vector<Push> pending;
-  std::vector<void*> owned;  // staging copies of host pushes
+  std::vector<void*> owned;  // (unused since the host ingest arena; kept empty)
+  HostIngest* ingest = nullptr;  // host columns -> HBM (pinned slots, copy stream, arena reset per watermark)
   int64_t push_seq = 0;
   uint64_t dropped = 0, processed = 0;
 
@@ -320,6 +322,8 @@ int alloc_all(scotty_op* op) {
   op->tcap = 0;
   HIPCHK(hipSetDevice(op->device));
   HIPCHK(hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking));
+  op->ingest = new HostIngest();
+  if (op->ingest->init(op->device, op->stream)) return fail(op, SCOTTY_ERR_HIP, "host ingest: stream / event creation");
   HIPCHK(hipMalloc(&op->d_meta, sizeof(DevMeta)));
   HIPCHK(hipHostMalloc(&op->h_snap, sizeof(DevMeta), hipHostMallocDefault));
   HIPCHK(hipMemset(op->d_meta, 0, sizeof(DevMeta)));
@@ -725,6 +729,7 @@ void scotty_destroy(scotty_op* op) {
   F(op->d_out);
   for (int k = 0; k < NPART; k++) { F(op->d_spart[k]); F(op->d_cpart[k]); F(op->d_bpart[k]); }
   for (void* p : op->owned) F(p);
+  delete op->ingest;
   if (op->h_snap) (void)hipHostFree(op->h_snap);
   if (op->h_out) (void)hipHostFree(op->h_out);
   for (auto& e : op->tev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -932,16 +937,18 @@ int scotty_process_elements(scotty_op* op, const int64_t* ts, const void* val, s
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
   if (op->keyed) return fail(op, SCOTTY_ERR_ARG, "keyed operator: use scotty_process_keyed_elements");
   if (n == 0) return SCOTTY_OK;
-  const size_t vb = value_bytes(op);
-  void* d = nullptr;
-  HIPCHK(hipMalloc(&d, n * 8 + n * vb + 16));
-  int64_t* d_ts = (int64_t*)d;
-  void* d_val = (unsigned char*)d + ((n * 8 + 15) / 16) * 16;
-  op->owned.push_back(d);
-  HIPCHK(hipMemcpyAsync(d_ts, ts, n * 8, hipMemcpyHostToDevice, op->stream));
-  HIPCHK(hipMemcpyAsync(d_val, val, n * vb, hipMemcpyHostToDevice, op->stream));
-  HIPCHK(hipStreamSynchronize(op->stream));  // host memory is consumed before return
+  // host columns -> HBM (host_ingest.h): pinned slots DMA'd in place, pageable input chunked through pinned
+  // staging; the copies stay in the ingest arena until the watermark (the grid path may replay a push)
+  int64_t* d_ts = nullptr;
+  void* d_val = nullptr;
+  HIPCHK(op->ingest->stage(ts, val, nullptr, n, value_bytes(op), true, &d_ts, &d_val, nullptr));
   return push_impl(op, d_ts, d_val, (int64_t)n, ts);
+}
+
+int scotty_host_buffers(scotty_op* op, size_t n, int64_t** ts, void** val, uint32_t** key) {
+  if (!op || !ts || !val || (op->keyed && !key)) return SCOTTY_ERR_ARG;
+  HIPCHK(op->ingest->host_buffers(n, value_bytes(op), op->keyed, ts, val, key));
+  return SCOTTY_OK;
 }
 
 int scotty_process_elements_device(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n) {
@@ -967,18 +974,12 @@ int scotty_process_keyed_elements(scotty_op* op, const uint32_t* key, const int6
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
   if (!op->keyed) return fail(op, SCOTTY_ERR_ARG, "not a keyed operator (create with SCOTTY_FLAG_KEYED)");
   if (n == 0) return SCOTTY_OK;
-  const size_t vb = value_bytes(op);
-  const size_t o_val = ((n * 8 + 15) / 16) * 16, o_key = o_val + ((n * vb + 15) / 16) * 16;
-  void* d = nullptr;
-  HIPCHK(hipMalloc(&d, o_key + n * 4 + 16));
-  HIPCHK(hipMemcpyAsync(d, ts, n * 8, hipMemcpyHostToDevice, op->stream));
-  HIPCHK(hipMemcpyAsync((unsigned char*)d + o_val, val, n * vb, hipMemcpyHostToDevice, op->stream));
-  HIPCHK(hipMemcpyAsync((unsigned char*)d + o_key, key, n * 4, hipMemcpyHostToDevice, op->stream));
-  int rc = keyed_push(op, (const uint32_t*)((unsigned char*)d + o_key), (const int64_t*)d,
-                      (unsigned char*)d + o_val, (int64_t)n);
-  (void)hipStreamSynchronize(op->stream);
-  (void)hipFree(d);
-  return rc;
+  // keyed pushes complete inside the call: the device copy goes to reusable scratch, not the arena
+  int64_t* d_ts = nullptr;
+  void* d_val = nullptr;
+  uint32_t* d_key = nullptr;
+  HIPCHK(op->ingest->stage(ts, val, key, n, value_bytes(op), false, &d_ts, &d_val, &d_key));
+  return keyed_push(op, d_key, d_ts, d_val, (int64_t)n);
 }
 
 int scotty_process_keyed_elements_device(scotty_op* op, const uint32_t* d_key, const int64_t* d_ts,
@@ -1009,6 +1010,7 @@ static int exact_watermark(scotty_op* op, int64_t wm, scotty_windows* out, bool 
   op->processed = op->x_pushed - r.dropped;
   for (void* p : op->owned) (void)hipFree(p);
   op->owned.clear();
+  op->ingest->reset();
   op->pending.clear();
   if (out) {
     std::memset(out, 0, sizeof(*out));
@@ -1271,6 +1273,7 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
   tresolve(op);
   for (void* p : op->owned) (void)hipFree(p);
   op->owned.clear();
+  op->ingest->reset();
   op->pending.clear();
   if (out) {
     // results: AggregateWindowState.getAggValues / hasValue (S/state/AggregateWindowState.java:41-49), lowered on
