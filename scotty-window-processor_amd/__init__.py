@@ -245,7 +245,8 @@ class SlicingWindowOperator:
     def _debug_stat(self, which):
         """Internal statistics of the last push (scotty_debug_stat in scotty_engine.cpp); tests and tools only.
         Keyed: 2 path of the last push (0 replay, 1 sort-free, 2 sort-free + replay of deferred keys), 3 deferred
-        tuples, 4 keys committed on the sort-free path."""
+        tuples, 4 keys committed on the sort-free path.  Any operator: 5 engine (1 grid path, 2 exact engine, 3 count
+        path), 6 time edges of the count path's last push."""
         f = self._l.scotty_debug_stat
         f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int]
         self._flush()

@@ -67,9 +67,9 @@ struct CMeta {
 constexpr int CSHARD_HDR = 16;
 __host__ __device__ inline int64_t cshard_words(int64_t cap) { return CSHARD_HDR + 8 * cap; }
 
-struct CWin {  // one context-free count window, registration order
+struct CWin {  // one context-free window, registration order
   int32_t kind;
-  int32_t pad;
+  int32_t measure;  // SCOTTY_MEASURE_COUNT, or SCOTTY_MEASURE_TIME (time windows on an in-order stream)
   int64_t a, b;
 };
 
@@ -97,6 +97,32 @@ struct CPushArgs {
   CMeta* meta;
   int32_t shard;         // ingest for a shard record: local prefix max only, no own-ts substitution
   int64_t ts0;           // shard: timestamp of the stream's first tuple (first slice start)
+  // time edges of the batch (time windows, in-order stream): batch position of the tuple that appends each edge
+  // and the edge, sorted by position then edge; at one position they follow the count edge
+  // (StreamSlicer.determineSlices checks the count edge first, S/StreamSlicer.java:36-44 then :46-83)
+  const int64_t* te_pos;
+  const int64_t* te_g;
+  int64_t n_te;
+  int32_t check_sorted;  // time windows: flag (CMeta.err bit 8) a batch that is not in timestamp order
+};
+
+// Time-edge candidates of one in-order batch: the union time grid from the pending edge N up to the batch max
+// (host-enumerated); per candidate the first tuple reaching it decides the edge (commit_kernel's rule: g == N, or
+// g == nextGrid(m(g)), or e(g) - g < maxLateness, S/StreamSlicer.java:55-84, :103-116).
+struct CTimeArgs {
+  const int64_t* ts;
+  int64_t n;
+  int64_t start;         // first batch position the candidates apply to (1 when position 0 is the stream's first)
+  int64_t prev_max;      // maxEventTime before position `start`
+  int64_t lateness;
+  const int64_t* cand;   // [n_cand] ascending
+  int64_t n_cand;
+  int64_t prev0;         // the grid point before cand[0] (JMIN: cand[0] is the pending edge itself)
+  int64_t* te_pos;       // out: [n_te] compacted edges
+  int64_t* te_g;
+  unsigned long long* n_te;
+  int32_t* flag;         // scratch [n_cand]
+  int64_t* pos;          // scratch [n_cand]
 };
 
 struct CShardArgs {
@@ -116,8 +142,10 @@ struct CWmArgs {
   int64_t wm;
   int64_t min_count, max_count;  // LazyAggregateStore.aggregate arguments (count part)
   int64_t gc_before;             // clearAfterWatermark: wm - maxLateness - maxFixedWindowSize
-  const int64_t* w_start;        // [nw] count windows
+  const int64_t* w_start;        // [nw] windows (count windows in count space)
   const int64_t* w_end;
+  const int32_t* w_meas;         // [nw] SCOTTY_MEASURE_* of each window
+  int64_t min_ts, max_ts;        // LazyAggregateStore.aggregate arguments (time part)
   int64_t nw;
   int32_t need, vt, n_aggs, prefix;  // prefix: all aggregations invertible integer kinds -> prefix sums
   int32_t agg_kind[8];

@@ -15,6 +15,7 @@ hipError_t launch_count_export(const CPushArgs& a, int64_t* rec, int64_t cap, hi
 hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hipStream_t st);
 hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st);
 hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st);
+hipError_t launch_count_time_edges(const CTimeArgs& a, hipStream_t st);
 
 #define CCHK(x)                                                      \
   do {                                                               \
@@ -82,6 +83,8 @@ CEngine::~CEngine() {
   for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
   dfree(d_pre_cnt); dfree(d_pre_sum); dfree(d_bsum);
   dfree(d_plan);
+  dfree(d_cand); dfree(d_cpos); dfree(d_te_pos); dfree(d_te_g); dfree(d_cflag); dfree(d_nte);
+  if (h_tmp) (void)hipHostFree(h_tmp);
 }
 
 int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
@@ -89,7 +92,9 @@ int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
   stream = st;
   vt = vt_;
   if (hipMalloc((void**)&d_meta, sizeof(CMeta)) != hipSuccess ||
-      hipHostMalloc((void**)&h_meta, sizeof(CMeta), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&h_meta, sizeof(CMeta), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&h_tmp, 8 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void**)&d_nte, sizeof(unsigned long long)) != hipSuccess) {
     e = "count engine: out of memory";
     return SCOTTY_ERR_NOMEM;
   }
@@ -104,20 +109,26 @@ int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
 }
 
 int CEngine::configure(const std::vector<XWinDef>& ws, const std::vector<int>& ag, int64_t lateness) {
-  std::vector<CWin> nw;
+  std::vector<CWin> nw, tw, all;
   int64_t mf = 0;
   for (const XWinDef& w : ws) {
-    if (w.kind == SCOTTY_WIN_SESSION || w.measure != SCOTTY_MEASURE_COUNT)
-      return fail(SCOTTY_ERR_UNSUPPORTED, "count path: only context-free count windows");
+    if (w.kind == SCOTTY_WIN_SESSION)
+      return fail(SCOTTY_ERR_UNSUPPORTED, "count path: only context-free windows");
     CWin c{};
     c.kind = w.kind;
+    c.measure = w.measure;
     c.a = w.a;
     c.b = w.b;
-    nw.push_back(c);
+    (w.measure == SCOTTY_MEASURE_COUNT ? nw : tw).push_back(c);
+    all.push_back(c);
     mf = std::max(mf, w.kind == SCOTTY_WIN_FIXED_BAND ? w.b : w.a);  // clearDelay (C/windowType/*.java)
   }
+  if (started && tw.size() != twins.size())
+    return fail(SCOTTY_ERR_UNSUPPORTED, "count path: time windows added after the first tuple");
   // mid-stream additions: the pending edge keeps its value (StreamSlicer recomputes it only at the next edge)
   wins = nw;
+  twins = tw;
+  reg = all;
   max_fixed = mf;
   aggs = ag;
   max_lateness = lateness;
@@ -135,6 +146,117 @@ int CEngine::configure(const std::vector<XWinDef>& ws, const std::vector<int>& a
   if (!wins.empty())
     CCHK(hipMemcpyAsync(d_wins, wins.data(), wins.size() * sizeof(CWin), hipMemcpyHostToDevice, stream));
   CCHK(hipStreamSynchronize(stream));
+  return SCOTTY_OK;
+}
+
+int64_t CEngine::next_time_point(int64_t x) const {
+  int64_t e = JMAX;
+  for (const CWin& w : twins) e = std::min(e, assign_next(w, x));
+  return e;
+}
+
+// Time edges of an in-order push (StreamSlicer.determineSlices' time branch, S/StreamSlicer.java:46-83): the
+// stream's first tuple walks calculateNextFixedEdge as the reference does (Long.MAX_VALUE start, edges < 0 not
+// appended, :103-116); after it every union grid point from the pending edge up to the batch max is a candidate
+// decided on the device by the first tuple reaching it.  Fills a.te_* (edges in position order).
+int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a) {
+  a.te_pos = nullptr;
+  a.te_g = nullptr;
+  a.n_te = 0;
+  if (twins.empty() || n <= 0) return SCOTTY_OK;
+  CCHK(hipMemcpyAsync(h_tmp, d_ts, 8, hipMemcpyDeviceToHost, stream));
+  CCHK(hipMemcpyAsync(h_tmp + 1, d_ts + n - 1, 8, hipMemcpyDeviceToHost, stream));
+  CCHK(hipStreamSynchronize(stream));
+  const int64_t t_first = h_tmp[0], t_last = h_tmp[1];
+  if (t_last < t_first || (started && t_first < h_prev_max))
+    return fail(SCOTTY_ERR_UNSUPPORTED, "count path with time windows: the stream must be in timestamp order "
+                                        "(scotty_tune \"count_path\" 1 promises it)");
+  std::vector<int64_t> first;  // edges the stream's first tuple appends (position 0)
+  int64_t start = 0, prev = h_prev_max;
+  int64_t N = t_pending;
+  if (!started) {
+    const int64_t te = t_first, L = max_lateness;
+    auto calc = [&](int64_t cur_edge) {  // calculateNextFixedEdge(te)
+      const int64_t cur = cur_edge == JMIN ? JMAX : cur_edge;
+      return next_time_point(std::max(jsub(te, L), cur));
+    };
+    N = calc(JMIN);
+    int guard = 0;
+    while (te > N) {
+      if (N >= 0) first.push_back(N);
+      N = calc(N);
+      if (++guard > (1 << 22) || N == JMIN)
+        return fail(SCOTTY_ERR_UNSUPPORTED, "the reference StreamSlicer loops forever on this configuration "
+                                            "(calculateNextFixedEdge, S/StreamSlicer.java:103-116)");
+    }
+    if (N == te) {
+      first.push_back(N);
+      N = calc(N);
+    }
+    start = 1;
+    prev = te;
+  }
+  if (start >= n) {
+    t_pending = N;
+    h_prev_max = std::max(h_prev_max, t_last);
+  }
+  std::vector<int64_t> cand;
+  if (start < n) {
+    for (int64_t g = N; g <= t_last; g = next_time_point(g)) {
+      cand.push_back(g);
+      if (cand.size() > ((size_t)1 << 22))
+        return fail(SCOTTY_ERR_UNSUPPORTED, "count path: more than 2^22 time grid points in one micro-batch");
+      if (next_time_point(g) <= g) break;  // JMAX / overflow: no further grid point
+    }
+    // the pending edge after the batch: the first grid point above its last (maximum) timestamp
+    t_pending = N > t_last ? N : (cand.empty() ? N : next_time_point(cand.back()));
+    h_prev_max = std::max(h_prev_max, t_last);
+  }
+  const int64_t nc = (int64_t)cand.size(), nf = (int64_t)first.size();
+  if (nc > tcap) {
+    dfree(d_cand); dfree(d_cpos); dfree(d_cflag);
+    tcap = nc + 1024;
+    CCHK(dalloc(&d_cand, tcap));
+    CCHK(dalloc(&d_cpos, tcap));
+    CCHK(dalloc(&d_cflag, tcap));
+  }
+  if (nc + nf > tecap) {
+    dfree(d_te_pos); dfree(d_te_g);
+    tecap = nc + nf + 1024;
+    CCHK(dalloc(&d_te_pos, tecap));
+    CCHK(dalloc(&d_te_g, tecap));
+  }
+  if (nf > 0) {
+    std::vector<int64_t> zeros(nf, 0);
+    CCHK(hipMemcpyAsync(d_te_pos, zeros.data(), nf * 8, hipMemcpyHostToDevice, stream));
+    CCHK(hipMemcpyAsync(d_te_g, first.data(), nf * 8, hipMemcpyHostToDevice, stream));
+  }
+  int64_t nte = nf;
+  if (nc > 0) {
+    CCHK(hipMemcpyAsync(d_cand, cand.data(), nc * 8, hipMemcpyHostToDevice, stream));
+    CTimeArgs t{};
+    t.ts = d_ts;
+    t.n = n;
+    t.start = start;
+    t.prev_max = prev;
+    t.lateness = max_lateness;
+    t.cand = d_cand;
+    t.n_cand = nc;
+    t.prev0 = JMIN;
+    t.te_pos = d_te_pos + nf;
+    t.te_g = d_te_g + nf;
+    t.n_te = d_nte;
+    t.flag = d_cflag;
+    t.pos = d_cpos;
+    CCHK(launch_count_time_edges(t, stream));
+    CCHK(hipMemcpyAsync(h_tmp + 2, d_nte, 8, hipMemcpyDeviceToHost, stream));
+    CCHK(hipStreamSynchronize(stream));
+    nte += h_tmp[2];
+  }
+  a.te_pos = d_te_pos;
+  a.te_g = d_te_g;
+  a.n_te = nte;
+  last_nte = nte;
   return SCOTTY_OK;
 }
 
@@ -198,7 +320,7 @@ int64_t CEngine::batch_edges_bound(int64_t lo_count, int64_t hi_count) const {
 
 // buffers and launch arguments for ingesting counts [C, C + n) (the whole stream's batch or a rank's chunk)
 int CEngine::prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, CPushArgs& a, int64_t& ebound,
-                     int64_t& maxp) {
+                     int64_t& maxp, int64_t n_te) {
   (void)range_lo;
   (void)range_hi;
   int64_t mark_from, extra = -1;
@@ -209,7 +331,7 @@ int CEngine::prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, C
     mark_from = pending;
   }
   const int64_t lo = std::max(C, mark_from), hi = C + n;
-  ebound = (extra >= C && extra < hi) ? 1 : 0;
+  ebound = ((extra >= C && extra < hi) ? 1 : 0) + n_te;
   maxp = 0;
   for (const CWin& w : wins) {
     const int64_t p = points_in(w, lo, hi);
@@ -281,10 +403,17 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
     n -= MAX_PUSH;
   }
   if (n <= 0) return SCOTTY_OK;
+  CPushArgs ta{};
+  int rc = time_edges(d_ts, n, ta);
+  if (rc) return rc;
   CPushArgs a;
   int64_t ebound = 0, maxp = 0;
-  int rc = prepare(count, n, count, count + n, a, ebound, maxp);
+  rc = prepare(count, n, count, count + n, a, ebound, maxp, ta.n_te);
   if (rc) return rc;
+  a.te_pos = ta.te_pos;
+  a.te_g = ta.te_g;
+  a.n_te = ta.n_te;
+  a.check_sorted = twins.empty() ? 0 : 1;
   if (tail_ub + ebound > scap) {
     rc = grow_slices(ebound);
     if (rc) return rc;
@@ -303,6 +432,8 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
 int CEngine::shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64_t ts0, int64_t n_before,
                         int64_t n_total, int64_t* d_rec) {
   if (failed) return SCOTTY_ERR_STATE;
+  if (!twins.empty())
+    return fail(SCOTTY_ERR_UNSUPPORTED, "sharded count path: time windows are not supported across shards yet");
   if (n_total > MAX_PUSH || n < 0 || n_before < 0 || n_before + n > n_total)
     return fail(SCOTTY_ERR_ARG, "shard chunk outside its micro-batch (or micro-batch above 2^28 tuples)");
   shard_total = n_total;
@@ -359,24 +490,27 @@ int CEngine::shard_commit(const int64_t* d_gathered, int world) {
   return SCOTTY_OK;
 }
 
-// ContextFreeWindow.triggerWindows of every count window with (lastCount, cend + 1), registration order
-// (S/WindowManager.java:104-118; C/windowType/TumblingWindow.java:34-39, SlidingWindow.java:50-57,
+// ContextFreeWindow.triggerWindows of every window in registration order: count windows with (lastCount, cend + 1),
+// time windows with (lastWatermark, watermark) (S/WindowManager.java:104-118; C/windowType/TumblingWindow.java:34-39, SlidingWindow.java:50-57,
 // FixedBandWindow.java:51-57)
-void CEngine::trigger(int64_t last, int64_t cur) {
+void CEngine::trigger(int64_t last_c, int64_t cur_c, int64_t last_t, int64_t cur_t) {
   rows.clear();
-  for (const CWin& w : wins) {
+  for (const CWin& w : reg) {
+    const bool tm = w.measure == SCOTTY_MEASURE_TIME;
+    const int64_t last = tm ? last_t : last_c, cur = tm ? cur_t : cur_c;
+    const int32_t ms = w.measure;
     if (w.kind == SCOTTY_WIN_TUMBLING) {
       const int64_t size = w.a;
       const int64_t ls = jsub(last, jmod(jadd(last, size), size));
-      for (int64_t s = ls; jadd(s, size) <= cur; s = jadd(s, size)) rows.push_back({s, jadd(s, size)});
+      for (int64_t s = ls; jadd(s, size) <= cur; s = jadd(s, size)) rows.push_back({s, jadd(s, size), ms});
     } else if (w.kind == SCOTTY_WIN_SLIDING) {
       const int64_t size = w.a, slide = w.b;
       const int64_t ls = jsub(cur, jmod(jadd(cur, slide), slide));
       for (int64_t s = ls; jadd(s, size) > last; s = jsub(s, slide))
-        if (s >= 0 && jadd(s, size) <= jadd(cur, 1)) rows.push_back({s, jadd(s, size)});
+        if (s >= 0 && jadd(s, size) <= jadd(cur, 1)) rows.push_back({s, jadd(s, size), ms});
     } else {
       const int64_t e = jadd(w.a, w.b);
-      if (last <= e && e <= cur) rows.push_back({w.a, e});
+      if (last <= e && e <= cur) rows.push_back({w.a, e, ms});
     }
   }
 }
@@ -406,6 +540,9 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     return fail(SCOTTY_ERR_UNSUPPORTED,
                 "a tuple older than its count slice would be inserted into an earlier LazySlice and shift records "
                 "(S/SliceManager.java:64-85): not implemented on the MI355X count path");
+  if (h_meta->err & 8)
+    return fail(SCOTTY_ERR_UNSUPPORTED, "count path with time windows: a micro-batch was not in timestamp order "
+                                        "(scotty_tune \"count_path\" 1 promises an in-order stream)");
   if (h_meta->err & 4)
     return fail(SCOTTY_ERR_NOMEM, "count-path shard record capacity exceeded (scotty_tune \"shard_count_cells\")");
   if (h_meta->err)
@@ -422,12 +559,17 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
           "S/WindowManager.java:109-112)";
     return SCOTTY_ERR_INDEX;
   }
-  trigger(last_count, jadd(h_meta->cend, 1));
+  trigger(last_count, jadd(h_meta->cend, 1), last_wm, wm);
   const int64_t nw = (int64_t)rows.size();
-  int64_t min_c = count, max_c = 0;
+  int64_t min_c = count, max_c = 0, min_t = JMAX, max_t = 0;  // S/WindowManager.java:61-71
   for (const Row& w : rows) {
-    min_c = std::min(min_c, w.start);
-    max_c = std::max(max_c, w.end);
+    if (w.meas == SCOTTY_MEASURE_TIME) {
+      min_t = std::min(min_t, w.start);
+      max_t = std::max(max_t, w.end);
+    } else {
+      min_c = std::min(min_c, w.start);
+      max_c = std::max(max_c, w.end);
+    }
   }
   if (nw > wcap) {
     dfree(d_wstart); dfree(d_wend); dfree(d_meas); dfree(d_has);
@@ -441,9 +583,6 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     CCHK(dalloc(&d_meas, wcap));
     CCHK(dalloc(&d_has, wcap));
     for (size_t k = 0; k < aggs.size(); k++) CCHK(dalloc(&d_vals[k], wcap));
-    std::vector<int32_t> ones(wcap, SCOTTY_MEASURE_COUNT);
-    CCHK(hipMemcpyAsync(d_meas, ones.data(), wcap * 4, hipMemcpyHostToDevice, stream));
-    CCHK(hipStreamSynchronize(stream));
   }
   const int64_t S_ub = tail_ub - head_lb + 2;
   if (prefix && S_ub > pcap) {
@@ -455,16 +594,22 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   }
   h_start.resize(nw);
   h_end.resize(nw);
+  h_meas.resize(nw);
   for (int64_t i = 0; i < nw; i++) {
     h_start[i] = rows[i].start;
     h_end[i] = rows[i].end;
+    h_meas[i] = rows[i].meas;
   }
   if (nw > 0) {
     CCHK(hipMemcpyAsync(d_wstart, h_start.data(), nw * 8, hipMemcpyHostToDevice, stream));
     CCHK(hipMemcpyAsync(d_wend, h_end.data(), nw * 8, hipMemcpyHostToDevice, stream));
+    CCHK(hipMemcpyAsync(d_meas, h_meas.data(), nw * 4, hipMemcpyHostToDevice, stream));
   }
   a.min_count = min_c;
   a.max_count = max_c;
+  a.min_ts = min_t;
+  a.max_ts = max_t;
+  a.w_meas = d_meas;
   a.gc_before = jsub(jsub(wm, max_lateness), max_fixed);
   a.w_start = d_wstart;
   a.w_end = d_wend;
@@ -503,7 +648,7 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   if (to_host && nw > 0) {
     r.start = h_start;
     r.end = h_end;
-    r.meas.assign(nw, SCOTTY_MEASURE_COUNT);
+    r.meas = h_meas;
     r.has.resize(nw);
     r.vals.assign(aggs.size(), std::vector<int64_t>(nw));
     CCHK(hipMemcpyAsync(r.has.data(), d_has, nw, hipMemcpyDeviceToHost, stream));

@@ -37,6 +37,8 @@ class CEngine {
   std::string err;
   bool failed = false;
 
+  int64_t last_nte = 0;  // time edges of the last push (debug stat)
+
  private:
   int grow_slices(int64_t need);
   int fail(int rc, const std::string& m) {
@@ -45,17 +47,22 @@ class CEngine {
     return rc;
   }
   int64_t next_point(int64_t x) const;  // smallest union count-grid point >= x (x >= 1)
-  int prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, CPushArgs& a, int64_t& ebound, int64_t& maxp);
+  int prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, CPushArgs& a, int64_t& ebound, int64_t& maxp,
+              int64_t n_te = 0);
   int64_t batch_edges_bound(int64_t lo_count, int64_t hi_count) const;
+  int time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a);
+  int64_t next_time_point(int64_t x) const;  // nextGrid over the time windows (calculateNextFixedEdge's min)
   int64_t shard_ts0 = INT64_MIN, shard_total = 0;
   long long* d_plan = nullptr;
   int plan_cap = 0;
-  void trigger(int64_t last_count, int64_t cend1);
+  void trigger(int64_t last_c, int64_t cur_c, int64_t last_t, int64_t cur_t);
 
   int device = 0;
   hipStream_t stream = nullptr;
   int vt = VT_I32;
-  std::vector<CWin> wins;
+  std::vector<CWin> wins;   // count windows (the device edge marking)
+  std::vector<CWin> twins;  // time windows: edges from the in-order stream's timestamps (time_edges)
+  std::vector<CWin> reg;    // every window in registration order (triggers)
   std::vector<int> aggs;
   int need = 0;
   int64_t max_lateness = 1000, max_fixed = 0;
@@ -64,7 +71,15 @@ class CEngine {
   int64_t count = 0;           // WindowManager.currentCount
   int64_t pending = INT64_MIN;  // StreamSlicer.min_next_edge_count
   int64_t last_wm = -1, last_count = 0;
+  int64_t t_pending = INT64_MIN;  // StreamSlicer.min_next_edge_ts (time windows)
+  int64_t h_prev_max = INT64_MIN; // StreamSlicer.maxEventTime after the last push (the stream is in order)
   bool started = false;
+  // time edges of the current push
+  int64_t tcap = 0, tecap = 0;
+  int64_t *d_cand = nullptr, *d_cpos = nullptr, *d_te_pos = nullptr, *d_te_g = nullptr;
+  int32_t* d_cflag = nullptr;
+  unsigned long long* d_nte = nullptr;
+  int64_t* h_tmp = nullptr;  // pinned scratch (batch ends, edge count)
   uint64_t dropped_ = 0;
   int64_t tail_ub = 0, head_lb = 0;  // slice range bounds between synchronisations
   // device
@@ -82,7 +97,9 @@ class CEngine {
   // watermark
   struct Row {
     int64_t start, end;
+    int32_t meas;
   };
+  std::vector<int32_t> h_meas;
   std::vector<Row> rows;
   int64_t wcap = 0, pcap = 0;
   int64_t *d_wstart = nullptr, *d_wend = nullptr;

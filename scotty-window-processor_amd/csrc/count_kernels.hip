@@ -77,6 +77,70 @@ __global__ __launch_bounds__(256) void count_mark_kernel(CPushArgs a) {
   for (int64_t m = first + g * step; m < hi; m += (int64_t)gridDim.x * blockDim.x * step) set(m);
 }
 
+// first time edge with batch position >= x
+__device__ __forceinline__ int64_t te_lb(const CPushArgs& a, int64_t x) {
+  int64_t l = 0, h = a.n_te;
+  while (l < h) {
+    const int64_t m = (l + h) >> 1;
+    if (a.te_pos[m] < x) l = m + 1; else h = m;
+  }
+  return l;
+}
+
+// ---------------------------------------------------------------- 1b. time edges (time windows, in-order stream)
+// Candidate k: the first tuple at or above cand[k] decides it (commit_kernel's rule, per candidate).
+__global__ void count_tcand_kernel(CTimeArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.n_cand) return;
+  const int64_t g = a.cand[k];
+  int64_t l = a.start, h = a.n;
+  while (l < h) {
+    const int64_t m = (l + h) >> 1;
+    if (a.ts[m] < g) l = m + 1; else h = m;
+  }
+  const int64_t p = l;  // < n: the host enumerates candidates up to the batch's last (= max) ts
+  const int64_t e = a.ts[p];
+  const int64_t m = p > a.start ? a.ts[p - 1] : a.prev_max;
+  // the pending edge is appended once crossed; a later grid point iff the running max before its first tuple
+  // reached the point before it, or that tuple lies within maxLateness of it (edges further back are skipped,
+  // calculateNextFixedEdge's max(te - maxLateness, edge)); `while (te > edge)` appends only edges >= 0
+  bool edge = k == 0 || a.cand[k - 1] <= m || (int64_t)((uint64_t)e - (uint64_t)g) < a.lateness;
+  edge = edge && (g >= 0 || e == g);
+  a.flag[k] = edge ? 1 : 0;
+  a.pos[k] = p;
+}
+
+// order-preserving compaction of the decided candidates (one workgroup; candidates per batch are few)
+__global__ __launch_bounds__(1024) void count_tcompact_kernel(CTimeArgs a) {
+  __shared__ int32_t wsum[16];
+  __shared__ long long base;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) base = 0;
+  __syncthreads();
+  for (int64_t k0 = 0; k0 < a.n_cand; k0 += 1024) {
+    const int64_t k = k0 + tid;
+    const bool f = k < a.n_cand && a.flag[k];
+    const unsigned long long bal = __ballot(f);
+    if (lane == 0) wsum[wid] = __popcll(bal);
+    __syncthreads();
+    int64_t before = base;
+    for (int w = 0; w < wid; w++) before += wsum[w];
+    if (f) {
+      const int64_t j = before + __popcll(bal & ((1ull << lane) - 1));
+      a.te_pos[j] = a.pos[k];
+      a.te_g[j] = a.cand[k];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      long long t = 0;
+      for (int w = 0; w < 16; w++) t += wsum[w];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *a.n_te = (unsigned long long)base;
+}
+
 // ---------------------------------------------------------------- 2. edges per step
 __global__ void count_stepc_kernel(CPushArgs a) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -87,6 +151,7 @@ __global__ void count_stepc_kernel(CPushArgs a) {
     const int64_t wi = s * 8 + k;
     if (wi < a.nwords) c += __popc(a.bits[wi]);
   }
+  if (a.n_te > 0) c += te_lb(a, (s + 1) * CSTEP) - te_lb(a, s * CSTEP);
   a.stepc[s] = c;
 }
 
@@ -213,12 +278,21 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         else v[j] = ok[j] ? ((const int64_t*)a.val)[idx[j]] : 0;
       }
     }
+    if (a.check_sorted) {  // the time-edge search (count_tcand_kernel) assumes a nondecreasing batch
+      const int64_t n0 = (int64_t)__shfl_down((long long)t[0], 1), n2 = (int64_t)__shfl_down((long long)t[2], 1);
+      const int64_t l2 = (int64_t)__shfl((long long)t[2], 0);
+      const int64_t s1 = lane < 63 ? n0 : l2;                                       // successor of i0 + 1
+      const int64_t s3 = lane < 63 ? n2 : (i1 + 2 < a.n ? a.ts[i1 + 2] : JMAX);  // successor of i1 + 1
+      const bool bad = (i0 + 1 < a.n && t[1] < t[0]) || (i0 + 2 < a.n && s1 < t[1]) ||
+                       (i1 + 1 < a.n && t[3] < t[2]) || (i1 + 2 < a.n && s3 < t[3]);
+      if (bad) atomicOr((unsigned long long*)&a.meta->err, 8ull);
+    }
     int64_t smax = JMIN;
 #pragma unroll
     for (int j = 0; j < 4; j++) smax = max(smax, t[j]);
     smax = wred(smax, [](long long p, long long q) { return p > q ? p : q; });
     if (lane == 0) a.stepmax[s] = smax;
-    // edge words of the step (wave-uniform)
+    // edge words of the step (wave-uniform), and the step's time edges [t0, t1)
     uint32_t wd[8];
     uint32_t any = 0;
 #pragma unroll
@@ -226,6 +300,12 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
       const int64_t wi = s * 8 + k;
       wd[k] = wi < a.nwords ? __builtin_amdgcn_readfirstlane(a.bits[wi]) : 0u;
       any |= wd[k];
+    }
+    int64_t t0 = 0, t1 = 0;
+    if (a.n_te > 0) {
+      t0 = uni(te_lb(a, base));
+      t1 = uni(te_lb(a, base + CSTEP));
+      if (t1 > t0) any |= 1u;
     }
     const int64_t sb = uni(a.stepbase[s]);
     if (any == 0) {
@@ -246,7 +326,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
     pre[0] = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) pre[k + 1] = pre[k] + __popc(wd[k]);
-    const int64_t last = sb + pre[8];
+    const int64_t last = sb + pre[8] + (t1 - t0);
     if (last != cur) {
       if (cur >= 0) flush();
       cur = last;
@@ -261,7 +341,9 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
       }
       const int o = off[j], q = o >> 5, b = o & 31;
       const uint32_t mask = (uint32_t)((2ull << b) - 1);
-      const int64_t cell = sb + pre[q] + __popc(wd[q] & mask);
+      int64_t tcnt = 0;  // time edges at or before this tuple (the tuple lands in the last slice appended)
+      for (int64_t k = t0; k < t1; k++) tcnt += a.te_pos[k] <= base + o ? 1 : 0;
+      const int64_t cell = sb + pre[q] + __popc(wd[q] & mask) + tcnt;
       if (cell == cur) {
         add(t[j], v[j]);
       } else {
@@ -341,12 +423,19 @@ __global__ __launch_bounds__(256) void count_edges_kernel(CPushArgs a) {
     pre[k + 1] = pre[k] + __popc(wd[k]);
   }
   const int64_t sb = a.stepbase[s];
+  int64_t t0 = 0, t1 = 0;
+  if (a.n_te > 0) {
+    t0 = te_lb(a, base);
+    t1 = te_lb(a, base + CSTEP);
+  }
   int64_t run = max((int64_t)before, ex);
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int o = 4 * lane + j, q = o >> 5, b = o & 31;
     if ((wd[q] >> b) & 1u) {
-      const int64_t e = sb + pre[q] + __popc(wd[q] & ((1u << b) - 1u));  // edges strictly before o
+      int64_t tb = 0;  // time edges of earlier tuples of the step (at this tuple they follow the count edge)
+      for (int64_t k = t0; k < t1; k++) tb += a.te_pos[k] < base + o ? 1 : 0;
+      const int64_t e = sb + pre[q] + __popc(wd[q] & ((1u << b) - 1u)) + tb;  // edges strictly before o
       a.cells.e_pos[e] = base + o;
       // max ts of every tuple before the edge (StreamSlicer.maxEventTime); the stream's first tuple sets it to its
       // own ts first (S/StreamSlicer.java:39-40)
@@ -354,6 +443,25 @@ __global__ __launch_bounds__(256) void count_edges_kernel(CPushArgs a) {
     }
     run = max(run, t[j]);
   }
+}
+
+// index, position and tStart (the edge itself, SliceManager.appendSlice(min_next_edge_ts)) of every time edge
+__global__ void count_tedges_kernel(CPushArgs a) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.n_te) return;
+  const int64_t p = a.te_pos[j], s = p / CSTEP, o = p - s * CSTEP;
+  int64_t cb = 0;  // count edges of the step at or before this tuple
+  for (int k = 0; k < 8; k++) {
+    const int64_t wi = s * 8 + k;
+    if (wi >= a.nwords) break;
+    const uint32_t w = a.bits[wi];
+    const int lo = k * 32;
+    if (o >= lo + 31) cb += __popc(w);
+    else if (o >= lo) cb += __popc(w & (uint32_t)((2ull << (o - lo)) - 1));
+  }
+  const int64_t e = a.stepbase[s] + cb + (j - te_lb(a, s * CSTEP));
+  a.cells.e_pos[e] = p;
+  a.cells.e_ts[e] = a.te_g[j];
 }
 
 // ---------------------------------------------------------------- 5. append
@@ -451,16 +559,17 @@ __global__ void count_wm_find_kernel(CWmArgs a) {
   m.wm_status = 0;
 }
 
-// LazyAggregateStore.aggregate start/end index (time terms with no time windows: minTs = MAX, maxTs = 0)
+// LazyAggregateStore.aggregate start/end index (S/aggregationstore/LazyAggregateStore.java:83-90; with no time
+// windows minTs = MAX, maxTs = 0)
 __global__ void count_wm_range_kernel(CWmArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   CMeta& m = *a.meta;
   const int64_t head = m.head, tail = m.tail, S = tail - head;
   auto rel = [&](int64_t i) { return i < head ? (int64_t)-1 : i - head; };
   // cLast is not stored; cStart is nondecreasing, findSliceIndexByCount = last slice with cStart <= c
-  int64_t si = max(rel(last_le(a.sl.ts, head, tail, JMAX)), (int64_t)0);
+  int64_t si = max(rel(last_le(a.sl.ts, head, tail, a.min_ts)), (int64_t)0);
   si = min(si, rel(last_le(a.sl.cs, head, tail, a.min_count)));
-  int64_t ei = min(S - 1, rel(last_le(a.sl.ts, head, tail, 0)));
+  int64_t ei = min(S - 1, rel(last_le(a.sl.ts, head, tail, a.max_ts)));
   ei = max(ei, rel(last_le(a.sl.cs, head, tail, a.max_count)));
   if (si < 0 && si <= ei) {
     m.range_err = 1;
@@ -566,20 +675,22 @@ __global__ __launch_bounds__(256) void count_wm_agg_kernel(CWmArgs a) {
   const int64_t wi = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   if (wi >= a.nw) return;
   const int64_t ws = a.w_start[wi], we = a.w_end[wi];
+  const bool tmeas = a.w_meas && a.w_meas[wi] == SCOTTY_MEASURE_TIME;
   const int64_t r_lo = a.meta->r_lo, r_hi = a.meta->r_hi;
-  // contained slices (AggregateWindowState.containsSlice, count measure: ws <= cStart && we >= cLast):
-  // cStart >= ws is a suffix, cLast = cStart + cnt <= we a prefix (both nondecreasing)
+  // contained slices (AggregateWindowState.containsSlice, S/state/AggregateWindowState.java:25-35): count
+  // measure ws <= cStart && we >= cLast, cStart >= ws a suffix and cLast = cStart + cnt <= we a prefix; time
+  // measure ws <= tStart && we > tLast, both nondecreasing on an in-order stream's slices
   int64_t l = r_lo, h = r_hi;
   while (l < h) {
     const int64_t mid = (l + h) >> 1;
-    if (a.sl.cs[mid] < ws) l = mid + 1; else h = mid;
+    if ((tmeas ? a.sl.ts[mid] : a.sl.cs[mid]) < ws) l = mid + 1; else h = mid;
   }
   const int64_t lo = l;
   l = lo;
   h = r_hi;
   while (l < h) {
     const int64_t mid = (l + h) >> 1;
-    if (a.sl.cs[mid] + (int64_t)a.sl.cnt[mid] <= we) l = mid + 1; else h = mid;
+    if (tmeas ? a.sl.tl[mid] < we : a.sl.cs[mid] + (int64_t)a.sl.cnt[mid] <= we) l = mid + 1; else h = mid;
   }
   const int64_t hi = l;
   uint64_t cnt = 0, sw = 0;
@@ -796,11 +907,20 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
                        premax_tmp);
   }
   hipLaunchKernelGGL(ck::count_edges_kernel, dim3((unsigned)((a.nsteps * 64 + 255) / 256)), dim3(256), 0, st, a);
+  if (a.n_te > 0)
+    hipLaunchKernelGGL(ck::count_tedges_kernel, dim3((unsigned)((a.n_te + 255) / 256)), dim3(256), 0, st, a);
   if (a.shard) return hipGetLastError();  // the caller exports (launch_count_export) instead of appending
   const unsigned ab = (unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 8192);
   if (a.vt == VT_F64) hipLaunchKernelGGL(ck::count_append_kernel<VT_F64>, dim3(ab), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(ck::count_append_kernel<VT_I32>, dim3(ab), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ck::count_finish_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_time_edges(const CTimeArgs& a, hipStream_t st) {
+  if (a.n_cand <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ck::count_tcand_kernel, dim3((unsigned)((a.n_cand + 255) / 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(ck::count_tcompact_kernel, dim3(1), dim3(1024), 0, st, a);
   return hipGetLastError();
 }
 

@@ -756,7 +756,7 @@ int scotty_add_window(scotty_op* op, int kind, int measure, int64_t a, int64_t b
   const bool exact_only = kind == SCOTTY_WIN_SESSION || measure == SCOTTY_MEASURE_COUNT;
   if (op->mode == 3) {  // count path: more count windows mid-stream (the pending count edge keeps its value)
     if (kind == SCOTTY_WIN_SESSION || measure != SCOTTY_MEASURE_COUNT)
-      return fail(op, SCOTTY_ERR_UNSUPPORTED, "time / session window added to a count-window operator after elements "
+      return fail(op, SCOTTY_ERR_UNSUPPORTED, "time / session window added to a count-path operator after elements "
                                               "were processed");
     op->xwins.push_back({kind, measure, a, b});
     int rc = op->c->configure(op->xwins, op->aggs, op->max_lateness);
@@ -849,9 +849,11 @@ static int decide_mode(scotty_op* op) {
     op->mode = 1;
     return SCOTTY_OK;
   }
+  // count path: context-free windows only, at least one of them on the count measure (time windows' edges come
+  // from the in-order stream's timestamps, CEngine::time_edges)
   bool count_only = !op->keyed && !op->xwins.empty() && op->x_count_on;
   for (const XWinDef& w : op->xwins)
-    if (w.kind == SCOTTY_WIN_SESSION || w.measure != SCOTTY_MEASURE_COUNT) count_only = false;
+    if (w.kind == SCOTTY_WIN_SESSION) count_only = false;
   if (count_only) {  // count_common.h: edges are a function of counts, one micro-batch = segmented reduction
     op->c = new CEngine();
     std::string e;
@@ -1428,7 +1430,10 @@ int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
 // 2 path of the last push (0 replay, 1 sort-free, 2 sort-free + replay of deferred keys), 3 deferred tuples,
 // 4 keys committed on the sort-free path).
 int64_t scotty_debug_stat(scotty_op* op, int which) {
-  if (!op || !op->x) return -1;
+  if (!op) return -1;
+  if (which == 5) return op->mode;  // 1 grid path, 2 exact engine, 3 count path
+  if (which == 6) return op->c ? op->c->last_nte : -1;
+  if (!op->x) return -1;
   switch (which) {
     case 0: return op->x->last_events;
     case 1: return op->x->last_segments;

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from helpers import product, build_ops, run_schedule, interval_schedule, same_windows
-from specs import Tumbling, Sliding, FixedBand, Count, SUM, COUNT, MIN, MAX, SUM_I64, MIN_I64, MAX_I64, \
+from specs import Tumbling, Sliding, FixedBand, Count, Time, SUM, COUNT, MIN, MAX, SUM_I64, MIN_I64, MAX_I64, \
     SUM_F64, MIN_F64, MAX_F64
 
 pytestmark = pytest.mark.gpu
@@ -123,6 +123,116 @@ def test_count_config5_reduced():
     for tune in ({"count_path": 1}, None):
         gpu, ora = build_ops(cfg, tune=tune)
         assert run_schedule(gpu, ora, ts, vals, interval_schedule(ts, 16, lag=0, pushes_per_interval=2)) > 1000
+
+
+def _time_windows(rng, scale):
+    """Steps are never powers of two: assignNextWindowStart(Long.MAX_VALUE) then wraps to Long.MIN_VALUE and the
+    reference's first calculateNextFixedEdge loops forever (both sides fail, test_count_path_hang_config)."""
+    def step(lo, hi):
+        v = int(rng.integers(lo, hi))
+        while v & (v - 1) == 0:
+            v += 1
+        return v
+    wins = []
+    for _ in range(int(rng.integers(1, 4))):
+        r = rng.random()
+        if r < 0.4:
+            wins.append(Tumbling(Time, step(1, scale)))
+        elif r < 0.85:
+            size = int(rng.integers(3, 4 * scale))
+            wins.append(Sliding(Time, size, min(size, step(1, size + 1))))
+        else:
+            wins.append(FixedBand(Time, int(rng.integers(0, 20 * scale)), int(rng.integers(1, 10 * scale))))
+    return wins
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_count_and_time_windows_on_count_path_match_oracle(pkg, seed):
+    """Count windows plus context-free time windows (SURVEY C5's shape) on the count path: the time edges come
+    from the in-order stream (CEngine::time_edges: the first tuple's calculateNextFixedEdge walk, then one
+    candidate per union grid point decided by the first tuple reaching it, S/StreamSlicer.java:46-83); triggers
+    in registration order with (lastWatermark, watermark) for time windows (S/WindowManager.java:104-118)."""
+    rng = np.random.default_rng(13000 + seed)
+    vt = ["i32", "i32", "i64", "f64"][seed % 4]
+    wins = _count_windows(rng, [20, 200, 2000][seed % 3]) + _time_windows(rng, [30, 300, 3000][(seed // 3) % 3])
+    order = rng.permutation(len(wins))
+    cfg = dict(windows=[wins[i] for i in order], aggs=_aggs(rng, vt), lateness=int(rng.choice([1, 7, 100, 5000])))
+    n = int(rng.integers(1000, 60_000))
+    ts, vals = _in_order_stream(rng, n, [0.3, 2, 25, 0.05][seed % 4], int(rng.integers(0, 5000)), vt)
+    gpu, ora = build_ops(cfg, vt, tune={"count_path": 1})
+    sched = interval_schedule(ts, int(rng.integers(1, 12)), lag=int(rng.integers(0, 50)),
+                              pushes_per_interval=int(rng.integers(1, 4)))
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
+    run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols)
+    assert gpu._debug_stat(5) == 3
+
+
+def test_survey_c5_reduced_matches_oracle(pkg):
+    """SURVEY C5 at reduced size: TumblingWindow(Count, 1000) + SlidingWindow(Time, 60000, 1000), SUM + COUNT,
+    in-order unique timestamps (tsgap 1..3 ms), a watermark per second of event time."""
+    rng = np.random.default_rng(13500)
+    cfg = dict(windows=[Tumbling(Count, 1000), Sliding(Time, 60000, 1000)], aggs=[SUM, COUNT], lateness=1)
+    n = 300_000
+    ts = 5 + np.cumsum(rng.integers(1, 4, size=n)).astype(np.int64)
+    vals = rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    gpu, ora = build_ops(cfg, tune={"count_path": 1})
+    sched = interval_schedule(ts, int((ts[-1] - ts[0]) // 1000), lag=0, pushes_per_interval=2)
+    assert run_schedule(gpu, ora, ts, vals, sched) > 800  # 300 count + 540 time windows
+    assert gpu._debug_stat(5) == 3
+
+
+@pytest.mark.parametrize("lateness", [1, 40, 100_000])
+def test_count_path_time_edges_small_pushes(pkg, lateness):
+    """One-tuple and few-tuple pushes (the first tuple's edge walk alone, candidates at batch ends), a first
+    timestamp far above 0 (edges in (te - maxLateness, te] from the first walk), ties at grid points."""
+    rng = np.random.default_rng(13600 + lateness)
+    cfg = dict(windows=[Sliding(Count, 7, 3), Tumbling(Time, 10), Sliding(Time, 25, 5)], aggs=[SUM, COUNT, MAX],
+               lateness=lateness)
+    ts = np.sort(rng.integers(100_000, 100_600, size=3000)).astype(np.int64)
+    ts[1000:1010] = ts[1000]  # a run of ties
+    vals = rng.integers(-1000, 1000, size=3000).astype(np.int32)
+    gpu, ora = build_ops(cfg, tune={"count_path": 1})
+    sched, lo = [], 0
+    for size in [1, 1, 2, 5, 1, 40, 300, 1, 700, 1950]:
+        hi = min(len(ts), lo + size)
+        sched += [("push", lo, hi), ("wm", int(ts[hi - 1]) - 3)]  # early ones throw on both sides (getSlice(-1))
+        lo = hi
+    assert run_schedule(gpu, ora, ts, vals, sched) > 0
+    assert gpu._debug_stat(5) == 3
+
+
+def test_count_path_hang_config(pkg):
+    """A time window whose step is a power of two: the reference's first calculateNextFixedEdge yields
+    Long.MIN_VALUE forever (S/StreamSlicer.java:53-69); the oracle and the count path both refuse."""
+    cfg = dict(windows=[Tumbling(Count, 10), Tumbling(Time, 64)], aggs=[SUM], lateness=1)
+    ts = np.arange(100, 200, dtype=np.int64)
+    vals = np.ones(len(ts), dtype=np.int32)
+    gpu, ora = build_ops(cfg, tune={"count_path": 1})
+    with pytest.raises(pkg.ScottyError):
+        gpu.processElements(ts, vals)
+        gpu.processWatermark(150)
+    assert ora.processElements(ts, vals) > 0  # the oracle reports the tuples whose processElement would hang
+
+
+def test_count_path_time_windows_reject_out_of_order(pkg):
+    """Time windows on the count path need the in-order promise: a batch out of timestamp order fails loudly
+    (within a batch at the watermark, across batches at the push) instead of slicing on a wrong search."""
+    cfg = dict(windows=[Tumbling(Count, 10), Tumbling(Time, 100)], aggs=[SUM], lateness=1000)
+    ts = np.arange(1000, 3000, dtype=np.int64)
+    vals = np.ones(len(ts), dtype=np.int32)
+    bad = ts.copy()
+    bad[700], bad[701] = bad[701], bad[700] - 50
+    gpu, _ = build_ops(cfg, tune={"count_path": 1})
+    gpu.processElements(bad, vals)
+    with pytest.raises(pkg.ScottyError) as e:
+        gpu.processWatermark(2500)
+    assert e.value.code == -2
+    gpu, _ = build_ops(cfg, tune={"count_path": 1})
+    gpu.processElements(ts[1000:], vals[1000:])
+    with pytest.raises(pkg.ScottyError) as e:
+        gpu.processElements(ts[:1000], vals[:1000])
+        gpu.processWatermark(2500)
+    assert e.value.code == -2
 
 
 @pytest.fixture(scope="module")
