@@ -193,6 +193,24 @@ def cpu_c5(pkg, rate):
                          "C5 from the stream start at %d tuples/ms (count windows fire every 1M-20M tuples)" % rate)
 
 
+def cpu_c5t(step):
+    def setup(op):
+        op.addWindowFunction(0)
+        op.addWindowFunction(1)
+        op.setMaxLateness(1)
+        op.addWindowAssigner(0, 1, 1000, 0)
+        op.addWindowAssigner(1, 0, 60_000, 1000)
+    rng = np.random.default_rng(16)
+
+    def gen(s):
+        ts = np.arange(s * step, (s + 1) * step, dtype=np.int64)
+        return ts, rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64)
+    return _cpu_nonkeyed(setup, gen, lambda s, lt, partial=False: lt, range(100000), CPU_BUDGET_S, 1 << 20, None,
+                         "SURVEY C5 from the stream start, unique ts, a watermark per %d tuples (the GPU leg's 2^26 "
+                         "would put LazyAggregateStore.aggregate's slices x windows scan at ~10^10 per watermark)"
+                         % step)
+
+
 def cpu_c4(keys, batch, threads):
     """KeyedScottyWindowOperator on T threads (key % T partitions): sparse warm-up (2^20 tuples per second for
     60 s, so every key's operator holds its sliding-window slices), then full-rate steps of the GPU leg."""
@@ -391,6 +409,62 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
                               "frac": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9 / HBM_PEAK_GBS}}
 
 
+def extra_c5t(pkg, dev, batch, steps, warm=3, rank=0, world=1, dist=None):
+    """TumblingWindow(Count, 1000) + SlidingWindow(Time, 60000, 1000), SUM_I32 + COUNT, non-keyed,
+    in-order with unique timestamps (ts = global arrival index), maxLateness 1, one watermark per micro-batch of
+    world * batch tuples; count path with time edges (CEngine::time_edges).  world > 1: arrival-range sharding,
+    rank r holds chunk r of every micro-batch, one all-gather of count-cell records per batch; weak scaling."""
+    import torch
+    G = world
+    g = torch.Generator(device=dev)
+    g.manual_seed(19 + rank)
+    if G > 1:
+        op = pkg.ShardedSlicingWindowOperator(device=dev.index)
+    else:
+        op = pkg.SlicingWindowOperator(device=dev.index)
+        op.tune("count_path", 1)  # in-order stream: count + time windows on the count path
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.addWindowFunction(pkg.AGG_COUNT)
+    op.setMaxLateness(1)
+    op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, 1000))
+    op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60000, 1000))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) + rank * batch
+    times, rows = [], 0
+    for s in range(warm + steps):
+        ts = base + s * G * batch
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        if dist is not None and s == warm:
+            dist.barrier()
+        t0 = time.perf_counter()
+        wm = (s + 1) * G * batch - 1
+        if G > 1:
+            op.processChunk(ts.data_ptr(), v.data_ptr(), batch, 0, n_before=rank * batch, n_total=G * batch,
+                            ts_before=s * G * batch + rank * batch - 1 if s * G + rank > 0 else -2**63, ts_last=wm)
+        else:
+            op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(wm)
+        torch.cuda.synchronize(dev)
+        if s >= warm:
+            times.append(time.perf_counter() - t0)
+            rows += n
+    elapsed = sum(times)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    return {"workload": "C5 (SURVEY): TumblingWindow(Count,1000) + SlidingWindow(Time,60000,1000), SUM_I32+COUNT, "
+                        "in-order unique ts (ts = arrival index), maxLateness=1, a watermark per %d-tuple micro-batch%s"
+                        % (batch * G, ", arrival-range sharded over %d GPUs (RCCL all-gather of count cells)" % G
+                           if G > 1 else ""),
+            "tuples_per_step": batch * G, "tuples_per_step_per_gpu": batch, "steps": steps,
+            "ms_per_step": 1e3 * elapsed / len(times), "value": batch * G * len(times) / elapsed, "unit": "tuples/s",
+            "scaling": "weak", "windows_emitted": rows,
+            "roofline_wall": {"achieved": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9,
+                              "frac": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9 / HBM_PEAK_GBS}}
+
+
 def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None):
     """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
     connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
@@ -503,7 +577,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
-    ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5,pcie); default all")
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5,c5t,pcie); default all")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
@@ -627,7 +701,7 @@ def main():
                                        % world) if sharded else "single GPU"},
             "roofline": roof,
         }
-    legs = set(x for x in args.only.split(",") if x) or {"c2s", "c3", "c4", "c5", "pcie"}
+    legs = set(x for x in args.only.split(",") if x) or {"c2s", "c3", "c4", "c5", "c5t", "pcie"}
     extra = {}
     if not args.no_extra:
         del batches
@@ -646,12 +720,16 @@ def main():
             if "c5" in legs:
                 extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)
                 log("bench: C5 done")
+            if "c5t" in legs:
+                extra["c5t"] = extra_c5t(pkg, dev, 1 << 26, 5)
+                log("bench: C5t done")
             if "pcie" in legs:
                 extra["pcie_inclusive"] = extra_pcie(pkg, sizes, 1 << 26, 5)
                 log("bench: PCIe-inclusive C2 done")
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
             extra = {"c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, rank=rank, world=world, dist=dist),
-                     "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist)}
+                     "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist),
+                     "c5t": extra_c5t(pkg, dev, 1 << 26, 5, rank=rank, world=world, dist=dist)}
     if rank == 0:
         if extra:
             res["extra"] = extra
@@ -661,7 +739,8 @@ def main():
             log("bench: CPU C2 done")
             threads = min(16, os.cpu_count() or 1)  # the box's CPU share for one GPU
             cb = {"c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
-                  "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000)}
+                  "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000),
+                  "c5t": lambda: cpu_c5t(1 << 20)}
             for name, fn in cb.items():
                 if name in extra:
                     extra[name]["cpu_baseline"] = fn()

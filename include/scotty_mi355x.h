@@ -144,8 +144,8 @@ int scotty_process_watermark_device(scotty_op* op, int64_t watermark_ts, scotty_
  *   3. scotty_shard_commit(op, gathered, G): every rank decides the same slice edges (StreamSlicer rule from
  *      the global first crossings, S/StreamSlicer.java:55-116) and folds every rank's partials.
  * Watermarks then run unchanged (and identically) on every rank.  Context-free time windows only (the grid
- * path) or count windows only (the count path, with scotty_shard_push_counted); other configurations return
- * SCOTTY_ERR_UNSUPPORTED. */
+ * path), or count windows with optional context-free time windows (the count path, with
+ * scotty_shard_push_counted / scotty_shard_push_timed); other configurations return SCOTTY_ERR_UNSUPPORTED. */
 size_t scotty_shard_xbytes(scotty_op* op);
 int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0, void* d_xbuf);
 int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world);
@@ -155,6 +155,14 @@ int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world);
  * only in-order streams; the record holds per-rank count cells (count_common.h). */
 int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
                               int64_t n_before, int64_t n_total, void* d_xbuf);
+/* Step 1 for count-path operators that also hold context-free TIME windows (in-order stream):
+ * additionally ts_before = the largest timestamp of the micro-batch's tuples on lower ranks (INT64_MIN if none)
+ * and ts_last = the micro-batch's largest timestamp (INT64_MIN if it is empty).  The time edges a chunk appends
+ * are decided from them locally (count_engine.cpp, CEngine::time_edges); callers gather {n, first ts, last ts}
+ * per rank before the push (one small all-gather, like the counts). */
+int scotty_shard_bounds(scotty_op* op, const int64_t* d_ts, size_t n, int64_t* first_last);  /* chunk's first/last ts */
+int scotty_shard_push_timed(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
+                            int64_t n_before, int64_t n_total, int64_t ts_before, int64_t ts_last, void* d_xbuf);
 
 /* Number of keys (operators) of a keyed op. */
 int64_t scotty_key_count(scotty_op* op);

@@ -150,6 +150,8 @@ def lib():
             "scotty_shard_push": (ctypes.c_int, [P, P, P, ctypes.c_size_t, i64, P]),
             "scotty_shard_commit": (ctypes.c_int, [P, P, ctypes.c_int]),
             "scotty_shard_push_counted": (ctypes.c_int, [P, P, P, ctypes.c_size_t, i64, i64, i64, P]),
+            "scotty_shard_push_timed": (ctypes.c_int, [P, P, P, ctypes.c_size_t, i64, i64, i64, i64, i64, P]),
+            "scotty_shard_bounds": (ctypes.c_int, [P, P, ctypes.c_size_t, P]),
             "scotty_dropped_count": (u64, [P]),
             "scotty_processed_count": (u64, [P]),
             "scotty_slice_count": (i64, [P]),
@@ -351,6 +353,17 @@ class SlicingWindowOperator:
         self._flush()
         self._check(self._l.scotty_shard_push_counted(self._h, ts_ptr, val_ptr, n, ts0, n_before, n_total, xbuf_ptr))
 
+    def shardPushTimed(self, ts_ptr, val_ptr, n, ts0, n_before, n_total, ts_before, ts_last, xbuf_ptr):
+        self._flush()
+        self._check(self._l.scotty_shard_push_timed(self._h, ts_ptr, val_ptr, n, ts0, n_before, n_total, ts_before,
+                                                    ts_last, xbuf_ptr))
+
+    def shardBounds(self, ts_ptr, n):
+        """(first, last) timestamp of a device chunk (INT64_MIN for an empty one)."""
+        out = (ctypes.c_int64 * 2)()
+        self._check(self._l.scotty_shard_bounds(self._h, ts_ptr, n, ctypes.addressof(out)))
+        return int(out[0]), int(out[1])
+
     def shardCommit(self, gathered_ptr, world):
         self._check(self._l.scotty_shard_commit(self._h, gathered_ptr, world))
 
@@ -490,9 +503,18 @@ class ShardedSlicingWindowOperator:
         self.dev = torch.device("cuda", device)
         self.staged = dist.get_backend(group) != "nccl"
         self._xb = None
+        self._assigned = []
 
-    def __getattr__(self, name):  # addWindowAssigner, addWindowFunction, setMaxLateness, processWatermark...
+    def __getattr__(self, name):  # addWindowFunction, setMaxLateness, processWatermark...
         return getattr(self.op, name)
+
+    def addWindowAssigner(self, window):
+        self.op.addWindowAssigner(window)
+        self._assigned.append(window)
+
+    def _count_and_time(self):
+        ms = {w.measure for w in self._assigned}
+        return {0, 1} <= ms  # SCOTTY_MEASURE_TIME, SCOTTY_MEASURE_COUNT
 
     def _bufs(self):
         if self._xb is None:
@@ -505,20 +527,31 @@ class ShardedSlicingWindowOperator:
                 self._hg = t.empty(words * self.world, dtype=t.int64)
         return self._xb, self._gb
 
-    def processChunk(self, ts_ptr, val_ptr, n, ts0=0, n_before=None, n_total=None):
+    def processChunk(self, ts_ptr, val_ptr, n, ts0=0, n_before=None, n_total=None, ts_before=None, ts_last=None):
         """This rank's arrival chunk of the next global micro-batch (device pointers); ts0 = the global first
         tuple's timestamp (read on the very first batch only).  n_before / n_total: tuples of the lower ranks /
-        of all ranks in this micro-batch (count windows number tuples globally); gathered when not given."""
-        if n_before is None or n_total is None:
+        of all ranks in this micro-batch (count windows number tuples globally); ts_before / ts_last: the largest
+        timestamp on the lower ranks / in the whole micro-batch (count + time windows); gathered when not given."""
+        timed = self._count_and_time()
+        if n_before is None or n_total is None or (timed and (ts_before is None or ts_last is None)):
+            # one small all-gather of {n, first ts, last ts} per rank (count windows number tuples globally; time
+            # windows on the count path decide a chunk's edges from the max ts before it, CEngine::time_edges)
             t = self.torch
-            mine = t.tensor([n], dtype=t.int64, device=self.dev if not self.staged else "cpu")
-            allv = t.empty(self.world, dtype=t.int64, device=mine.device)
+            first, last = self.op.shardBounds(ts_ptr, n) if timed else (0, 0)
+            mine = t.tensor([n, first, last], dtype=t.int64, device=self.dev if not self.staged else "cpu")
+            allv = t.empty(3 * self.world, dtype=t.int64, device=mine.device)
             self.dist.all_gather_into_tensor(allv, mine, group=self.group)
-            sizes = allv.tolist()
+            g = allv.view(self.world, 3).tolist()
             r = self.dist.get_rank(self.group)
-            n_before, n_total = int(sum(sizes[:r])), int(sum(sizes))
+            n_before, n_total = int(sum(x[0] for x in g[:r])), int(sum(x[0] for x in g))
+            lasts = [x[2] for x in g if x[0] > 0]
+            ts_before = max([x[2] for x in g[:r] if x[0] > 0], default=-2**63)
+            ts_last = max(lasts, default=-2**63)
         xb, gb = self._bufs()
-        self.op.shardPushCounted(ts_ptr, val_ptr, n, ts0, n_before, n_total, xb.data_ptr())
+        if timed:
+            self.op.shardPushTimed(ts_ptr, val_ptr, n, ts0, n_before, n_total, ts_before, ts_last, xb.data_ptr())
+        else:
+            self.op.shardPushCounted(ts_ptr, val_ptr, n, ts0, n_before, n_total, xb.data_ptr())
         if self.staged:
             self._hx.copy_(xb)
             self.dist.all_gather_into_tensor(self._hg, self._hx, group=self.group)

@@ -159,23 +159,39 @@ int64_t CEngine::next_time_point(int64_t x) const {
 // stream's first tuple walks calculateNextFixedEdge as the reference does (Long.MAX_VALUE start, edges < 0 not
 // appended, :103-116); after it every union grid point from the pending edge up to the batch max is a candidate
 // decided on the device by the first tuple reaching it.  Fills a.te_* (edges in position order).
-int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a) {
+// Sharded (sh != nullptr): this chunk's part of a global micro-batch.  With maxLateness >= 0 the pending edge after
+// a tuple is the first grid point above it, so the first grid point above the max ts before the chunk
+// (sh->ts_before) is an edge wherever it is first reached, and the chunk decides exactly the grid points in
+// (ts before, chunk max]; the pending edge, maxEventTime and the batch's candidate count (the commit's slice bound)
+// are computed identically on every rank from the batch max (sh->ts_last).
+int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const ShardTime* sh) {
   a.te_pos = nullptr;
   a.te_g = nullptr;
   a.n_te = 0;
-  if (twins.empty() || n <= 0) return SCOTTY_OK;
-  CCHK(hipMemcpyAsync(h_tmp, d_ts, 8, hipMemcpyDeviceToHost, stream));
-  CCHK(hipMemcpyAsync(h_tmp + 1, d_ts + n - 1, 8, hipMemcpyDeviceToHost, stream));
-  CCHK(hipStreamSynchronize(stream));
-  const int64_t t_first = h_tmp[0], t_last = h_tmp[1];
-  if (t_last < t_first || (started && t_first < h_prev_max))
+  shard_te_bound = 0;
+  if (twins.empty() || (sh ? sh->n_total : n) <= 0) return SCOTTY_OK;
+  if (max_lateness < 0)
+    return fail(SCOTTY_ERR_UNSUPPORTED, "count path with time windows: negative maxLateness");
+  int64_t t_first = JMAX, t_last = JMIN;
+  if (n > 0) {
+    CCHK(hipMemcpyAsync(h_tmp, d_ts, 8, hipMemcpyDeviceToHost, stream));
+    CCHK(hipMemcpyAsync(h_tmp + 1, d_ts + n - 1, 8, hipMemcpyDeviceToHost, stream));
+    CCHK(hipStreamSynchronize(stream));
+    t_first = h_tmp[0];
+    t_last = h_tmp[1];
+  }
+  const int64_t before = sh ? sh->ts_before : JMIN;       // max ts of the batch's tuples before this chunk
+  const int64_t batch_last = sh ? sh->ts_last : t_last;  // max ts of the whole batch
+  const int64_t stream_first = sh ? sh->ts0 : t_first;   // the stream's first tuple (first batch only)
+  const bool first_here = !started && (sh ? sh->n_before == 0 : true) && n > 0;
+  if (n > 0 && (t_last < t_first || (started && t_first < h_prev_max) || t_first < before))
     return fail(SCOTTY_ERR_UNSUPPORTED, "count path with time windows: the stream must be in timestamp order "
                                         "(scotty_tune \"count_path\" 1 promises it)");
   std::vector<int64_t> first;  // edges the stream's first tuple appends (position 0)
-  int64_t start = 0, prev = h_prev_max;
+  int64_t start = 0, prev = std::max(h_prev_max, before);
   int64_t N = t_pending;
-  if (!started) {
-    const int64_t te = t_first, L = max_lateness;
+  if (!started) {  // every rank replays the first tuple's walk: its pending edge is the batch's first candidate
+    const int64_t te = stream_first, L = max_lateness;
     auto calc = [&](int64_t cur_edge) {  // calculateNextFixedEdge(te)
       const int64_t cur = cur_edge == JMIN ? JMAX : cur_edge;
       return next_time_point(std::max(jsub(te, L), cur));
@@ -193,25 +209,27 @@ int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a) {
       first.push_back(N);
       N = calc(N);
     }
-    start = 1;
-    prev = te;
+    if (first_here) start = 1;
+    prev = std::max(prev, te);
   }
-  if (start >= n) {
-    t_pending = N;
-    h_prev_max = std::max(h_prev_max, t_last);
-  }
+  const int64_t nf_all = (int64_t)first.size();
+  if (!first_here) first.clear();
+  // union grid from the pending edge up to the batch max: the chunk's candidates are the points in (prev, t_last]
   std::vector<int64_t> cand;
-  if (start < n) {
-    for (int64_t g = N; g <= t_last; g = next_time_point(g)) {
-      cand.push_back(g);
-      if (cand.size() > ((size_t)1 << 22))
-        return fail(SCOTTY_ERR_UNSUPPORTED, "count path: more than 2^22 time grid points in one micro-batch");
-      if (next_time_point(g) <= g) break;  // JMAX / overflow: no further grid point
+  int64_t n_all = 0, g = N;
+  for (; g <= batch_last; g = next_time_point(g)) {
+    if (++n_all > ((int64_t)1 << 22))
+      return fail(SCOTTY_ERR_UNSUPPORTED, "count path: more than 2^22 time grid points in one micro-batch");
+    if (g > prev && start < n && g <= t_last) cand.push_back(g);
+    if (next_time_point(g) <= g) {  // JMAX / overflow: no further grid point
+      g = next_time_point(g);
+      break;
     }
-    // the pending edge after the batch: the first grid point above its last (maximum) timestamp
-    t_pending = N > t_last ? N : (cand.empty() ? N : next_time_point(cand.back()));
-    h_prev_max = std::max(h_prev_max, t_last);
   }
+  // the pending edge after the batch: the first grid point above its last (maximum) timestamp
+  t_pending = n_all > 0 ? g : N;
+  h_prev_max = std::max(h_prev_max, batch_last);
+  shard_te_bound = nf_all + n_all;
   const int64_t nc = (int64_t)cand.size(), nf = (int64_t)first.size();
   if (nc > tcap) {
     dfree(d_cand); dfree(d_cpos); dfree(d_cflag);
@@ -404,7 +422,7 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
   }
   if (n <= 0) return SCOTTY_OK;
   CPushArgs ta{};
-  int rc = time_edges(d_ts, n, ta);
+  int rc = time_edges(d_ts, n, ta, nullptr);
   if (rc) return rc;
   CPushArgs a;
   int64_t ebound = 0, maxp = 0;
@@ -430,18 +448,24 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
 }
 
 int CEngine::shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64_t ts0, int64_t n_before,
-                        int64_t n_total, int64_t* d_rec) {
+                        int64_t n_total, int64_t ts_before, int64_t ts_last, int64_t* d_rec) {
   if (failed) return SCOTTY_ERR_STATE;
-  if (!twins.empty())
-    return fail(SCOTTY_ERR_UNSUPPORTED, "sharded count path: time windows are not supported across shards yet");
   if (n_total > MAX_PUSH || n < 0 || n_before < 0 || n_before + n > n_total)
     return fail(SCOTTY_ERR_ARG, "shard chunk outside its micro-batch (or micro-batch above 2^28 tuples)");
   shard_total = n_total;
   if (pending == JMIN) shard_ts0 = ts0;
+  ShardTime sh{ts0, n_before, n_total, ts_before, ts_last};
+  CPushArgs ta{};
+  int rc = time_edges(d_ts, n, ta, &sh);
+  if (rc) return rc;
   CPushArgs a;
   int64_t ebound = 0, maxp = 0;
-  int rc = prepare(count + n_before, std::max<int64_t>(n, 1), count, count + n_total, a, ebound, maxp);
+  rc = prepare(count + n_before, std::max<int64_t>(n, 1), count, count + n_total, a, ebound, maxp, ta.n_te);
   if (rc) return rc;
+  a.te_pos = ta.te_pos;
+  a.te_g = ta.te_g;
+  a.n_te = ta.n_te;
+  a.check_sorted = twins.empty() ? 0 : 1;
   a.n = n;
   a.ts = d_ts;
   a.val = d_val;
@@ -463,7 +487,7 @@ int CEngine::shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64
 
 int CEngine::shard_commit(const int64_t* d_gathered, int world) {
   if (failed) return SCOTTY_ERR_STATE;
-  const int64_t eb = batch_edges_bound(count, count + shard_total);
+  const int64_t eb = batch_edges_bound(count, count + shard_total) + shard_te_bound;
   if (tail_ub + eb > scap) {
     int rc = grow_slices(eb);
     if (rc) return rc;
@@ -486,7 +510,7 @@ int CEngine::shard_commit(const int64_t* d_gathered, int world) {
   count += shard_total;
   pending = (pending != JMIN && pending >= count) ? pending : next_point(count);
   tail_ub += eb;
-  started = true;
+  started = started || shard_total > 0;
   return SCOTTY_OK;
 }
 

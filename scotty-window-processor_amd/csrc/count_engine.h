@@ -23,7 +23,7 @@ class CEngine {
   // records of shard_words() int64 each, every rank commits them
   int64_t shard_words() const { return cshard_words(shard_cap); }
   int shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64_t ts0, int64_t n_before, int64_t n_total,
-                 int64_t* d_rec);
+                 int64_t ts_before, int64_t ts_last, int64_t* d_rec);
   int shard_commit(const int64_t* d_gathered, int world);
   int64_t shard_cap = 1 << 16;  // cells per rank record (scotty_tune "shard_count_cells")
   int watermark(int64_t wm, XResult& r, bool to_host);
@@ -37,6 +37,7 @@ class CEngine {
   std::string err;
   bool failed = false;
 
+  bool has_time_windows() const { return !twins.empty(); }
   int64_t last_nte = 0;  // time edges of the last push (debug stat)
 
  private:
@@ -50,7 +51,11 @@ class CEngine {
   int prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, CPushArgs& a, int64_t& ebound, int64_t& maxp,
               int64_t n_te = 0);
   int64_t batch_edges_bound(int64_t lo_count, int64_t hi_count) const;
-  int time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a);
+  struct ShardTime {  // a rank's chunk within a global micro-batch (shard_push)
+    int64_t ts0, n_before, n_total, ts_before, ts_last;
+  };
+  int time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const ShardTime* sh);
+  int64_t shard_te_bound = 0;  // time-edge candidates of the current sharded batch (all ranks)
   int64_t next_time_point(int64_t x) const;  // nextGrid over the time windows (calculateNextFixedEdge's min)
   int64_t shard_ts0 = INT64_MIN, shard_total = 0;
   long long* d_plan = nullptr;

@@ -460,7 +460,7 @@ __global__ void count_tedges_kernel(CPushArgs a) {
     else if (o >= lo) cb += __popc(w & (uint32_t)((2ull << (o - lo)) - 1));
   }
   const int64_t e = a.stepbase[s] + cb + (j - te_lb(a, s * CSTEP));
-  a.cells.e_pos[e] = p;
+  a.cells.e_pos[e] = a.shard ? ~p : p;  // shard records mark time edges (their tStart is the edge itself)
   a.cells.e_ts[e] = a.te_g[j];
 }
 
@@ -762,8 +762,9 @@ __global__ __launch_bounds__(256) void count_export_kernel(CPushArgs a, int64_t*
       c[4] = (int64_t)a.cells.p[1][j];
       c[5] = (int64_t)a.cells.p[2][j];
     }
-    if (j < E) {
-      edges[2 * j] = a.C + a.cells.e_pos[j];
+    if (j < E) {  // time edges: count word ~(global count)
+      const int64_t p = a.cells.e_pos[j];
+      edges[2 * j] = p >= 0 ? a.C + p : ~(a.C + ~p);
       edges[2 * j + 1] = a.cells.e_ts[j];
     }
   }
@@ -798,13 +799,17 @@ __global__ __launch_bounds__(256) void count_shard_append_kernel(CShardArgs a) {
   const int64_t pm = a.plan[2 * r + 1];
   for (int64_t j = 1 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= E; j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t* c = cells + 6 * j;
-    int64_t st = max(pm, edges[2 * (j - 1) + 1]);
-    if (st == JMIN) st = a.ts0;  // the stream's first tuple sets maxEventTime to its own ts (S/StreamSlicer.java:39-40)
+    const int64_t ec = edges[2 * (j - 1)];
+    int64_t st = edges[2 * (j - 1) + 1];  // time edge: the grid point itself
+    if (ec >= 0) {  // count edge: maxEventTime before its tuple
+      st = max(pm, st);
+      if (st == JMIN) st = a.ts0;  // the stream's first tuple sets maxEventTime to its own ts (S/StreamSlicer.java:39-40)
+    }
     const int64_t k = off + j - 1;
     if (c[0] != 0 && c[2] < st) atomicOr((unsigned long long*)&a.meta->err, 1ull);
     a.sl.ts[k] = st;
     a.sl.tl[k] = max(st, c[1]);
-    a.sl.cs[k] = edges[2 * (j - 1)];
+    a.sl.cs[k] = ec >= 0 ? ec : ~ec;
     a.sl.cnt[k] = (unsigned long long)c[0];
     a.sl.p[0][k] = (unsigned long long)c[3];
     a.sl.p[1][k] = (unsigned long long)c[4];

@@ -1126,8 +1126,9 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
   return SCOTTY_OK;
 }
 
-int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
-                              int64_t n_before, int64_t n_total, void* d_xbuf) {
+static int shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
+                              int64_t n_before, int64_t n_total, bool timed, int64_t ts_before, int64_t ts_last,
+                              void* d_xbuf) {
   if (!op || !d_xbuf || (n && (!d_ts || !d_val))) return SCOTTY_ERR_ARG;
   if (op->failed) return fail(op, SCOTTY_ERR_STATE, "operator failed earlier: " + op->err);
   if (op->keyed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "keyed operators shard by key: no exchange needed");
@@ -1136,10 +1137,33 @@ int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_
   int rc = decide_mode(op);
   if (rc) return rc;
   if (op->mode != 3) return scotty_shard_push(op, d_ts, d_val, n, ts0, d_xbuf);
-  rc = op->c->shard_push(d_ts, d_val, (int64_t)n, ts0, n_before, n_total, (int64_t*)d_xbuf);
+  if (!timed && op->c->has_time_windows())
+    return fail(op, SCOTTY_ERR_ARG, "count + time windows: use scotty_shard_push_timed (the batch's timestamp "
+                                    "bounds decide the time edges)");
+  rc = op->c->shard_push(d_ts, d_val, (int64_t)n, ts0, n_before, n_total, ts_before, ts_last, (int64_t*)d_xbuf);
   if (rc) return fail(op, rc, op->c->err);
   op->shard_count_total = n_total;
   return SCOTTY_OK;
+}
+
+int scotty_shard_bounds(scotty_op* op, const int64_t* d_ts, size_t n, int64_t* first_last) {
+  if (!op || !first_last || (n && !d_ts)) return SCOTTY_ERR_ARG;
+  first_last[0] = first_last[1] = INT64_MIN;
+  if (n == 0) return SCOTTY_OK;
+  HIPCHK(hipMemcpyAsync(first_last, d_ts, 8, hipMemcpyDeviceToHost, op->stream));
+  HIPCHK(hipMemcpyAsync(first_last + 1, d_ts + n - 1, 8, hipMemcpyDeviceToHost, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  return SCOTTY_OK;
+}
+
+int scotty_shard_push_counted(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
+                              int64_t n_before, int64_t n_total, void* d_xbuf) {
+  return shard_push_counted(op, d_ts, d_val, n, ts0, n_before, n_total, false, INT64_MIN, INT64_MIN, d_xbuf);
+}
+
+int scotty_shard_push_timed(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
+                            int64_t n_before, int64_t n_total, int64_t ts_before, int64_t ts_last, void* d_xbuf) {
+  return shard_push_counted(op, d_ts, d_val, n, ts0, n_before, n_total, true, ts_before, ts_last, d_xbuf);
 }
 
 int scotty_shard_commit(scotty_op* op, const void* d_gathered, int world) {

@@ -39,6 +39,27 @@ def case(cid):
         vals = rng.integers(-1000, 1000, size=n, dtype=np.int64).astype(np.int32)
         sched = interval_schedule(ts, 9, lag=3, pushes_per_interval=3)
         return cfg, ts, vals, sched
+    elif cid == 6:  # count + sliding time windows, in-order unique timestamps
+        cfg = dict(windows=[Tumbling(Count, 1000), Sliding(Time, 60000, 1000)], aggs=[SUM, COUNT], lateness=1)
+        n = 200_000
+        ts = 5 + np.cumsum(rng.integers(1, 4, size=n)).astype(np.int64)
+        vals = rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+        sched = interval_schedule(ts, 80, lag=0, pushes_per_interval=2)
+        return cfg, ts, vals, sched
+    elif cid == 7:  # count + time windows with ties, lateness > slide, tiny pushes (empty chunks on a rank)
+        cfg = dict(windows=[Sliding(Time, 50, 7), Tumbling(Count, 13), Tumbling(Time, 11), FixedBand(Count, 100, 900)],
+                   aggs=[SUM, COUNT, MIN], lateness=30)
+        n = 20_000
+        ts = 3000 + np.sort(rng.integers(0, 6000, size=n)).astype(np.int64)
+        vals = rng.integers(-1000, 1000, size=n, dtype=np.int64).astype(np.int32)
+        sched = []
+        lo = 0
+        for size in [1, 1, 3, 2, 50, 1, 400] + [997] * 19 + [n]:
+            hi = min(n, lo + size)
+            if hi > lo:
+                sched += [("push", lo, hi), ("wm", int(ts[hi - 1]) - 2)]
+            lo = hi
+        return cfg, ts, vals, sched
     else:           # lateness edge skipping on jumps + fixed band
         cfg = dict(windows=[Tumbling(Time, 13), FixedBand(Time, 5000, 2000)], aggs=[SUM, MAX], lateness=3)
         ts, vals = wl.stream(120_000, 2, t0=7, ooo_frac=0.05, max_delay=2, seed=cid,

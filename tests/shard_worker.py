@@ -40,7 +40,13 @@ def main():
             op.processChunk(t.data_ptr(), v.data_ptr(), b - a, int(ts[0]))
             torch.cuda.synchronize(dev)
         else:
-            ws = op.processWatermark(st[1])
+            try:
+                ws = op.processWatermark(st[1])
+            except pkg.ScottyError as e:  # IndexOutOfBoundsException in the reference: the test expects it too
+                if e.code != -5:
+                    raise
+                res.append([["index_error"]])
+                continue
             res.append([list(w.key()[:4]) + [list(w.key()[4])] for w in ws] + [["dropped", op.droppedCount()]])
     if rank == 0:
         json.dump(res, open(out, "w"))
