@@ -87,10 +87,13 @@ struct CPushArgs {
   int32_t need, vt;
   int64_t* stepc;        // [nsteps] edges per step
   int64_t* stepbase;     // [nsteps] exclusive scan of stepc
-  long long* stepmax;    // [nsteps] max ts per step (every tuple, dropped ones too)
-  long long* steppre;    // [nsteps] inclusive prefix max of stepmax
+  int64_t* stepte;       // [nsteps + 1] first time edge at or after each step (te_lb), n_te at the end
+  uint32_t* steptp;      // [nsteps] the step's time edges as packed in-step offsets (count_stepc_kernel)
+  long long* stepmax;    // [nwaves] max ts per ingest wave (every tuple, dropped ones too)
+  long long* steppre;    // [nwaves] inclusive prefix max of stepmax
   int64_t nsteps;
   int64_t per_wave;      // steps per wave
+  int64_t nwaves;        // ceil(nsteps / per_wave)
   CCells cells;
   int64_t cell_cap;
   CSlices sl;
@@ -115,13 +118,15 @@ struct CTimeArgs {
   int64_t start;         // first batch position the candidates apply to (1 when position 0 is the stream's first)
   int64_t prev_max;      // maxEventTime before position `start`
   int64_t lateness;
-  const int64_t* cand;   // [n_cand] ascending
+  const int64_t* cand;   // [n_cand] ascending (step == 0)
+  int64_t step, cand0;   // step > 0: cand[k] = cand0 + k * step (one common period, no array)
   int64_t n_cand;
   int64_t prev0;         // the grid point before cand[0] (JMIN: cand[0] is the pending edge itself)
   int64_t* te_pos;       // out: [n_te] compacted edges
   int64_t* te_g;
   unsigned long long* n_te;
-  int32_t* flag;         // scratch [n_cand]
+  int64_t* flag;         // scratch [n_cand] 0/1
+  int64_t* off;          // scratch [n_cand] exclusive scan of flag
   int64_t* pos;          // scratch [n_cand]
 };
 

@@ -4,6 +4,7 @@
 #include "count_engine.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 namespace scotty {
@@ -15,7 +16,7 @@ hipError_t launch_count_export(const CPushArgs& a, int64_t* rec, int64_t cap, hi
 hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hipStream_t st);
 hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st);
 hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st);
-hipError_t launch_count_time_edges(const CTimeArgs& a, hipStream_t st);
+hipError_t launch_count_time_edges(const CTimeArgs& a, int64_t* scan_tmp, hipStream_t st);
 
 #define CCHK(x)                                                      \
   do {                                                               \
@@ -75,15 +76,19 @@ CEngine::~CEngine() {
   dfree(d_wins);
   dfree(sl.ts); dfree(sl.tl); dfree(sl.cs); dfree(sl.cnt);
   for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  dfree(spare.ts); dfree(spare.tl); dfree(spare.cs); dfree(spare.cnt);
+  for (int k = 0; k < NPART; k++) dfree(spare.p[k]);
   dfree(cells.cnt); dfree(cells.tl); dfree(cells.tf); dfree(cells.e_pos); dfree(cells.e_ts);
   for (int k = 0; k < NPART; k++) dfree(cells.p[k]);
   dfree(d_bits); dfree(d_stepc); dfree(d_stepbase); dfree(d_scan); dfree(d_stepmax); dfree(d_steppre);
+  dfree(d_stepte); dfree(d_steptp);
   dfree(d_premax);
   dfree(d_wstart); dfree(d_wend); dfree(d_meas); dfree(d_has);
   for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
   dfree(d_pre_cnt); dfree(d_pre_sum); dfree(d_bsum);
   dfree(d_plan);
   dfree(d_cand); dfree(d_cpos); dfree(d_te_pos); dfree(d_te_g); dfree(d_cflag); dfree(d_nte);
+  dfree(d_coff); dfree(d_cscan);
   if (h_tmp) (void)hipHostFree(h_tmp);
 }
 
@@ -129,6 +134,15 @@ int CEngine::configure(const std::vector<XWinDef>& ws, const std::vector<int>& a
   wins = nw;
   twins = tw;
   reg = all;
+  tstep = 0;  // one common period of every time window (tumbling size / sliding slide), else 0
+  for (const CWin& w : tw) {
+    const int64_t p = w.kind == SCOTTY_WIN_TUMBLING ? w.a : w.kind == SCOTTY_WIN_SLIDING ? w.b : -1;
+    if (p <= 0 || (tstep != 0 && p != tstep)) {
+      tstep = 0;
+      break;
+    }
+    tstep = p;
+  }
   max_fixed = mf;
   aggs = ag;
   max_lateness = lateness;
@@ -216,31 +230,48 @@ int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const Shar
   if (!first_here) first.clear();
   // union grid from the pending edge up to the batch max: the chunk's candidates are the points in (prev, t_last]
   std::vector<int64_t> cand;
-  int64_t n_all = 0, g = N;
-  for (; g <= batch_last; g = next_time_point(g)) {
-    if (++n_all > ((int64_t)1 << 22))
-      return fail(SCOTTY_ERR_UNSUPPORTED, "count path: more than 2^22 time grid points in one micro-batch");
-    if (g > prev && start < n && g <= t_last) cand.push_back(g);
-    if (next_time_point(g) <= g) {  // JMAX / overflow: no further grid point
-      g = next_time_point(g);
-      break;
+  int64_t n_all = 0, g = N, c0 = 0, nc = 0;
+  const int64_t P = tstep;
+  const bool arith = P > 0 && N >= 0 && N % P == 0 && batch_last < JMAX - P;
+  if (arith) {  // one period (the grid is N + kP): candidates are generated on the device (CTimeArgs.step)
+    n_all = batch_last >= N ? (batch_last - N) / P + 1 : 0;
+    g = N + n_all * P;
+    if (start < n && t_last >= N) {
+      const int64_t k_lo = prev >= N ? (prev - N) / P + 1 : 0, k_hi = (t_last - N) / P;
+      c0 = N + k_lo * P;
+      nc = std::max<int64_t>(0, k_hi - k_lo + 1);
     }
+  } else {
+    for (; g <= batch_last; g = next_time_point(g)) {
+      if (++n_all > ((int64_t)1 << 22))
+        return fail(SCOTTY_ERR_UNSUPPORTED, "count path: more than 2^22 time grid points in one micro-batch");
+      if (g > prev && start < n && g <= t_last) cand.push_back(g);
+      if (next_time_point(g) <= g) {  // JMAX / overflow: no further grid point
+        g = next_time_point(g);
+        break;
+      }
+    }
+    nc = (int64_t)cand.size();
   }
+  if (nc > ((int64_t)1 << 26))
+    return fail(SCOTTY_ERR_UNSUPPORTED, "count path: more than 2^26 time grid points in one micro-batch");
   // the pending edge after the batch: the first grid point above its last (maximum) timestamp
   t_pending = n_all > 0 ? g : N;
   h_prev_max = std::max(h_prev_max, batch_last);
   shard_te_bound = nf_all + n_all;
-  const int64_t nc = (int64_t)cand.size(), nf = (int64_t)first.size();
+  const int64_t nf = (int64_t)first.size();
   if (nc > tcap) {
-    dfree(d_cand); dfree(d_cpos); dfree(d_cflag);
-    tcap = nc + 1024;
+    dfree(d_cand); dfree(d_cpos); dfree(d_cflag); dfree(d_coff); dfree(d_cscan);
+    tcap = nc + nc / 2 + 1024;
     CCHK(dalloc(&d_cand, tcap));
     CCHK(dalloc(&d_cpos, tcap));
     CCHK(dalloc(&d_cflag, tcap));
+    CCHK(dalloc(&d_coff, tcap));
+    CCHK(dalloc(&d_cscan, tcap / 512 + 64));
   }
   if (nc + nf > tecap) {
     dfree(d_te_pos); dfree(d_te_g);
-    tecap = nc + nf + 1024;
+    tecap = nc + nf + (nc + nf) / 2 + 1024;
     CCHK(dalloc(&d_te_pos, tecap));
     CCHK(dalloc(&d_te_g, tecap));
   }
@@ -251,8 +282,10 @@ int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const Shar
   }
   int64_t nte = nf;
   if (nc > 0) {
-    CCHK(hipMemcpyAsync(d_cand, cand.data(), nc * 8, hipMemcpyHostToDevice, stream));
+    if (!arith) CCHK(hipMemcpyAsync(d_cand, cand.data(), nc * 8, hipMemcpyHostToDevice, stream));
     CTimeArgs t{};
+    t.step = arith ? P : 0;
+    t.cand0 = c0;
     t.ts = d_ts;
     t.n = n;
     t.start = start;
@@ -265,8 +298,9 @@ int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const Shar
     t.te_g = d_te_g + nf;
     t.n_te = d_nte;
     t.flag = d_cflag;
+    t.off = d_coff;
     t.pos = d_cpos;
-    CCHK(launch_count_time_edges(t, stream));
+    CCHK(launch_count_time_edges(t, d_cscan, stream));
     CCHK(hipMemcpyAsync(h_tmp + 2, d_nte, 8, hipMemcpyDeviceToHost, stream));
     CCHK(hipStreamSynchronize(stream));
     nte += h_tmp[2];
@@ -294,13 +328,26 @@ int CEngine::grow_slices(int64_t need_more) {
     head_lb = head;
     return SCOTTY_OK;
   }
-  const int64_t ncap = std::max<int64_t>({(S + need_more) * 2, scap, 4096});
+  // steady state: the retained range moves between two buffer sets of the same capacity (no allocation); room
+  // for ~8 micro-batches of slices between moves
+  int64_t ncap = std::max<int64_t>({(S + need_more) * 8, scap, 4096});
   CSlices n{};
-  CCHK(dalloc(&n.ts, ncap));
-  CCHK(dalloc(&n.tl, ncap));
-  CCHK(dalloc(&n.cs, ncap));
-  CCHK(dalloc(&n.cnt, ncap));
-  for (int k = 0; k < NPART; k++) CCHK(dalloc(&n.p[k], ncap));
+  if (spare_cap >= S + need_more) {
+    n = spare;
+    ncap = spare_cap;
+  } else {
+    if (spare_cap) {
+      dfree(spare.ts); dfree(spare.tl); dfree(spare.cs); dfree(spare.cnt);
+      for (int k = 0; k < NPART; k++) dfree(spare.p[k]);
+    }
+    CCHK(dalloc(&n.ts, ncap));
+    CCHK(dalloc(&n.tl, ncap));
+    CCHK(dalloc(&n.cs, ncap));
+    CCHK(dalloc(&n.cnt, ncap));
+    for (int k = 0; k < NPART; k++) CCHK(dalloc(&n.p[k], ncap));
+  }
+  spare = CSlices{};
+  spare_cap = 0;
   if (S > 0) {
     CCHK(hipMemcpyAsync(n.ts, sl.ts + head, S * 8, hipMemcpyDeviceToDevice, stream));
     CCHK(hipMemcpyAsync(n.tl, sl.tl + head, S * 8, hipMemcpyDeviceToDevice, stream));
@@ -313,8 +360,13 @@ int CEngine::grow_slices(int64_t need_more) {
   h_meta->tail = S;
   CCHK(hipMemcpyAsync(d_meta, h_meta, sizeof(CMeta), hipMemcpyHostToDevice, stream));
   CCHK(hipStreamSynchronize(stream));
-  dfree(sl.ts); dfree(sl.tl); dfree(sl.cs); dfree(sl.cnt);
-  for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  if (scap >= ncap / 2 && sl.ts) {  // keep the old set as the next move's target
+    spare = sl;
+    spare_cap = scap;
+  } else {
+    dfree(sl.ts); dfree(sl.tl); dfree(sl.cs); dfree(sl.cnt);
+    for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  }
   sl = n;
   scap = ncap;
   tail_ub = S;
@@ -366,9 +418,12 @@ int CEngine::prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, C
   }
   if (nsteps > stcap) {
     dfree(d_stepc); dfree(d_stepbase); dfree(d_scan); dfree(d_stepmax); dfree(d_steppre); dfree(d_premax);
+    dfree(d_stepte); dfree(d_steptp);
     stcap = nsteps + nsteps / 4 + 64;
     CCHK(dalloc(&d_stepc, stcap));
     CCHK(dalloc(&d_stepbase, stcap));
+    CCHK(dalloc(&d_stepte, stcap + 1));
+    CCHK(dalloc(&d_steptp, stcap));
     CCHK(dalloc(&d_scan, stcap / 512 + 64));
     CCHK(dalloc(&d_stepmax, stcap));
     CCHK(dalloc(&d_steppre, stcap));
@@ -399,10 +454,13 @@ int CEngine::prepare(int64_t C, int64_t n, int64_t range_lo, int64_t range_hi, C
   a.vt = vt;
   a.stepc = d_stepc;
   a.stepbase = d_stepbase;
+  a.stepte = d_stepte;
+  a.steptp = d_steptp;
   a.stepmax = d_stepmax;
   a.steppre = d_steppre;
   a.nsteps = nsteps;
-  a.per_wave = std::max<int64_t>(1, (nsteps + 4095) / 4096);  // ~1024 workgroups of 4 waves
+  a.per_wave = std::max<int64_t>(1, (nsteps + 16383) / 16384);  // ~4096 workgroups of 4 waves
+  a.nwaves = (nsteps + a.per_wave - 1) / a.per_wave;
   a.cells = cells;
   a.cell_cap = ebound + 1;
   a.sl = sl;
@@ -422,8 +480,10 @@ int CEngine::push(const int64_t* d_ts, const void* d_val, int64_t n, hipEvent_t 
   }
   if (n <= 0) return SCOTTY_OK;
   CPushArgs ta{};
+  const auto h0 = std::chrono::steady_clock::now();
   int rc = time_edges(d_ts, n, ta, nullptr);
   if (rc) return rc;
+  last_te_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
   CPushArgs a;
   int64_t ebound = 0, maxp = 0;
   rc = prepare(count, n, count, count + n, a, ebound, maxp, ta.n_te);

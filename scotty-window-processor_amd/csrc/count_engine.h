@@ -38,7 +38,8 @@ class CEngine {
   bool failed = false;
 
   bool has_time_windows() const { return !twins.empty(); }
-  int64_t last_nte = 0;  // time edges of the last push (debug stat)
+  int64_t last_nte = 0;
+  double last_te_us = 0;  // host time of the last push's time-edge step (debug stat)  // time edges of the last push (debug stat)
 
  private:
   int grow_slices(int64_t need);
@@ -76,13 +77,16 @@ class CEngine {
   int64_t count = 0;           // WindowManager.currentCount
   int64_t pending = INT64_MIN;  // StreamSlicer.min_next_edge_count
   int64_t last_wm = -1, last_count = 0;
-  int64_t t_pending = INT64_MIN;  // StreamSlicer.min_next_edge_ts (time windows)
+  int64_t t_pending = INT64_MIN;
+  int64_t tstep = 0;
+  CSlices spare{};                 // second slice buffer set (grow_slices moves the retained range into it)
+  int64_t spare_cap = 0;               // common period of the time windows (device-generated candidates), or 0  // StreamSlicer.min_next_edge_ts (time windows)
   int64_t h_prev_max = INT64_MIN; // StreamSlicer.maxEventTime after the last push (the stream is in order)
   bool started = false;
   // time edges of the current push
   int64_t tcap = 0, tecap = 0;
   int64_t *d_cand = nullptr, *d_cpos = nullptr, *d_te_pos = nullptr, *d_te_g = nullptr;
-  int32_t* d_cflag = nullptr;
+  int64_t *d_cflag = nullptr, *d_coff = nullptr, *d_cscan = nullptr;
   unsigned long long* d_nte = nullptr;
   int64_t* h_tmp = nullptr;  // pinned scratch (batch ends, edge count)
   uint64_t dropped_ = 0;
@@ -97,7 +101,8 @@ class CEngine {
   CCells cells{};
   int64_t bcap = 0, stcap = 0;
   uint32_t* d_bits = nullptr;
-  int64_t *d_stepc = nullptr, *d_stepbase = nullptr, *d_scan = nullptr;
+  int64_t *d_stepc = nullptr, *d_stepbase = nullptr, *d_scan = nullptr, *d_stepte = nullptr;
+  uint32_t* d_steptp = nullptr;
   long long *d_stepmax = nullptr, *d_steppre = nullptr, *d_premax = nullptr;
   // watermark
   struct Row {

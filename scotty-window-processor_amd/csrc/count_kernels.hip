@@ -92,7 +92,7 @@ __device__ __forceinline__ int64_t te_lb(const CPushArgs& a, int64_t x) {
 __global__ void count_tcand_kernel(CTimeArgs a) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.n_cand) return;
-  const int64_t g = a.cand[k];
+  const int64_t g = a.step ? a.cand0 + k * a.step : a.cand[k];
   int64_t l = a.start, h = a.n;
   while (l < h) {
     const int64_t m = (l + h) >> 1;
@@ -104,41 +104,22 @@ __global__ void count_tcand_kernel(CTimeArgs a) {
   // the pending edge is appended once crossed; a later grid point iff the running max before its first tuple
   // reached the point before it, or that tuple lies within maxLateness of it (edges further back are skipped,
   // calculateNextFixedEdge's max(te - maxLateness, edge)); `while (te > edge)` appends only edges >= 0
-  bool edge = k == 0 || a.cand[k - 1] <= m || (int64_t)((uint64_t)e - (uint64_t)g) < a.lateness;
+  const int64_t gp = k == 0 ? 0 : (a.step ? g - a.step : a.cand[k - 1]);
+  bool edge = k == 0 || gp <= m || (int64_t)((uint64_t)e - (uint64_t)g) < a.lateness;
   edge = edge && (g >= 0 || e == g);
   a.flag[k] = edge ? 1 : 0;
   a.pos[k] = p;
 }
 
-// order-preserving compaction of the decided candidates (one workgroup; candidates per batch are few)
-__global__ __launch_bounds__(1024) void count_tcompact_kernel(CTimeArgs a) {
-  __shared__ int32_t wsum[16];
-  __shared__ long long base;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) base = 0;
-  __syncthreads();
-  for (int64_t k0 = 0; k0 < a.n_cand; k0 += 1024) {
-    const int64_t k = k0 + tid;
-    const bool f = k < a.n_cand && a.flag[k];
-    const unsigned long long bal = __ballot(f);
-    if (lane == 0) wsum[wid] = __popcll(bal);
-    __syncthreads();
-    int64_t before = base;
-    for (int w = 0; w < wid; w++) before += wsum[w];
-    if (f) {
-      const int64_t j = before + __popcll(bal & ((1ull << lane) - 1));
-      a.te_pos[j] = a.pos[k];
-      a.te_g[j] = a.cand[k];
-    }
-    __syncthreads();
-    if (tid == 0) {
-      long long t = 0;
-      for (int w = 0; w < 16; w++) t += wsum[w];
-      base += t;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) *a.n_te = (unsigned long long)base;
+// order-preserving compaction of the decided candidates (offsets: exclusive scan of the flags)
+__global__ void count_tscatter_kernel(CTimeArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= a.n_cand) return;
+  if (k == a.n_cand - 1) *a.n_te = (unsigned long long)(a.off[k] + a.flag[k]);
+  if (!a.flag[k]) return;
+  const int64_t j = a.off[k];
+  a.te_pos[j] = a.pos[k];
+  a.te_g[j] = a.step ? a.cand0 + k * a.step : a.cand[k];
 }
 
 // ---------------------------------------------------------------- 2. edges per step
@@ -151,7 +132,19 @@ __global__ void count_stepc_kernel(CPushArgs a) {
     const int64_t wi = s * 8 + k;
     if (wi < a.nwords) c += __popc(a.bits[wi]);
   }
-  if (a.n_te > 0) c += te_lb(a, (s + 1) * CSTEP) - te_lb(a, s * CSTEP);
+  if (a.n_te > 0) {
+    const int64_t lo = te_lb(a, s * CSTEP), hi = te_lb(a, (s + 1) * CSTEP);
+    c += hi - lo;
+    a.stepte[s] = lo;
+    if (s == a.nsteps - 1) a.stepte[a.nsteps] = a.n_te;
+    // up to 3 time edges of the step as packed in-step offsets (count | o0 << 8 | o1 << 16 | o2 << 24), else 255
+    uint32_t pk = 255u;
+    if (hi - lo <= 3) {
+      pk = (uint32_t)(hi - lo);
+      for (int64_t k = lo; k < hi; k++) pk |= (uint32_t)(a.te_pos[k] - s * CSTEP) << (8 * (1 + (k - lo)));
+    }
+    a.steptp[s] = pk;
+  }
   a.stepc[s] = c;
 }
 
@@ -201,6 +194,11 @@ __device__ __forceinline__ void cell_add(const CCells& c, int64_t j, uint64_t n,
   if constexpr ((NEED & NEED_MAX) != 0) atomicMax((long long*)&c.p[2][j], (long long)mx);
 }
 
+// One wave per run of per_wave consecutive steps (256 tuples each, 4 per lane: offsets 2l, 2l+1, 128+2l, 129+2l).
+// Steps without an edge only accumulate into the wave's current cell (per-lane registers, no cross-lane work); a
+// step with edges reduces each of its cells once (masked wave reduction) and writes the count edges' records.
+// The max ts before a count edge: in-order batches take the previous tuple's ts; otherwise the wave's running max
+// plus the in-step prefix here, completed across waves by count_efix_kernel (wavemax -> wavepre).
 template <int VT, int NEED>
 __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   const int lane = threadIdx.x & 63;
@@ -215,6 +213,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   int64_t tmax = JMIN, tmin = JMAX, mn = ID_MIN, mx = ID_MAX;
   int64_t cur = -1;
   uint32_t n_late = 0;
+  int64_t lmax = JMIN;  // running max of this lane's tuples in the wave (dropped ones too)
   auto flush = [&]() {
     const uint64_t c = wred(cnt, [](unsigned long long p, unsigned long long q) { return p + q; });
     if (c != 0) {
@@ -249,11 +248,10 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   };
   typedef long long v2i64 __attribute__((ext_vector_type(2)));
   typedef int v2i32 __attribute__((ext_vector_type(2)));
-  for (int64_t s = s0; s < s1; s++) {
+  // a step's tuples, its edge-bitmap word (lanes 0-7), slice base and packed time edges
+  auto ld = [&](int64_t s, int64_t* t, int64_t* v, bool* ok, uint32_t& bw, int64_t& sbv, uint32_t& tpv) {
     const int64_t base = s * CSTEP;
     const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
-    int64_t t[4], v[4];
-    bool ok[4];
     if (base + CSTEP <= a.n) {
       const v2i64 ta = __builtin_nontemporal_load((const v2i64*)(a.ts + i0));
       const v2i64 tb = __builtin_nontemporal_load((const v2i64*)(a.ts + i1));
@@ -278,36 +276,64 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         else v[j] = ok[j] ? ((const int64_t*)a.val)[idx[j]] : 0;
       }
     }
-    if (a.check_sorted) {  // the time-edge search (count_tcand_kernel) assumes a nondecreasing batch
+    const int64_t wi = s * 8 + lane;
+    bw = lane < 8 && wi < a.nwords ? a.bits[wi] : 0u;
+    sbv = a.stepbase[s];
+    tpv = a.n_te > 0 ? a.steptp[s] : 0u;
+  };
+  int64_t nt[4], nv[4], nsb;
+  bool nok[4];
+  uint32_t nbw, ntp;
+  ld(s0, nt, nv, nok, nbw, nsb, ntp);
+  // in-order batches: the ts before the wave's first tuple (a count edge's slice start)
+  int64_t prev_last = JMIN;
+  if (a.check_sorted) prev_last = s0 > 0 ? a.ts[s0 * CSTEP - 1] : (a.shard ? JMIN : (int64_t)a.meta->prev_max);
+  for (int64_t s = s0; s < s1; s++) {
+    const int64_t base = s * CSTEP;
+    const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
+    int64_t t[4], v[4];
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      t[j] = nt[j];
+      v[j] = nv[j];
+      ok[j] = nok[j];
+    }
+    const uint32_t bw = nbw, tp = __builtin_amdgcn_readfirstlane(ntp);
+    const int64_t sb = uni(nsb);
+    const bool more = s + 1 < s1;
+    if (more) ld(s + 1, nt, nv, nok, nbw, nsb, ntp);
+    int64_t before_step = JMIN;  // ts of the tuple before this step (in-order batches)
+    if (a.check_sorted) {
+      before_step = prev_last;
+      prev_last = (int64_t)__shfl((long long)t[3], 63);
+      // the time-edge search (count_tcand_kernel) assumes a nondecreasing batch
       const int64_t n0 = (int64_t)__shfl_down((long long)t[0], 1), n2 = (int64_t)__shfl_down((long long)t[2], 1);
       const int64_t l2 = (int64_t)__shfl((long long)t[2], 0);
-      const int64_t s1 = lane < 63 ? n0 : l2;                                       // successor of i0 + 1
-      const int64_t s3 = lane < 63 ? n2 : (i1 + 2 < a.n ? a.ts[i1 + 2] : JMAX);  // successor of i1 + 1
-      const bool bad = (i0 + 1 < a.n && t[1] < t[0]) || (i0 + 2 < a.n && s1 < t[1]) ||
+      const int64_t nx = more ? (int64_t)__shfl((long long)nt[0], 0) : (i1 + 2 < a.n ? a.ts[i1 + 2] : JMAX);
+      const int64_t s1_ = lane < 63 ? n0 : l2;  // successor of i0 + 1
+      const int64_t s3 = lane < 63 ? n2 : nx;   // successor of i1 + 1
+      const bool bad = (i0 + 1 < a.n && t[1] < t[0]) || (i0 + 2 < a.n && s1_ < t[1]) ||
                        (i1 + 1 < a.n && t[3] < t[2]) || (i1 + 2 < a.n && s3 < t[3]);
       if (bad) atomicOr((unsigned long long*)&a.meta->err, 8ull);
     }
-    int64_t smax = JMIN;
-#pragma unroll
-    for (int j = 0; j < 4; j++) smax = max(smax, t[j]);
-    smax = wred(smax, [](long long p, long long q) { return p > q ? p : q; });
-    if (lane == 0) a.stepmax[s] = smax;
-    // edge words of the step (wave-uniform), and the step's time edges [t0, t1)
+    // edge words of the step (wave-uniform) and its time edges
     uint32_t wd[8];
-    uint32_t any = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int64_t wi = s * 8 + k;
-      wd[k] = wi < a.nwords ? __builtin_amdgcn_readfirstlane(a.bits[wi]) : 0u;
-      any |= wd[k];
-    }
+    for (int k = 0; k < 8; k++) wd[k] = __builtin_amdgcn_readlane(bw, k);
+    uint32_t any = wd[0] | wd[1] | wd[2] | wd[3] | wd[4] | wd[5] | wd[6] | wd[7];
+    // packed in-step offsets (count_stepc_kernel), or the [t0, t1) range of te_pos when > 3
     int64_t t0 = 0, t1 = 0;
+    const bool tpacked = (tp & 255u) != 255u;
     if (a.n_te > 0) {
-      t0 = uni(te_lb(a, base));
-      t1 = uni(te_lb(a, base + CSTEP));
+      if (!tpacked) {
+        t0 = uni(a.stepte[s]);
+        t1 = uni(a.stepte[s + 1]);
+      } else {
+        t1 = tp & 255u;
+      }
       if (t1 > t0) any |= 1u;
     }
-    const int64_t sb = uni(a.stepbase[s]);
     if (any == 0) {
       if (sb != cur) {
         if (cur >= 0) flush();
@@ -316,22 +342,155 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         if (!ok[j]) continue;
+        lmax = max(lmax, t[j]);
         if (t[j] < first_start) n_late++;
         else add(t[j], v[j]);
       }
       continue;
     }
-    // a step with edges: the wave keeps the step's last cell in registers, other tuples go to their cell directly
+    // time edges at in-step offsets <= o (le) or < o
+    auto tcount = [&](int o, bool le) -> int64_t {
+      int64_t c = 0;
+      if (tpacked) {
+        const int tn = (int)(tp & 255u);
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+          const int oi = (int)((tp >> (8 * (i + 1))) & 255u);
+          c += (i < tn && (le ? oi <= o : oi < o)) ? 1 : 0;
+        }
+      } else {
+        for (int64_t k = t0; k < t1; k++) c += (le ? a.te_pos[k] <= base + o : a.te_pos[k] < base + o) ? 1 : 0;
+      }
+      return c;
+    };
+    // a step with edges: cell of every tuple (count edge before the time edges at one position)
     int pre[9];
     pre[0] = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) pre[k + 1] = pre[k] + __popc(wd[k]);
     const int64_t last = sb + pre[8] + (t1 - t0);
+    const int off[4] = {2 * lane, 2 * lane + 1, 128 + 2 * lane, 129 + 2 * lane};
+    int64_t cell[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int o = off[j], q = o >> 5, b = o & 31;
+      const uint32_t mask = (uint32_t)((2ull << b) - 1);
+      // time edges at or before this tuple (the tuple lands in the last slice appended)
+      cell[j] = sb + pre[q] + __popc(wd[q] & mask) + tcount(o, true);
+    }
+    // count edges: batch position and the max ts of every tuple before them
+    if (pre[8] != 0) {
+      int64_t prv[4];
+      if (a.check_sorted) {  // in-order: the previous tuple's ts
+        const int64_t p1 = (int64_t)__shfl_up((long long)t[1], 1), p3 = (int64_t)__shfl_up((long long)t[3], 1);
+        const int64_t l63 = (int64_t)__shfl((long long)t[1], 63);
+        prv[0] = lane == 0 ? before_step : p1;
+        prv[1] = t[0];
+        prv[2] = lane == 0 ? l63 : p3;
+        prv[3] = t[2];
+      } else {  // the wave's running max before the step, then the in-step exclusive prefix max
+        const int64_t W = wred(lmax, [](long long p, long long q) { return p > q ? p : q; });
+        int64_t ia = max(t[0], t[1]), ib = max(t[2], t[3]);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int64_t ua = (int64_t)__shfl_up((long long)ia, o), ub = (int64_t)__shfl_up((long long)ib, o);
+          if (lane >= o) {
+            ia = max(ia, ua);
+            ib = max(ib, ub);
+          }
+        }
+        const int64_t tot_a = (int64_t)__shfl((long long)ia, 63);
+        int64_t ea = (int64_t)__shfl_up((long long)ia, 1), eb = (int64_t)__shfl_up((long long)ib, 1);
+        if (lane == 0) ea = eb = JMIN;
+        prv[0] = max(W, ea);
+        prv[1] = max(prv[0], t[0]);
+        prv[2] = max(max(W, tot_a), eb);
+        prv[3] = max(prv[2], t[2]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int o = off[j], q = o >> 5, b = o & 31;
+        if (!ok[j] || !((wd[q] >> b) & 1u)) continue;
+        // edges strictly before o: count edges, then the time edges of earlier tuples
+        const int64_t e = sb + pre[q] + __popc(wd[q] & ((1u << b) - 1u)) + tcount(o, false);
+        a.cells.e_pos[e] = base + o;
+        // in-order: final (the stream's first tuple sets maxEventTime to its own ts, S/StreamSlicer.java:39-40);
+        // otherwise a partial completed by count_efix_kernel
+        a.cells.e_ts[e] = (a.check_sorted && prv[j] == JMIN && !a.shard) ? t[j] : prv[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (ok[j]) lmax = max(lmax, t[j]);
+    int64_t c_lo = JMAX;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (ok[j]) c_lo = min(c_lo, cell[j]);
+    c_lo = wred(c_lo, [](long long p, long long q) { return p < q ? p : q; });
+    if (last - c_lo <= 8) {
+      // few cells: one masked wave reduction per cell before the last; the last stays in registers
+      for (int64_t c = c_lo; c < last; c++) {
+        uint64_t kc = 0, kw = 0;
+        double kf = 0.0;
+        int64_t kt = JMIN, kn = JMAX, km = ID_MIN, kx = ID_MAX;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if (!ok[j] || cell[j] != c || t[j] < first_start) continue;
+          uint64_t w;
+          int64_t l, h;
+          lift<VT>(v[j], w, l, h);
+          kc++;
+          kt = max(kt, t[j]);
+          kn = min(kn, t[j]);
+          if constexpr ((NEED & NEED_SUM) != 0) {
+            if constexpr (VT == VT_F64) kf += __longlong_as_double((long long)w);
+            else kw += w;
+          }
+          if constexpr ((NEED & NEED_MIN) != 0) km = min(km, l);
+          if constexpr ((NEED & NEED_MAX) != 0) kx = max(kx, h);
+        }
+        if (c == cur) {  // the slice carried over from the previous step: registers
+          cnt += kc;
+          tmax = max(tmax, kt);
+          tmin = min(tmin, kn);
+          sw += kw;
+          sf += kf;
+          mn = min(mn, km);
+          mx = max(mx, kx);
+          continue;
+        }
+        const uint64_t rc = wred(kc, [](unsigned long long p, unsigned long long q) { return p + q; });
+        if (rc == 0) continue;
+        const int64_t rt = wred(kt, [](long long p, long long q) { return p > q ? p : q; });
+        const int64_t rn = wred(kn, [](long long p, long long q) { return p < q ? p : q; });
+        uint64_t rw = 0;
+        double rf = 0.0;
+        if constexpr ((NEED & NEED_SUM) != 0) {
+          if constexpr (VT == VT_F64) rf = wred(kf, [](double p, double q) { return p + q; });
+          else rw = wred(kw, [](unsigned long long p, unsigned long long q) { return p + q; });
+        }
+        int64_t rm = ID_MIN, rx = ID_MAX;
+        if constexpr ((NEED & NEED_MIN) != 0) rm = wred(km, [](long long p, long long q) { return p < q ? p : q; });
+        if constexpr ((NEED & NEED_MAX) != 0) rx = wred(kx, [](long long p, long long q) { return p > q ? p : q; });
+        if (lane == 0) cell_add<VT, NEED>(a.cells, c, rc, rt, rn, rw, rf, rm, rx);
+      }
+      if (last != cur) {
+        if (cur >= 0) flush();
+        cur = last;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (!ok[j]) continue;
+        if (t[j] < first_start) n_late++;
+        else if (cell[j] == last) add(t[j], v[j]);
+      }
+      continue;
+    }
+    // many edges in the step: the last cell in registers, other tuples straight to their cell
     if (last != cur) {
       if (cur >= 0) flush();
       cur = last;
     }
-    const int off[4] = {2 * lane, 2 * lane + 1, 128 + 2 * lane, 129 + 2 * lane};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       if (!ok[j]) continue;
@@ -339,24 +498,35 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         n_late++;
         continue;
       }
-      const int o = off[j], q = o >> 5, b = o & 31;
-      const uint32_t mask = (uint32_t)((2ull << b) - 1);
-      int64_t tcnt = 0;  // time edges at or before this tuple (the tuple lands in the last slice appended)
-      for (int64_t k = t0; k < t1; k++) tcnt += a.te_pos[k] <= base + o ? 1 : 0;
-      const int64_t cell = sb + pre[q] + __popc(wd[q] & mask) + tcnt;
-      if (cell == cur) {
+      if (cell[j] == cur) {
         add(t[j], v[j]);
       } else {
         uint64_t w;
         int64_t l, h;
         lift<VT>(v[j], w, l, h);
-        cell_add<VT, NEED>(a.cells, cell, 1, t[j], t[j], w, __longlong_as_double((long long)w), l, h);
+        cell_add<VT, NEED>(a.cells, cell[j], 1, t[j], t[j], w, __longlong_as_double((long long)w), l, h);
       }
     }
   }
   if (cur >= 0) flush();
   const uint32_t nl = wred(n_late, [](uint32_t p, uint32_t q) { return p + q; });
   if (lane == 0 && nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
+  const int64_t wm = wred(lmax, [](long long p, long long q) { return p > q ? p : q; });
+  if (lane == 0) a.stepmax[wave] = wm;  // per-wave max (the prefix over waves: count_premax_*)
+}
+
+// count edges of unsorted batches: complete the max ts before each edge with the waves before its own
+__global__ void count_efix_kernel(CPushArgs a) {
+  const int64_t E = a.meta->n_edges;
+  const int64_t span = a.per_wave * CSTEP;
+  const long long prev = a.shard ? JMIN : a.meta->prev_max;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = a.cells.e_pos[e], w = p / span;
+    int64_t m = max((int64_t)prev, a.cells.e_ts[e]);
+    if (w > 0) m = max(m, (int64_t)a.steppre[w - 1]);
+    // the stream's first tuple sets maxEventTime to its own ts (S/StreamSlicer.java:39-40)
+    a.cells.e_ts[e] = (m == JMIN && !a.shard) ? a.ts[p] : m;
+  }
 }
 
 // ---------------------------------------------------------------- 4. edge positions and slice starts
@@ -386,63 +556,6 @@ __global__ void count_premax_carry_kernel(long long* out, int64_t n, const long 
   const long long c = bsum_incl[b - 1];
   const int64_t i = b * 1024 + threadIdx.x;
   if (i < n) out[i] = max(out[i], c);
-}
-
-__global__ __launch_bounds__(256) void count_edges_kernel(CPushArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (s >= a.nsteps) return;
-  if (a.stepc[s] == 0) return;
-  const int64_t base = s * CSTEP;
-  const int64_t prev = a.shard ? JMIN : a.meta->prev_max;  // shard records carry the chunk-local prefix
-  long long before = s > 0 ? a.steppre[s - 1] : JMIN;
-  before = max(before, (long long)prev);
-  // lane l holds offsets 4l .. 4l+3
-  int64_t t[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int64_t i = base + 4 * lane + j;
-    t[j] = i < a.n ? a.ts[i] : JMIN;
-  }
-  int64_t lm = max(max(t[0], t[1]), max(t[2], t[3]));
-  int64_t ex = lm;  // exclusive prefix max over lanes
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t u = (int64_t)__shfl_up((long long)ex, o);
-    if (lane >= o) ex = max(ex, u);
-  }
-  ex = (int64_t)__shfl_up((long long)ex, 1);
-  if (lane == 0) ex = JMIN;
-  uint32_t wd[8];
-  int pre[9];
-  pre[0] = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int64_t wi = s * 8 + k;
-    wd[k] = wi < a.nwords ? a.bits[wi] : 0u;
-    pre[k + 1] = pre[k] + __popc(wd[k]);
-  }
-  const int64_t sb = a.stepbase[s];
-  int64_t t0 = 0, t1 = 0;
-  if (a.n_te > 0) {
-    t0 = te_lb(a, base);
-    t1 = te_lb(a, base + CSTEP);
-  }
-  int64_t run = max((int64_t)before, ex);
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const int o = 4 * lane + j, q = o >> 5, b = o & 31;
-    if ((wd[q] >> b) & 1u) {
-      int64_t tb = 0;  // time edges of earlier tuples of the step (at this tuple they follow the count edge)
-      for (int64_t k = t0; k < t1; k++) tb += a.te_pos[k] < base + o ? 1 : 0;
-      const int64_t e = sb + pre[q] + __popc(wd[q] & ((1u << b) - 1u)) + tb;  // edges strictly before o
-      a.cells.e_pos[e] = base + o;
-      // max ts of every tuple before the edge (StreamSlicer.maxEventTime); the stream's first tuple sets it to its
-      // own ts first (S/StreamSlicer.java:39-40)
-      a.cells.e_ts[e] = (run == JMIN && !a.shard) ? t[j] : run;
-    }
-    run = max(run, t[j]);
-  }
 }
 
 // index, position and tStart (the edge itself, SliceManager.appendSlice(min_next_edge_ts)) of every time edge
@@ -516,7 +629,7 @@ __global__ void count_finish_kernel(CPushArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   CMeta& m = *a.meta;
   m.tail += m.n_edges;
-  m.prev_max = max(m.prev_max, (int64_t)a.steppre[a.nsteps - 1]);
+  m.prev_max = max(m.prev_max, (int64_t)a.steppre[a.nwaves - 1]);
   m.late_total += m.late_push;
 }
 
@@ -743,7 +856,7 @@ __global__ __launch_bounds__(256) void count_export_kernel(CPushArgs a, int64_t*
   const int64_t E = m.n_edges;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g == 0) {
-    rec[0] = a.steppre[a.nsteps - 1];
+    rec[0] = a.steppre[a.nwaves - 1];
     rec[1] = (int64_t)m.late_push;
     rec[2] = E;
     rec[3] = a.n;
@@ -857,6 +970,7 @@ __global__ void count_shard_merge_kernel(CShardArgs a) {
 }  // namespace ck
 
 // ---------------------------------------------------------------- launch wrappers
+hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
 template <int VT, int NEED>
 static void launch_ingest_cn(const CPushArgs& a, hipStream_t st) {
   const int64_t waves = (a.nsteps + a.per_wave - 1) / a.per_wave;
@@ -875,8 +989,6 @@ static void launch_ingest_cv(const CPushArgs& a, hipStream_t st) {
     default: launch_ingest_cn<VT, 7>(a, st); break;
   }
 }
-
-hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
 
 // everything of one push after the bitmap was cleared; premax_tmp: >= nsteps/1024 + 2 words
 hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, int64_t* scan_tmp,
@@ -900,18 +1012,20 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
   else if (a.vt == VT_I64) launch_ingest_cv<VT_I64>(a, st);
   else launch_ingest_cv<VT_F64>(a, st);
   if (ingest_end) (void)hipEventRecord(ingest_end, st);
-  // step prefix max
-  const int64_t nb = (a.nsteps + 1023) / 1024;
+  // prefix max over the wave maxima
+  const int64_t nb = (a.nwaves + 1023) / 1024;
   hipLaunchKernelGGL(ck::count_premax_block_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.stepmax, a.steppre,
-                     a.nsteps, premax_tmp);
+                     a.nwaves, premax_tmp);
   if (nb > 1) {
     hipLaunchKernelGGL(ck::count_premax_block_kernel, dim3((unsigned)((nb + 1023) / 1024)), dim3(1024), 0, st,
                        premax_tmp, premax_tmp, nb, premax_tmp + nb);
-    if (nb > 1024) return hipErrorInvalidValue;  // > 2^28 tuples per push: split the push
-    hipLaunchKernelGGL(ck::count_premax_carry_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.steppre, a.nsteps,
+    if (nb > 1024) return hipErrorInvalidValue;  // > 2^20 waves per push: split the push
+    hipLaunchKernelGGL(ck::count_premax_carry_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.steppre, a.nwaves,
                        premax_tmp);
   }
-  hipLaunchKernelGGL(ck::count_edges_kernel, dim3((unsigned)((a.nsteps * 64 + 255) / 256)), dim3(256), 0, st, a);
+  if (!a.check_sorted)  // unsorted batches: complete the count edges' slice starts
+    hipLaunchKernelGGL(ck::count_efix_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((a.cell_cap + 255) / 256, 4096))),
+                       dim3(256), 0, st, a);
   if (a.n_te > 0)
     hipLaunchKernelGGL(ck::count_tedges_kernel, dim3((unsigned)((a.n_te + 255) / 256)), dim3(256), 0, st, a);
   if (a.shard) return hipGetLastError();  // the caller exports (launch_count_export) instead of appending
@@ -922,10 +1036,13 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
   return hipGetLastError();
 }
 
-hipError_t launch_count_time_edges(const CTimeArgs& a, hipStream_t st) {
+hipError_t launch_count_time_edges(const CTimeArgs& a, int64_t* scan_tmp, hipStream_t st) {
   if (a.n_cand <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ck::count_tcand_kernel, dim3((unsigned)((a.n_cand + 255) / 256)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(ck::count_tcompact_kernel, dim3(1), dim3(1024), 0, st, a);
+  const unsigned nb = (unsigned)((a.n_cand + 255) / 256);
+  hipLaunchKernelGGL(ck::count_tcand_kernel, dim3(nb), dim3(256), 0, st, a);
+  hipError_t e = launch_scan_i64(a.flag, a.off, a.n_cand, scan_tmp, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ck::count_tscatter_kernel, dim3(nb), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

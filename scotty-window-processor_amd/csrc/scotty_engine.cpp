@@ -1457,6 +1457,7 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
   if (!op) return -1;
   if (which == 5) return op->mode;  // 1 grid path, 2 exact engine, 3 count path
   if (which == 6) return op->c ? op->c->last_nte : -1;
+  if (which == 7) return op->c ? (int64_t)op->c->last_te_us : -1;
   if (!op->x) return -1;
   switch (which) {
     case 0: return op->x->last_events;

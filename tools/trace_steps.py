@@ -1,61 +1,39 @@
-"""Per-step kernel breakdown from a rocprofv3 kernel trace (run_kernel_trace.csv).
-
-A "step" of a grid-path leg starts at a cix_build_kernel launch (one per micro-batch).  Prints, for the last
---steps steps before the --leg-th grid-path operator boundary, every scotty kernel's average duration per step and
-the step's summed device time.  Legs are separated where the ingest kernel's template changes or a gap of more than
---gap-ms seconds occurs between launches.
-
-    python tools/trace_steps.py gpurun_out/prof_c2s/run_kernel_trace.csv --steps 5
-"""
+"""Per-step kernel breakdown of a bench leg from a rocprofv3 kernel trace: a step starts at the kernel named by
+--first (e.g. count_mark_kernel for the count path); the --steps longest steps are averaged.  Also prints the
+step's span (first kernel start to last kernel end) so host gaps show as span - device time."""
 import argparse
-import csv
 import collections
-
-
-def short(name):
-    n = name.split("(")[0].replace("void ", "").replace("scotty::", "")
-    return n
+import csv
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
+    ap.add_argument("--first", required=True)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--gap-ms", type=float, default=200.0)
     args = ap.parse_args()
-    rows = [r for r in csv.DictReader(open(args.trace)) if "at::" not in r["Kernel_Name"]]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # split into legs at long idle gaps
-    legs, cur, last_end = [], [], None
-    for r in rows:
-        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        if last_end is not None and s - last_end > args.gap_ms * 1e6 and cur:
-            legs.append(cur)
-            cur = []
-        cur.append(r)
-        last_end = e
-    if cur:
-        legs.append(cur)
-    for li, leg in enumerate(legs):
-        starts = [i for i, r in enumerate(leg) if "cix_build_kernel" in r["Kernel_Name"]] + [len(leg)]
-        starts_all = starts[-(args.steps + 1):]
-        if len(starts_all) < 2:
-            continue
+    rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = [r for r in rows if "at::native" not in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows) if args.first in r["Kernel_Name"]] + [len(rows)]
+    steps = []
+    for a, b in zip(starts[:-1], starts[1:]):
         per = collections.defaultdict(float)
-        cnt = collections.defaultdict(int)
-        total = 0.0
-        nsteps = len(starts_all) - 1
-        for a, b in zip(starts_all[:-1], starts_all[1:]):
-            for r in leg[a:b]:
-                d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-                per[short(r["Kernel_Name"])] += d
-                cnt[short(r["Kernel_Name"])] += 1
-                total += d
-        span = (int(leg[starts_all[-1] - 1]["End_Timestamp"]) - int(leg[starts_all[0]]["Start_Timestamp"])) / 1e3
-        print("leg %d: %d steps, device %.1f us/step, wall span %.1f us/step" % (li, nsteps, total / nsteps,
-                                                                                span / nsteps))
-        for k in sorted(per, key=lambda k: -per[k]):
-            print("   %-50s %8.1f us/step  (%d launches)" % (k[:50], per[k] / nsteps, cnt[k]))
+        for r in rows[a:b]:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            per[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scotty::", "")[:60]] += d
+        span = (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+        steps.append((per, span))
+    steps.sort(key=lambda p: -sum(p[0].values()))
+    sel = steps[:args.steps]
+    tot = collections.defaultdict(float)
+    for p, _ in sel:
+        for k, v in p.items():
+            tot[k] += v
+    k = len(sel)
+    print("%d largest steps: device %.1f us/step, span %.1f us/step" % (k, sum(tot.values()) / k,
+                                                                       sum(s for _, s in sel) / k))
+    for name in sorted(tot, key=lambda x: -tot[x]):
+        print("  %-60s %8.1f us/step" % (name, tot[name] / k))
 
 
 if __name__ == "__main__":
