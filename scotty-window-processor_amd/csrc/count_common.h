@@ -141,6 +141,13 @@ struct CShardArgs {
   CMeta* meta;
 };
 
+// Window rows of one window's trigger as an arithmetic run: start = first + k * step, end = start + size
+// (k < count); generated on the device in registration order (count_rows_kernel)
+struct CRowSeg {
+  int64_t first, step, count, size;
+  int64_t meas;
+};
+
 struct CWmArgs {
   CSlices sl;
   CMeta* meta;

@@ -17,6 +17,8 @@ hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hip
 hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st);
 hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st);
 hipError_t launch_count_time_edges(const CTimeArgs& a, int64_t* scan_tmp, hipStream_t st);
+hipError_t launch_count_rows(const CRowSeg* segs, const int64_t* seg_off, int nseg, int64_t* w_start, int64_t* w_end,
+                             int32_t* w_meas, int64_t nw, hipStream_t st);
 
 #define CCHK(x)                                                      \
   do {                                                               \
@@ -76,6 +78,8 @@ CEngine::~CEngine() {
   dfree(d_wins);
   dfree(sl.ts); dfree(sl.tl); dfree(sl.cs); dfree(sl.cnt);
   for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
+  if (h_segs) (void)hipHostFree(h_segs);
+  dfree(d_segbuf);
   dfree(spare.ts); dfree(spare.tl); dfree(spare.cs); dfree(spare.cnt);
   for (int k = 0; k < NPART; k++) dfree(spare.p[k]);
   dfree(cells.cnt); dfree(cells.tl); dfree(cells.tf); dfree(cells.e_pos); dfree(cells.e_ts);
@@ -337,7 +341,9 @@ int CEngine::grow_slices(int64_t need_more) {
     ncap = spare_cap;
   } else {
     if (spare_cap) {
-      dfree(spare.ts); dfree(spare.tl); dfree(spare.cs); dfree(spare.cnt);
+      if (h_segs) (void)hipHostFree(h_segs);
+  dfree(d_segbuf);
+  dfree(spare.ts); dfree(spare.tl); dfree(spare.cs); dfree(spare.cnt);
       for (int k = 0; k < NPART; k++) dfree(spare.p[k]);
     }
     CCHK(dalloc(&n.ts, ncap));
@@ -599,6 +605,67 @@ void CEngine::trigger(int64_t last_c, int64_t cur_c, int64_t last_t, int64_t cur
   }
 }
 
+// trigger() as arithmetic runs, one per window (rows stay in registration order); false when a bound is too close
+// to the int64 range for plain arithmetic (the loop in trigger() then reproduces Java's wrap-around)
+bool CEngine::trigger_segs(int64_t last_c, int64_t cur_c, int64_t last_t, int64_t cur_t) {
+  constexpr int64_t LIM = (int64_t)1 << 61;
+  auto ok = [&](int64_t x) { return x > -LIM && x < LIM; };
+  auto cdiv = [](int64_t p, int64_t q) { return (p + q - 1) / q; };  // p > 0, q > 0
+  std::vector<CRowSeg> segs;
+  segs.reserve(reg.size());
+  for (const CWin& w : reg) {
+    const bool tm = w.measure == SCOTTY_MEASURE_TIME;
+    const int64_t last = tm ? last_t : last_c, cur = tm ? cur_t : cur_c;
+    if (!ok(last) || !ok(cur) || !ok(w.a) || !ok(w.b)) return false;
+    CRowSeg g{0, 0, 0, 0, w.measure};
+    if (w.kind == SCOTTY_WIN_TUMBLING) {  // s = ls + k size while s + size <= cur
+      const int64_t size = w.a, ls = last - jmod(last + size, size);
+      g.first = ls;
+      g.step = size;
+      g.size = size;
+      g.count = cur - ls - size >= 0 ? (cur - ls - size) / size + 1 : 0;
+    } else if (w.kind == SCOTTY_WIN_SLIDING) {  // s = ls - k slide while s + size > last; s >= 0, s + size <= cur + 1
+      const int64_t size = w.a, slide = w.b, ls = cur - jmod(cur + slide, slide);
+      const int64_t k_end = ls + size > last ? cdiv(ls + size - last, slide) : 0;
+      const int64_t k_lo = ls + size - cur - 1 > 0 ? cdiv(ls + size - cur - 1, slide) : 0;
+      const int64_t k_hi = std::min(k_end - 1, ls >= 0 ? ls / slide : (int64_t)-1);
+      g.first = ls - k_lo * slide;
+      g.step = -slide;
+      g.size = size;
+      g.count = std::max<int64_t>(0, k_hi - k_lo + 1);
+    } else {
+      const int64_t e = w.a + w.b;
+      g.first = w.a;
+      g.size = w.b;
+      g.count = (last <= e && e <= cur) ? 1 : 0;
+    }
+    segs.push_back(g);
+  }
+  nseg = (int)segs.size();
+  if (nseg + (nseg + 1) > segcap) {
+    if (h_segs) (void)hipHostFree(h_segs);
+    dfree(d_segbuf);
+    h_segs = nullptr;
+    d_segbuf = nullptr;
+    segcap = 2 * nseg + 64;
+    if (hipHostMalloc((void**)&h_segs, segcap * sizeof(CRowSeg), hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&d_segbuf, segcap * sizeof(CRowSeg)) != hipSuccess) {
+      segcap = 0;
+      return false;
+    }
+  }
+  (void)hipStreamSynchronize(stream);  // the pinned runs of the previous watermark were read
+  int64_t* off = (int64_t*)(h_segs + nseg);
+  int64_t o = 0;
+  for (int i = 0; i < nseg; i++) {
+    h_segs[i] = segs[i];
+    off[i] = o;
+    o += segs[i].count;
+  }
+  off[nseg] = o;
+  return true;
+}
+
 int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   r.n = 0;
   r.start.clear(); r.end.clear(); r.meas.clear(); r.has.clear(); r.key.clear();
@@ -643,17 +710,30 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
           "S/WindowManager.java:109-112)";
     return SCOTTY_ERR_INDEX;
   }
-  trigger(last_count, jadd(h_meta->cend, 1), last_wm, wm);
-  const int64_t nw = (int64_t)rows.size();
+  const bool segs = trigger_segs(last_count, jadd(h_meta->cend, 1), last_wm, wm);
+  if (!segs) trigger(last_count, jadd(h_meta->cend, 1), last_wm, wm);
+  int64_t nw = 0;
   int64_t min_c = count, max_c = 0, min_t = JMAX, max_t = 0;  // S/WindowManager.java:61-71
-  for (const Row& w : rows) {
-    if (w.meas == SCOTTY_MEASURE_TIME) {
-      min_t = std::min(min_t, w.start);
-      max_t = std::max(max_t, w.end);
+  auto bound = [&](int32_t meas, int64_t st, int64_t en) {
+    if (meas == SCOTTY_MEASURE_TIME) {
+      min_t = std::min(min_t, st);
+      max_t = std::max(max_t, en);
     } else {
-      min_c = std::min(min_c, w.start);
-      max_c = std::max(max_c, w.end);
+      min_c = std::min(min_c, st);
+      max_c = std::max(max_c, en);
     }
+  };
+  if (segs) {
+    for (int i = 0; i < nseg; i++) {
+      const CRowSeg& g = h_segs[i];
+      if (g.count == 0) continue;
+      const int64_t s_a = g.first, s_b = g.first + (g.count - 1) * g.step;
+      bound((int32_t)g.meas, std::min(s_a, s_b), std::max(s_a, s_b) + g.size);
+    }
+    nw = ((int64_t*)(h_segs + nseg))[nseg];
+  } else {
+    for (const Row& w : rows) bound(w.meas, w.start, w.end);
+    nw = (int64_t)rows.size();
   }
   if (nw > wcap) {
     dfree(d_wstart); dfree(d_wend); dfree(d_meas); dfree(d_has);
@@ -676,18 +756,26 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     CCHK(dalloc(&d_pre_sum, pcap));
     CCHK(dalloc(&d_bsum, 2 * (pcap / 1024 + 2)));
   }
-  h_start.resize(nw);
-  h_end.resize(nw);
-  h_meas.resize(nw);
-  for (int64_t i = 0; i < nw; i++) {
-    h_start[i] = rows[i].start;
-    h_end[i] = rows[i].end;
-    h_meas[i] = rows[i].meas;
-  }
-  if (nw > 0) {
-    CCHK(hipMemcpyAsync(d_wstart, h_start.data(), nw * 8, hipMemcpyHostToDevice, stream));
-    CCHK(hipMemcpyAsync(d_wend, h_end.data(), nw * 8, hipMemcpyHostToDevice, stream));
-    CCHK(hipMemcpyAsync(d_meas, h_meas.data(), nw * 4, hipMemcpyHostToDevice, stream));
+  if (segs) {  // rows generated on the device from the runs
+    if (nw > 0) {
+      CCHK(hipMemcpyAsync(d_segbuf, h_segs, nseg * sizeof(CRowSeg) + (nseg + 1) * 8, hipMemcpyHostToDevice, stream));
+      CCHK(launch_count_rows((const CRowSeg*)d_segbuf, (const int64_t*)((CRowSeg*)d_segbuf + nseg), nseg, d_wstart,
+                             d_wend, d_meas, nw, stream));
+    }
+  } else {
+    h_start.resize(nw);
+    h_end.resize(nw);
+    h_meas.resize(nw);
+    for (int64_t i = 0; i < nw; i++) {
+      h_start[i] = rows[i].start;
+      h_end[i] = rows[i].end;
+      h_meas[i] = rows[i].meas;
+    }
+    if (nw > 0) {
+      CCHK(hipMemcpyAsync(d_wstart, h_start.data(), nw * 8, hipMemcpyHostToDevice, stream));
+      CCHK(hipMemcpyAsync(d_wend, h_end.data(), nw * 8, hipMemcpyHostToDevice, stream));
+      CCHK(hipMemcpyAsync(d_meas, h_meas.data(), nw * 4, hipMemcpyHostToDevice, stream));
+    }
   }
   a.min_count = min_c;
   a.max_count = max_c;
@@ -730,9 +818,18 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   r.d_has = d_has;
   for (size_t k = 0; k < aggs.size(); k++) r.d_vals[k] = d_vals[k];
   if (to_host && nw > 0) {
-    r.start = h_start;
-    r.end = h_end;
-    r.meas = h_meas;
+    if (segs) {
+      r.start.resize(nw);
+      r.end.resize(nw);
+      r.meas.resize(nw);
+      CCHK(hipMemcpyAsync(r.start.data(), d_wstart, nw * 8, hipMemcpyDeviceToHost, stream));
+      CCHK(hipMemcpyAsync(r.end.data(), d_wend, nw * 8, hipMemcpyDeviceToHost, stream));
+      CCHK(hipMemcpyAsync(r.meas.data(), d_meas, nw * 4, hipMemcpyDeviceToHost, stream));
+    } else {
+      r.start = h_start;
+      r.end = h_end;
+      r.meas = h_meas;
+    }
     r.has.resize(nw);
     r.vals.assign(aggs.size(), std::vector<int64_t>(nw));
     CCHK(hipMemcpyAsync(r.has.data(), d_has, nw, hipMemcpyDeviceToHost, stream));

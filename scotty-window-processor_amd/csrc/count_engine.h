@@ -111,6 +111,11 @@ class CEngine {
   };
   std::vector<int32_t> h_meas;
   std::vector<Row> rows;
+  bool trigger_segs(int64_t last_c, int64_t cur_c, int64_t last_t, int64_t cur_t);  // false: use trigger()
+  CRowSeg* h_segs = nullptr;  // pinned: the runs, then nseg + 1 offsets
+  int64_t segcap = 0;         // runs h_segs / d_segbuf hold
+  int nseg = 0;
+  void* d_segbuf = nullptr;
   int64_t wcap = 0, pcap = 0;
   int64_t *d_wstart = nullptr, *d_wend = nullptr;
   int32_t* d_meas = nullptr;

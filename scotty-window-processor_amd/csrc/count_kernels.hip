@@ -842,6 +842,23 @@ __global__ __launch_bounds__(256) void count_wm_agg_kernel(CWmArgs a) {
   }
 }
 
+// rows of the triggered windows from per-window arithmetic runs (seg_off: exclusive prefix of the run lengths)
+__global__ void count_rows_kernel(const CRowSeg* segs, const int64_t* seg_off, int nseg, int64_t* w_start,
+                                  int64_t* w_end, int32_t* w_meas, int64_t nw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nw) return;
+  int l = 0, h = nseg - 1;  // last run with seg_off <= i
+  while (l < h) {
+    const int m = (l + h + 1) >> 1;
+    if (seg_off[m] <= i) l = m; else h = m - 1;
+  }
+  const CRowSeg g = segs[l];
+  const int64_t st = g.first + (i - seg_off[l]) * g.step;
+  w_start[i] = st;
+  w_end[i] = st + g.size;
+  w_meas[i] = (int32_t)g.meas;
+}
+
 __global__ void count_gc_kernel(CWmArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   CMeta& m = *a.meta;
@@ -1057,6 +1074,14 @@ hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hip
   const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_edges + 255) / 256, 4096));
   hipLaunchKernelGGL(ck::count_shard_append_kernel, dim3(bx, (unsigned)a.world), dim3(256), 0, st, a);
   hipLaunchKernelGGL(ck::count_shard_merge_kernel, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_rows(const CRowSeg* segs, const int64_t* seg_off, int nseg, int64_t* w_start, int64_t* w_end,
+                             int32_t* w_meas, int64_t nw, hipStream_t st) {
+  if (nw <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ck::count_rows_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, segs, seg_off, nseg,
+                     w_start, w_end, w_meas, nw);
   return hipGetLastError();
 }
 
