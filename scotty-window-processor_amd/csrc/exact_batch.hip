@@ -98,6 +98,8 @@ struct XBArgs {
   int32_t vt;
   int32_t cfg_nctx_host;   // session windows (host copy, decides which passes run)
   int64_t* sufmin;         // [sc] suffix minimum of tStart over [i, tail) (unsorted slice lists only)
+  int32_t* tjump;          // [ntiles] (sessions) some item after the tile's first exceeds the tile's running max
+                           // by more than the smallest gap: only then can a tuple other than the first open a session
 };
 
 namespace xb {
@@ -349,9 +351,38 @@ __global__ void xb_prep_kernel(XBArgs a) {
   if (lane == 0) *a.snap = sn;
 }
 
+// tile maxima; with session windows also the tile's jump flag (tjump), from the staged rows in arrival order
 __global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   const int64_t base = (int64_t)blockIdx.x * XB_TILE;
+  if (a.cfg_nctx_host > 0) {
+    __shared__ long long tb[XB_LDS];
+    __shared__ int s_jump;
+    if (threadIdx.x == 0) s_jump = 0;
+    stage_tile(a.ts, a.n, blockIdx.x, tb);
+    const long long* row = tb + threadIdx.x * (XB_ITEMS + 1);
+    int64_t rmax = JMIN;
+#pragma unroll
+    for (int j = 0; j < XB_ITEMS; j++) rmax = max(rmax, (int64_t)row[j]);  // padding items are JMIN
+    int64_t lp = block_excl_max(rmax, wtot);  // local exclusive prefix (no carry)
+    const int64_t gap = a.snap->min_gap;
+    bool jump = false;
+#pragma unroll
+    for (int j = 0; j < XB_ITEMS; j++) {
+      const int64_t t = row[j];
+      if (lp != JMIN && t != JMIN && t > jadd(lp, gap)) jump = true;
+      lp = max(lp, t);
+    }
+    if (jump) s_jump = 1;
+    const int64_t m = wmax(rmax);
+    if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      a.tmax[blockIdx.x] = max(max(wtot[0], wtot[1]), max(wtot[2], wtot[3]));
+      a.tjump[blockIdx.x] = s_jump;
+    }
+    return;
+  }
   int64_t m = JMIN;
 #pragma unroll
   for (int r = 0; r < XB_ITEMS; r++) {
@@ -392,9 +423,29 @@ __global__ __launch_bounds__(1024) void xb_carry_kernel(XBArgs a) {
 }
 
 // pass 1: count new-session in-order tuples per context and tile
+// a tile without a jump, once the batch's running max has left p_start (no batch-start special case): only its
+// first item can open a session; its new-session bits and the running max before it
+__device__ __forceinline__ bool tile_simple(const XBArgs& a, int64_t tile, int& nsm0, int64_t* pb0) {
+  const XSnap& sn = *a.snap;
+  const int64_t carry = max((int64_t)a.pcarry[tile], sn.p_start);
+  if (a.tjump[tile] || carry <= sn.p_start) return false;
+  const int64_t t0 = a.ts[tile * XB_TILE];
+  nsm0 = t0 >= carry ? newsess_bits(a, t0, carry, pb0) : 0;
+  return true;
+}
+
 __global__ __launch_bounds__(XB_THREADS) void xb_nscount_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
+  {
+    int nsm0;
+    int64_t pb0[XMAXCTX];
+    if (tile_simple(a, blockIdx.x, nsm0, pb0)) {
+      if (threadIdx.x == 0)
+        for (int k = 0; k < a.cfg->n_ctx; k++) a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x] = (nsm0 >> k) & 1;
+      return;
+    }
+  }
   TileItems it;
   load_tile(a, blockIdx.x, it, wtot, tb);
   int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
@@ -450,6 +501,22 @@ __global__ __launch_bounds__(1024) void xb_rows_scan_kernel(int64_t* cnt, int64_
 __global__ __launch_bounds__(XB_THREADS) void xb_nswrite_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
+  {
+    int nsm0;
+    int64_t pb0[XMAXCTX];
+    if (tile_simple(a, blockIdx.x, nsm0, pb0)) {
+      if (threadIdx.x == 0)
+        for (int k = 0; k < a.cfg->n_ctx; k++) {
+          if (!((nsm0 >> k) & 1)) continue;
+          const int64_t off = a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+          if (off < a.ns_cap) {
+            a.ns_start[(int64_t)k * a.ns_cap + off] = a.ts[(int64_t)blockIdx.x * XB_TILE];
+            a.ns_pb[(int64_t)k * a.ns_cap + off] = pb0[k];
+          }
+        }
+      return;
+    }
+  }
   TileItems it;
   load_tile(a, blockIdx.x, it, wtot, tb);
   int64_t cnt[XMAXCTX] = {0, 0, 0, 0};
@@ -558,37 +625,13 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   uint64_t nsm_all = 0;  // 4 new-session bits per item
   uint32_t io_ev = 0;    // in-order events, evaluated once
   uint32_t io = 0;       // in-order items
-  {
-    TileWalk w(a, it, true);
-    for (int j = 0; j < it.cnt; j++) {
-      const int64_t t = it.row[j];
-      if (t >= w.p) {
-        io |= 1u << j;
-        int64_t pb[XMAXCTX];
-        int nsm = 0;
-        if (inorder_event(a, t, w.p, w.g(c), it.base + j, nsm, pb)) io_ev |= 1u << j;
-        nsm_all |= (uint64_t)nsm << (4 * j);
-#pragma unroll
-        for (int k = 0; k < XMAXCTX; k++)
-          if (nsm & (1 << k)) loc[k]++;
-      }
-      w.next(t);
-    }
-  }
-  for (int k = 0; k < c->n_ctx; k++)
-    nsb[k] = block_excl_sum(loc[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+  int nsm0 = 0;
+  int64_t pb0[XMAXCTX];
   uint32_t bits = 0;
   int64_t nev = 0;
   int64_t tail_m = JMIN;  // max after this thread's last event
   bool has = false;
-  TileWalk w(a, it, false);
-  for (int j = 0; j < it.cnt; j++) {
-    const int64_t t = it.row[j];
-    const bool ev = ((io >> j) & 1) ? ((io_ev >> j) & 1) != 0 : classify(a, t, w.p, JMAX, it.base + j, nsb);
-    const int nsm = (int)((nsm_all >> (4 * j)) & 15u);
-#pragma unroll
-    for (int k = 0; k < XMAXCTX; k++)
-      if (nsm & (1 << k)) nsb[k]++;
+  auto mark = [&](int j, bool ev, int64_t t) {
     if (ev) {
       bits |= 1u << j;
       nev++;
@@ -597,7 +640,59 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
     } else {
       tail_m = max(tail_m, t);
     }
-    w.next(t);
+  };
+  if (c->n_ctx > 0 && tile_simple(a, blockIdx.x, nsm0, pb0)) {
+    // only the tile's first item can open a session: the sessions before each item need no block scan, and one
+    // walk classifies in-order and out-of-order items alike
+    for (int k = 0; k < c->n_ctx; k++)
+      nsb[k] = a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x] + (threadIdx.x > 0 ? (nsm0 >> k) & 1 : 0);
+    TileWalk w(a, it, true);
+    for (int j = 0; j < it.cnt; j++) {
+      const int64_t t = it.row[j];
+      bool ev;
+      if (t >= w.p) {
+        int64_t pb[XMAXCTX];
+        int nsm = 0;
+        ev = inorder_event(a, t, w.p, w.g(c), it.base + j, nsm, pb);
+      } else {
+        ev = classify(a, t, w.p, JMAX, it.base + j, nsb);
+      }
+      if (threadIdx.x == 0 && j == 0)
+        for (int k = 0; k < c->n_ctx; k++) nsb[k] += (nsm0 >> k) & 1;
+      mark(j, ev, t);
+      w.next(t);
+    }
+  } else {
+    {
+      TileWalk w(a, it, true);
+      for (int j = 0; j < it.cnt; j++) {
+        const int64_t t = it.row[j];
+        if (t >= w.p) {
+          io |= 1u << j;
+          int64_t pb[XMAXCTX];
+          int nsm = 0;
+          if (inorder_event(a, t, w.p, w.g(c), it.base + j, nsm, pb)) io_ev |= 1u << j;
+          nsm_all |= (uint64_t)nsm << (4 * j);
+#pragma unroll
+          for (int k = 0; k < XMAXCTX; k++)
+            if (nsm & (1 << k)) loc[k]++;
+        }
+        w.next(t);
+      }
+    }
+    for (int k = 0; k < c->n_ctx; k++)
+      nsb[k] = block_excl_sum(loc[k], wtot, nullptr) + a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x];
+    TileWalk w(a, it, false);
+    for (int j = 0; j < it.cnt; j++) {
+      const int64_t t = it.row[j];
+      const bool ev = ((io >> j) & 1) ? ((io_ev >> j) & 1) != 0 : classify(a, t, w.p, JMAX, it.base + j, nsb);
+      const int nsm = (int)((nsm_all >> (4 * j)) & 15u);
+#pragma unroll
+      for (int k = 0; k < XMAXCTX; k++)
+        if (nsm & (1 << k)) nsb[k]++;
+      mark(j, ev, t);
+      w.next(t);
+    }
   }
   // bitmap: 16 bits per thread, two threads per word
   {
@@ -684,6 +779,10 @@ __global__ __launch_bounds__(XB_THREADS) void xb_evwrite_kernel(XBArgs a) {
   __shared__ long long s_tail[XB_THREADS];
   __shared__ int s_has[XB_THREADS];
   __shared__ long long tb[XB_LDS];
+  {  // a tile without events writes nothing (ev_cnt holds exclusive offsets)
+    const int64_t nxt = blockIdx.x + 1 < a.ntiles ? a.ev_cnt[blockIdx.x + 1] : a.ctl->ev_total;
+    if (nxt == a.ev_cnt[blockIdx.x]) return;
+  }
   stage_tile(a.ts, a.n, blockIdx.x, tb);
   const int64_t base = (int64_t)blockIdx.x * XB_TILE + (int64_t)threadIdx.x * XB_ITEMS;
   const int cnt = (int)max((int64_t)0, min((int64_t)XB_ITEMS, a.n - base));

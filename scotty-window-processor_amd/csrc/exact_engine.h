@@ -166,6 +166,7 @@ class XEngine {
   int64_t *xb_nscnt = nullptr, *xb_nstot = nullptr, *xb_nsstart = nullptr, *xb_nspb = nullptr;
   int64_t* xb_evcnt = nullptr;
   int32_t* xb_seghas = nullptr;
+  int32_t* xb_tjump = nullptr;  // per-tile session-jump flags (exact_batch.hip, xb_tilemax_kernel)
   uint32_t* xb_bits = nullptr;
   int64_t *xb_evpos = nullptr, *xb_evt = nullptr, *xb_evv = nullptr, *xb_eppos = nullptr;
   long long* xb_evm = nullptr;
