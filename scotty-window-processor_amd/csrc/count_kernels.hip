@@ -43,6 +43,11 @@ __device__ __forceinline__ T wred(T v, F f) {
   for (int o = 32; o > 0; o >>= 1) v = f(v, (T)__shfl_xor(v, o));
   return v;
 }
+// full-wave DPP reductions (x::dpp_reduce; every lane active): the ingest kernel's flushes and edge steps
+__device__ __forceinline__ uint64_t rsum(uint64_t v) { return x::fsum64(v); }
+__device__ __forceinline__ int64_t rmax(int64_t v) { return x::fmax64(v); }
+__device__ __forceinline__ int64_t rmin(int64_t v) { return x::fmin64(v); }
+__device__ __forceinline__ double rsumf(double v) { return x::fsumf(v); }
 __device__ __forceinline__ int64_t uni(int64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
@@ -215,19 +220,19 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   uint32_t n_late = 0;
   int64_t lmax = JMIN;  // running max of this lane's tuples in the wave (dropped ones too)
   auto flush = [&]() {
-    const uint64_t c = wred(cnt, [](unsigned long long p, unsigned long long q) { return p + q; });
+    const uint64_t c = rsum(cnt);
     if (c != 0) {
-      const int64_t tm = wred(tmax, [](long long p, long long q) { return p > q ? p : q; });
-      const int64_t tn = wred(tmin, [](long long p, long long q) { return p < q ? p : q; });
+      const int64_t tm = rmax(tmax);
+      const int64_t tn = rmin(tmin);
       uint64_t s = 0;
       double f = 0.0;
       if constexpr ((NEED & NEED_SUM) != 0) {
-        if constexpr (VT == VT_F64) f = wred(sf, [](double p, double q) { return p + q; });
-        else s = wred(sw, [](unsigned long long p, unsigned long long q) { return p + q; });
+        if constexpr (VT == VT_F64) f = rsumf(sf);
+        else s = rsum(sw);
       }
       int64_t m1 = ID_MIN, m2 = ID_MAX;
-      if constexpr ((NEED & NEED_MIN) != 0) m1 = wred(mn, [](long long p, long long q) { return p < q ? p : q; });
-      if constexpr ((NEED & NEED_MAX) != 0) m2 = wred(mx, [](long long p, long long q) { return p > q ? p : q; });
+      if constexpr ((NEED & NEED_MIN) != 0) m1 = rmin(mn);
+      if constexpr ((NEED & NEED_MAX) != 0) m2 = rmax(mx);
       if (lane == 0) cell_add<VT, NEED>(a.cells, cur, c, tm, tn, s, f, m1, m2);
     }
     cnt = 0; sw = 0; sf = 0.0; tmax = JMIN; tmin = JMAX; mn = ID_MIN; mx = ID_MAX;
@@ -389,7 +394,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         prv[2] = lane == 0 ? l63 : p3;
         prv[3] = t[2];
       } else {  // the wave's running max before the step, then the in-step exclusive prefix max
-        const int64_t W = wred(lmax, [](long long p, long long q) { return p > q ? p : q; });
+        const int64_t W = rmax(lmax);
         int64_t ia = max(t[0], t[1]), ib = max(t[2], t[3]);
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -426,7 +431,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; j++)
       if (ok[j]) c_lo = min(c_lo, cell[j]);
-    c_lo = wred(c_lo, [](long long p, long long q) { return p < q ? p : q; });
+    c_lo = rmin(c_lo);
     if (last - c_lo <= 8) {
       // few cells: one masked wave reduction per cell before the last; the last stays in registers
       for (int64_t c = c_lo; c < last; c++) {
@@ -459,19 +464,19 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
           mx = max(mx, kx);
           continue;
         }
-        const uint64_t rc = wred(kc, [](unsigned long long p, unsigned long long q) { return p + q; });
+        const uint64_t rc = rsum(kc);
         if (rc == 0) continue;
-        const int64_t rt = wred(kt, [](long long p, long long q) { return p > q ? p : q; });
-        const int64_t rn = wred(kn, [](long long p, long long q) { return p < q ? p : q; });
+        const int64_t rt = rmax(kt);
+        const int64_t rn = rmin(kn);
         uint64_t rw = 0;
         double rf = 0.0;
         if constexpr ((NEED & NEED_SUM) != 0) {
-          if constexpr (VT == VT_F64) rf = wred(kf, [](double p, double q) { return p + q; });
-          else rw = wred(kw, [](unsigned long long p, unsigned long long q) { return p + q; });
+          if constexpr (VT == VT_F64) rf = rsumf(kf);
+          else rw = rsum(kw);
         }
         int64_t rm = ID_MIN, rx = ID_MAX;
-        if constexpr ((NEED & NEED_MIN) != 0) rm = wred(km, [](long long p, long long q) { return p < q ? p : q; });
-        if constexpr ((NEED & NEED_MAX) != 0) rx = wred(kx, [](long long p, long long q) { return p > q ? p : q; });
+        if constexpr ((NEED & NEED_MIN) != 0) rm = rmin(km);
+        if constexpr ((NEED & NEED_MAX) != 0) rx = rmax(kx);
         if (lane == 0) cell_add<VT, NEED>(a.cells, c, rc, rt, rn, rw, rf, rm, rx);
       }
       if (last != cur) {
@@ -511,7 +516,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   if (cur >= 0) flush();
   const uint32_t nl = wred(n_late, [](uint32_t p, uint32_t q) { return p + q; });
   if (lane == 0 && nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
-  const int64_t wm = wred(lmax, [](long long p, long long q) { return p > q ? p : q; });
+  const int64_t wm = rmax(lmax);
   if (lane == 0) a.stepmax[wave] = wm;  // per-wave max (the prefix over waves: count_premax_*)
 }
 

@@ -1070,15 +1070,16 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
     const int s_ref = __builtin_amdgcn_readlane(si, ref);
     const bool in_ref = act && si == s_ref;
     const unsigned int c_ref = (unsigned int)__popcll(__ballot(in_ref));
-    const int64_t tmx_r = wmax(in_ref ? t : JMIN);
-    const int64_t tmn_r = wmin(in_ref ? t : JMAX);
+    // DPP reductions: every lane of the block is active here
+    const int64_t tmx_r = fmax64(in_ref ? t : JMIN);
+    const int64_t tmn_r = lazy ? fmin64(in_ref ? t : JMAX) : JMAX;
     uint64_t sw_r = 0;
     if (need & NEED_SUM) {
-      if constexpr (VT == VT_F64) sw_r = (uint64_t)__double_as_longlong(wsumf(in_ref ? __longlong_as_double(vb) : 0.0));
-      else sw_r = wsum(in_ref ? lf.sum : 0);
+      if constexpr (VT == VT_F64) sw_r = (uint64_t)__double_as_longlong(fsumf(in_ref ? __longlong_as_double(vb) : 0.0));
+      else sw_r = fsum64(in_ref ? lf.sum : 0);
     }
-    const int64_t mn_r = (need & NEED_MIN) ? wmin(in_ref ? lf.mn : ID_MIN) : ID_MIN;
-    const int64_t mx_r = (need & NEED_MAX) ? wmax(in_ref ? lf.mx : ID_MAX) : ID_MAX;
+    const int64_t mn_r = (need & NEED_MIN) ? fmin64(in_ref ? lf.mn : ID_MIN) : ID_MIN;
+    const int64_t mx_r = (need & NEED_MAX) ? fmax64(in_ref ? lf.mx : ID_MAX) : ID_MAX;
     auto update = [&](int tgt, unsigned int c_, int64_t tmx, int64_t tmn, uint64_t sw, int64_t mn, int64_t mx) {
       if (tgt >= wbase && tgt < wbase + XW) {
         const int k = tgt - wbase;

@@ -42,6 +42,47 @@ __device__ __forceinline__ double wsumf(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
+// Full-wave reductions over DPP row shifts / broadcasts (no LDS crossbar): the gfx9 inclusive-scan sequence
+// (row_shr 1-3 of the lane's own value, row_shr 4 / 8 within the row, row_bcast 15 / 31 across rows) leaves the
+// total in lane 63, which is broadcast.  Every lane of the wave must be active at the call.
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ uint64_t dpp64(uint64_t id, uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)id, (int)(uint32_t)v, CTRL, ROW, BANK, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(id >> 32), (int)(uint32_t)(v >> 32), CTRL, ROW, BANK, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+template <class F>
+__device__ __forceinline__ uint64_t dpp_reduce(uint64_t x, uint64_t id, F f) {
+  uint64_t v = f(x, dpp64<0x111, 0xF, 0xF>(id, x));  // row_shr:1
+  v = f(v, dpp64<0x112, 0xF, 0xF>(id, x));           // row_shr:2 (of the lane's own value)
+  v = f(v, dpp64<0x113, 0xF, 0xF>(id, x));           // row_shr:3
+  v = f(v, dpp64<0x114, 0xF, 0xE>(id, v));           // row_shr:4, banks 1-3
+  v = f(v, dpp64<0x118, 0xF, 0xC>(id, v));           // row_shr:8, banks 2-3
+  v = f(v, dpp64<0x142, 0xA, 0xF>(id, v));           // row_bcast:15 into rows 1, 3
+  v = f(v, dpp64<0x143, 0xC, 0xF>(id, v));           // row_bcast:31 into rows 2, 3
+  return (uint64_t)rl64((int64_t)v, 63);
+}
+__device__ __forceinline__ int64_t fmax64(int64_t v) {
+  return (int64_t)dpp_reduce((uint64_t)v, (uint64_t)JMIN,
+                             [](uint64_t p, uint64_t q) { return (uint64_t)max((int64_t)p, (int64_t)q); });
+}
+__device__ __forceinline__ int64_t fmin64(int64_t v) {
+  return (int64_t)dpp_reduce((uint64_t)v, (uint64_t)JMAX,
+                             [](uint64_t p, uint64_t q) { return (uint64_t)min((int64_t)p, (int64_t)q); });
+}
+__device__ __forceinline__ uint64_t fsum64(uint64_t v) {
+  return dpp_reduce(v, 0ull, [](uint64_t p, uint64_t q) { return p + q; });
+}
+__device__ __forceinline__ double fsumf(double v) {
+  return __longlong_as_double((long long)dpp_reduce((uint64_t)__double_as_longlong(v), (uint64_t)__double_as_longlong(0.0),
+                                                    [](uint64_t p, uint64_t q) {
+                                                      return (uint64_t)__double_as_longlong(
+                                                          __longlong_as_double((long long)p) +
+                                                          __longlong_as_double((long long)q));
+                                                    }));
+}
+
 // exclusive prefix max over lanes (lane 0 gets JMIN)
 __device__ __forceinline__ int64_t excl_pmax(int64_t v, int lane) {
   int64_t inc = v;
