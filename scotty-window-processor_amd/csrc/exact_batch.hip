@@ -351,38 +351,12 @@ __global__ void xb_prep_kernel(XBArgs a) {
   if (lane == 0) *a.snap = sn;
 }
 
-// tile maxima; with session windows also the tile's jump flag (tjump), from the staged rows in arrival order
+// tile maxima; with session windows also the tile's jump flag (tjump).  A tuple after the tile's first one opens a
+// session only if it exceeds the running max before it (>= the first ts) by more than a gap, so
+// tmax <= first + min_gap rules it out (conservative near the int64 range, where jadd wraps).
 __global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   const int64_t base = (int64_t)blockIdx.x * XB_TILE;
-  if (a.cfg_nctx_host > 0) {
-    __shared__ long long tb[XB_LDS];
-    __shared__ int s_jump;
-    if (threadIdx.x == 0) s_jump = 0;
-    stage_tile(a.ts, a.n, blockIdx.x, tb);
-    const long long* row = tb + threadIdx.x * (XB_ITEMS + 1);
-    int64_t rmax = JMIN;
-#pragma unroll
-    for (int j = 0; j < XB_ITEMS; j++) rmax = max(rmax, (int64_t)row[j]);  // padding items are JMIN
-    int64_t lp = block_excl_max(rmax, wtot);  // local exclusive prefix (no carry)
-    const int64_t gap = a.snap->min_gap;
-    bool jump = false;
-#pragma unroll
-    for (int j = 0; j < XB_ITEMS; j++) {
-      const int64_t t = row[j];
-      if (lp != JMIN && t != JMIN && t > jadd(lp, gap)) jump = true;
-      lp = max(lp, t);
-    }
-    if (jump) s_jump = 1;
-    const int64_t m = wmax(rmax);
-    if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      a.tmax[blockIdx.x] = max(max(wtot[0], wtot[1]), max(wtot[2], wtot[3]));
-      a.tjump[blockIdx.x] = s_jump;
-    }
-    return;
-  }
   int64_t m = JMIN;
 #pragma unroll
   for (int r = 0; r < XB_ITEMS; r++) {
@@ -392,37 +366,99 @@ __global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
   m = wmax(m);
   if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) a.tmax[blockIdx.x] = max(max(wtot[0], wtot[1]), max(wtot[2], wtot[3]));
-}
-
-// single workgroup: exclusive carries over tiles (prefix max of tile maxima)
-__global__ __launch_bounds__(1024) void xb_carry_kernel(XBArgs a) {
-  __shared__ long long wt[16];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int64_t carry = JMIN;
-  for (int64_t b0 = 0; b0 < a.ntiles; b0 += 1024) {
-    const int64_t i = b0 + tid;
-    const int64_t v = i < a.ntiles ? (int64_t)a.tmax[i] : JMIN;
-    int64_t inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t u = (int64_t)__shfl_up((long long)inc, o);
-      if (lane >= o) inc = max(inc, u);
+  if (threadIdx.x == 0) {
+    const int64_t tm = max(max(wtot[0], wtot[1]), max(wtot[2], wtot[3]));
+    a.tmax[blockIdx.x] = tm;
+    if (a.cfg_nctx_host > 0) {
+      const int64_t gap = a.snap->min_gap, t0 = a.ts[base];
+      const bool safe = gap >= 0 && t0 <= JMAX - gap && tm <= JMAX - gap;
+      a.tjump[blockIdx.x] = (safe && tm <= t0 + gap) ? 0 : 1;
     }
-    if (lane == 63) wt[wid] = inc;
-    __syncthreads();
-    int64_t before = carry;
-    for (int w = 0; w < wid; w++) before = max(before, (int64_t)wt[w]);
-    int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
-    if (lane == 0) ex = JMIN;
-    if (i < a.ntiles) a.pcarry[i] = max(before, ex);
-    int64_t tot = carry;
-    for (int w = 0; w < 16; w++) tot = max(tot, (int64_t)wt[w]);
-    __syncthreads();
-    carry = tot;
   }
 }
 
-// pass 1: count new-session in-order tuples per context and tile
+// Single-workgroup exclusive scans over the per-tile values (16 consecutive tiles per thread and round, so a
+// 2^26-tuple batch takes one round): V is a pair (h, t) combined by op(prev, cur); identity id.
+struct SPair {
+  int64_t h, t;
+};
+template <class Op>
+__device__ __forceinline__ SPair wg_scan16(int64_t n, SPair id, SPair carry, Op op, SPair (*ld)(const XBArgs&, int64_t, int),
+                                           void (*st)(const XBArgs&, int64_t, int, SPair), const XBArgs& a, int row) {
+  __shared__ long long wh[16], wt[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int64_t c0 = 0; c0 < n; c0 += 1024 * 16) {
+    const int64_t b = c0 + (int64_t)tid * 16;
+    SPair loc[16];
+    SPair acc = id;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const SPair v = b + j < n ? ld(a, b + j, row) : id;
+      loc[j] = acc;
+      acc = op(acc, v);
+    }
+    SPair inc = acc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      SPair u;
+      u.h = (int64_t)__shfl_up((long long)inc.h, o);
+      u.t = (int64_t)__shfl_up((long long)inc.t, o);
+      if (lane >= o) inc = op(u, inc);
+    }
+    if (lane == 63) {
+      wh[wid] = inc.h;
+      wt[wid] = inc.t;
+    }
+    __syncthreads();
+    SPair before = carry;
+    for (int w = 0; w < wid; w++) before = op(before, SPair{wh[w], wt[w]});
+    SPair ex;
+    ex.h = (int64_t)__shfl_up((long long)inc.h, 1);
+    ex.t = (int64_t)__shfl_up((long long)inc.t, 1);
+    if (lane == 0) ex = id;
+    const SPair pre = op(before, ex);
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (b + j < n) st(a, b + j, row, op(pre, loc[j]));
+    SPair tot = carry;
+    for (int w = 0; w < 16; w++) tot = op(tot, SPair{wh[w], wt[w]});
+    __syncthreads();
+    carry = tot;
+  }
+  return carry;
+}
+
+struct OpMax {
+  __device__ SPair operator()(SPair p, SPair q) const { return SPair{0, max(p.t, q.t)}; }
+};
+struct OpSum {
+  __device__ SPair operator()(SPair p, SPair q) const { return SPair{0, p.t + q.t}; }
+};
+struct OpSeg {  // segmented max: a tile with an event resets the running max
+  __device__ SPair operator()(SPair p, SPair q) const { return SPair{p.h | q.h, q.h ? q.t : max(p.t, q.t)}; }
+};
+__device__ SPair ld_tmax(const XBArgs& a, int64_t k, int) { return SPair{0, (int64_t)a.tmax[k]}; }
+__device__ void st_pcarry(const XBArgs& a, int64_t k, int, SPair v) { a.pcarry[k] = v.t; }
+__device__ SPair ld_seg(const XBArgs& a, int64_t k, int) { return SPair{a.seg_has[k], (int64_t)a.seg_tail[k]}; }
+__device__ void st_mcarry(const XBArgs& a, int64_t k, int, SPair v) { a.m_carry[k] = v.t; }
+
+// exclusive carries over tiles (prefix max of tile maxima)
+__global__ __launch_bounds__(1024) void xb_carry_kernel(XBArgs a) {
+  (void)wg_scan16(a.ntiles, SPair{0, JMIN}, SPair{0, JMIN}, OpMax{}, ld_tmax, st_pcarry, a, 0);
+}
+
+// exclusive scan of per-tile counts (rows of length ntiles), totals to tot[row]
+__device__ SPair ld_row(const XBArgs& a, int64_t k, int row) { return SPair{0, a.ev_cnt[(int64_t)row * a.ntiles + k]}; }
+__device__ void st_row(const XBArgs& a, int64_t k, int row, SPair v) { a.ev_cnt[(int64_t)row * a.ntiles + k] = v.t; }
+__global__ __launch_bounds__(1024) void xb_rows_scan_kernel(XBArgs a, int64_t* cnt, int rows, int64_t* tot) {
+  XBArgs b = a;
+  b.ev_cnt = cnt;  // the rows to scan in place (ev_cnt or ns_cnt)
+  for (int r = 0; r < rows; r++) {
+    const SPair t = wg_scan16(b.ntiles, SPair{0, 0}, SPair{0, 0}, OpSum{}, ld_row, st_row, b, r);
+    if (threadIdx.x == 0 && tot) tot[r] = t.t;
+  }
+}
+
 // a tile without a jump, once the batch's running max has left p_start (no batch-start special case): only its
 // first item can open a session; its new-session bits and the running max before it
 __device__ __forceinline__ bool tile_simple(const XBArgs& a, int64_t tile, int& nsm0, int64_t* pb0) {
@@ -465,35 +501,6 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nscount_kernel(XBArgs a) {
     int64_t tot;
     (void)block_excl_sum(cnt[k], wtot, &tot);
     if (threadIdx.x == 0) a.ns_cnt[(int64_t)k * a.ntiles + blockIdx.x] = tot;
-  }
-}
-
-// single workgroup: exclusive scan of per-tile counts (rows of length ntiles), totals to tot[row]
-__global__ __launch_bounds__(1024) void xb_rows_scan_kernel(int64_t* cnt, int64_t ntiles, int rows, int64_t* tot) {
-  __shared__ long long wt[16];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int r = 0; r < rows; r++) {
-    int64_t* c = cnt + (int64_t)r * ntiles;
-    int64_t carry = 0;
-    for (int64_t b0 = 0; b0 < ntiles; b0 += 1024) {
-      const int64_t i = b0 + tid;
-      const int64_t v = i < ntiles ? c[i] : 0;
-      int64_t inc = v;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t u = (int64_t)__shfl_up((long long)inc, o);
-        if (lane >= o) inc += u;
-      }
-      if (lane == 63) wt[wid] = inc;
-      __syncthreads();
-      int64_t before = carry;
-      for (int w = 0; w < wid; w++) before += wt[w];
-      if (i < ntiles) c[i] = before + inc - v;
-      int64_t t = carry;
-      for (int w = 0; w < 16; w++) t += wt[w];
-      __syncthreads();
-      carry = t;
-    }
-    if (tid == 0 && tot) tot[r] = carry;
   }
 }
 
@@ -720,57 +727,10 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   }
 }
 
-// single workgroup: carries of the segmented max over tiles (same operator as in xb_evwrite_kernel)
+// carries of the segmented max over tiles (same operator as in xb_evwrite_kernel)
 __global__ __launch_bounds__(1024) void xb_mcarry_kernel(XBArgs a) {
-  __shared__ long long st_[16];
-  __shared__ int sh_[16];
-  const int tid = threadIdx.x, ln = tid & 63, wd = tid >> 6;
-  int64_t cm = JMIN;  // carry into the current chunk
-  for (int64_t b0 = 0; b0 < a.ntiles; b0 += 1024) {
-    const int64_t k = b0 + tid;
-    int hh = k < a.ntiles ? a.seg_has[k] : 0;
-    int64_t tt = k < a.ntiles ? (int64_t)a.seg_tail[k] : JMIN;
-    const int h0 = hh;
-    const int64_t t0 = tt;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int h2 = __shfl_up(hh, o);
-      const int64_t t2 = (int64_t)__shfl_up((long long)tt, o);
-      if (ln >= o) {
-        tt = hh ? tt : max(t2, tt);
-        hh = hh | h2;
-      }
-    }
-    if (ln == 63) {
-      st_[wd] = tt;
-      sh_[wd] = hh;
-    }
-    __syncthreads();
-    // exclusive value for tile k
-    int hx = 0;
-    int64_t tx = JMIN;
-    {
-      const int hp = __shfl_up(hh, 1);
-      const int64_t tp = (int64_t)__shfl_up((long long)tt, 1);
-      if (ln > 0) {
-        hx = hp;
-        tx = tp;
-      }
-    }
-    for (int w = wd - 1; w >= 0 && !hx; w--) {
-      tx = max(tx, (int64_t)st_[w]);
-      hx = sh_[w];
-    }
-    const int64_t ex = hx ? tx : max(cm, tx);
-    if (k < a.ntiles) a.m_carry[k] = ex;
-    // carry for the next chunk: fold the whole chunk
-    int64_t nc = cm;
-    for (int w = 0; w < 16; w++) nc = sh_[w] ? (int64_t)st_[w] : max(nc, (int64_t)st_[w]);
-    (void)h0;
-    (void)t0;
-    __syncthreads();
-    cm = nc;
-  }
-  if (tid == 0) a.ctl->m_tail = cm;
+  const SPair t = wg_scan16(a.ntiles, SPair{0, JMIN}, SPair{0, JMIN}, OpSeg{}, ld_seg, st_mcarry, a, 0);
+  if (threadIdx.x == 0) a.ctl->m_tail = t.t;
 }
 
 // pass 4: write the compacted events (position, ts, value, max ts since the previous event)
@@ -1184,15 +1144,14 @@ hipError_t xb_classify_phase(XBArgs& a, int phase, hipStream_t st) {
       hipLaunchKernelGGL(xb::xb_carry_kernel, dim3(1), dim3(1024), 0, st, a);
       if (a.cfg_nctx_host > 0) {
         hipLaunchKernelGGL(xb::xb_nscount_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
-        hipLaunchKernelGGL(xb::xb_rows_scan_kernel, dim3(1), dim3(1024), 0, st, a.ns_cnt, a.ntiles,
-                           a.cfg_nctx_host, a.ns_tot);
+        hipLaunchKernelGGL(xb::xb_rows_scan_kernel, dim3(1), dim3(1024), 0, st, a, a.ns_cnt, a.cfg_nctx_host,
+                           a.ns_tot);
       }
       break;
     case 1:  // new-session chains, classification, event counts
       if (a.cfg_nctx_host > 0) hipLaunchKernelGGL(xb::xb_nswrite_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
       hipLaunchKernelGGL(xb::xb_classify_kernel, dim3(nt), dim3(XB_THREADS), 0, st, a);
-      hipLaunchKernelGGL(xb::xb_rows_scan_kernel, dim3(1), dim3(1024), 0, st, a.ev_cnt, a.ntiles, 1,
-                         &a.ctl->ev_total);
+      hipLaunchKernelGGL(xb::xb_rows_scan_kernel, dim3(1), dim3(1024), 0, st, a, a.ev_cnt, 1, &a.ctl->ev_total);
       hipLaunchKernelGGL(xb::xb_mcarry_kernel, dim3(1), dim3(1024), 0, st, a);
       break;
     case 2:  // compacted events

@@ -309,7 +309,34 @@ __device__ int64_t wm_triggers(Op& o, int64_t wm, int64_t* w_start, int64_t* w_e
       lo = o.s.lastCount;
       hi = jadd(o.cl[idx], 1);
     }
-    if (kind == 0) {  // TumblingWindow.triggerWindows :34-39
+    constexpr int64_t LIM = (int64_t)1 << 61;
+    const bool arith = kind <= 1 && lo > -LIM && lo < LIM && hi > -LIM && hi < LIM && a < LIM && b < LIM;
+    if (arith) {  // the trigger loops below as one arithmetic run: ws = first + i * step, i < cnt (lanes split it)
+      int64_t first, step, cnt;
+      if (kind == 0) {
+        const int64_t ls = lo - jmod(lo + a, a);
+        first = ls;
+        step = a;
+        cnt = hi - ls - a >= 0 ? (hi - ls - a) / a + 1 : 0;
+      } else {
+        const int64_t ls = hi - jmod(hi + b, b);
+        const int64_t k_end = ls + a > lo ? (ls + a - lo + b - 1) / b : 0;
+        const int64_t k_lo = ls + a - hi - 1 > 0 ? (ls + a - hi - 1 + b - 1) / b : 0;
+        const int64_t k_hi = min(k_end - 1, ls >= 0 ? ls / b : (int64_t)-1);
+        first = ls - k_lo * b;
+        step = -b;
+        cnt = max((int64_t)0, k_hi - k_lo + 1);
+      }
+      if (!DRY)
+        for (int64_t i = o.lane; i < cnt; i += 64) {
+          const int64_t ws = first + i * step;
+          w_start[off + k + i] = ws;
+          w_end[off + k + i] = ws + a;
+          w_meas[off + k + i] = meas;
+          w_op[off + k + i] = opid;
+        }
+      k += cnt;
+    } else if (kind == 0) {  // TumblingWindow.triggerWindows :34-39
       const int64_t ls = jsub(lo, jmod(jadd(lo, a), a));
       for (int64_t ws = ls; jadd(ws, a) <= hi; ws = jadd(ws, a)) emit(ws, jadd(ws, a), meas);
     } else if (kind == 1) {  // SlidingWindow.triggerWindows :50-57
