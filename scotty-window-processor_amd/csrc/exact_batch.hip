@@ -251,19 +251,56 @@ struct TileWalk {
   __device__ __forceinline__ void next(int64_t t) { p = max(p, t); }
 };
 
-// in-order tuple t (t >= p): contexts in which it starts a new session (the chain of in-batch sessions), and
-// the end of the session before it
-__device__ __forceinline__ int newsess_bits(const XBArgs& a, int64_t t, int64_t p, int64_t* pb) {
+// The batch snapshot and configuration fields the per-tuple classification reads, loaded once per thread
+// (uniform: scalar registers) instead of from global memory at every tuple.
+struct XBH {
+  int64_t n0, nc0, c0, oldest, min_gap, p_start;
+  int32_t started, n_ctx, has_time, has_fixed, has_count, lazy;
+  int64_t gap[XMAXCTX], lim[XMAXCTX], last_start[XMAXCTX], stored_end[XMAXCTX];
+  int32_t ns[XMAXCTX], inv[XMAXCTX];
+};
+__device__ __forceinline__ XBH hoist(const XBArgs& a) {
   const XSnap& sn = *a.snap;
   const XCfg* c = a.cfg;
+  XBH h;
+  h.n0 = sn.n0;
+  h.nc0 = sn.nc0;
+  h.c0 = sn.c0;
+  h.oldest = sn.oldest;
+  h.min_gap = sn.min_gap;
+  h.p_start = sn.p_start;
+  h.started = sn.started;
+  h.n_ctx = c->n_ctx;
+  h.has_time = c->has_time;
+  h.has_fixed = c->has_fixed;
+  h.has_count = c->has_count;
+  h.lazy = c->lazy;
+#pragma unroll
+  for (int k = 0; k < XMAXCTX; k++) {
+    const bool on = k < h.n_ctx;
+    h.gap[k] = on ? c->gap[k] : 0;
+    h.lim[k] = on ? sn.lim[k] : JMIN;
+    h.last_start[k] = on ? sn.last_start[k] : JMAX;
+    h.stored_end[k] = on ? sn.stored_end[k] : JMIN;
+    h.ns[k] = on ? sn.ns[k] : 0;
+    h.inv[k] = on ? sn.inv[k] : 0;
+  }
+  return h;
+}
+
+// in-order tuple t (t >= p): contexts in which it starts a new session (the chain of in-batch sessions), and
+// the end of the session before it
+__device__ __forceinline__ int newsess_bits(const XBH& h, int64_t t, int64_t p, int64_t* pb) {
   int nsmask = 0;
-  for (int k = 0; k < c->n_ctx; k++) {
-    const int64_t gap = c->gap[k];
+#pragma unroll
+  for (int k = 0; k < XMAXCTX; k++) {
+    if (k >= h.n_ctx) break;
+    const int64_t gap = h.gap[k];
     bool nw;
     int64_t before;
-    if (!sn.inv[k] && p == sn.p_start) {
-      nw = sn.ns[k] == 0 || t > jadd(sn.stored_end[k], gap);
-      before = sn.ns[k] == 0 ? JMIN : sn.stored_end[k];
+    if (!h.inv[k] && p == h.p_start) {
+      nw = h.ns[k] == 0 || t > jadd(h.stored_end[k], gap);
+      before = h.ns[k] == 0 ? JMIN : h.stored_end[k];
     } else {
       nw = t > jadd(p, gap);
       before = p;
@@ -275,39 +312,44 @@ __device__ __forceinline__ int newsess_bits(const XBArgs& a, int64_t t, int64_t 
   }
   return nsmask;
 }
+__device__ __forceinline__ int newsess_bits(const XBArgs& a, int64_t t, int64_t p, int64_t* pb) {
+  const XBH h = hoist(a);
+  return newsess_bits(h, t, p, pb);
+}
 
-// in-order classification (depends on P only).  Returns event; sets new-session bits per context.
-__device__ __forceinline__ bool inorder_event(const XBArgs& a, int64_t t, int64_t p, int64_t g, int64_t pos,
-                                              int& nsmask, int64_t* pb) {
-  const XSnap& sn = *a.snap;
-  const XCfg* c = a.cfg;
+// in-order classification (depends on P only).  Returns event; sets new-session bits per context (want_ns).
+__device__ __forceinline__ bool inorder_event(const XBH& h, const XCfg* c, int64_t t, int64_t p, int64_t g,
+                                              int64_t pos, int& nsmask, int64_t* pb, bool want_ns = true) {
   bool ev = false;
   nsmask = 0;
-  if (c->has_time) {
-    if (c->has_fixed) {
-      if ((sn.n0 == JMIN && p == sn.p_start) || (p < sn.n0 && t >= sn.n0) || (p >= sn.n0 && t >= g)) ev = true;
+  if (h.has_time) {
+    if (h.has_fixed) {
+      if ((h.n0 == JMIN && p == h.p_start) || (p < h.n0 && t >= h.n0) || (p >= h.n0 && t >= g)) ev = true;
     }
-    if (c->n_ctx > 0) {
-      if (t >= jadd(p, sn.min_gap)) ev = true;
+    if (h.n_ctx > 0) {
+      if (t >= jadd(p, h.min_gap)) ev = true;
       // calculateNextFlexEdge (S/StreamSlicer.java:118-130): te >= max(maxEventTime, pending edge) + gap, in
       // Java long arithmetic -- with no time window the pending edge is Long.MAX_VALUE and the sum wraps, so
       // every in-order tuple opens a flexible slice.  Pending edge here: n0 until crossed, then nextGrid(P).
-      const int64_t pend = !c->has_fixed ? JMIN : (p < sn.n0 ? sn.n0 : g);
+      const int64_t pend = !h.has_fixed ? JMIN : (p < h.n0 ? h.n0 : g);
       const int64_t tc = max(p, pend);
-      for (int k = 0; k < c->n_ctx; k++)
-        if (t >= jadd(tc, c->gap[k])) ev = true;
+#pragma unroll
+      for (int k = 0; k < XMAXCTX; k++)
+        if (k < h.n_ctx && t >= jadd(tc, h.gap[k])) ev = true;
     }
   }
-  for (int k = 0; k < c->n_ctx; k++) {
-    if (!sn.inv[k] && p == sn.p_start) ev = true;
-    if (t <= sn.lim[k]) ev = true;
+#pragma unroll
+  for (int k = 0; k < XMAXCTX; k++) {
+    if (k >= h.n_ctx) break;
+    if (!h.inv[k] && p == h.p_start) ev = true;
+    if (t <= h.lim[k]) ev = true;
   }
-  nsmask = newsess_bits(a, t, p, pb);
-  if (c->has_count) {
-    const int64_t cnt = jadd(sn.c0, pos);
-    if (sn.nc0 == JMIN || cnt == sn.nc0 || (cnt > sn.nc0 && on_count_grid(c, cnt))) ev = true;
+  if (want_ns) nsmask = newsess_bits(h, t, p, pb);
+  if (h.has_count) {
+    const int64_t cnt = jadd(h.c0, pos);
+    if (h.nc0 == JMIN || cnt == h.nc0 || (cnt > h.nc0 && on_count_grid(c, cnt))) ev = true;
   }
-  if (!sn.started && pos == 0) ev = true;
+  if (!h.started && pos == 0) ev = true;
   return ev;
 }
 
@@ -568,8 +610,7 @@ __global__ __launch_bounds__(XB_THREADS) void xb_nswrite_kernel(XBArgs a) {
 }
 
 // is out-of-order tuple t (before it: m in-batch new sessions of context k, running max p) inside a session
-__device__ __forceinline__ bool ooo_inside(const XBArgs& a, int k, int64_t t, int64_t p, int64_t m) {
-  const XSnap& sn = *a.snap;
+__device__ __forceinline__ bool ooo_inside(const XBArgs& a, const XBH& h, int k, int64_t t, int64_t p, int64_t m) {
   const XCfg* c = a.cfg;
   const int64_t* nss = a.ns_start + (int64_t)k * a.ns_cap;
   const int64_t* nsp = a.ns_pb + (int64_t)k * a.ns_cap;
@@ -582,11 +623,11 @@ __device__ __forceinline__ bool ooo_inside(const XBArgs& a, int k, int64_t t, in
     const int64_t end = lo + 1 < m ? nsp[lo + 1] : p;
     return t <= end;
   }
-  const int ns = sn.ns[k];
+  const int ns = h.ns[k];
   if (ns == 0) return false;
   // the batch-start last session, extended by the in-order tuples
-  const int64_t end0 = m > 0 ? nsp[0] : ((sn.inv[k] || p > sn.p_start) ? p : sn.stored_end[k]);
-  if (t >= sn.last_start[k]) return t <= end0 && t > sn.lim[k];
+  const int64_t end0 = m > 0 ? nsp[0] : ((h.inv[k] || p > h.p_start) ? p : h.stored_end[k]);
+  if (t >= h.last_start[k]) return t <= end0 && t > h.lim[k];
   // settled sessions of the batch start: first session within reach of t must contain it (getSession)
   const int64_t* st_ = a.ss.start + (int64_t)k * c->sesscap;
   const int64_t* en_ = a.ss.end + (int64_t)k * c->sesscap;
@@ -600,21 +641,18 @@ __device__ __forceinline__ bool ooo_inside(const XBArgs& a, int k, int64_t t, in
   return t <= en_[lo] && (lo == 0 || rch[lo - 1] < t);
 }
 
-__device__ __forceinline__ bool classify(const XBArgs& a, int64_t t, int64_t p, int64_t g, int64_t pos,
-                                         const int64_t* ns_before) {
-  const XSnap& sn = *a.snap;
-  const XCfg* c = a.cfg;
-  if (t >= p) {
-    int nsm;
-    int64_t pb[XMAXCTX];
-    return inorder_event(a, t, p, g, pos, nsm, pb);
-  }
-  if (!sn.started) return true;
-  if (t < sn.oldest || c->has_count) return true;
-  if (c->n_ctx > 0) {
-    if (c->lazy) return true;
-    for (int k = 0; k < c->n_ctx; k++)
-      if (!ooo_inside(a, k, t, p, ns_before[k])) return true;
+// out-of-order tuple (t < p): an event unless it falls inside a session of every context
+__device__ __forceinline__ bool ooo_event(const XBArgs& a, const XBH& h, int64_t t, int64_t p,
+                                          const int64_t* ns_before) {
+  if (!h.started) return true;
+  if (t < h.oldest || h.has_count) return true;
+  if (h.n_ctx > 0) {
+    if (h.lazy) return true;
+#pragma unroll
+    for (int k = 0; k < XMAXCTX; k++) {  // unrolled: h's arrays stay in registers
+      if (k >= h.n_ctx) break;
+      if (!ooo_inside(a, h, k, t, p, ns_before[k])) return true;
+    }
   }
   return false;
 }
@@ -648,6 +686,7 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
       tail_m = max(tail_m, t);
     }
   };
+  const XBH h = hoist(a);
   if (c->n_ctx > 0 && tile_simple(a, blockIdx.x, nsm0, pb0)) {
     // only the tile's first item can open a session: the sessions before each item need no block scan, and one
     // walk classifies in-order and out-of-order items alike
@@ -660,9 +699,9 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
       if (t >= w.p) {
         int64_t pb[XMAXCTX];
         int nsm = 0;
-        ev = inorder_event(a, t, w.p, w.g(c), it.base + j, nsm, pb);
+        ev = inorder_event(h, c, t, w.p, w.g(c), it.base + j, nsm, pb, false);
       } else {
-        ev = classify(a, t, w.p, JMAX, it.base + j, nsb);
+        ev = ooo_event(a, h, t, w.p, nsb);
       }
       if (threadIdx.x == 0 && j == 0)
         for (int k = 0; k < c->n_ctx; k++) nsb[k] += (nsm0 >> k) & 1;
@@ -678,7 +717,7 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
           io |= 1u << j;
           int64_t pb[XMAXCTX];
           int nsm = 0;
-          if (inorder_event(a, t, w.p, w.g(c), it.base + j, nsm, pb)) io_ev |= 1u << j;
+          if (inorder_event(h, c, t, w.p, w.g(c), it.base + j, nsm, pb)) io_ev |= 1u << j;
           nsm_all |= (uint64_t)nsm << (4 * j);
 #pragma unroll
           for (int k = 0; k < XMAXCTX; k++)
@@ -692,7 +731,7 @@ __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
     TileWalk w(a, it, false);
     for (int j = 0; j < it.cnt; j++) {
       const int64_t t = it.row[j];
-      const bool ev = ((io >> j) & 1) ? ((io_ev >> j) & 1) != 0 : classify(a, t, w.p, JMAX, it.base + j, nsb);
+      const bool ev = ((io >> j) & 1) ? ((io_ev >> j) & 1) != 0 : ooo_event(a, h, t, w.p, nsb);
       const int nsm = (int)((nsm_all >> (4 * j)) & 15u);
 #pragma unroll
       for (int k = 0; k < XMAXCTX; k++)
