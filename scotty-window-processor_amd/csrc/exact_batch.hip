@@ -958,7 +958,6 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
   const XBCtl& ctl = *a.ctl;
   const int64_t s0 = ctl.seg_start;
   const int64_t s1 = ctl.seg_end < 0 ? a.n : ctl.seg_end;
-  const int lane = threadIdx.x & 63;
   const XCfg* cfg = a.cfg;
   const int need = cfg->need;
   const bool lazy = cfg->lazy != 0;
@@ -992,6 +991,68 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
       e_tail[k] = a.ep_tail[k];
     }
   __syncthreads();
+  // the newest TK search keys in registers: out-of-order tuples a few slices back resolve without LDS lookups
+  constexpr int TK = 16;
+  const int ktop = max(wbase, wtop - TK);
+  int64_t tk[TK];
+#pragma unroll
+  for (int k = 0; k < TK; k++) tk[k] = ktop + k < wtop ? (int64_t)w_key[ktop + k - wbase] : JMAX;
+  // the wave's running partial of the slice in-order tuples land in (the last slice present at their arrival);
+  // it is reduced and flushed only when that slice changes (an event appended a slice) and at the end
+  int s_acc = -1;
+  uint32_t acnt = 0;
+  int64_t atmx = JMIN, atmn = JMAX, amn = ID_MIN, amx = ID_MAX;
+  uint64_t asw = 0;
+  double asf = 0.0;
+  // one slice update: LDS window when the slice is in it, else the slice arrays
+  auto update = [&](int tgt, unsigned int c_, int64_t tmx, int64_t tmn, uint64_t sw, int64_t mn, int64_t mx) {
+    if (tgt >= wbase && tgt < wbase + XW) {
+      const int k = tgt - wbase;
+      atomicAdd(&w_cnt[k], c_);
+      atomicMax(&w_tl[k], (long long)tmx);
+      if (lazy) atomicMin(&w_tf[k], (long long)tmn);  // tFirst only feeds LazySlice record moves
+      if (need & NEED_SUM) {
+        if constexpr (VT == VT_F64) atomicAdd((double*)&w_p0[k], __longlong_as_double((long long)sw));
+        else atomicAdd(&w_p0[k], (unsigned long long)sw);
+      }
+      if (need & NEED_MIN) atomicMin(&w_p1[k], (long long)mn);
+      if (need & NEED_MAX) atomicMax(&w_p2[k], (long long)mx);
+    } else {
+      atomicAdd(&a.sl.cnt[tgt], (unsigned long long)c_);
+      atomicAdd((unsigned long long*)&a.sl.cl[tgt], (unsigned long long)c_);
+      atomicMax((long long*)&a.sl.tl[tgt], (long long)tmx);
+      if (lazy) atomicMin((long long*)&a.sl.tf[tgt], (long long)tmn);
+      if (need & NEED_SUM) {
+        if constexpr (VT == VT_F64) atomicAdd((double*)&a.sl.p[0][tgt], __longlong_as_double((long long)sw));
+        else atomicAdd(&a.sl.p[0][tgt], (unsigned long long)sw);
+      }
+      if (need & NEED_MIN) atomicMin((long long*)&a.sl.p[1][tgt], (long long)mn);
+      if (need & NEED_MAX) atomicMax((long long*)&a.sl.p[2][tgt], (long long)mx);
+    }
+  };
+  auto flush_acc = [&]() {  // DPP reductions: every lane of the block is active at the call sites
+    if (s_acc < 0) return;
+    const uint64_t c_ = fsum64(acnt);
+    if (c_ != 0) {
+      const int64_t tmx = fmax64(atmx);
+      const int64_t tmn = lazy ? fmin64(atmn) : JMAX;
+      uint64_t sw = 0;
+      if (need & NEED_SUM) {
+        if constexpr (VT == VT_F64) sw = (uint64_t)__double_as_longlong(fsumf(asf));
+        else sw = fsum64(asw);
+      }
+      const int64_t mn = (need & NEED_MIN) ? fmin64(amn) : ID_MIN;
+      const int64_t mx = (need & NEED_MAX) ? fmax64(amx) : ID_MAX;
+      if ((threadIdx.x & 63) == 0) update(s_acc, (unsigned int)c_, tmx, tmn, sw, mn, mx);
+    }
+    acnt = 0;
+    atmx = JMIN;
+    atmn = JMAX;
+    amn = ID_MIN;
+    amx = ID_MAX;
+    asw = 0;
+    asf = 0.0;
+  };
   const int64_t total = s1 - s0;
   int64_t chunk = (total + gridDim.x - 1) / gridDim.x;
   chunk = ((chunk + 255) / 256) * 256;
@@ -1032,14 +1093,20 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
       while (ecur + 1 < nep && epos(ecur + 1) < iw) ecur++;
     }
     bool act = i < b1 && !((wd >> (i & 31)) & 1);
-    int si = -1;
+    int si = -1, last = -1;
     if (act) {
       // last epoch entry with pos < i: the last slice present at arrival (a few steps from the wave cursor)
       int64_t lo = ecur;
       while (lo + 1 < nep && epos(lo + 1) < i) lo++;
-      const int last = etail(lo) - 1;
+      last = etail(lo) - 1;
+      int rk = -1;  // last key <= t among the register keys below `last`
+#pragma unroll
+      for (int k = 0; k < TK; k++)
+        if (ktop + k < last && tk[k] <= t) rk = ktop + k;
       if (t >= (last >= wbase ? (int64_t)w_ts[last - wbase] : a.sl.ts[last])) {
         si = last;
+      } else if (rk >= 0) {
+        si = rk;
       } else if (last > wbase && t >= w_key[0]) {  // in the LDS window: last key <= t in [wbase, last)
         int l = 0, h = last - wbase;
         while (l < h) {
@@ -1063,50 +1130,28 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
     const Lift lf = lift(VT, vb);
     const unsigned long long am = __ballot(act);
     if (!am) continue;
-    // the slice of the wave's highest active lane (the open slice for in-order tuples) takes one combined
-    // update; lanes targeting other slices (out-of-order tuples) update theirs individually
+    // the in-order target of the wave's highest active lane; a change flushes the running partial
     const int ref = 63 - __clzll((long long)am);
-    const int s_ref = __builtin_amdgcn_readlane(si, ref);
-    const bool in_ref = act && si == s_ref;
-    const unsigned int c_ref = (unsigned int)__popcll(__ballot(in_ref));
-    // DPP reductions: every lane of the block is active here
-    const int64_t tmx_r = fmax64(in_ref ? t : JMIN);
-    const int64_t tmn_r = lazy ? fmin64(in_ref ? t : JMAX) : JMAX;
-    uint64_t sw_r = 0;
-    if (need & NEED_SUM) {
-      if constexpr (VT == VT_F64) sw_r = (uint64_t)__double_as_longlong(fsumf(in_ref ? __longlong_as_double(vb) : 0.0));
-      else sw_r = fsum64(in_ref ? lf.sum : 0);
+    const int s_ref = __builtin_amdgcn_readlane(last, ref);
+    if (s_ref != s_acc) {
+      flush_acc();
+      s_acc = s_ref;
     }
-    const int64_t mn_r = (need & NEED_MIN) ? fmin64(in_ref ? lf.mn : ID_MIN) : ID_MIN;
-    const int64_t mx_r = (need & NEED_MAX) ? fmax64(in_ref ? lf.mx : ID_MAX) : ID_MAX;
-    auto update = [&](int tgt, unsigned int c_, int64_t tmx, int64_t tmn, uint64_t sw, int64_t mn, int64_t mx) {
-      if (tgt >= wbase && tgt < wbase + XW) {
-        const int k = tgt - wbase;
-        atomicAdd(&w_cnt[k], c_);
-        atomicMax(&w_tl[k], (long long)tmx);
-        if (lazy) atomicMin(&w_tf[k], (long long)tmn);  // tFirst only feeds LazySlice record moves
-        if (need & NEED_SUM) {
-          if constexpr (VT == VT_F64) atomicAdd((double*)&w_p0[k], __longlong_as_double((long long)sw));
-          else atomicAdd(&w_p0[k], (unsigned long long)sw);
-        }
-        if (need & NEED_MIN) atomicMin(&w_p1[k], (long long)mn);
-        if (need & NEED_MAX) atomicMax(&w_p2[k], (long long)mx);
-      } else {
-        atomicAdd(&a.sl.cnt[tgt], (unsigned long long)c_);
-        atomicAdd((unsigned long long*)&a.sl.cl[tgt], (unsigned long long)c_);
-        atomicMax((long long*)&a.sl.tl[tgt], (long long)tmx);
-        if (lazy) atomicMin((long long*)&a.sl.tf[tgt], (long long)tmn);
-        if (need & NEED_SUM) {
-          if constexpr (VT == VT_F64) atomicAdd((double*)&a.sl.p[0][tgt], __longlong_as_double((long long)sw));
-          else atomicAdd(&a.sl.p[0][tgt], (unsigned long long)sw);
-        }
-        if (need & NEED_MIN) atomicMin((long long*)&a.sl.p[1][tgt], (long long)mn);
-        if (need & NEED_MAX) atomicMax((long long*)&a.sl.p[2][tgt], (long long)mx);
+    if (act && si == s_acc) {
+      acnt++;
+      atmx = max(atmx, t);
+      atmn = min(atmn, t);
+      if (need & NEED_SUM) {
+        if constexpr (VT == VT_F64) asf += __longlong_as_double(vb);
+        else asw += lf.sum;
       }
-    };
-    if (lane == ref) update(s_ref, c_ref, tmx_r, tmn_r, sw_r, mn_r, mx_r);
-    if (act && !in_ref) update(si, 1u, t, t, lf.sum, lf.mn, lf.mx);
+      if (need & NEED_MIN) amn = min(amn, lf.mn);
+      if (need & NEED_MAX) amx = max(amx, lf.mx);
+    } else if (act) {
+      update(si, 1u, t, t, lf.sum, lf.mn, lf.mx);
+    }
   }
+  flush_acc();
 
   __syncthreads();
   for (int k = threadIdx.x; k < XW; k += 256) {
