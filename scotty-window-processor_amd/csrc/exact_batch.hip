@@ -98,6 +98,7 @@ struct XBArgs {
   int32_t vt;
   int32_t cfg_nctx_host;   // session windows (host copy, decides which passes run)
   int64_t* sufmin;         // [sc] suffix minimum of tStart over [i, tail) (unsorted slice lists only)
+  long long* tmin;         // [ntiles] tile min (sessions: the quiet-tile test of xb_classify_kernel)
   int32_t* tjump;          // [ntiles] (sessions) some item after the tile's first exceeds the tile's running max
                            // by more than the smallest gap: only then can a tuple other than the first open a session
 };
@@ -399,19 +400,29 @@ __global__ void xb_prep_kernel(XBArgs a) {
 __global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   const int64_t base = (int64_t)blockIdx.x * XB_TILE;
-  int64_t m = JMIN;
+  __shared__ long long wmn[4];
+  int64_t m = JMIN, mn = JMAX;
 #pragma unroll
   for (int r = 0; r < XB_ITEMS; r++) {
     const int64_t i = base + r * XB_THREADS + threadIdx.x;
-    if (i < a.n) m = max(m, a.ts[i]);
+    if (i < a.n) {
+      const int64_t t = a.ts[i];
+      m = max(m, t);
+      mn = min(mn, t);
+    }
   }
   m = wmax(m);
-  if ((threadIdx.x & 63) == 0) wtot[threadIdx.x >> 6] = m;
+  if (a.cfg_nctx_host > 0) mn = wmin(mn);
+  if ((threadIdx.x & 63) == 0) {
+    wtot[threadIdx.x >> 6] = m;
+    wmn[threadIdx.x >> 6] = mn;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t tm = max(max(wtot[0], wtot[1]), max(wtot[2], wtot[3]));
     a.tmax[blockIdx.x] = tm;
     if (a.cfg_nctx_host > 0) {
+      a.tmin[blockIdx.x] = min(min(wmn[0], wmn[1]), min(wmn[2], wmn[3]));
       const int64_t gap = a.snap->min_gap, t0 = a.ts[base];
       const bool safe = gap >= 0 && t0 <= JMAX - gap && tm <= JMAX - gap;
       a.tjump[blockIdx.x] = (safe && tm <= t0 + gap) ? 0 : 1;
@@ -658,12 +669,63 @@ __device__ __forceinline__ bool ooo_event(const XBArgs& a, const XBH& h, int64_t
 }
 
 // pass 3: classify every tuple; event bitmap; per-tile event counts and segmented-max aggregates
+// A quiet tile (sessions, no count windows): no tuple after the first can be an event, so only the first is
+// classified.  In-order tuples after it: no jump beyond min_gap (strict, tmax < first + min_gap), no grid point in
+// (carry, tmax], all above every settled session's reach; out-of-order ones: no in-batch session before the tile
+// and tmin at or above every context's last session start and reach and the oldest slice (inside the last
+// session, which ends at the running max).  Returns true with *ev0 the first tuple's classification.
+__device__ bool quiet_tile(const XBArgs& a, const XBH& h, int64_t tile, bool* ev0) {
+  const XCfg* c = a.cfg;
+  if (h.n_ctx == 0 || h.has_count || h.lazy || !h.started || a.tjump[tile]) return false;
+  const int64_t carry = max((int64_t)a.pcarry[tile], h.p_start);
+  if (carry <= h.p_start || carry < 0) return false;
+  const int64_t base = tile * XB_TILE, tm = a.tmax[tile], tn = a.tmin[tile], t0 = a.ts[base];
+  if (h.min_gap < 0 || t0 > JMAX - h.min_gap || !(tm < t0 + h.min_gap)) return false;
+  int64_t nsb[XMAXCTX] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < XMAXCTX; k++) {
+    if (k >= h.n_ctx) break;
+    nsb[k] = a.ns_cnt[(int64_t)k * a.ntiles + tile];
+    if (nsb[k] != 0 || h.ns[k] == 0) return false;
+    if (carry <= h.lim[k] || tn <= h.lim[k] || tn < h.last_start[k]) return false;
+  }
+  if (tn < h.oldest) return false;
+  int64_t g = JMAX;
+  if (h.has_time && h.has_fixed) {
+    g = next_grid_lane(c, carry);
+    if (carry < h.n0 ? tm >= h.n0 : tm >= g) return false;
+  }
+  if (t0 >= carry) {
+    int nsm;
+    int64_t pb[XMAXCTX];
+    *ev0 = inorder_event(h, c, t0, carry, carry < h.n0 ? h.n0 : g, base, nsm, pb, false);
+  } else {
+    *ev0 = ooo_event(a, h, t0, carry, nsb);
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(XB_THREADS) void xb_classify_kernel(XBArgs a) {
   __shared__ long long wtot[4];
   __shared__ long long tb[XB_LDS];
+  const XCfg* c = a.cfg;
+  {
+    const XBH hq = hoist(a);
+    bool ev0 = false;
+    if (quiet_tile(a, hq, blockIdx.x, &ev0) && !ev0) {  // no event in the tile: zero bitmap words, no walk
+      const int64_t base = (int64_t)blockIdx.x * XB_TILE;
+      const int64_t w0 = base >> 5, w1 = min((a.n + 31) >> 5, (base + XB_TILE) >> 5);
+      for (int64_t w = w0 + threadIdx.x; w < w1; w += XB_THREADS) a.evbits[w] = 0u;
+      if (threadIdx.x == 0) {
+        a.ev_cnt[blockIdx.x] = 0;
+        a.seg_tail[blockIdx.x] = a.tmax[blockIdx.x];
+        a.seg_has[blockIdx.x] = 0;
+      }
+      return;
+    }
+  }
   TileItems it;
   load_tile(a, blockIdx.x, it, wtot, tb);
-  const XCfg* c = a.cfg;
   // new sessions before each item: carry (exclusive offsets of the tile) + local exclusive count
   int64_t nsb[XMAXCTX] = {0, 0, 0, 0};
   int64_t loc[XMAXCTX] = {0, 0, 0, 0};

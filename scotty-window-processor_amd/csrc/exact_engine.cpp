@@ -90,6 +90,7 @@ struct XBArgs {
   int32_t vt;
   int32_t cfg_nctx_host;
   int64_t* sufmin;
+  long long* tmin;
   int32_t* tjump;
 };
 hipError_t xb_classify_phase(XBArgs& a, int phase, hipStream_t st);
@@ -154,7 +155,7 @@ void XEngine::release() {
   for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
   if (h_misc) (void)hipHostFree(h_misc);
   dfree(xb_snap); dfree(xb_ctl); dfree(xb_reach); dfree(xb_tmax); dfree(xb_pcarry); dfree(xb_segtail);
-  dfree(xb_tjump);
+  dfree(xb_tjump); dfree(xb_tmin);
   dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
   dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
   dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
@@ -575,12 +576,13 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
   if (nt > xb_tcap) {
     XCHK(hipStreamSynchronize(stream));
     dfree(xb_tmax); dfree(xb_pcarry); dfree(xb_segtail); dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_evcnt);
-    dfree(xb_seghas); dfree(xb_tjump);
+    dfree(xb_seghas); dfree(xb_tjump); dfree(xb_tmin);
     const int64_t c = std::max<int64_t>(nt, 64);
     XCHK(dalloc(&xb_tmax, c)); XCHK(dalloc(&xb_pcarry, c)); XCHK(dalloc(&xb_segtail, c));
     XCHK(dalloc(&xb_mcarry, c)); XCHK(dalloc(&xb_nscnt, (size_t)c * XMAXCTX)); XCHK(dalloc(&xb_evcnt, c));
     XCHK(dalloc(&xb_seghas, c));
     XCHK(dalloc(&xb_tjump, c));
+    XCHK(dalloc(&xb_tmin, c));
     xb_tcap = c;
   }
   if (n > xb_ncap) {
@@ -626,6 +628,7 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
   a.cfg_nctx_host = cfg.n_ctx;
   a.sufmin = xb_sufmin;
   a.tjump = xb_tjump;
+  a.tmin = xb_tmin;
   XCHK(hipMemsetAsync(xb_ctl, 0, xb_ctl_bytes(), stream));
   if (resume) {
     const int32_t one = 1;

@@ -166,7 +166,8 @@ class XEngine {
   int64_t *xb_nscnt = nullptr, *xb_nstot = nullptr, *xb_nsstart = nullptr, *xb_nspb = nullptr;
   int64_t* xb_evcnt = nullptr;
   int32_t* xb_seghas = nullptr;
-  int32_t* xb_tjump = nullptr;  // per-tile session-jump flags (exact_batch.hip, xb_tilemax_kernel)
+  int32_t* xb_tjump = nullptr;
+  long long* xb_tmin = nullptr;  // per-tile minimum ts (quiet-tile test)  // per-tile session-jump flags (exact_batch.hip, xb_tilemax_kernel)
   uint32_t* xb_bits = nullptr;
   int64_t *xb_evpos = nullptr, *xb_evt = nullptr, *xb_evv = nullptr, *xb_eppos = nullptr;
   long long* xb_evm = nullptr;
