@@ -1,5 +1,6 @@
-"""Per-step kernel breakdown of the C3 leg (exact batch path) from a rocprofv3 kernel trace: a step starts at
-xb_prep_kernel; the last --steps steps whose push carried the full batch (the longest steps) are printed."""
+"""Per-step kernel breakdown of the C3 leg (exact batch path) from a rocprofv3 kernel trace: a step (one push
+round) starts at xb_prep_kernel.  Prints the median round (the steady state) and the largest one (a pause step
+with many events and apply segments)."""
 import argparse
 import collections
 import csv
@@ -8,7 +9,6 @@ import csv
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--steps", type=int, default=5)
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "at::native" not in r["Kernel_Name"]]
@@ -20,16 +20,12 @@ def main():
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             per[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scotty::", "")[:60]] += d
         steps.append(per)
-    steps.sort(key=lambda p: -sum(p.values()))
-    sel = steps[:args.steps]
-    tot = collections.defaultdict(float)
-    for p in sel:
-        for k, v in p.items():
-            tot[k] += v
-    k = len(sel)
-    print("C3: %d largest steps, device %.1f us/step" % (k, sum(tot.values()) / k))
-    for name in sorted(tot, key=lambda x: -tot[x]):
-        print("  %-60s %8.1f us/step" % (name, tot[name] / k))
+    order = sorted(range(len(steps)), key=lambda i: sum(steps[i].values()))
+    for label, i in (("median", order[len(order) // 2]), ("largest", order[-1])):
+        p = steps[i]
+        print("C3 %s round of %d: device %.1f us" % (label, len(steps), sum(p.values())))
+        for name in sorted(p, key=lambda x: -p[x])[:14]:
+            print("  %-60s %8.1f us" % (name, p[name]))
 
 
 if __name__ == "__main__":
