@@ -164,6 +164,18 @@ int scotty_shard_bounds(scotty_op* op, const int64_t* d_ts, size_t n, int64_t* f
 int scotty_shard_push_timed(scotty_op* op, const int64_t* d_ts, const void* d_val, size_t n, int64_t ts0,
                             int64_t n_before, int64_t n_total, int64_t ts_before, int64_t ts_last, void* d_xbuf);
 
+/* ---- key-hash routing of ONE keyed stream over G ranks (no collective on the hot path).
+ * The SPE's keyBy: key k goes to rank keyGroup(k) * G / max_parallelism with keyGroup(k) = murmurHash(k) %
+ * max_parallelism (Flink's KeyGroupRangeAssignment, which routes tuples to the reference's per-task operators,
+ * F/KeyedScottyWindowOperator.java:56-66).  max_parallelism <= 0 means 128 (the SPE's default for G <= 85). */
+int32_t scotty_key_shard(uint32_t key, int world, int max_parallelism);
+/* Stable split of a host micro-batch by that shard: out_* hold the G sub-batches back to back, shard s at
+ * [offsets[s], offsets[s+1]) (offsets has G+1 entries), each in arrival order.  val_bytes = 4 or 8.  threads <= 0:
+ * all hardware threads.  Rank s then pushes its sub-batch with scotty_process_keyed_elements. */
+int scotty_route_keyed(const uint32_t* key, const int64_t* ts, const void* val, size_t val_bytes, size_t n,
+                       int world, int max_parallelism, int threads, uint32_t* out_key, int64_t* out_ts, void* out_val,
+                       uint64_t* offsets);
+
 /* Number of keys (operators) of a keyed op. */
 int64_t scotty_key_count(scotty_op* op);
 

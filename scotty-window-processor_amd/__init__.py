@@ -121,7 +121,7 @@ def header_functions():
     """Function names declared by include/scotty_mi355x.h."""
     import re
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|uint64_t|int64_t)\s+(scotty_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|uint64_t|int64_t|int32_t)\s+(scotty_\w+)\(", txt, re.M)))
 
 
 def lib():
@@ -161,6 +161,9 @@ def lib():
             "scotty_device_timing": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                     ctypes.POINTER(u64)]),
             "scotty_sync": (ctypes.c_int, [P]),
+            "scotty_key_shard": (ctypes.c_int32, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
+            "scotty_route_keyed": (ctypes.c_int, [P, P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_int, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -482,6 +485,42 @@ class KeyedSlicingWindowOperator(SlicingWindowOperator):
 
     def keyCount(self):
         return self._l.scotty_key_count(self._h)
+
+
+class KeyedShardRouter:
+    """Host-side keyBy of one keyed stream over G ranks (scotty_route_keyed): key k goes to rank
+    keyGroup(k) * G // maxParallelism, keyGroup(k) = murmurHash(k) % maxParallelism -- the SPE's key-group
+    assignment that routes tuples to the reference's per-task operators (F/KeyedScottyWindowOperator.java:56-66).
+    route() is a stable split: every shard keeps its tuples' arrival order.  Host-only (no GPU needed); rank r then
+    feeds route(...)[r] to its own KeyedSlicingWindowOperator, with no collective."""
+
+    def __init__(self, world, max_parallelism=128, threads=0):
+        if not 0 < world <= max_parallelism:
+            raise ValueError("need 0 < world <= max_parallelism")
+        self.world, self.max_parallelism, self.threads = world, max_parallelism, threads
+        self._l = lib()
+
+    def shardOf(self, key):
+        return int(self._l.scotty_key_shard(key & 0xFFFFFFFF, self.world, self.max_parallelism))
+
+    def route(self, keys, ts, values):
+        """-> list of G (keys, ts, values) triples, shard r's tuples in arrival order."""
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        t = np.ascontiguousarray(ts, dtype=np.int64)
+        v = np.ascontiguousarray(values)
+        if v.dtype not in (np.int32, np.int64, np.float64):
+            raise ValueError("values must be int32, int64 or float64")
+        n = len(k)
+        assert len(t) == n and len(v) == n
+        ok, ot, ov = np.empty_like(k), np.empty_like(t), np.empty_like(v)
+        off = np.zeros(self.world + 1, dtype=np.uint64)
+        rc = self._l.scotty_route_keyed(k.ctypes.data, t.ctypes.data, v.ctypes.data, v.dtype.itemsize, n,
+                                        self.world, self.max_parallelism, self.threads, ok.ctypes.data,
+                                        ot.ctypes.data, ov.ctypes.data, off.ctypes.data)
+        if rc != 0:
+            raise ScottyError(rc, "scotty_route_keyed failed")
+        o = off.astype(np.int64)
+        return [(ok[o[r]:o[r + 1]], ot[o[r]:o[r + 1]], ov[o[r]:o[r + 1]]) for r in range(self.world)]
 
 
 class ShardedSlicingWindowOperator:

@@ -391,9 +391,9 @@ def test_keyed_large_batch_count_property(pkg):
 
 
 def test_keyed_hash_sharding_equals_single_operator(pkg):
-    """SURVEY §8(e) keyed: ranks own disjoint key sets (hash(key) mod G) and need no collective.  G=3 keyed
-    operators fed by a key partition of one stream (the arrival order of each key kept) leave exactly the rows
-    of one operator fed the whole stream."""
+    """SURVEY §8(e) keyed: ranks own disjoint key sets (the router's key groups) and need no collective.  G=3
+    keyed operators fed by KeyedShardRouter's split of one stream (each shard in arrival order) leave exactly the
+    rows of one operator fed the whole stream."""
     rng = np.random.default_rng(77)
     n = 200_000
     ts, vals = product().workloads.stream(n, 4, t0=100, ooo_frac=0.2, max_delay=300, seed=77)
@@ -410,7 +410,7 @@ def test_keyed_hash_sharding_equals_single_operator(pkg):
         return op
 
     G = 3
-    shard = (keys.astype(np.uint64) * 2654435761 >> 7) % G  # any key hash; the SPE's keyBy in production
+    router = pkg.KeyedShardRouter(G)  # the product's host-side keyBy (scotty_route_keyed)
     whole, parts = make(), [make() for _ in range(G)]
     sched = interval_schedule(ts, 8, lag=400)
     total = 0
@@ -420,10 +420,9 @@ def test_keyed_hash_sharding_equals_single_operator(pkg):
             if hi <= lo:
                 continue
             whole.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
-            for r in range(G):
-                m = shard[lo:hi] == r
-                if m.any():
-                    parts[r].processElements(keys[lo:hi][m], ts[lo:hi][m], vals[lo:hi][m])
+            for r, (k, t, v) in enumerate(router.route(keys[lo:hi], ts[lo:hi], vals[lo:hi])):
+                if len(k):
+                    parts[r].processElements(k, t, v)
         else:
             exp = {}
             for k, w in whole.processWatermark(step[1]):
