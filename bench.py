@@ -468,7 +468,7 @@ def extra_c5t(pkg, dev, batch, steps, warm=3, rank=0, world=1, dist=None):
 def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None):
     """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
     connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
-    with no collective -- rank r owns the keys k with k mod world == r (what an upstream keyBy delivers), `keys`
+    with no collective -- rank r owns the keys KeyedShardRouter(world) assigns it (what an upstream keyBy delivers), `keys`
     is the global key count, `batch` the tuples per rank per step (weak scaling); the timed region is bracketed
     by barriers and the max over ranks is taken."""
     import torch
@@ -485,10 +485,13 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     warm = 61
-    shard_keys = max(1, keys // world)
+    # the keys this rank owns under the product's key-hash router (scotty_key_shard: the SPE's key groups)
+    allk = np.arange(keys, dtype=np.uint32)
+    own = pkg.KeyedShardRouter(world).route(allk, allk.astype(np.int64), allk.astype(np.int32))[rank][0]
+    own = torch.from_numpy(own.astype(np.int32)).to(dev)
     times, rows, elapsed = [], 0, 0.0
     for s in range(warm + steps):
-        k = torch.randint(0, shard_keys, (batch,), device=dev, dtype=torch.int32, generator=g) * world + rank
+        k = own[torch.randint(0, len(own), (batch,), device=dev, dtype=torch.int64, generator=g)]
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         ts = base + s * 1000
         torch.cuda.synchronize(dev)

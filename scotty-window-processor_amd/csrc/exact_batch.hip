@@ -1007,6 +1007,16 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
   }
 }
 
+// A load on a rarely taken branch whose value is used after the branch: waited for INSIDE the branch (the empty asm
+// uses the value there), so the common path past the join carries no wait -- a wait there would be vmcnt(0), draining
+// every outstanding prefetch.  Atomic, so the compiler cannot fold it with an LDS load into one flat load either.
+template <class T>
+__device__ __forceinline__ T gload(const T* p) {
+  T v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("" ::"v"(v));
+  return v;
+}
+
 // apply the simple tuples of [seg_start, seg_end) (all CUs).  Each workgroup streams a contiguous range and
 // accumulates into an LDS window over the newest XW slices (LDS atomics), flushed once per touched slice;
 // wave-uniform runs (in-order tuples all in the current slice) are reduced in registers first.
@@ -1053,12 +1063,33 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
       e_tail[k] = a.ep_tail[k];
     }
   __syncthreads();
-  // the newest TK search keys in registers: out-of-order tuples a few slices back resolve without LDS lookups
-  constexpr int TK = 16;
-  const int ktop = max(wbase, wtop - TK);
-  int64_t tk[TK];
-#pragma unroll
-  for (int k = 0; k < TK; k++) tk[k] = ktop + k < wtop ? (int64_t)w_key[ktop + k - wbase] : JMAX;
+  // bucket index over the window's search keys (sorted: tStart, or its suffix minimum on an unsorted list):
+  // kidx[b] = keys <= kbase + (b << kshift), so the last key <= t lies between kidx[b] and kidx[b + 1] -- usually one
+  // LDS load and at most one compare per out-of-order tuple instead of a bisection of the window
+  constexpr int NB = 1024;
+  __shared__ unsigned short kidx[NB + 1];
+  const int nw = wtop - wbase;
+  const int64_t kbase = w_key[0];
+  int kshift = 0;
+  if (nw > 1) {
+    const uint64_t span = (uint64_t)w_key[nw - 1] - (uint64_t)kbase;
+    while (kshift < 63 && (span >> kshift) >= (uint64_t)NB) kshift++;
+  }
+  for (int b = threadIdx.x; b <= NB; b += 256) {
+    int c = nw;
+    if (b < NB) {
+      const uint64_t d = (uint64_t)b << kshift;
+      const int64_t x = d > (uint64_t)(JMAX - kbase) ? JMAX : (int64_t)((uint64_t)kbase + d);  // saturating
+      int l = 0, h = nw;
+      while (l < h) {
+        const int mid = (l + h) >> 1;
+        if (w_key[mid] <= x) l = mid + 1; else h = mid;
+      }
+      c = l;
+    }
+    kidx[b] = (unsigned short)c;
+  }
+  __syncthreads();
   // the wave's running partial of the slice in-order tuples land in (the last slice present at their arrival);
   // it is reduced and flushed only when that slice changes (an event appended a slice) and at the end
   int s_acc = -1;
@@ -1120,21 +1151,28 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
   chunk = ((chunk + 255) / 256) * 256;
   const int64_t b0 = s0 + (int64_t)blockIdx.x * chunk;
   const int64_t b1 = min(s1, b0 + chunk);
-  // software pipelined: the next iteration's tuple and event word are in flight while this one is combined
+  // software pipelined XD iterations deep: the tuples and event words of the next XD - 1 iterations are in flight
+  // while one is combined (one iteration's loads alone keep too few bytes in flight per CU to approach HBM rate)
+  constexpr int XD = 4;
+  // unconditional loads (the index clamped into the batch): a load under a branch makes the compiler wait for it at
+  // the join, which serialises the pipeline
+  const int64_t jmax = max(b1, (int64_t)1) - 1;
   auto ld = [&](int64_t i, int64_t& t, int64_t& vb, uint32_t& wd) {
-    if (i < b1) {
-      t = a.ts[i];
-      if constexpr (VT == VT_I32) vb = (int64_t)((const int32_t*)a.val)[i];
-      else vb = ((const int64_t*)a.val)[i];
-      wd = a.evbits[i >> 5];
-    }
+    const int64_t j = min(i, jmax);
+    t = __builtin_nontemporal_load(a.ts + j);
+    if constexpr (VT == VT_I32) vb = (int64_t)__builtin_nontemporal_load((const int32_t*)a.val + j);
+    else vb = __builtin_nontemporal_load((const int64_t*)a.val + j);
+    wd = a.evbits[j >> 5];
   };
-  int64_t t_n = 0, v_n = 0;
-  uint32_t wd_n = 0;
-  ld(b0 + threadIdx.x, t_n, v_n, wd_n);
+  int64_t t_q[XD] = {}, v_q[XD] = {};
+  uint32_t wd_q[XD] = {};
+#pragma unroll
+  for (int d = 0; d < XD; d++) ld(b0 + d * 256 + threadIdx.x, t_q[d], v_q[d], wd_q[d]);
   // epoch cursor of this wave (indices only increase): last epoch entry with pos < the wave's first index
-  auto epos = [&](int64_t k) -> int64_t { return ep_lds ? (int64_t)e_pos[k] : a.ep_pos[k]; };
-  auto etail = [&](int64_t k) -> int { return ep_lds ? e_tail[k] : a.ep_tail[k]; };
+  // LDS-or-HBM reads: the HBM side as an atomic load, so the compiler cannot fold the two into one load through a
+  // selected (flat) address -- a flat load waits for every outstanding load and would drain the prefetch pipeline
+  auto epos = [&](int64_t k) -> int64_t { return ep_lds ? (int64_t)e_pos[k] : gload(a.ep_pos + k); };
+  auto etail = [&](int64_t k) -> int { return ep_lds ? e_tail[k] : gload(a.ep_tail + k); };
   int64_t ecur = 0;
   {
     int64_t lo = 0, hi = nep;
@@ -1145,72 +1183,74 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
     }
     ecur = lo;
   }
-  for (int64_t i0 = b0; i0 < b1; i0 += 256) {
-    const int64_t i = i0 + threadIdx.x;
-    const int64_t t = t_n, vb = v_n;
-    const uint32_t wd = wd_n;
-    ld(i + 256, t_n, v_n, wd_n);
-    {
-      const int64_t iw = i0 + (threadIdx.x & ~63);
-      while (ecur + 1 < nep && epos(ecur + 1) < iw) ecur++;
-    }
-    bool act = i < b1 && !((wd >> (i & 31)) & 1);
-    int si = -1, last = -1;
-    if (act) {
-      // last epoch entry with pos < i: the last slice present at arrival (a few steps from the wave cursor)
-      int64_t lo = ecur;
-      while (lo + 1 < nep && epos(lo + 1) < i) lo++;
-      last = etail(lo) - 1;
-      int rk = -1;  // last key <= t among the register keys below `last`
+  for (int64_t i00 = b0; i00 < b1; i00 += 256 * XD) {
 #pragma unroll
-      for (int k = 0; k < TK; k++)
-        if (ktop + k < last && tk[k] <= t) rk = ktop + k;
-      if (t >= (last >= wbase ? (int64_t)w_ts[last - wbase] : a.sl.ts[last])) {
-        si = last;
-      } else if (rk >= 0) {
-        si = rk;
-      } else if (last > wbase && t >= w_key[0]) {  // in the LDS window: last key <= t in [wbase, last)
-        int l = 0, h = last - wbase;
-        while (l < h) {
-          const int mid = (l + h) >> 1;
-          if (w_key[mid] <= t) l = mid + 1; else h = mid;
+    for (int d = 0; d < XD; d++) {
+      const int64_t i0 = i00 + d * 256;
+      const int64_t i = i0 + threadIdx.x;
+      const int64_t t = t_q[d], vb = v_q[d];
+      const uint32_t wd = wd_q[d];
+      ld(i + 256 * XD, t_q[d], v_q[d], wd_q[d]);
+      {
+        const int64_t iw = i0 + (threadIdx.x & ~63);
+        while (ecur + 1 < nep && epos(ecur + 1) < iw) ecur++;
+      }
+      bool act = i < b1 && !((wd >> (i & 31)) & 1);
+      int si = -1, last = -1;
+      if (act) {
+        // last epoch entry with pos < i: the last slice present at arrival (a few steps from the wave cursor)
+        int64_t lo = ecur;
+        while (lo + 1 < nep && epos(lo + 1) < i) lo++;
+        last = etail(lo) - 1;
+        if (t >= (last >= wbase ? (int64_t)w_ts[last - wbase] : gload(a.sl.ts + last))) {
+          si = last;
+        } else if (last > wbase && t >= kbase) {  // in the LDS window: last key <= t in [wbase, last)
+          const uint64_t bo = ((uint64_t)t - (uint64_t)kbase) >> kshift;
+          const int b = bo < (uint64_t)NB ? (int)bo : NB - 1;
+          const int lim = last - wbase;
+          int h = min((int)kidx[b + 1], lim);
+          int l = min((int)kidx[b], h);
+          while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (w_key[mid] <= t) l = mid + 1; else h = mid;
+          }
+          si = wbase + l - 1;
+        } else {  // last slice in [head, last) with tStart <= t (suffix-min keys on an unsorted list)
+          int l = head, h = min(last, wbase);
+          while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (sk[mid] <= t) l = mid + 1; else h = mid;
+          }
+          si = l - 1;
         }
-        si = wbase + l - 1;
-      } else {  // last slice in [head, last) with tStart <= t (suffix-min keys on an unsorted list)
-        int l = head, h = min(last, wbase);
-        while (l < h) {
-          const int mid = (l + h) >> 1;
-          if (sk[mid] <= t) l = mid + 1; else h = mid;
+        if (si < head) {  // cannot happen for a simple tuple (t >= oldest); counted, never silently lost
+          atomicAdd((int*)&a.ctl->pad, 1);
+          act = false;
         }
-        si = l - 1;
       }
-      if (si < head) {  // cannot happen for a simple tuple (t >= oldest); counted, never silently lost
-        atomicAdd((int*)&a.ctl->pad, 1);
-        act = false;
+      const Lift lf = lift(VT, vb);
+      const unsigned long long am = __ballot(act);
+      if (!am) continue;
+      // the in-order target of the wave's highest active lane; a change flushes the running partial
+      const int ref = 63 - __clzll((long long)am);
+      const int s_ref = __builtin_amdgcn_readlane(last, ref);
+      if (s_ref != s_acc) {
+        flush_acc();
+        s_acc = s_ref;
       }
-    }
-    const Lift lf = lift(VT, vb);
-    const unsigned long long am = __ballot(act);
-    if (!am) continue;
-    // the in-order target of the wave's highest active lane; a change flushes the running partial
-    const int ref = 63 - __clzll((long long)am);
-    const int s_ref = __builtin_amdgcn_readlane(last, ref);
-    if (s_ref != s_acc) {
-      flush_acc();
-      s_acc = s_ref;
-    }
-    if (act && si == s_acc) {
-      acnt++;
-      atmx = max(atmx, t);
-      atmn = min(atmn, t);
-      if (need & NEED_SUM) {
-        if constexpr (VT == VT_F64) asf += __longlong_as_double(vb);
-        else asw += lf.sum;
+      if (act && si == s_acc) {
+        acnt++;
+        atmx = max(atmx, t);
+        atmn = min(atmn, t);
+        if (need & NEED_SUM) {
+          if constexpr (VT == VT_F64) asf += __longlong_as_double(vb);
+          else asw += lf.sum;
+        }
+        if (need & NEED_MIN) amn = min(amn, lf.mn);
+        if (need & NEED_MAX) amx = max(amx, lf.mx);
+      } else if (act) {
+        update(si, 1u, t, t, lf.sum, lf.mn, lf.mx);
       }
-      if (need & NEED_MIN) amn = min(amn, lf.mn);
-      if (need & NEED_MAX) amx = max(amx, lf.mx);
-    } else if (act) {
-      update(si, 1u, t, t, lf.sum, lf.mn, lf.mx);
     }
   }
   flush_acc();
