@@ -28,6 +28,7 @@
 
 #include <cstdlib>
 
+#include "exact_batch.h"
 #include "exact_op.h"
 
 namespace scotty {
@@ -61,47 +62,11 @@ struct XBCtl {
   int32_t resume;          // the next event is the stop event of the previous segment
   int32_t pad;
   int64_t m_tail;          // max ts after the batch's last event (JMIN if none)
+  int32_t retry;           // the round outgrew the event / new-session buffers: nothing was applied, the host
+                           // grows them (ev_total, ns_tot) and runs the round again
+  int32_t pad2;
 };
 
-struct XBArgs {
-  const int64_t* ts;
-  const void* val;
-  int64_t n;
-  int64_t ntiles;
-  const XCfg* cfg;
-  XState* st;              // op 0
-  XSlices sl;
-  XSess ss;
-  XSnap* snap;
-  int64_t* reach;          // [XMAXCTX * sesscap] prefix max of (end + gap) over batch-start sessions
-  long long* tmax;         // [ntiles] tile max
-  long long* pcarry;       // [ntiles] exclusive prefix max carry
-  int64_t* ns_cnt;         // [XMAXCTX][ntiles] new sessions per tile -> exclusive offsets
-  int64_t* ns_tot;         // [XMAXCTX]
-  int64_t* ns_start;       // [XMAXCTX][ns_cap]
-  int64_t* ns_pb;          // [XMAXCTX][ns_cap]
-  int64_t ns_cap;
-  int64_t* ev_cnt;         // [ntiles] events per tile -> exclusive offsets
-  long long* seg_tail;     // [ntiles] max ts after the tile's last event (or tile max)
-  int32_t* seg_has;        // [ntiles] tile has an event
-  long long* m_carry;      // [ntiles] max ts since the last event before the tile
-  uint32_t* evbits;        // [n/32+1] event bitmap
-  int64_t* ev_pos;         // [ev_cap]
-  int64_t* ev_t;
-  int64_t* ev_v;
-  long long* ev_m;         // max ts strictly between the previous event and this one (JMIN if none)
-  int64_t ev_cap;
-  XBCtl* ctl;
-  int64_t* ep_pos;         // [ep_cap] epoch entries: event position, tail after it
-  int32_t* ep_tail;
-  int64_t ep_cap;
-  int32_t vt;
-  int32_t cfg_nctx_host;   // session windows (host copy, decides which passes run)
-  int64_t* sufmin;         // [sc] suffix minimum of tStart over [i, tail) (unsorted slice lists only)
-  long long* tmin;         // [ntiles] tile min (sessions: the quiet-tile test of xb_classify_kernel)
-  int32_t* tjump;          // [ntiles] (sessions) some item after the tile's first exceeds the tile's running max
-                           // by more than the smallest gap: only then can a tuple other than the first open a session
-};
 
 namespace xb {
 using namespace x;
@@ -402,14 +367,15 @@ __global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
   const int64_t base = (int64_t)blockIdx.x * XB_TILE;
   __shared__ long long wmn[4];
   int64_t m = JMIN, mn = JMAX;
+  // unconditional loads (indices past the batch clamp to its last tuple, which lies in this tile when any index
+  // does, so the extrema are unchanged): all XB_ITEMS loads are in flight before the first use
+  int64_t v[XB_ITEMS];
+#pragma unroll
+  for (int r = 0; r < XB_ITEMS; r++) v[r] = __builtin_nontemporal_load(a.ts + min(base + r * XB_THREADS + threadIdx.x, a.n - 1));
 #pragma unroll
   for (int r = 0; r < XB_ITEMS; r++) {
-    const int64_t i = base + r * XB_THREADS + threadIdx.x;
-    if (i < a.n) {
-      const int64_t t = a.ts[i];
-      m = max(m, t);
-      mn = min(mn, t);
-    }
+    m = max(m, v[r]);
+    mn = min(mn, v[r]);
   }
   m = wmax(m);
   if (a.cfg_nctx_host > 0) mn = wmin(mn);
@@ -430,23 +396,41 @@ __global__ __launch_bounds__(XB_THREADS) void xb_tilemax_kernel(XBArgs a) {
   }
 }
 
-// Single-workgroup exclusive scans over the per-tile values (16 consecutive tiles per thread and round, so a
-// 2^26-tuple batch takes one round): V is a pair (h, t) combined by op(prev, cur); identity id.
+// Single-workgroup exclusive scans over the per-tile values: V is a pair (h, t) combined by op(prev, cur); identity
+// id.  Rounds of 8192 values: coalesced loads into LDS, 8 consecutive values per thread scanned in registers, the
+// results back through LDS and stored coalesced (strided per-thread global accesses left each wave instruction
+// touching 64 cache lines).
 struct SPair {
   int64_t h, t;
 };
+constexpr int SCAN_IT = 8;
+constexpr int SCAN_CH = 1024 * SCAN_IT;
 template <class Op>
 __device__ __forceinline__ SPair wg_scan16(int64_t n, SPair id, SPair carry, Op op, SPair (*ld)(const XBArgs&, int64_t, int),
                                            void (*st)(const XBArgs&, int64_t, int, SPair), const XBArgs& a, int row) {
   __shared__ long long wh[16], wt[16];
+  __shared__ long long st_t[SCAN_CH];
+  __shared__ int st_h[SCAN_CH];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int64_t c0 = 0; c0 < n; c0 += 1024 * 16) {
-    const int64_t b = c0 + (int64_t)tid * 16;
-    SPair loc[16];
+  if (n <= 0) return carry;
+  for (int64_t c0 = 0; c0 < n; c0 += SCAN_CH) {
+    {
+      SPair v[SCAN_IT];
+#pragma unroll
+      for (int j = 0; j < SCAN_IT; j++) v[j] = ld(a, min(c0 + j * 1024 + tid, n - 1), row);
+#pragma unroll
+      for (int j = 0; j < SCAN_IT; j++) {
+        const bool in = c0 + j * 1024 + tid < n;
+        st_t[j * 1024 + tid] = in ? v[j].t : id.t;
+        st_h[j * 1024 + tid] = (int)(in ? v[j].h : id.h);
+      }
+    }
+    __syncthreads();
+    SPair loc[SCAN_IT];
     SPair acc = id;
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const SPair v = b + j < n ? ld(a, b + j, row) : id;
+    for (int j = 0; j < SCAN_IT; j++) {
+      const SPair v{(int64_t)st_h[tid * SCAN_IT + j], (int64_t)st_t[tid * SCAN_IT + j]};
       loc[j] = acc;
       acc = op(acc, v);
     }
@@ -471,10 +455,19 @@ __device__ __forceinline__ SPair wg_scan16(int64_t n, SPair id, SPair carry, Op 
     if (lane == 0) ex = id;
     const SPair pre = op(before, ex);
 #pragma unroll
-    for (int j = 0; j < 16; j++)
-      if (b + j < n) st(a, b + j, row, op(pre, loc[j]));
+    for (int j = 0; j < SCAN_IT; j++) {
+      const SPair r = op(pre, loc[j]);
+      st_t[tid * SCAN_IT + j] = r.t;
+      st_h[tid * SCAN_IT + j] = (int)r.h;
+    }
     SPair tot = carry;
     for (int w = 0; w < 16; w++) tot = op(tot, SPair{wh[w], wt[w]});
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SCAN_IT; j++) {
+      const int64_t k = c0 + j * 1024 + tid;
+      if (k < n) st(a, k, row, SPair{(int64_t)st_h[j * 1024 + tid], (int64_t)st_t[j * 1024 + tid]});
+    }
     __syncthreads();
     carry = tot;
   }
@@ -625,6 +618,7 @@ __device__ __forceinline__ bool ooo_inside(const XBArgs& a, const XBH& h, int k,
   const XCfg* c = a.cfg;
   const int64_t* nss = a.ns_start + (int64_t)k * a.ns_cap;
   const int64_t* nsp = a.ns_pb + (int64_t)k * a.ns_cap;
+  m = min(m, a.ns_cap);  // an overflowing round is retried (XBCtl.retry); never read past the buffer
   if (m > 0 && t >= nss[0]) {
     int64_t lo = 0, hi = m;  // last idx < m with nss[idx] <= t
     while (hi - lo > 1) {
@@ -938,12 +932,31 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
   if (ctl.done || o.s.err) {
     return;
   }
+  long long* dbg = a.dbg;
+  int nd = 0;
+  auto stamp = [&]() {
+    if (dbg && nd < 255) {
+      const long long c = (long long)__builtin_amdgcn_s_memtime();
+      if (lane == 0) dbg[1 + nd] = c;
+      nd++;
+    }
+  };
+  stamp();
+  {  // buffers sized from the previous rounds: an overflow changes nothing and is retried by the host
+    bool over = ctl.ev_total + 4 > a.ev_cap;
+    for (int k = 0; k < cfg->n_ctx; k++) over |= a.ns_tot[k] > a.ns_cap;
+    if (over) {
+      if (lane == 0) a.ctl->retry = 1;
+      return;
+    }
+  }
   // segment start: compaction is only safe here (slice indices are stable within a segment)
   if (o.s.tail + 64 > cfg->sc && o.s.head > 0) {
     o.move_range(0, o.s.head, o.s.tail - o.s.head);
     o.s.tail -= o.s.head;
     o.s.head = 0;
   }
+  stamp();
   int64_t ep = 0;
   if (lane == 0) {
     a.ep_pos[0] = ctl.seg_start - 1;
@@ -953,8 +966,21 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
   int64_t e = ctl.ev_next;
   bool first = true;
   ctl.stopped = 0;
+  // the compacted events are fetched 64 at a time, one per lane, and broadcast: no load round trip per event
+  int64_t fb = JMIN;  // first event held in the lanes
+  int64_t f_pos = 0, f_t = 0, f_v = 0, f_m = 0;
   for (; e < ctl.ev_total; e++) {
-    const int64_t pos = a.ev_pos[e], t = a.ev_t[e], vb = a.ev_v[e], m = a.ev_m[e];
+    if (fb == JMIN || e >= fb + 64) {
+      fb = e;
+      const int64_t k = min(e + lane, ctl.ev_total - 1);
+      f_pos = a.ev_pos[k];
+      f_t = a.ev_t[k];
+      f_v = a.ev_v[k];
+      f_m = a.ev_m[k];
+    }
+    const int src = (int)(e - fb);
+    const int64_t pos = (int64_t)__shfl((long long)f_pos, src), t = (int64_t)__shfl((long long)f_t, src);
+    const int64_t vb = (int64_t)__shfl((long long)f_v, src), m = (int64_t)__shfl((long long)f_m, src);
     reconstruct(o, cfg, m);
     o.s.currentCount = jadd(a.snap->c0, pos);
     // an out-of-order event of an operator with sessions may split / shift / merge older slices: the simple
@@ -970,8 +996,11 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
     }
     first = false;
     o.exc = 0;
+    stamp();
     o.determine_slices(t);
+    stamp();
     if (!o.exc) o.manager_process(t, vb);
+    stamp();
     if (xerr_tuple_failed(o.exc)) {
       o.s.dropped++;
       o.exc = 0;
@@ -1001,9 +1030,11 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
   ctl.ep_count = ep;
   ctl.resume = 0;
   __threadfence_block();
+  stamp();
   if (lane == 0) {
     *a.st = o.s;
     *a.ctl = ctl;
+    if (dbg) dbg[0] = nd;
   }
 }
 
@@ -1028,6 +1059,7 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
   __shared__ long long w_tl[XW], w_tf[XW], w_p1[XW], w_p2[XW];
   __shared__ unsigned long long w_p0[XW];
   const XBCtl& ctl = *a.ctl;
+  if (ctl.retry) return;
   const int64_t s0 = ctl.seg_start;
   const int64_t s1 = ctl.seg_end < 0 ? a.n : ctl.seg_end;
   const XCfg* cfg = a.cfg;
@@ -1304,6 +1336,7 @@ __global__ __launch_bounds__(1024) void xb_sufmin_kernel(XBArgs a) {
 __global__ void xb_next_segment_kernel(XBArgs a) {
   if (threadIdx.x != 0) return;
   XBCtl c = *a.ctl;
+  if (c.retry) return;
   if (c.stopped) {
     c.seg_start = c.seg_end;
     c.resume = 1;

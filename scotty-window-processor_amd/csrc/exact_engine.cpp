@@ -2,10 +2,12 @@
 // result assembly.  Per-tuple work runs only in gfx950 kernels (exact_kernels.hip, keyed_kernels.hip);
 // the host sequences launches on the op's stream and owns the window/function configuration, like the
 // reference's WindowManager registration (S/WindowManager.java:121-151).
+#include "exact_batch.h"
 #include "exact_engine.h"
 #include "keyed_grid.h"
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstddef>
 #include <cstring>
@@ -51,55 +53,6 @@ hipError_t launch_kg_dgather(const uint32_t* key, const int64_t* ts, const void*
                              hipStream_t st);
 }  // namespace scotty
 
-// batch-parallel path (exact_batch.hip): the argument block mirrors XBArgs there
-namespace scotty {
-struct XSnap;
-struct XBCtl;
-struct XBArgs {
-  const int64_t* ts;
-  const void* val;
-  int64_t n;
-  int64_t ntiles;
-  const XCfg* cfg;
-  XState* st;
-  XSlices sl;
-  XSess ss;
-  XSnap* snap;
-  int64_t* reach;
-  long long* tmax;
-  long long* pcarry;
-  int64_t* ns_cnt;
-  int64_t* ns_tot;
-  int64_t* ns_start;
-  int64_t* ns_pb;
-  int64_t ns_cap;
-  int64_t* ev_cnt;
-  long long* seg_tail;
-  int32_t* seg_has;
-  long long* m_carry;
-  uint32_t* evbits;
-  int64_t* ev_pos;
-  int64_t* ev_t;
-  int64_t* ev_v;
-  long long* ev_m;
-  int64_t ev_cap;
-  XBCtl* ctl;
-  int64_t* ep_pos;
-  int32_t* ep_tail;
-  int64_t ep_cap;
-  int32_t vt;
-  int32_t cfg_nctx_host;
-  int64_t* sufmin;
-  long long* tmin;
-  int32_t* tjump;
-};
-hipError_t xb_classify_phase(XBArgs& a, int phase, hipStream_t st);
-hipError_t xb_events(XBArgs& a, hipStream_t st);
-hipError_t xb_apply(XBArgs& a, hipStream_t st);
-int64_t xb_tile();
-size_t xb_snap_bytes();
-size_t xb_ctl_bytes();
-}  // namespace scotty
 
 namespace scotty {
 
@@ -176,7 +129,7 @@ int XEngine::init(int dev, hipStream_t st, int value_type, bool is_keyed, std::s
   (void)e_out;
   XCHK(dalloc(&d_cfg, 1));
   XCHK(dalloc(&d_misc, 8));
-  XCHK(hipHostMalloc((void**)&h_misc, 8 * sizeof(int64_t), hipHostMallocDefault));
+  XCHK(hipHostMalloc((void**)&h_misc, 16 * sizeof(int64_t), hipHostMallocDefault));
   XCHK(dalloc(&d_newcnt, 1));
   XCHK(dalloc(&d_full, 1));
   XCHK(dalloc(&d_need, 4));
@@ -629,58 +582,79 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
   a.sufmin = xb_sufmin;
   a.tjump = xb_tjump;
   a.tmin = xb_tmin;
-  XCHK(hipMemsetAsync(xb_ctl, 0, xb_ctl_bytes(), stream));
-  if (resume) {
-    const int32_t one = 1;
-    XCHK(hipMemcpyAsync((unsigned char*)xb_ctl + 48, &one, 4, hipMemcpyHostToDevice, stream));  // XBCtl.resume
-  }
-  XCHK(xb_classify_phase(a, 0, stream));
-  if (cfg.n_ctx > 0) {
-    XCHK(hipMemcpyAsync(h_misc, xb_nstot, 8 * cfg.n_ctx, hipMemcpyDeviceToHost, stream));
+  // One host synchronisation per round: the event and new-session buffers keep their size from earlier rounds; a
+  // round that outgrows them applies nothing (XBCtl.retry) and runs again with grown buffers.
+  for (int attempt = 0;; attempt++) {
+    a.ns_start = xb_nsstart;
+    a.ns_pb = xb_nspb;
+    a.ns_cap = xb_nscap;
+    a.ev_pos = xb_evpos;
+    a.ev_t = xb_evt;
+    a.ev_v = xb_evv;
+    a.ev_m = xb_evm;
+    a.ev_cap = xb_evcap;
+    a.ep_pos = xb_eppos;
+    a.ep_tail = xb_eptail;
+    a.ep_cap = xb_evcap + 4;
+    XCHK(hipMemsetAsync(xb_ctl, 0, xb_ctl_bytes(), stream));
+    if (resume) {
+      const int32_t one = 1;
+      XCHK(hipMemcpyAsync((unsigned char*)xb_ctl + 48, &one, 4, hipMemcpyHostToDevice, stream));  // XBCtl.resume
+    }
+    XCHK(xb_classify_phase(a, 0, stream));
+    XCHK(xb_classify_phase(a, 1, stream));
+    XCHK(xb_classify_phase(a, 2, stream));
+    static long long* d_dbg = nullptr;
+    const bool prof = getenv("SCOTTY_XB_PROF") != nullptr;
+    if (prof && !d_dbg) XCHK(hipMalloc(&d_dbg, 256 * 8));
+    a.dbg = prof ? d_dbg : nullptr;
+    XCHK(xb_events(a, stream));
+    if (prof) {  // debugging aid: clock stamps of the event pass (100 MHz-ish s_memtime ticks, see MI355X guide)
+      long long h[256];
+      XCHK(hipMemcpyAsync(h, d_dbg, sizeof(h), hipMemcpyDeviceToHost, stream));
+      XCHK(hipStreamSynchronize(stream));
+      fprintf(stderr, "xb events pass stamps (%lld):", h[0]);
+      for (int i = 2; i <= h[0] && i < 256; i++) fprintf(stderr, " %lld", h[i] - h[i - 1]);
+      fprintf(stderr, "\n");
+    }
+    XCHK(xb_apply(a, stream));
+    static_assert(sizeof(int64_t) * 9 >= 68, "XBCtl layout");
+    XCHK(hipMemcpyAsync(h_misc, xb_ctl, 72, hipMemcpyDeviceToHost, stream));
+    if (cfg.n_ctx > 0) XCHK(hipMemcpyAsync(h_misc + 9, xb_nstot, 8 * cfg.n_ctx, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
+    const int64_t nev = h_misc[0];
+    const int32_t retry = ((const int32_t*)(h_misc + 8))[0];
+    if (!retry) {
+      last_events += nev;
+      const int32_t stopped = ((const int32_t*)(h_misc + 5))[0];
+      if (stopped) *stop_at = h_misc[3];  // XBCtl.seg_end
+      const int32_t lost = ((const int32_t*)(h_misc + 6))[1];  // XBCtl.pad: simple tuples without a slice
+      if (lost) {
+        err = "internal: simple tuple without a slice (" + std::to_string(lost) + ")";
+        failed = true;
+        return SCOTTY_ERR_STATE;
+      }
+      return SCOTTY_OK;
+    }
+    if (attempt >= 2) {
+      err = "internal: exact batch buffers did not converge";
+      failed = true;
+      return SCOTTY_ERR_STATE;
+    }
     int64_t mx = 1;
-    for (int k = 0; k < cfg.n_ctx; k++) mx = std::max<int64_t>(mx, h_misc[k]);
+    for (int k = 0; k < cfg.n_ctx; k++) mx = std::max<int64_t>(mx, h_misc[9 + k]);
     if (mx > xb_nscap) {
       dfree(xb_nsstart); dfree(xb_nspb);
-      xb_nscap = std::max<int64_t>(mx, 1024);
+      xb_nscap = std::max<int64_t>({mx, 2 * xb_nscap, (int64_t)1024});
       XCHK(dalloc(&xb_nsstart, (size_t)xb_nscap * XMAXCTX));
       XCHK(dalloc(&xb_nspb, (size_t)xb_nscap * XMAXCTX));
     }
-  }
-  a.ns_start = xb_nsstart;
-  a.ns_pb = xb_nspb;
-  a.ns_cap = xb_nscap;
-  XCHK(xb_classify_phase(a, 1, stream));
-  XCHK(hipMemcpyAsync(h_misc, xb_ctl, 8, hipMemcpyDeviceToHost, stream));  // XBCtl.ev_total
-  XCHK(hipStreamSynchronize(stream));
-  const int64_t nev = h_misc[0];
-  if (nev + 4 > xb_evcap) {
-    dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_evm); dfree(xb_eppos); dfree(xb_eptail);
-    xb_evcap = std::max<int64_t>(nev + 4, 4096);
-    XCHK(dalloc(&xb_evpos, xb_evcap)); XCHK(dalloc(&xb_evt, xb_evcap)); XCHK(dalloc(&xb_evv, xb_evcap));
-    XCHK(dalloc(&xb_evm, xb_evcap)); XCHK(dalloc(&xb_eppos, xb_evcap + 4)); XCHK(dalloc(&xb_eptail, xb_evcap + 4));
-  }
-  a.ev_pos = xb_evpos;
-  a.ev_t = xb_evt;
-  a.ev_v = xb_evv;
-  a.ev_m = xb_evm;
-  a.ev_cap = xb_evcap;
-  a.ep_pos = xb_eppos;
-  a.ep_tail = xb_eptail;
-  a.ep_cap = xb_evcap + 4;
-  XCHK(xb_classify_phase(a, 2, stream));
-  last_events += nev;
-  XCHK(xb_events(a, stream));
-  XCHK(xb_apply(a, stream));
-  XCHK(hipMemcpyAsync(h_misc, xb_ctl, 48, hipMemcpyDeviceToHost, stream));
-  XCHK(hipStreamSynchronize(stream));
-  const int32_t stopped = ((const int32_t*)(h_misc + 5))[0];
-  if (stopped) *stop_at = h_misc[3];  // XBCtl.seg_end
-  XCHK(hipMemcpy(h_misc, (unsigned char*)xb_ctl + 52, 4, hipMemcpyDeviceToHost));
-  if (*(int32_t*)h_misc) {
-    err = "internal: simple tuple without a slice (" + std::to_string(*(int32_t*)h_misc) + ")";
-    failed = true;
-    return SCOTTY_ERR_STATE;
+    if (nev + 4 > xb_evcap) {
+      dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_evm); dfree(xb_eppos); dfree(xb_eptail);
+      xb_evcap = std::max<int64_t>({nev + 4, 2 * xb_evcap, (int64_t)4096});
+      XCHK(dalloc(&xb_evpos, xb_evcap)); XCHK(dalloc(&xb_evt, xb_evcap)); XCHK(dalloc(&xb_evv, xb_evcap));
+      XCHK(dalloc(&xb_evm, xb_evcap)); XCHK(dalloc(&xb_eppos, xb_evcap + 4)); XCHK(dalloc(&xb_eptail, xb_evcap + 4));
+    }
   }
   return SCOTTY_OK;
 }

@@ -265,3 +265,52 @@ def test_device_timing_classes(pkg):
     assert t["ingest"][1] == 4 and t["watermark"][1] == 4 and t["result_copy"][1] == 4
     assert t["push_other"][1] == 8
     assert all(v[0] > 0 for v in t.values()), t
+
+
+def test_f64_sum_at_bench_scale(pkg):
+    """SUM_F64 at the bench's batch size (2 micro-batches of 2^26 tuples, 1000 tumbling windows of 50-1000 ms): the
+    grid path's partials reassociate the reference's arrival-order fold (atomicAdd(double) per cell, then slices, then
+    windows), so every window is checked against its exactly rounded sum (long double prefix sums on the host) within
+    the north_star's 1e-6 relative, and COUNT bit-exactly.  Positive values: no cancellation, so the relative bound
+    measures the kernel's rounding alone."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rate = (1 << 26) // 1000
+    sizes = [50 + (x % 951) for x in pkg.workloads.random_tumbling_sizes()]
+    op = pkg.SlicingWindowOperator(device=0, value_type=pkg.VALUE_F64)
+    op.addWindowFunction(pkg.AGG_SUM_F64)
+    op.addWindowFunction(pkg.AGG_COUNT)
+    op.setMaxLateness(1)
+    for s in sizes:
+        op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Time, s))
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    n = 1 << 26
+    host_v = []
+    rows = []
+    for step in range(2):
+        ts = torch.arange(n, device=dev, dtype=torch.int64) // rate + step * 1000
+        v = torch.rand(n, device=dev, dtype=torch.float64, generator=g) * 1000.0
+        torch.cuda.synchronize(dev)
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), n)
+        rows += op.processWatermark(step * 1000 + 999)
+        host_v.append(v.cpu().numpy())
+        del ts, v
+    vals = np.concatenate(host_v).astype(np.longdouble)
+    pre = np.concatenate([[np.longdouble(0)], np.cumsum(vals)])
+    checked = 0
+    worst = 0.0
+    for w in rows:
+        lo, hi = max(0, w.getStart()) * rate, min(2000, w.getEnd()) * rate
+        lo, hi = min(lo, 2 * n), min(hi, 2 * n)
+        if hi <= lo:
+            assert not w.hasValue()
+            continue
+        exp_sum, exp_cnt = pre[hi] - pre[lo], hi - lo
+        s, c = w.getAggValues()
+        assert c == exp_cnt
+        rel = abs(float((np.longdouble(s) - exp_sum) / exp_sum))
+        worst = max(worst, rel)
+        assert rel <= 1e-6, (w.getStart(), w.getEnd(), s, float(exp_sum))
+        checked += 1
+    assert checked > 1000 and worst < 1e-6
