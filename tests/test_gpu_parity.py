@@ -276,7 +276,7 @@ def test_f64_sum_at_bench_scale(pkg):
     import torch
     dev = torch.device("cuda", 0)
     rate = (1 << 26) // 1000
-    sizes = [50 + (x % 951) for x in pkg.workloads.random_tumbling_sizes()]
+    sizes = [_not_pow2(50 + (x % 951)) for x in pkg.workloads.random_tumbling_sizes()]
     op = pkg.SlicingWindowOperator(device=0, value_type=pkg.VALUE_F64)
     op.addWindowFunction(pkg.AGG_SUM_F64)
     op.addWindowFunction(pkg.AGG_COUNT)
@@ -298,11 +298,11 @@ def test_f64_sum_at_bench_scale(pkg):
         del ts, v
     vals = np.concatenate(host_v).astype(np.longdouble)
     pre = np.concatenate([[np.longdouble(0)], np.cumsum(vals)])
+    ts_all = np.concatenate([np.arange(n, dtype=np.int64) // rate + k * 1000 for k in range(2)])  # non-decreasing
     checked = 0
     worst = 0.0
     for w in rows:
-        lo, hi = max(0, w.getStart()) * rate, min(2000, w.getEnd()) * rate
-        lo, hi = min(lo, 2 * n), min(hi, 2 * n)
+        lo, hi = np.searchsorted(ts_all, [w.getStart(), w.getEnd()], side="left")
         if hi <= lo:
             assert not w.hasValue()
             continue
