@@ -11,6 +11,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--first", required=True)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--median", action="store_true", help="average the --steps steps around the median instead")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "at::native" not in r["Kernel_Name"]]
@@ -24,13 +25,17 @@ def main():
         span = (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
         steps.append((per, span))
     steps.sort(key=lambda p: -sum(p[0].values()))
-    sel = steps[:args.steps]
+    if args.median:
+        m = len(steps) // 2
+        sel = steps[max(0, m - args.steps // 2):max(0, m - args.steps // 2) + args.steps]
+    else:
+        sel = steps[:args.steps]
     tot = collections.defaultdict(float)
     for p, _ in sel:
         for k, v in p.items():
             tot[k] += v
     k = len(sel)
-    print("%d largest steps: device %.1f us/step, span %.1f us/step" % (k, sum(tot.values()) / k,
+    print(("%d " + ("median" if args.median else "largest") + " steps: device %.1f us/step, span %.1f us/step") % (k, sum(tot.values()) / k,
                                                                        sum(s for _, s in sel) / k))
     for name in sorted(tot, key=lambda x: -tot[x]):
         print("  %-60s %8.1f us/step" % (name, tot[name] / k))
