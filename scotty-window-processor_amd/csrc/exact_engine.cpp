@@ -682,7 +682,7 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
     kg_built = n_ops;
   }
   const int vb = vt == VT_I32 ? 4 : 8;
-  const int rec = vt == VT_I32 ? 16 : 24;
+  const int rec = vt == VT_I32 ? 12 : 16;  // KRec<4> / KRec<8> (keyed_grid.hip)
   const int64_t nbk = (int64_t)(kgcap >> KG_RB);
   const int tile = kg_tile(vt, nbk, kg_variant);
   const int64_t ntiles = (n + tile - 1) / tile;
@@ -750,9 +750,9 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
   if (hc->flag) return SCOTTY_OK;
   *deferred = (int64_t)hc->deferred;
   for (int i = 0; i < KG_SHARDS; i++) last_kg_keys += (int64_t)hc->keys_shard[i];
-  if (hc->defer_keys > 0) {  // known keys the commit deferred: mark their tuples, clear the flags
+  if (hc->deferred > 0) {  // tuples of keys the bucket kernel missed or the commit deferred: mark, clear the flags
     XCHK(launch_kg_mark_deferred(a, stream));
-    XCHK(hipMemsetAsync(d_kgdflag, 0, n_ops, stream));
+    if (hc->defer_keys > 0) XCHK(hipMemsetAsync(d_kgdflag, 0, n_ops, stream));
   }
   return SCOTTY_OK;
 }

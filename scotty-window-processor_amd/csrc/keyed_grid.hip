@@ -158,54 +158,50 @@ __global__ __launch_bounds__(PT) void kg_hist_kernel(KgArgs a) {
   }
 }
 
-// records: 4-byte values {key, ts - ts_first, value, index}; 8-byte values {key, ts - ts_first, index, 0, value}
+// records: 4-byte values {key, ts - ts_first, value} (12 B); 8-byte values {key, ts - ts_first, value} (16 B).  A
+// record carries no tuple index: a tuple the bucket kernel cannot fold (its key is not in the bucket's LDS table
+// slice) is found again by kg_mark_deferred_kernel with the same probe rule.
 template <int VB>
 struct KRec;
 template <>
 struct KRec<4> {
+  uint32_t x, y, z;
+  __device__ uint32_t key() const { return x; }
+  __device__ uint32_t toff() const { return y; }
+  __device__ int64_t vbits() const { return (int64_t)(int32_t)z; }
+  __device__ static KRec load(const void* p, int64_t i) {
+    const uint32_t* q = (const uint32_t*)p + 3 * i;
+    return KRec{q[0], q[1], q[2]};
+  }
+  __device__ void store(void* p, int64_t i) const {
+    uint32_t* q = (uint32_t*)p + 3 * i;
+    q[0] = x;
+    q[1] = y;
+    q[2] = z;
+  }
+  __device__ void store_lds(uint32_t* s, int i) const {
+    s[3 * i] = x;
+    s[3 * i + 1] = y;
+    s[3 * i + 2] = z;
+  }
+  __device__ static KRec load_lds(const uint32_t* s, int i) { return KRec{s[3 * i], s[3 * i + 1], s[3 * i + 2]}; }
+  __device__ static KRec make(uint32_t k, uint32_t toff, const void* val, int64_t i) {
+    return KRec{k, toff, (uint32_t)((const int32_t*)val)[i]};
+  }
+};
+template <>
+struct KRec<8> {
   uint4 w;
   __device__ uint32_t key() const { return w.x; }
   __device__ uint32_t toff() const { return w.y; }
-  __device__ uint32_t idx() const { return w.w; }
-  __device__ int64_t vbits() const { return (int64_t)(int32_t)w.z; }
+  __device__ int64_t vbits() const { return (int64_t)(((uint64_t)w.w << 32) | w.z); }
   __device__ static KRec load(const void* p, int64_t i) { return KRec{((const uint4*)p)[i]}; }
   __device__ void store(void* p, int64_t i) const { ((uint4*)p)[i] = w; }
   __device__ void store_lds(uint32_t* s, int i) const { ((uint4*)s)[i] = w; }
   __device__ static KRec load_lds(const uint32_t* s, int i) { return KRec{((const uint4*)s)[i]}; }
   __device__ static KRec make(uint32_t k, uint32_t toff, const void* val, int64_t i) {
-    return KRec{make_uint4(k, toff, (uint32_t)((const int32_t*)val)[i], (uint32_t)i)};
-  }
-};
-template <>
-struct KRec<8> {
-  uint2 a, b, c;
-  __device__ uint32_t key() const { return a.x; }
-  __device__ uint32_t toff() const { return a.y; }
-  __device__ uint32_t idx() const { return b.x; }
-  __device__ int64_t vbits() const { return (int64_t)(((uint64_t)c.y << 32) | c.x); }
-  __device__ static KRec load(const void* p, int64_t i) {
-    const uint2* q = (const uint2*)p + 3 * i;
-    return KRec{q[0], q[1], q[2]};
-  }
-  __device__ void store(void* p, int64_t i) const {
-    uint2* q = (uint2*)p + 3 * i;
-    q[0] = a;
-    q[1] = b;
-    q[2] = c;
-  }
-  __device__ void store_lds(uint32_t* s, int i) const {
-    uint2* q = (uint2*)s + 3 * i;
-    q[0] = a;
-    q[1] = b;
-    q[2] = c;
-  }
-  __device__ static KRec load_lds(const uint32_t* s, int i) {
-    const uint2* q = (const uint2*)s + 3 * i;
-    return KRec{q[0], q[1], q[2]};
-  }
-  __device__ static KRec make(uint32_t k, uint32_t toff, const void* val, int64_t i) {
     const uint64_t v = (uint64_t)((const int64_t*)val)[i];
-    return KRec{make_uint2(k, toff), make_uint2((uint32_t)i, 0u), make_uint2((uint32_t)v, (uint32_t)(v >> 32))};
+    return KRec{make_uint4(k, toff, (uint32_t)v, (uint32_t)(v >> 32))};
   }
 };
 
@@ -217,7 +213,7 @@ template <int VB, int T, int NBS, int ST>
 __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   constexpr int IT = T / ST;
   constexpr int PER = NBS / ST;
-  __shared__ __attribute__((aligned(16))) uint32_t stage[T * (VB == 4 ? 4 : 6)];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[T * (VB == 4 ? 3 : 4)];
   __shared__ int32_t cnt[NBS], tst[NBS], base[NBS];
   __shared__ int32_t wsum[ST / 64];
   if (a.ctl->flag) return;
@@ -291,7 +287,7 @@ template <int T, int NBS, int ST>
 __global__ __launch_bounds__(ST) void kg_scatter2_kernel(KgArgs a) {
   constexpr int IT = T / ST;
   constexpr int PER = NBS / ST;
-  __shared__ __attribute__((aligned(16))) uint32_t stage[T * 4];
+  __shared__ __attribute__((aligned(16))) uint32_t stage[T * 3];
   __shared__ int32_t cnt[NBS];
   __shared__ int32_t wsum[ST / 64];
   if (a.ctl->flag) return;
@@ -443,8 +439,7 @@ __device__ __forceinline__ void kg_bucket_body(const KgArgs& a) {
   uint32_t miss = 0;
   auto fold = [&](const KRec<VB>& rec) {
     const int p = lds_probe(L.tab, rec.key(), a.kmask, region);
-    if (p < 0) {
-      a.mark[rec.idx()] = 1;
+    if (p < 0) {  // found again and marked by kg_mark_deferred_kernel
       miss++;
       return;
     }
@@ -692,21 +687,25 @@ __global__ __launch_bounds__(256) void kg_commit_kernel(KgArgs a, int64_t n_ops)
   }
 }
 
-// Tuples of known keys deferred by the commit (rare: capacity, long edge walks, state the rule does not cover)
+// Tuples left to the replay path: keys the bucket kernel could not fold (not in the bucket's LDS slice of the key
+// table -- new keys, or probed past the spill: the same rule as lds_probe) and known keys the commit deferred (rare:
+// capacity, long edge walks, state the rule does not cover)
 __global__ void kg_mark_deferred_kernel(KgArgs a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t key = a.key[i];
     const unsigned long long tag = ((unsigned long long)key + 1) << 32;
-    uint64_t h = (uint64_t)khash(key) & a.kmask;
-    for (uint64_t probe = 0; probe <= a.kmask; probe++) {
-      const unsigned long long e = a.ktab[h];
+    const uint64_t h = (uint64_t)khash(key) & a.kmask;
+    const uint64_t region = (h >> KG_RB) << KG_RB;
+    bool m = true;
+    for (int p = (int)(h - region); p < KG_RP; p++) {
+      const unsigned long long e = a.ktab[(region + p) & a.kmask];
       if ((e & 0xFFFFFFFF00000000ull) == tag) {
-        if (a.dflag[(uint32_t)e]) a.mark[i] = 1;
+        m = a.dflag[(uint32_t)e] != 0;
         break;
       }
       if (e == 0) break;
-      h = (h + 1) & a.kmask;
     }
+    if (m) a.mark[i] = 1;
   }
 }
 
