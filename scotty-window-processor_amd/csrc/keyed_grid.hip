@@ -796,12 +796,19 @@ hipError_t launch_kg_partition(const KgArgs& a, int vt, hipStream_t st) {
 
 // tuples per partition tile: the LDS stage holds one tile (16-byte records: 8192 when the bucket counters fit
 // 2048 entries, else 4096; 24-byte records: 4096; variant 2: 4096)
-int kg_tile(int vt, int64_t nbk, int variant) { return vt == VT_I32 && nbk <= 2048 && variant != 2 ? 8192 : 4096; }
+int kg_tile(int vt, int64_t nbk, int variant) {
+  if (vt == VT_I32 && nbk <= 2048 && variant == 3) return 5632;
+  return vt == VT_I32 && nbk <= 2048 && variant != 2 ? 8192 : 4096;
+}
 
 hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st) {
   const unsigned grid = (unsigned)(((a.ntiles + 7) / 8) * 8);
   if (vt == VT_I32 && a.tile == 4096 && a.variant == 2) {
     hipLaunchKernelGGL((kg::kg_scatter2_kernel<4096, 2048, 1024>), dim3(grid), dim3(1024), 0, st, a);
+    return hipGetLastError();
+  }
+  if (vt == VT_I32 && a.tile == 5632 && a.variant == 3) {  // 74 KB of LDS: two workgroups per CU
+    hipLaunchKernelGGL((kg::kg_scatter2_kernel<5632, 2048, 512>), dim3(grid), dim3(512), 0, st, a);
     return hipGetLastError();
   }
   if (vt == VT_I32) {
