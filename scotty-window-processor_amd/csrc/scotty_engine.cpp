@@ -1407,7 +1407,7 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only)
-    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;
+    if (op->mode != 0 || value < 0 || value > 3) return SCOTTY_ERR_ARG;
     op->x_kg_variant = (int32_t)value;
     if (op->x) op->x->kg_variant = op->x_kg_variant;
     return SCOTTY_OK;
