@@ -176,6 +176,13 @@ int scotty_route_keyed(const uint32_t* key, const int64_t* ts, const void* val, 
                        int world, int max_parallelism, int threads, uint32_t* out_key, int64_t* out_ts, void* out_val,
                        uint64_t* offsets);
 
+/* Stream ordering for callers that run the exchange on their own stream (e.g. RCCL through torch.distributed):
+ * op_waits == 0: `stream` waits for the work queued on the op's stream so far (the exchange record of a shard push
+ * is complete before the all-gather reads it); op_waits != 0: the op's stream waits for the work queued on `stream`
+ * (the gathered records have landed before scotty_shard_commit reads them).  With scotty_tune("shard_async", 1) the
+ * shard pushes then return without a host synchronisation.  `stream` is a hipStream_t (NULL: the default stream). */
+int scotty_stream_order(scotty_op* op, void* stream, int op_waits);
+
 /* Number of keys (operators) of a keyed op. */
 int64_t scotty_key_count(scotty_op* op);
 
@@ -209,7 +216,8 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
  * segmented-reduction count path; an out-of-order tuple that would move records then fails loudly -- without the
  * promise they run on the exact engine, which keeps the record sets), "ingest_blocks", "shard_cells" / "shard_cands" (cells /
  * edge candidates per rank record of the time-window exchange), "shard_count_cells" (count cells per rank record
- * of the count-window exchange). */
+ * of the count-window exchange), "shard_async" 1 (shard pushes return without a host synchronisation: the caller
+ * orders its collective's stream with scotty_stream_order). */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */

@@ -162,6 +162,7 @@ def lib():
                                                     ctypes.POINTER(u64)]),
             "scotty_sync": (ctypes.c_int, [P]),
             "scotty_key_shard": (ctypes.c_int32, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
+            "scotty_stream_order": (ctypes.c_int, [P, P, ctypes.c_int]),
             "scotty_route_keyed": (ctypes.c_int, [P, P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                                   ctypes.c_int, ctypes.c_int, P, P, P, P]),
         }
@@ -367,6 +368,11 @@ class SlicingWindowOperator:
         self._check(self._l.scotty_shard_bounds(self._h, ts_ptr, n, ctypes.addressof(out)))
         return int(out[0]), int(out[1])
 
+    def streamOrder(self, stream, op_waits):
+        """scotty_stream_order: op_waits=False: `stream` (a hipStream_t handle) waits for the op's queued work;
+        True: the op's stream waits for the work queued on `stream`."""
+        self._check(self._l.scotty_stream_order(self._h, stream, 1 if op_waits else 0))
+
     def shardCommit(self, gathered_ptr, world):
         self._check(self._l.scotty_shard_commit(self._h, gathered_ptr, world))
 
@@ -541,8 +547,11 @@ class ShardedSlicingWindowOperator:
         self.world = dist.get_world_size(group)
         self.dev = torch.device("cuda", device)
         self.staged = dist.get_backend(group) != "nccl"
+        if not self.staged:  # RCCL: the all-gather's stream is ordered after the push by events, no host sync
+            self.op.tune("shard_async", 1)
         self._xb = None
         self._assigned = []
+        self._measures = set()
 
     def __getattr__(self, name):  # addWindowFunction, setMaxLateness, processWatermark...
         return getattr(self.op, name)
@@ -550,10 +559,10 @@ class ShardedSlicingWindowOperator:
     def addWindowAssigner(self, window):
         self.op.addWindowAssigner(window)
         self._assigned.append(window)
+        self._measures.add(window.measure)  # kept incrementally: per-chunk checks must not walk 1000 windows
 
     def _count_and_time(self):
-        ms = {w.measure for w in self._assigned}
-        return {0, 1} <= ms  # SCOTTY_MEASURE_TIME, SCOTTY_MEASURE_COUNT
+        return {0, 1} <= self._measures  # SCOTTY_MEASURE_TIME, SCOTTY_MEASURE_COUNT
 
     def _bufs(self):
         if self._xb is None:
@@ -572,6 +581,12 @@ class ShardedSlicingWindowOperator:
         of all ranks in this micro-batch (count windows number tuples globally); ts_before / ts_last: the largest
         timestamp on the lower ranks / in the whole micro-batch (count + time windows); gathered when not given."""
         timed = self._count_and_time()
+        counted = 1 in self._measures  # SCOTTY_MEASURE_COUNT
+        if not counted:  # time windows only (the grid path): no count offsets, no extra collective
+            xb, gb = self._bufs()
+            self.op.shardPush(ts_ptr, val_ptr, n, ts0, xb.data_ptr())
+            self._exchange(xb, gb)
+            return
         if n_before is None or n_total is None or (timed and (ts_before is None or ts_last is None)):
             # one small all-gather of {n, first ts, last ts} per rank (count windows number tuples globally; time
             # windows on the count path decide a chunk's edges from the max ts before it, CEngine::time_edges)
@@ -591,14 +606,20 @@ class ShardedSlicingWindowOperator:
             self.op.shardPushTimed(ts_ptr, val_ptr, n, ts0, n_before, n_total, ts_before, ts_last, xb.data_ptr())
         else:
             self.op.shardPushCounted(ts_ptr, val_ptr, n, ts0, n_before, n_total, xb.data_ptr())
+        self._exchange(xb, gb)
+
+    def _exchange(self, xb, gb):
+        """All-gather of the ranks' exchange records (RCCL for "nccl", host-staged for "gloo"), then the commit."""
         if self.staged:
             self._hx.copy_(xb)
             self.dist.all_gather_into_tensor(self._hg, self._hx, group=self.group)
             gb.copy_(self._hg)
             self.torch.cuda.synchronize(self.dev)
         else:
+            cur = self.torch.cuda.current_stream(self.dev).cuda_stream
+            self.op.streamOrder(cur, False)  # the record is complete before the collective reads it
             self.dist.all_gather_into_tensor(gb, xb, group=self.group)
-            self.torch.cuda.current_stream(self.dev).synchronize()  # the commit runs on the op's own stream
+            self.op.streamOrder(cur, True)  # the gathered records have landed before the commit reads them
         self.op.shardCommit(gb.data_ptr(), self.world)
 
 

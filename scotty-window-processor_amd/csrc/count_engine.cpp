@@ -547,7 +547,7 @@ int CEngine::shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64
     CCHK(hipMemsetAsync(d_rec, 0, shard_words() * 8, stream));
     CCHK(hipMemcpyAsync(d_rec, h.data(), CSHARD_HDR * 8, hipMemcpyHostToDevice, stream));
   }
-  CCHK(hipStreamSynchronize(stream));  // the record is read by the collective on another stream
+  if (!shard_async) CCHK(hipStreamSynchronize(stream));  // the record is read by the collective on another stream
   return SCOTTY_OK;
 }
 

@@ -26,6 +26,7 @@ class CEngine {
                  int64_t ts_before, int64_t ts_last, int64_t* d_rec);
   int shard_commit(const int64_t* d_gathered, int world);
   int64_t shard_cap = 1 << 16;  // cells per rank record (scotty_tune "shard_count_cells")
+  bool shard_async = false;     // scotty_tune "shard_async": shard_push returns without a host sync
   int watermark(int64_t wm, XResult& r, bool to_host);
   int set_last_watermark(int64_t lw) {
     last_wm = lw;

@@ -64,6 +64,8 @@ struct scotty_op {
   int device = 0;
   int vt = VT_I32;
   hipStream_t stream = nullptr;
+  hipEvent_t order_ev = nullptr;  // scotty_stream_order
+  bool shard_async = false;       // scotty_tune("shard_async", 1): shard pushes return without a host sync
   std::string err;
   bool failed = false;
 
@@ -734,6 +736,7 @@ void scotty_destroy(scotty_op* op) {
   if (op->h_out) (void)hipHostFree(op->h_out);
   for (auto& e : op->tev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  if (op->order_ev) (void)hipEventDestroy(op->order_ev);
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
   delete op->c;
@@ -861,6 +864,7 @@ static int decide_mode(scotty_op* op) {
     if (!rc) rc = op->c->configure(op->xwins, op->aggs, op->max_lateness);
     if (!rc && op->last_watermark != -1) rc = op->c->set_last_watermark(op->last_watermark);
     op->c->shard_cap = op->count_shard_cap;
+    op->c->shard_async = op->shard_async;
     if (rc) {
       op->failed = true;
       return fail(op, rc, e.empty() ? op->c->err : e);
@@ -1122,7 +1126,9 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
   a.n = (int64_t)n;
   a.xbuf = (int64_t*)d_xbuf;
   HIPCHK(launch_shard_export(a, op->stream));
-  HIPCHK(hipStreamSynchronize(op->stream));  // the record is complete when the caller starts the all-gather
+  // the record is complete when the caller starts the all-gather -- unless the caller orders its collective's stream
+  // after the op's stream itself (shard_async + scotty_stream_order)
+  if (!op->shard_async) HIPCHK(hipStreamSynchronize(op->stream));
   return SCOTTY_OK;
 }
 
@@ -1406,6 +1412,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->x) op->x->kg_off = op->x_kg_off;
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "shard_async") == 0) {  // shard pushes without a host sync (the caller orders its streams)
+    if (value < 0 || value > 1) return SCOTTY_ERR_ARG;
+    op->shard_async = value != 0;
+    if (op->c) op->c->shard_async = op->shard_async;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only)
     if (op->mode != 0 || value < 0 || value > 3) return SCOTTY_ERR_ARG;
     op->x_kg_variant = (int32_t)value;
@@ -1482,6 +1494,20 @@ int64_t scotty_debug_dump(scotty_op* op, int64_t key_slot, int64_t* out, int64_t
 int scotty_sync(scotty_op* op) {
   if (!op) return SCOTTY_ERR_ARG;
   HIPCHK(hipStreamSynchronize(op->stream));
+  return SCOTTY_OK;
+}
+
+int scotty_stream_order(scotty_op* op, void* stream, int op_waits) {
+  if (!op) return SCOTTY_ERR_ARG;
+  if (!op->order_ev) HIPCHK(hipEventCreateWithFlags(&op->order_ev, hipEventDisableTiming));
+  hipStream_t ext = (hipStream_t)stream;
+  if (op_waits) {
+    HIPCHK(hipEventRecord(op->order_ev, ext));
+    HIPCHK(hipStreamWaitEvent(op->stream, op->order_ev, 0));
+  } else {
+    HIPCHK(hipEventRecord(op->order_ev, op->stream));
+    HIPCHK(hipStreamWaitEvent(ext, op->order_ev, 0));
+  }
   return SCOTTY_OK;
 }
 

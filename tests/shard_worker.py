@@ -17,7 +17,10 @@ from shard_cases import case  # noqa: E402
 
 def main():
     out, cid = sys.argv[1], int(sys.argv[2])
-    dist.init_process_group("gloo")
+    backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend)
     rank, world = dist.get_rank(), dist.get_world_size()
     pkg = product()
     cfg, ts, vals, sched = case(cid)

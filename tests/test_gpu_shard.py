@@ -17,15 +17,33 @@ from oracle.oracle import JavaError
 pytestmark = pytest.mark.gpu
 
 
+def _run_sharded(tmp_path, cid, nproc, backend):
+    out = str(tmp_path / "w.json")
+    port = str(29500 + cid + 8 * nproc + (os.getpid() % 400))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                        "--master-addr", "127.0.0.1", "--master-port", port,
+                        os.path.join(ROOT, "tests", "shard_worker.py"), out, str(cid), backend],
+                       env=env, capture_output=True, text=True, timeout=240)
+    return r, out
+
+
+@pytest.mark.parametrize("cid", [0, 4, 6])
+def test_rccl_exchange_single_rank_matches_oracle(tmp_path, cid):
+    """The RCCL ("nccl") exchange path -- device all-gather ordered against the operator's stream by events
+    (scotty_stream_order, shard_async), no host synchronisation -- on one rank of this one-GPU box: time windows,
+    count windows, count + time windows."""
+    r, out = _run_sharded(tmp_path, cid, 1, "nccl")
+    _check(r, out, cid)
+
+
 @pytest.mark.parametrize("cid", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_two_rank_sharded_stream_matches_oracle(tmp_path, cid):
-    out = str(tmp_path / "w.json")
-    port = str(29500 + cid + (os.getpid() % 400))
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", port,
-                        os.path.join(ROOT, "tests", "shard_worker.py"), out, str(cid)],
-                       env=env, capture_output=True, text=True, timeout=240)
+    r, out = _run_sharded(tmp_path, cid, 2, "gloo")
+    _check(r, out, cid)
+
+
+def _check(r, out, cid):
     tb = r.stderr.find("Traceback")
     assert r.returncode == 0, r.stderr[tb:tb + 3000] if tb >= 0 else r.stderr[-3000:]
     got = json.load(open(out))
