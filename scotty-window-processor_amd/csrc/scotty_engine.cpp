@@ -65,6 +65,9 @@ struct scotty_op {
   int vt = VT_I32;
   hipStream_t stream = nullptr;
   hipEvent_t order_ev = nullptr;  // scotty_stream_order
+  hipEvent_t wm_ev = nullptr;     // grid watermark: the packed result has landed (the host waits on this, not the stream)
+  bool cix_ready = false;         // the cell index on the device matches the current slice store (built at the end
+                                  // of the last watermark, overlapping the host's result handling)
   bool shard_async = false;       // scotty_tune("shard_async", 1): shard pushes return without a host sync
   std::string err;
   bool failed = false;
@@ -220,9 +223,15 @@ int tend(scotty_op* op, scotty_op::TEv& e) {
   op->tev_pending.push_back(e);
   return SCOTTY_OK;
 }
-// after a stream synchronisation: fold every recorded interval into its class
+// after a synchronisation: fold every completed interval into its class; intervals still running (the cell index
+// built behind a watermark's result transfer) stay pending until the next resolve
 void tresolve(scotty_op* op) {
+  std::vector<scotty_op::TEv> keep;
   for (auto& e : op->tev_pending) {
+    if (hipEventQuery(e.b) == hipErrorNotReady) {
+      keep.push_back(e);
+      continue;
+    }
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
       op->t_cls_ms[e.cls] += ms;
@@ -230,7 +239,7 @@ void tresolve(scotty_op* op) {
     }
     op->ev_pool.push_back({e.a, e.b});
   }
-  op->tev_pending.clear();
+  op->tev_pending.swap(keep);
 }
 
 int agg_value_type(int kind) {
@@ -309,6 +318,7 @@ void build_grid(scotty_op* op, int64_t n_pending, int64_t horizon_end) {
 }
 
 int upload_grid(scotty_op* op) {
+  op->cix_ready = false;  // the cell index covers grid cells
   HIPCHK(hipMemcpyAsync(op->d_grid, op->grid.data(), op->grid.size() * 8, hipMemcpyHostToDevice, op->stream));
   // DevMeta.j0 = 0, gcount = grid.size()  (offsets of DevMeta fields)
   int64_t v[2] = {0, (int64_t)op->grid.size()};
@@ -440,6 +450,7 @@ bool first_walk(const scotty_op* op, int64_t te, std::vector<int64_t>& edges, in
 int compact_if_needed(scotty_op* op) {
   DevMeta& m = *op->h_snap;
   if (m.tail < op->scap / 2 || m.head == 0) return SCOTTY_OK;
+  op->cix_ready = false;  // slices move
   const int64_t live = m.tail - m.head;
   int64_t* tmp = nullptr;
   HIPCHK(hipMalloc(&tmp, std::max<int64_t>(live, 1) * 8));
@@ -467,6 +478,27 @@ int sync_snapshot(scotty_op* op) {
   return SCOTTY_OK;
 }
 
+// Cell index build over the current slice store (cix_build_kernel, class PUSH_OTHER): it reads only operator state,
+// so the grid watermark enqueues it behind the result transfer for the next micro-batch.
+int enqueue_cix(scotty_op* op) {
+  if (!op->d_cix) {
+    HIPCHK(hipMalloc(&op->d_cix, CIX_CAP * 4));
+    HIPCHK(hipMalloc(&op->d_cixmeta, 8 * 8));
+  }
+  IngestArgs ia{};
+  ia.s_tstart = op->d_tstart;
+  ia.grid = op->d_grid;
+  ia.meta = op->d_meta;
+  ia.cix = op->d_cix;
+  ia.cix_meta = op->d_cixmeta;
+  ia.cix_margin = std::max<int64_t>(4 * op->last_span, 4000);
+  scotty_op::TEv tx;
+  int rc = tbegin(op, tx, SCOTTY_TIME_PUSH_OTHER);
+  if (rc) return rc;
+  HIPCHK(launch_cix_build(ia, op->stream));
+  return tend(op, tx);
+}
+
 // Ingest launch of one micro-batch (no host synchronisation); *tile_out = the arrival tile size used.
 int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t* tile_out) {
   int rc = ensure_tiles(op, n);
@@ -489,12 +521,11 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   ia.cix = op->d_cix;
   ia.cix_meta = op->d_cixmeta;
   ia.cix_margin = std::max<int64_t>(4 * op->last_span, 4000);
-  scotty_op::TEv tx;
-  rc = tbegin(op, tx, SCOTTY_TIME_PUSH_OTHER);
-  if (rc) return rc;
-  HIPCHK(launch_cix_build(ia, op->stream));
-  rc = tend(op, tx);
-  if (rc) return rc;
+  if (!op->cix_ready) {
+    rc = enqueue_cix(op);
+    if (rc) return rc;
+  }
+  op->cix_ready = false;  // this micro-batch changes the slice store
   // tile: power of two >= TILE_MIN with at most NT_MAX tiles (the commit kernel keeps them in LDS)
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
@@ -620,6 +651,7 @@ int maybe_extend_grid(scotty_op* op, bool force) {
 }
 
 int replay_after_overflow(scotty_op* op) {
+  op->cix_ready = false;
   for (int attempt = 0; attempt < 4; attempt++) {
     DevMeta& m = *op->h_snap;
     if (!m.overflow) return SCOTTY_OK;
@@ -737,6 +769,7 @@ void scotty_destroy(scotty_op* op) {
   for (auto& e : op->tev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& e : op->ev_pending) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (op->order_ev) (void)hipEventDestroy(op->order_ev);
+  if (op->wm_ev) (void)hipEventDestroy(op->wm_ev);
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
   delete op->c;
@@ -1256,7 +1289,13 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
       HIPCHK(hipMemcpyAsync(op->h_out, op->d_out, L.total, hipMemcpyDeviceToHost, op->stream));
       rc = tend(op, tc);
       if (rc) return rc;
-      HIPCHK(hipStreamSynchronize(op->stream));
+      // the next micro-batch's cell index is built while the host handles this result
+      if (!op->wm_ev) HIPCHK(hipEventCreateWithFlags(&op->wm_ev, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(op->wm_ev, op->stream));
+      rc = enqueue_cix(op);
+      if (rc) return rc;
+      op->cix_ready = true;
+      HIPCHK(hipEventSynchronize(op->wm_ev));
       std::memcpy(op->h_snap, op->h_out, sizeof(DevMeta));
       if (!op->h_snap->overflow) break;
       rc = replay_after_overflow(op);
