@@ -341,7 +341,7 @@ __global__ void xb_prep_kernel(XBArgs a) {
     sn.min_gap = min(sn.min_gap, c->gap[k]);
     const int64_t* st_ = a.ss.start + (int64_t)k * c->sesscap;
     const int64_t* en_ = a.ss.end + (int64_t)k * c->sesscap;
-    const int ns = s.nsess[k];
+    const int ns = s.ns(k);
     sn.ns[k] = ns;
     sn.last_start[k] = ns > 0 ? st_[ns - 1] : JMAX;
     sn.stored_end[k] = ns > 0 ? en_[ns - 1] : JMIN;
@@ -916,7 +916,7 @@ __device__ __forceinline__ void reconstruct(Op& o, const XCfg* cfg, int64_t m) {
     if (m >= o.ts[cur] && m > o.tl[cur]) o.tl[cur] = m;
   }
   for (int c = 0; c < cfg->n_ctx; c++) {
-    const int ns = o.s.nsess[c];
+    const int ns = o.s.ns(c);
     if (ns > 0 && m > o.se[c][ns - 1]) o.se[c][ns - 1] = m;
   }
 }

@@ -80,6 +80,17 @@ struct XState {          // 128 B
   int32_t started, unsorted;                                        // store non-empty; tStart order broken
   int32_t err, key;                                                 // fatal error; key of this op
   int32_t nsess[XMAXCTX];
+  // context c's session count through constant indices only: a runtime index into nsess keeps the whole XState of
+  // a kernel in scratch memory (every field access then a scratch round trip)
+  __host__ __device__ int32_t ns(int c) const {
+    return c == 0 ? nsess[0] : c == 1 ? nsess[1] : c == 2 ? nsess[2] : nsess[3];
+  }
+  __host__ __device__ void set_ns(int c, int32_t v) {
+    if (c == 0) nsess[0] = v;
+    else if (c == 1) nsess[1] = v;
+    else if (c == 2) nsess[2] = v;
+    else nsess[3] = v;
+  }
   uint64_t dropped;                                                 // tuples whose processing threw
   int64_t wlo, whi;                                                 // watermark: slice scan range
   int32_t pending;                                                  // batch deferred: capacity too small

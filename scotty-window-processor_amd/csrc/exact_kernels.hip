@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
       if (cfg->n_ctx > 0) bound += 3.0 * (double)seglen;
       const double need_s = (double)(o.s.tail - o.s.head) + bound + 2.0;
       int need_x = 0;
-      for (int c = 0; c < cfg->n_ctx; c++) need_x = max(need_x, o.s.nsess[c]);
+      for (int c = 0; c < cfg->n_ctx; c++) need_x = max(need_x, o.s.ns(c));
       const int64_t need_ss = cfg->n_ctx > 0 ? (int64_t)need_x + seglen + 1 : 0;
       // records: every tuple adds at most one record; the live arena range is compacted first when needed
       int64_t need_r = 0;
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
         const bool in_order_m = t >= tl_j;
         int ext_mask = 0;
         for (int c = 0; c < cfg->n_ctx; c++) {
-          const int ns = o.s.nsess[c];
+          const int ns = o.s.ns(c);
           const int64_t gap = cfg->gap[c];
           if (ns == 0) {
             simple = false;
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
           o.s.maxEventTime = max(o.s.maxEventTime, pmax);
           o.s.currentCount = jadd(o.s.currentCount, jstar - j0);
           for (int c = 0; c < cfg->n_ctx; c++) {
-            const int ns = o.s.nsess[c];
+            const int ns = o.s.ns(c);
             const int64_t emax = wmax(act && ((ext_mask >> c) & 1) ? t : JMIN);
             if (ns > 0 && emax != JMIN && emax > o.se[c][ns - 1]) o.se[c][ns - 1] = emax;
           }
@@ -350,7 +350,7 @@ __device__ int64_t wm_triggers(Op& o, int64_t wm, int64_t* w_start, int64_t* w_e
   }
   for (int c = 0; c < cfg->n_ctx; c++) {  // SessionContext.triggerWindows (SessionWindow.java:108-119)
     const int64_t gap = cfg->gap[c];
-    const int ns = o.s.nsess[c];
+    const int ns = o.s.ns(c);
     if (ns == 0) {
       o.exc = XERR_WM_INDEX;  // getWindow(0) on an empty context
       return k;
@@ -365,7 +365,7 @@ __device__ int64_t wm_triggers(Op& o, int64_t wm, int64_t* w_start, int64_t* w_e
         o.ss[c][j - i] = o.ss[c][j];
         o.se[c][j - i] = o.se[c][j];
       }
-      o.s.nsess[c] = ns - i;
+      o.s.set_ns(c, ns - i);
     }
   }
   return k;
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
   const int64_t cw = jsub(a.wm, cfg->max_lateness);
   int64_t first = cw;
   for (int c = 0; c < cfg->n_ctx; c++)
-    for (int i = 0; i < o.s.nsess[c]; i++) first = min(first, o.ss[c][i]);
+    for (int i = 0; i < o.s.ns(c); i++) first = min(first, o.ss[c][i]);
   const int64_t t = min(jsub(cw, cfg->max_fixed), first);
   const int idx = o.find_ts(t);
   if (idx > o.s.head) o.s.head = idx;

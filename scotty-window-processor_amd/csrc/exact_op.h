@@ -157,8 +157,16 @@ struct Op {
   int64_t *ts, *te, *tl, *tf, *cs, *cl;
   int32_t* ty;
   unsigned long long *cnt, *p0, *p1, *p2;
-  int64_t* ss[XMAXCTX];
-  int64_t* se[XMAXCTX];
+  // session columns of context c: ss[c][i] / se[c][i] (start / end of session i), computed from one base pointer
+  // (an array of per-context pointers indexed by a loop variable was kept in scratch memory, adding a dependent
+  // scratch load to every session access)
+  struct SessCol {
+    int64_t* base;
+    int64_t stride;
+    int cmax;
+    __device__ __forceinline__ int64_t* operator[](int c) const { return base + (int64_t)min(c, cmax) * stride; }
+  };
+  SessCol ss, se;
   // records mode: per-slice record ranges, non-null flags, the op's record arena
   int64_t *rlo, *rhi, *rts, *rv;
   int32_t* nn;
@@ -178,11 +186,9 @@ struct Op {
       rlo = rhi = rts = rv = nullptr;
       nn = nullptr;
     }
-    for (int c2 = 0; c2 < XMAXCTX; c2++) {
-      const int64_t sb = (op * c->ctx_alloc + min(c2, max(c->ctx_alloc - 1, 0))) * (int64_t)c->sesscap;
-      ss[c2] = sx.start + sb;
-      se[c2] = sx.end + sb;
-    }
+    const int64_t sb = op * c->ctx_alloc * (int64_t)c->sesscap;
+    ss = SessCol{sx.start + sb, (int64_t)c->sesscap, max(c->ctx_alloc - 1, 0)};
+    se = SessCol{sx.end + sb, (int64_t)c->sesscap, max(c->ctx_alloc - 1, 0)};
     exc = 0;
     lane = ln;
   }
@@ -745,7 +751,7 @@ struct Op {
 
   // ---------------------------------------------------------------- SessionContext (SessionWindow.java:40-116)
   __device__ void add_window(int c, int i, int64_t start, int64_t end, Mod* mods, int& nm) {  // WindowContext :19-25
-    const int n = s.nsess[c];
+    const int n = s.ns(c);
     if (i < 0 || i > n) {
       exc = XERR_INDEX;
       return;
@@ -760,14 +766,14 @@ struct Op {
     }
     ss[c][i] = start;
     se[c][i] = end;
-    s.nsess[c] = n + 1;
+    s.set_ns(c, n + 1);
     if (mods && nm + 2 <= XMAXMODS) {
       mods[nm++] = Mod{2, 0, start};
       mods[nm++] = Mod{2, 0, end};
     }
   }
   __device__ void remove_window(int c, int i, Mod* mods, int& nm) {  // :48-52
-    const int n = s.nsess[c];
+    const int n = s.ns(c);
     if (i < 0 || i >= n) {
       exc = XERR_INDEX;
       return;
@@ -780,10 +786,10 @@ struct Op {
       ss[c][k] = ss[c][k + 1];
       se[c][k] = se[c][k + 1];
     }
-    s.nsess[c] = n - 1;
+    s.set_ns(c, n - 1);
   }
   __device__ void merge_with_pre(int c, int idx, Mod* mods, int& nm) {  // :39-46
-    if (idx < 0 || idx >= s.nsess[c] || idx - 1 < 0) {
+    if (idx < 0 || idx >= s.ns(c) || idx - 1 < 0) {
       exc = XERR_INDEX;
       return;
     }
@@ -792,7 +798,7 @@ struct Op {
   }
   __device__ int get_session(int c, int64_t pos) {  // :89-101
     const int64_t gap = cfg->gap[c];
-    const int n = s.nsess[c];
+    const int n = s.ns(c);
     int i = 0;
     for (; i < n; i++) {
       const int64_t st = ss[c][i], en = se[c][i];
@@ -803,7 +809,7 @@ struct Op {
   }
   __device__ void session_update(int c, int64_t pos, Mod* mods, int& nm) {  // :42-87
     const int64_t gap = cfg->gap[c];
-    if (s.nsess[c] == 0) {  // hasActiveWindows() returns isEmpty() (WindowContext.java:15-17)
+    if (s.ns(c) == 0) {  // hasActiveWindows() returns isEmpty() (WindowContext.java:15-17)
       add_window(c, 0, pos, pos, mods, nm);
       return;
     }
@@ -823,7 +829,7 @@ struct Op {
       }
     } else if (en < pos && jadd(en, gap) >= pos) {
       se[c][si] = pos;  // shiftEnd
-      if (si < s.nsess[c] - 1) {
+      if (si < s.ns(c) - 1) {
         if (jadd(se[c][si], gap) >= ss[c][si + 1]) merge_with_pre(c, si + 1, mods, nm);
       }
     } else if (jadd(en, gap) < pos) {
