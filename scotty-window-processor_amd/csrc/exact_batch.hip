@@ -926,7 +926,10 @@ __global__ __launch_bounds__(64) void xb_events_kernel(XBArgs a) {
   const int lane = threadIdx.x;
   const XCfg* cfg = a.cfg;
   XBCtl ctl = *a.ctl;
-  Op o;
+  // the operator's state lives in LDS, shared by the wave's lanes (all hold the same values): as a private object it
+  // sat in scratch memory, and every step of the event walk paid a scratch round trip
+  __shared__ Op o_lds;
+  Op& o = o_lds;
   o.bind(cfg, a.sl, a.ss, 0, lane);
   o.s = *a.st;
   if (ctl.done || o.s.err) {

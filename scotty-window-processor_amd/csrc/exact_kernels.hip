@@ -286,7 +286,7 @@ __device__ int64_t wm_triggers(Op& o, int64_t wm, int64_t* w_start, int64_t* w_e
   const XCfg* cfg = o.cfg;
   int64_t k = 0;
   auto emit = [&](int64_t st, int64_t en, int32_t meas) {
-    if (!DRY && o.lane == 0) {
+    if (!DRY && __lane_id() == 0) {
       w_start[off + k] = st;
       w_end[off + k] = en;
       w_meas[off + k] = meas;
@@ -328,7 +328,7 @@ __device__ int64_t wm_triggers(Op& o, int64_t wm, int64_t* w_start, int64_t* w_e
         cnt = max((int64_t)0, k_hi - k_lo + 1);
       }
       if (!DRY)
-        for (int64_t i = o.lane; i < cnt; i += 64) {
+        for (int64_t i = __lane_id(); i < cnt; i += 64) {
           const int64_t ws = first + i * step;
           w_start[off + k + i] = ws;
           w_end[off + k + i] = ws + a;

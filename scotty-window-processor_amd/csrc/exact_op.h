@@ -151,6 +151,7 @@ struct Mod {  // C/windowType/windowContext/{Shift,Delete,Add}Modification.java
 };
 
 // ======================================================================== one operator, wave-uniform
+#define LANE_ID ((int)__lane_id())
 struct Op {
   const XCfg* cfg;
   // slice arrays of this op (already offset by op * sc)
@@ -172,7 +173,7 @@ struct Op {
   int32_t* nn;
   XState s;
   int32_t exc;
-  int lane;
+  // the lane index is read from the hardware, not stored: an Op may live in LDS, shared by its wave's lanes
 
   __device__ void bind(const XCfg* c, const XSlices& sl, const XSess& sx, int64_t op, int ln) {
     cfg = c;
@@ -190,7 +191,7 @@ struct Op {
     ss = SessCol{sx.start + sb, (int64_t)c->sesscap, max(c->ctx_alloc - 1, 0)};
     se = SessCol{sx.end + sb, (int64_t)c->sesscap, max(c->ctx_alloc - 1, 0)};
     exc = 0;
-    lane = ln;
+    (void)ln;
   }
 
   // ---------------------------------------------------------------- slice list primitives
@@ -208,7 +209,7 @@ struct Op {
     const bool rec = cfg->records != 0;
     if (dst < src) {
       for (int b = 0; b < n; b += 64) {
-        const int i = b + lane;
+        const int i = b + LANE_ID;
         int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, r0 = 0, r1 = 0;
         int32_t a6 = 0, r2 = 0;
         unsigned long long a7 = 0, a8 = 0, a9 = 0, a10 = 0;
@@ -229,7 +230,7 @@ struct Op {
       }
     } else {
       for (int b = n; b > 0; b -= 64) {
-        const int i = b - 1 - lane;
+        const int i = b - 1 - LANE_ID;
         int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, r0 = 0, r1 = 0;
         int32_t a6 = 0, r2 = 0;
         unsigned long long a7 = 0, a8 = 0, a9 = 0, a10 = 0;
@@ -310,7 +311,7 @@ struct Op {
       return lo - 1 >= s.head ? lo - 1 : -1;
     }
     for (int b = s.tail - 1; b >= s.head; b -= 64) {
-      const int i = b - lane;
+      const int i = b - LANE_ID;
       const bool hit = i >= s.head && ts[i] <= t;
       const unsigned long long m = __ballot(hit);
       if (m) return b - (__ffsll((long long)m) - 1);
@@ -320,7 +321,7 @@ struct Op {
   // LazyAggregateStore.findSliceIndexByCount (:41-49)
   __device__ int find_count(int64_t c) {
     for (int b = s.tail - 1; b >= s.head; b -= 64) {
-      const int i = b - lane;
+      const int i = b - LANE_ID;
       const bool hit = i >= s.head && cs[i] <= c;
       const unsigned long long m = __ballot(hit);
       if (m) return b - (__ffsll((long long)m) - 1);
@@ -330,7 +331,7 @@ struct Op {
   // LazyAggregateStore.findSliceByEnd (:127-135)
   __device__ int find_end(int64_t e) {
     for (int b = s.tail - 1; b >= s.head; b -= 64) {
-      const int i = b - lane;
+      const int i = b - LANE_ID;
       const bool hit = i >= s.head && te[i] == e;
       const unsigned long long m = __ballot(hit);
       if (m) return b - (__ffsll((long long)m) - 1);
@@ -366,7 +367,7 @@ struct Op {
     if (n <= 0 || dst == src) return;
     if (dst < src) {
       for (int64_t b = 0; b < n; b += 64) {
-        const int64_t i = b + lane;
+        const int64_t i = b + LANE_ID;
         int64_t a = 0, v = 0;
         if (i < n) { a = rts[src + i]; v = rv[src + i]; }
         __builtin_amdgcn_wave_barrier();
@@ -375,7 +376,7 @@ struct Op {
       }
     } else {
       for (int64_t b = n; b > 0; b -= 64) {
-        const int64_t i = b - 1 - lane;
+        const int64_t i = b - 1 - LANE_ID;
         int64_t a = 0, v = 0;
         if (i >= 0) { a = rts[src + i]; v = rv[src + i]; }
         __builtin_amdgcn_wave_barrier();
@@ -387,7 +388,7 @@ struct Op {
   }
   // record ranges of slices [from, tail) move by d
   __device__ void rec_adjust(int from, int64_t d) {
-    for (int i = from + lane; i < s.tail; i += 64) {
+    for (int i = from + LANE_ID; i < s.tail; i += 64) {
       rlo[i] += d;
       rhi[i] += d;
     }
@@ -397,7 +398,7 @@ struct Op {
   __device__ int64_t rec_lb(int64_t lo, int64_t hi, int64_t t) {
     while (hi - lo > 64) {
       const int64_t stride = (hi - lo + 63) >> 6;
-      const int64_t p = lo + (int64_t)lane * stride;
+      const int64_t p = lo + (int64_t)LANE_ID * stride;
       const unsigned long long bal = __ballot(p < hi && rts[p] >= t);
       if (bal == 0) {
         lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
@@ -409,7 +410,7 @@ struct Op {
         hi = pf;
       }
     }
-    const int64_t p = lo + lane;
+    const int64_t p = lo + LANE_ID;
     const unsigned long long bal = __ballot(p < hi && rts[p] >= t);
     return bal ? lo + __ffsll((long long)bal) - 1 : hi;
   }
@@ -440,7 +441,7 @@ struct Op {
     uint64_t c = 0, sw = 0;
     double sf = 0.0;
     int64_t mn = ID_MIN, mx = ID_MAX;
-    for (int64_t p = rlo[i] + lane; p < rhi[i]; p += 64) {
+    for (int64_t p = rlo[i] + LANE_ID; p < rhi[i]; p += 64) {
       const Lift l = lift(cfg->vt, rv[p]);
       c++;
       if (cfg->vt == VT_F64) sf += __longlong_as_double((long long)l.sum);
@@ -613,7 +614,7 @@ struct Op {
     const int64_t base = rlo[s.head];
     if (base <= 0) return;
     rec_move(0, base, s.rend - base);
-    for (int i = s.head + lane; i < s.tail; i += 64) {
+    for (int i = s.head + LANE_ID; i < s.tail; i += 64) {
       rlo[i] -= base;
       rhi[i] -= base;
     }
@@ -843,7 +844,7 @@ struct Op {
     const int64_t cur = s.nextEdgeTs == JMIN ? JMAX : s.nextEdgeTs;
     const int64_t t_c = max(jsub(te_, cfg->max_lateness), cur);
     int64_t e = JMAX;
-    for (int w = lane; w < cfg->n_cf; w += 64) {
+    for (int w = LANE_ID; w < cfg->n_cf; w += 64) {
       if (cfg->cf_measure[w] != SCOTTY_MEASURE_TIME_) continue;
       e = min(e, assign_next(w, t_c));
     }
@@ -854,7 +855,7 @@ struct Op {
     const int64_t cur = s.nextEdgeCount == JMIN ? 0 : s.nextEdgeCount;
     const int64_t t_c = max(s.currentCount, cur);
     int64_t e = JMAX;
-    for (int w = lane; w < cfg->n_cf; w += 64) {
+    for (int w = LANE_ID; w < cfg->n_cf; w += 64) {
       if (cfg->cf_measure[w] != SCOTTY_MEASURE_COUNT_) continue;
       e = min(e, assign_next(w, t_c));
     }
