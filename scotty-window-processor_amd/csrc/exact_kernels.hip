@@ -39,6 +39,7 @@ __device__ __forceinline__ void load_tuple(const XBatchArgs& a, int64_t i, int64
 
 template <int VT>
 __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
+  __shared__ Op o_lds[4];
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const XCfg* cfg = a.cfg;
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(256) void replay_kernel(XBatchArgs a) {
       b1 = a.seg_end[op];
     }
     if (b1 <= b0) continue;
-    Op o;
+    Op& o = o_lds[threadIdx.x >> 6];  // per-wave operator state in LDS (a private Op sat in scratch)
     o.bind(cfg, a.sl, a.ss, op, lane);
     o.s = a.st[op];
     if (o.s.err) continue;
@@ -377,10 +378,11 @@ __device__ __forceinline__ void wm_prologue(Op& o, int64_t wm) {
 }
 
 __global__ __launch_bounds__(256) void wm_count_kernel(XWmArgs a) {
+  __shared__ Op o_lds[4];
   const int lane = threadIdx.x & 63;
   const int64_t op = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (op >= a.n_ops) return;
-  Op o;
+  Op& o = o_lds[threadIdx.x >> 6];  // per-wave operator state in LDS (a private Op sat in scratch)
   o.bind(a.cfg, a.sl, a.ss, op, lane);
   o.s = a.st[op];
   int64_t k = 0;
@@ -400,10 +402,11 @@ __global__ __launch_bounds__(256) void wm_count_kernel(XWmArgs a) {
 
 // emits the rows, computes the aggregation scan range and runs the watermark's state changes + GC
 __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
+  __shared__ Op o_lds[4];
   const int lane = threadIdx.x & 63;
   const int64_t op = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (op >= a.n_ops) return;
-  Op o;
+  Op& o = o_lds[threadIdx.x >> 6];  // per-wave operator state in LDS (a private Op sat in scratch)
   o.bind(a.cfg, a.sl, a.ss, op, lane);
   o.s = a.st[op];
   const XCfg* cfg = a.cfg;
