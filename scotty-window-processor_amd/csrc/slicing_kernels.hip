@@ -581,16 +581,36 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   };
   const int64_t w1_full = w0 + ((w1 - w0) / 256) * 256;  // end of the full steps
   if constexpr (PIPE) {
-    Step cur, nxt;
-    if (w0 < w1_full) load_step(w0, cur);
-    for (int64_t s = w0; s < w1_full; s += 256) {
-      if (s + 256 < w1_full) load_step(s + 256, nxt);
-      int64_t t[4];
-      V v[4];
-      unpack(cur, t, v);
-      process_full(t, v);
-      tile_done(s);
-      cur = nxt;
+    // two full steps in flight ahead of the one being combined; loads are unconditional (a step index past the
+    // wave's range is clamped to its last full step), so no load sits under a branch whose join would drain them
+    const int64_t nfull = (w1_full - w0) / 256;
+    const int64_t last = w0 + (nfull - 1) * 256;
+    auto cl = [&](int64_t x) { return x < last ? x : last; };
+    if (nfull > 0) {
+      Step b0, b1;
+      load_step(w0, b0);
+      load_step(cl(w0 + 256), b1);
+      const int64_t npair = nfull / 2;
+      for (int64_t k = 0; k < npair; k++) {
+        const int64_t s = w0 + k * 512;
+        int64_t t[4];
+        V v[4];
+        unpack(b0, t, v);
+        load_step(cl(s + 512), b0);
+        process_full(t, v);
+        tile_done(s);
+        unpack(b1, t, v);
+        load_step(cl(s + 768), b1);
+        process_full(t, v);
+        tile_done(s + 256);
+      }
+      if (nfull & 1) {
+        int64_t t[4];
+        V v[4];
+        unpack(b0, t, v);
+        process_full(t, v);
+        tile_done(w0 + npair * 512);
+      }
     }
   } else {
     for (int64_t s = w0; s < w1_full; s += 256) {
@@ -1260,6 +1280,7 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
       case 1: return launch_ingest_t<VT_I32, NEED_SUM, 1>(a, nblocks, st);
       case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
       case 3: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
+      case 7: return launch_ingest_t<VT_I32, NEED_SUM, 7>(a, nblocks, st);
       default: return launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st);
     }
   }
