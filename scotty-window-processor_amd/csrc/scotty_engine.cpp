@@ -26,6 +26,7 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_wm(const WmArgs& a, hipStream_t st);
+hipError_t launch_wm_publish(const void* d_src, void* h_dst_dev, int64_t bytes, hipStream_t st);
 hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
 hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st);
 hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st);
@@ -123,7 +124,8 @@ struct scotty_op {
   int64_t wdef_cap = 0;
   bool wdef_dirty = true;
   unsigned char* d_out = nullptr;
-  unsigned char* h_out = nullptr;  // pinned
+  unsigned char* h_out = nullptr;  // pinned, host-mapped
+  void* h_out_dev = nullptr;       // device address of h_out (null: plain DMA transfer)
   int64_t out_cap = 0;
 
   // ---- pushes of the current watermark interval (replayed after a horizon overflow)
@@ -393,8 +395,11 @@ int ensure_wm_out(scotty_op* op, int64_t bytes) {
   op->d_out = nullptr;
   op->h_out = nullptr;
   op->out_cap = std::max<int64_t>(bytes + bytes / 2, 1 << 16);
+  op->out_cap = (op->out_cap + 15) & ~(int64_t)15;
   HIPCHK(hipMalloc(&op->d_out, op->out_cap));
-  HIPCHK(hipHostMalloc(&op->h_out, op->out_cap, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc(&op->h_out, op->out_cap, hipHostMallocMapped));
+  op->h_out_dev = nullptr;
+  if (hipHostGetDevicePointer(&op->h_out_dev, op->h_out, 0) != hipSuccess) op->h_out_dev = nullptr;
   return SCOTTY_OK;
 }
 
@@ -1286,7 +1291,8 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
       rc = tend(op, tw);
       if (!rc) rc = tbegin(op, tc, SCOTTY_TIME_RESULT_COPY);
       if (rc) return rc;
-      HIPCHK(hipMemcpyAsync(op->h_out, op->d_out, L.total, hipMemcpyDeviceToHost, op->stream));
+      if (op->h_out_dev) HIPCHK(launch_wm_publish(op->d_out, op->h_out_dev, L.total, op->stream));
+      else HIPCHK(hipMemcpyAsync(op->h_out, op->d_out, L.total, hipMemcpyDeviceToHost, op->stream));
       rc = tend(op, tc);
       if (rc) return rc;
       // the next micro-batch's cell index is built while the host handles this result

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/scotty_mi355x.h"
 #include "device_common.h"
 
@@ -384,7 +386,20 @@ __global__ __launch_bounds__(256) void wm_windows_kernel(WmArgs a) {
   if (lane == 0) a.out[L.has + wi] = has ? 1 : 0;
 }
 
+// The packed result into host-mapped pinned memory: one small kernel (16-byte stores over PCIe) instead of a DMA
+// transfer, whose setup latency dominated these few-KB copies of every watermark.
+__global__ __launch_bounds__(256) void wm_publish_kernel(const uint4* src, uint4* dst, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace wk
+
+hipError_t launch_wm_publish(const void* d_src, void* h_dst_dev, int64_t bytes, hipStream_t st) {
+  const int64_t n16 = (bytes + 15) / 16;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(64, (n16 + 255) / 256));
+  hipLaunchKernelGGL(wk::wm_publish_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)d_src, (uint4*)h_dst_dev, n16);
+  return hipGetLastError();
+}
 
 hipError_t launch_wm(const WmArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(wk::wm_prep_kernel, dim3(1), dim3(1024), 0, st, a);
