@@ -2,6 +2,7 @@
 // pending count edge exactly (edges are a function of counts), launches one push as a chain of kernels without
 // synchronising, and synchronises once per watermark (count trigger) plus once for the results.
 #include "count_engine.h"
+#include "host_copy.h"
 
 #include <algorithm>
 #include <chrono>
@@ -101,7 +102,7 @@ int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
   stream = st;
   vt = vt_;
   if (hipMalloc((void**)&d_meta, sizeof(CMeta)) != hipSuccess ||
-      hipHostMalloc((void**)&h_meta, sizeof(CMeta), hipHostMallocDefault) != hipSuccess ||
+      mapped_host_alloc((void**)&h_meta, (void**)&h_meta_dev, sizeof(CMeta)) != hipSuccess ||
       hipHostMalloc((void**)&h_tmp, 8 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
       hipMalloc((void**)&d_nte, sizeof(unsigned long long)) != hipSuccess) {
     e = "count engine: out of memory";
@@ -683,7 +684,7 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.meta = d_meta;
   a.wm = wm;
   CCHK(launch_count_wm_find(a, stream));
-  CCHK(hipMemcpyAsync(h_meta, d_meta, sizeof(CMeta), hipMemcpyDeviceToHost, stream));
+  CCHK(launch_copy_to_host(d_meta, h_meta_dev, sizeof(CMeta), stream));
   CCHK(hipStreamSynchronize(stream));
   dropped_ = h_meta->late_total;
   r.dropped = dropped_;
@@ -799,7 +800,7 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.has_value = d_has;
   if (nw > 0) {  // LazyAggregateStore.aggregate runs only with windows (S/WindowManager.java:73-75)
     CCHK(launch_count_wm_agg(a, (S_ub + 1023) / 1024 + 1, d_bsum, stream));
-    CCHK(hipMemcpyAsync(h_meta, d_meta, sizeof(CMeta), hipMemcpyDeviceToHost, stream));
+    CCHK(launch_copy_to_host(d_meta, h_meta_dev, sizeof(CMeta), stream));
     CCHK(hipStreamSynchronize(stream));
     if (h_meta->range_err) {
       err = "processWatermark threw IndexOutOfBoundsException (LazyAggregateStore.aggregate: a window starts before "

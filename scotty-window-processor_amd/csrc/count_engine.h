@@ -94,7 +94,8 @@ class CEngine {
   int64_t tail_ub = 0, head_lb = 0;  // slice range bounds between synchronisations
   // device
   CMeta* d_meta = nullptr;
-  CMeta* h_meta = nullptr;  // pinned
+  CMeta* h_meta = nullptr;  // pinned, host-mapped
+  CMeta* h_meta_dev = nullptr;
   CWin* d_wins = nullptr;
   int64_t scap = 0;
   CSlices sl{};

@@ -4,6 +4,7 @@
 // reference's WindowManager registration (S/WindowManager.java:121-151).
 #include "exact_batch.h"
 #include "exact_engine.h"
+#include "host_copy.h"
 #include "keyed_grid.h"
 
 #include <algorithm>
@@ -129,7 +130,7 @@ int XEngine::init(int dev, hipStream_t st, int value_type, bool is_keyed, std::s
   (void)e_out;
   XCHK(dalloc(&d_cfg, 1));
   XCHK(dalloc(&d_misc, 8));
-  XCHK(hipHostMalloc((void**)&h_misc, 16 * sizeof(int64_t), hipHostMallocDefault));
+  XCHK(mapped_host_alloc((void**)&h_misc, (void**)&h_misc_dev, 16 * sizeof(int64_t)));
   XCHK(dalloc(&d_newcnt, 1));
   XCHK(dalloc(&d_full, 1));
   XCHK(dalloc(&d_need, 4));
@@ -619,8 +620,8 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
     }
     XCHK(xb_apply(a, stream));
     static_assert(sizeof(int64_t) * 9 >= 68, "XBCtl layout");
-    XCHK(hipMemcpyAsync(h_misc, xb_ctl, 72, hipMemcpyDeviceToHost, stream));
-    if (cfg.n_ctx > 0) XCHK(hipMemcpyAsync(h_misc + 9, xb_nstot, 8 * cfg.n_ctx, hipMemcpyDeviceToHost, stream));
+    XCHK(launch_copy_to_host(xb_ctl, h_misc_dev, 72, stream));
+    if (cfg.n_ctx > 0) XCHK(launch_copy_to_host(xb_nstot, h_misc_dev + 9, 8 * cfg.n_ctx, stream));
     XCHK(hipStreamSynchronize(stream));
     const int64_t nev = h_misc[0];
     const int32_t retry = ((const int32_t*)(h_misc + 8))[0];
@@ -715,7 +716,7 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
   }
   if (!d_kgctl) {
     XCHK(dalloc((unsigned char**)&d_kgctl, sizeof(KgCtl)));
-    XCHK(hipHostMalloc(&h_kgctl, sizeof(KgCtl), hipHostMallocDefault));
+    XCHK(mapped_host_alloc(&h_kgctl, &h_kgctl_dev, sizeof(KgCtl)));
   }
   KgArgs a{};
   a.key = d_key;
@@ -743,7 +744,8 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
   XCHK(launch_kg_scatter(a, vt, stream));
   XCHK(launch_kg_bucket(a, vt, mm, n_ops, stream));
   KgCtl* hc = (KgCtl*)h_kgctl;
-  XCHK(hipMemcpyAsync(hc, d_kgctl, sizeof(KgCtl), hipMemcpyDeviceToHost, stream));
+  static_assert(sizeof(KgCtl) % 4 == 0, "KgCtl copied in words");
+  XCHK(launch_copy_to_host(d_kgctl, h_kgctl_dev, sizeof(KgCtl), stream));
   XCHK(hipStreamSynchronize(stream));
   (void)vb;
   *flag_out = hc->flag;

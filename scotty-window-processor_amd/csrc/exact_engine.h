@@ -131,7 +131,8 @@ class XEngine {
   void* d_kgrec = nullptr;
   uint8_t* d_kgmark = nullptr;
   void* d_kgctl = nullptr;
-  void* h_kgctl = nullptr;   // pinned copy of the control block
+  void* h_kgctl = nullptr;   // pinned, host-mapped copy of the control block
+  void* h_kgctl_dev = nullptr;
   uint32_t* d_kgkey = nullptr;
   int64_t* d_kgts = nullptr;
   void* d_kgval = nullptr;
@@ -151,7 +152,8 @@ class XEngine {
   int64_t wcap = 0, rcap = 0;
   int64_t *d_wcount = nullptr, *d_woff = nullptr, *d_scan64 = nullptr;
   int64_t* d_misc = nullptr;
-  int64_t* h_misc = nullptr;
+  int64_t* h_misc = nullptr;     // pinned, host-mapped
+  int64_t* h_misc_dev = nullptr;
   int64_t *d_w_start = nullptr, *d_w_end = nullptr;
   int32_t *d_w_meas = nullptr, *d_w_op = nullptr;
   uint32_t* d_w_key = nullptr;

@@ -1,0 +1,23 @@
+// host_copy.h -- small device-to-host reads through host-mapped pinned memory.
+//
+// The engines read a few bytes of control state back after their launches (event counts, batch flags, watermark
+// scalars).  A DMA transfer of such a block costs ~10-20 us of setup; a one-wave kernel writing it into
+// host-mapped pinned memory costs a kernel launch, and the host reads the bytes once the stream (or an event)
+// has completed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace scotty {
+
+// copy `bytes` (a multiple of 4) from device memory to the device address of a host-mapped buffer
+hipError_t launch_copy_to_host(const void* d_src, void* h_dst_dev, size_t bytes, hipStream_t st);
+
+// pinned, host-mapped allocation: *h host address, *d its device address
+inline hipError_t mapped_host_alloc(void** h, void** d, size_t bytes) {
+  hipError_t e = hipHostMalloc(h, bytes, hipHostMallocMapped);
+  if (e != hipSuccess) return e;
+  return hipHostGetDevicePointer(d, *h, 0);
+}
+
+}  // namespace scotty

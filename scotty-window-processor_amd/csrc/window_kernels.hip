@@ -392,7 +392,17 @@ __global__ __launch_bounds__(256) void wm_publish_kernel(const uint4* src, uint4
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
 
+__global__ __launch_bounds__(64) void copy_words_kernel(const uint32_t* src, uint32_t* dst, int64_t n) {
+  for (int64_t i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+
 }  // namespace wk
+
+hipError_t launch_copy_to_host(const void* d_src, void* h_dst_dev, size_t bytes, hipStream_t st) {
+  hipLaunchKernelGGL(wk::copy_words_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)d_src, (uint32_t*)h_dst_dev,
+                     (int64_t)(bytes / 4));
+  return hipGetLastError();
+}
 
 hipError_t launch_wm_publish(const void* d_src, void* h_dst_dev, int64_t bytes, hipStream_t st) {
   const int64_t n16 = (bytes + 15) / 16;
