@@ -999,7 +999,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
     a.w_key = d_w_key;
     XCHK(launch_lane_wm_emit(a, true, stream));
-    XCHK(hipMemcpyAsync(h_misc, d_misc, 4 * 8, hipMemcpyDeviceToHost, stream));
+    XCHK(launch_copy_to_host(d_misc, h_misc_dev, 4 * 8, stream));
     XCHK(hipStreamSynchronize(stream));
     prefix_stale = false;
     have_wm = true;
@@ -1017,9 +1017,9 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   XCHK(hipMemsetAsync(d_misc, 0, 3 * 8, stream));
   XCHK(lane_mode() ? launch_lane_wm_count(a, stream) : launch_wm_count(a, stream));
   XCHK(launch_scan_i64(d_wcount, d_woff, n_ops, d_scan64, stream));
-  XCHK(hipMemcpyAsync(h_misc, d_misc, 3 * 8, hipMemcpyDeviceToHost, stream));
-  XCHK(hipMemcpyAsync(h_misc + 3, d_woff + n_ops - 1, 8, hipMemcpyDeviceToHost, stream));
-  XCHK(hipMemcpyAsync(h_misc + 4, d_wcount + n_ops - 1, 8, hipMemcpyDeviceToHost, stream));
+  XCHK(launch_copy_to_host(d_misc, h_misc_dev, 3 * 8, stream));
+  XCHK(launch_copy_to_host(d_woff + n_ops - 1, h_misc_dev + 3, 8, stream));
+  XCHK(launch_copy_to_host(d_wcount + n_ops - 1, h_misc_dev + 4, 8, stream));
   XCHK(hipStreamSynchronize(stream));
   r.dropped = (uint64_t)h_misc[1];
   int rc = op_error((int32_t)h_misc[2]);
