@@ -1226,18 +1226,32 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
       const int64_t t = t_q[d], vb = v_q[d];
       const uint32_t wd = wd_q[d];
       ld(i + 256 * XD, t_q[d], v_q[d], wd_q[d]);
-      {
-        const int64_t iw = i0 + (threadIdx.x & ~63);
-        while (ecur + 1 < nep && epos(ecur + 1) < iw) ecur++;
+      const int64_t iw = i0 + (int64_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63));
+      while (ecur + 1 < nep && epos(ecur + 1) < iw) ecur++;
+      // usually no epoch entry falls among the wave's 64 tuples: then every lane's last slice present at arrival is
+      // the cursor's, looked up once for the wave
+      const bool uni = !(ecur + 1 < nep && epos(ecur + 1) < iw + 63);
+      int last_u = -1;
+      int64_t tl_u = 0;
+      if (uni) {
+        last_u = __builtin_amdgcn_readfirstlane(etail(ecur) - 1);
+        tl_u = last_u >= wbase ? (int64_t)w_ts[last_u - wbase] : gload(a.sl.ts + last_u);
       }
       bool act = i < b1 && !((wd >> (i & 31)) & 1);
       int si = -1, last = -1;
       if (act) {
-        // last epoch entry with pos < i: the last slice present at arrival (a few steps from the wave cursor)
-        int64_t lo = ecur;
-        while (lo + 1 < nep && epos(lo + 1) < i) lo++;
-        last = etail(lo) - 1;
-        if (t >= (last >= wbase ? (int64_t)w_ts[last - wbase] : gload(a.sl.ts + last))) {
+        int64_t tl;
+        if (uni) {
+          last = last_u;
+          tl = tl_u;
+        } else {
+          // last epoch entry with pos < i: the last slice present at arrival (a few steps from the wave cursor)
+          int64_t lo = ecur;
+          while (lo + 1 < nep && epos(lo + 1) < i) lo++;
+          last = etail(lo) - 1;
+          tl = last >= wbase ? (int64_t)w_ts[last - wbase] : gload(a.sl.ts + last);
+        }
+        if (t >= tl) {
           si = last;
         } else if (last > wbase && t >= kbase) {  // in the LDS window: last key <= t in [wbase, last)
           const uint64_t bo = ((uint64_t)t - (uint64_t)kbase) >> kshift;
