@@ -1,5 +1,6 @@
 """Rehearsal of bench.py's multi-GPU legs on ONE GPU: 2 ranks (torch.distributed.run, gloo, both on cuda:0)
-run the key-hash sharded C4 leg and the time-range sharded C5 leg at reduced batch sizes.  The driver runs the
+run the key-hash sharded C4 leg (router-owned keys) and the time-range sharded C5 / C5t legs at reduced batch
+sizes.  The driver runs the
 real thing (nccl, one GPU per rank) at round end; this checks the rank logic, exchange and timing code paths.
 
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 \
@@ -25,8 +26,9 @@ def main():
     dev = torch.device("cuda", 0)
     c4 = bench.extra_c4(pkg, dev, 1 << 20, 1 << 16, 3, rank=rank, world=world, dist=dist)
     c5 = bench.extra_c5(pkg, dev, 1 << 22, 3, n_windows=100, lo=10_000, hi=200_000, rank=rank, world=world, dist=dist)
+    c5t = bench.extra_c5t(pkg, dev, 1 << 20, 3, rank=rank, world=world, dist=dist)
     if rank == 0:
-        print(json.dumps({"c4": c4, "c5": c5}), flush=True)
+        print(json.dumps({"c4": c4, "c5": c5, "c5t": c5t}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
