@@ -185,6 +185,10 @@ struct KRec<4> {
     s[3 * i + 2] = z;
   }
   __device__ static KRec load_lds(const uint32_t* s, int i) { return KRec{s[3 * i], s[3 * i + 1], s[3 * i + 2]}; }
+  __device__ void set(uint32_t k, uint32_t toff) {
+    x = k;
+    y = toff;
+  }
   __device__ static KRec make(uint32_t k, uint32_t toff, const void* val, int64_t i) {
     return KRec{k, toff, (uint32_t)((const int32_t*)val)[i]};
   }
@@ -199,11 +203,46 @@ struct KRec<8> {
   __device__ void store(void* p, int64_t i) const { ((uint4*)p)[i] = w; }
   __device__ void store_lds(uint32_t* s, int i) const { ((uint4*)s)[i] = w; }
   __device__ static KRec load_lds(const uint32_t* s, int i) { return KRec{((const uint4*)s)[i]}; }
+  __device__ void set(uint32_t k, uint32_t toff) {
+    w.x = k;
+    w.y = toff;
+  }
   __device__ static KRec make(uint32_t k, uint32_t toff, const void* val, int64_t i) {
     const uint64_t v = (uint64_t)((const int64_t*)val)[i];
     return KRec{make_uint4(k, toff, (uint32_t)v, (uint32_t)(v >> 32))};
   }
 };
+
+// A tile's records and buckets.  Every load is unconditional (the index clamped to the batch), so the tile's loads
+// are all in flight before the first is used -- a load under `if (i < n)` whose value is used after the branch joins
+// is waited for with vmcnt(0) there, which serialised the IT rounds.  Tuples past the batch count into the sentinel
+// bucket NBS (never scanned, never stored).
+template <int VB, int IT, int ST, int NBS>
+__device__ __forceinline__ bool tile_records(const KgArgs& a, int64_t i0, int tid, int64_t f, int32_t* cnt,
+                                             KRec<VB> (&rec)[IT], int32_t (&bk)[IT], int32_t (&rk)[IT]) {
+  uint32_t kk[IT];
+  int64_t tt[IT], tp[IT];
+#pragma unroll
+  for (int j = 0; j < IT; j++) {
+    const int64_t i = i0 + j * ST + tid;
+    const int64_t ic = i < a.n ? i : a.n - 1;
+    kk[j] = __builtin_nontemporal_load(a.key + ic);
+    tt[j] = a.ts[ic];
+    tp[j] = a.ts[ic > 0 ? ic - 1 : 0];
+    rec[j] = KRec<VB>::make(0, 0, a.val, ic);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < IT; j++) {
+    const int64_t i = i0 + j * ST + tid;
+    const bool in = i < a.n;
+    bad |= in && i > 0 && tp[j] > tt[j];  // not in order: the bucket and commit kernels see the flag and skip
+    rec[j].set(kk[j], (uint32_t)(tt[j] - f));
+    bk[j] = in ? (int32_t)bucket_of(kk[j], a.kmask) : NBS;
+    rk[j] = atomicAdd(&cnt[bk[j]], 1);
+  }
+  return bad;
+}
 
 // Scatter into bucket runs, staged in LDS: a tile is counted per bucket, ranked, laid out bucket by bucket in LDS
 // and written as contiguous per-bucket runs (a wave writes a few runs, not 64 scattered records).  Order inside a
@@ -214,7 +253,7 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   constexpr int IT = T / ST;
   constexpr int PER = NBS / ST;
   __shared__ __attribute__((aligned(16))) uint32_t stage[T * (VB == 4 ? 3 : 4)];
-  __shared__ int32_t cnt[NBS], tst[NBS], base[NBS];
+  __shared__ int32_t cnt[NBS + 1], tst[NBS], base[NBS];
   __shared__ int32_t wsum[ST / 64];
   if (a.ctl->flag) return;
   const int64_t tile = tile_of(a.ntiles);
@@ -229,20 +268,7 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   const int64_t i0 = tile * T;
   KRec<VB> rec[IT];
   int32_t bk[IT], rk[IT];
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < IT; j++) {
-    const int64_t i = i0 + j * ST + tid;
-    bk[j] = -1;
-    if (i < a.n) {
-      const uint32_t k = __builtin_nontemporal_load(a.key + i);
-      const int64_t t = a.ts[i];
-      bad |= i > 0 && a.ts[i - 1] > t;  // not in order: the bucket and commit kernels see the flag and skip
-      rec[j] = KRec<VB>::make(k, (uint32_t)(t - f), a.val, i);
-      bk[j] = (int32_t)bucket_of(k, a.kmask);
-      rk[j] = atomicAdd(&cnt[bk[j]], 1);
-    }
-  }
+  const bool bad = tile_records<VB, IT, ST, NBS>(a, i0, tid, f, cnt, rec, bk, rk);
   if (__ballot(bad) && (tid & 63) == 0) atomicOr(&a.ctl->flag, KG_UNSORTED);
   __syncthreads();
   // tile-local exclusive scan of the bucket counts
@@ -271,7 +297,7 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < IT; j++)
-    if (bk[j] >= 0) rec[j].store_lds(stage, tst[bk[j]] + rk[j]);
+    if (bk[j] < NBS) rec[j].store_lds(stage, tst[bk[j]] + rk[j]);
   __syncthreads();
   const int nt = (int)min((int64_t)T, a.n - i0);
   for (int i = tid; i < nt; i += ST) {
@@ -288,7 +314,7 @@ __global__ __launch_bounds__(ST) void kg_scatter2_kernel(KgArgs a) {
   constexpr int IT = T / ST;
   constexpr int PER = NBS / ST;
   __shared__ __attribute__((aligned(16))) uint32_t stage[T * 3];
-  __shared__ int32_t cnt[NBS];
+  __shared__ int32_t cnt[NBS + 1];
   __shared__ int32_t wsum[ST / 64];
   if (a.ctl->flag) return;
   const int64_t tile = tile_of(a.ntiles);
@@ -300,20 +326,7 @@ __global__ __launch_bounds__(ST) void kg_scatter2_kernel(KgArgs a) {
   const int64_t i0 = tile * T;
   KRec<4> rec[IT];
   int32_t bk[IT], rk[IT];
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < IT; j++) {
-    const int64_t i = i0 + j * ST + tid;
-    bk[j] = -1;
-    if (i < a.n) {
-      const uint32_t k = __builtin_nontemporal_load(a.key + i);
-      const int64_t t = a.ts[i];
-      bad |= i > 0 && a.ts[i - 1] > t;
-      rec[j] = KRec<4>::make(k, (uint32_t)(t - f), a.val, i);
-      bk[j] = (int32_t)bucket_of(k, a.kmask);
-      rk[j] = atomicAdd(&cnt[bk[j]], 1);
-    }
-  }
+  const bool bad = tile_records<4, IT, ST, NBS>(a, i0, tid, f, cnt, rec, bk, rk);
   if (__ballot(bad) && lane == 0) atomicOr(&a.ctl->flag, KG_UNSORTED);
   __syncthreads();
   int32_t loc[PER], sacc = 0;
@@ -341,7 +354,7 @@ __global__ __launch_bounds__(ST) void kg_scatter2_kernel(KgArgs a) {
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < IT; j++)
-    if (bk[j] >= 0) rec[j].store_lds(stage, cnt[bk[j]] + rk[j]);
+    if (bk[j] < NBS) rec[j].store_lds(stage, cnt[bk[j]] + rk[j]);
   __syncthreads();
   for (int b = tid; b < a.nbk; b += ST) cnt[b] = a.hist[(int64_t)b * a.ntiles + tile] - cnt[b];
   __syncthreads();
