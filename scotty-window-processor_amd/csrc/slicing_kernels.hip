@@ -159,15 +159,44 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
     a.cix_meta[4] = span_end;
   }
   // thread per cell: cell c owns the buckets whose point first + (k << shift) lies in [start(c), start(c+1));
-  // cells are sorted, so a thread stops at its first cell starting at or beyond span_end
+  // cells are sorted, so the block stops at its first cell starting at or beyond span_end.  A cell owning more
+  // than CIX_RUN buckets (cells of seconds at one bucket per ms) is queued in LDS and written by the whole block,
+  // not by its one thread bucket after bucket.
+  constexpr int CIX_RUN = 16;
+  __shared__ int64_t l_k0[256], l_k1[256];
+  __shared__ uint32_t l_c[256];
+  __shared__ int l_n;
   const uint64_t round = ((uint64_t)1 << shift) - 1;
-  for (int64_t c = g; c < ctot; c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t sc0 = cv.start(c);
-    if (c > 0 && sc0 >= span_end) break;
-    const int64_t sc1 = c + 1 < ctot ? cv.start(c + 1) : INT64_MAX;
-    const int64_t k0 = c == 0 ? 0 : (int64_t)(((uint64_t)(sc0 - first) + round) >> shift);
-    const int64_t k1 = sc1 >= span_end ? n : min(n, (int64_t)(((uint64_t)(sc1 - first) + round) >> shift));
-    for (int64_t k = k0; k < k1; k++) a.cix[k] = (uint32_t)c;
+  for (int64_t cb = (int64_t)blockIdx.x * blockDim.x; cb < ctot; cb += (int64_t)gridDim.x * blockDim.x) {
+    if (threadIdx.x == 0) l_n = 0;
+    __syncthreads();
+    const int64_t c = cb + threadIdx.x;
+    bool done = c >= ctot;
+    if (!done) {
+      const int64_t sc0 = cv.start(c);
+      if (c > 0 && sc0 >= span_end) {
+        done = true;
+      } else {
+        const int64_t sc1 = c + 1 < ctot ? cv.start(c + 1) : INT64_MAX;
+        const int64_t k0 = c == 0 ? 0 : (int64_t)(((uint64_t)(sc0 - first) + round) >> shift);
+        const int64_t k1 = sc1 >= span_end ? n : min(n, (int64_t)(((uint64_t)(sc1 - first) + round) >> shift));
+        if (k1 - k0 > CIX_RUN) {
+          const int i = atomicAdd(&l_n, 1);
+          l_k0[i] = k0;
+          l_k1[i] = k1;
+          l_c[i] = (uint32_t)c;
+        } else {
+          for (int64_t k = k0; k < k1; k++) a.cix[k] = (uint32_t)c;
+        }
+      }
+    }
+    __syncthreads();
+    const int nl = l_n;
+    for (int i = 0; i < nl; i++) {
+      const uint32_t cc = l_c[i];
+      for (int64_t k = l_k0[i] + threadIdx.x; k < l_k1[i]; k += blockDim.x) a.cix[k] = cc;
+    }
+    if (__syncthreads_or(done)) break;
   }
 }
 
