@@ -308,6 +308,109 @@ __global__ void scan_add_kernel(T* out, int64_t n, const T* block_off) {
   if (i < n) out[i] += block_off[blockIdx.x];
 }
 
+// Large int32 scans: reduce-then-scan over 4096-element tiles (a wavefront owns 1024 contiguous elements as 4 rows
+// of 64 lanes x int4, so every load and store instruction is a contiguous 1 KB).  Two passes over the data --
+// read (tile sums), read + write (scan) -- instead of the one-element-per-thread block scan plus a separate add
+// pass over the whole array.
+constexpr int SC_T = 256, SC_TILE = 4096;
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+__device__ __forceinline__ void tile_load(const int32_t* in, int64_t n, int64_t w0, int lane, bool full,
+                                          int4 (&v)[4]) {
+  if (full) {
+    const int4* p = (const int4*)(in + w0);
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = p[q * 64 + lane];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t e = w0 + (int64_t)(q * 64 + lane) * 4;
+      v[q] = make_int4(e < n ? in[e] : 0, e + 1 < n ? in[e + 1] : 0, e + 2 < n ? in[e + 2] : 0,
+                       e + 3 < n ? in[e + 3] : 0);
+    }
+  }
+}
+__global__ __launch_bounds__(SC_T) void scan_reduce_i32_kernel(const int32_t* in, int64_t n, int32_t* sums) {
+  __shared__ int32_t ws[SC_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * SC_TILE;
+  int4 v[4];
+  tile_load(in, n, b0 + wid * 1024, lane, b0 + SC_TILE <= n, v);
+  int32_t s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) s += v[q].x + v[q].y + v[q].z + v[q].w;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) ws[wid] = s;
+  __syncthreads();
+  if (tid == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(SC_T) void scan_apply_i32_kernel(const int32_t* in, int32_t* out, int64_t n,
+                                                              const int32_t* tile_off) {
+  __shared__ int32_t ws[SC_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * SC_TILE, w0 = b0 + wid * 1024;
+  const bool full = b0 + SC_TILE <= n;
+  int4 v[4];
+  tile_load(in, n, w0, lane, full, v);
+  int32_t ex[4], carry = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int32_t c = v[q].x + v[q].y + v[q].z + v[q].w;
+    const int32_t inc = wave_incl_scan(c, lane);
+    ex[q] = carry + inc - c;
+    carry += __shfl(inc, 63);
+  }
+  if (lane == 0) ws[wid] = carry;
+  __syncthreads();
+  int32_t base = tile_off[blockIdx.x];
+  for (int w = 0; w < wid; w++) base += ws[w];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    int4 o;
+    o.x = base + ex[q];
+    o.y = o.x + v[q].x;
+    o.z = o.y + v[q].y;
+    o.w = o.z + v[q].z;
+    const int64_t e = w0 + (int64_t)(q * 64 + lane) * 4;
+    if (full) {
+      ((int4*)out)[e >> 2] = o;
+    } else {
+      if (e < n) out[e] = o.x;
+      if (e + 1 < n) out[e + 1] = o.y;
+      if (e + 2 < n) out[e + 2] = o.z;
+      if (e + 3 < n) out[e + 3] = o.w;
+    }
+  }
+}
+
+// The tile sums (<= 64 Ki of them): one workgroup, a contiguous run per thread -- one launch instead of the
+// block scan's three.
+constexpr int SS_T = 1024, SS_MAX = 65536;
+__global__ __launch_bounds__(SS_T) void scan_small_i32_kernel(int32_t* a, int n) {
+  __shared__ int32_t ws[SS_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int per = (n + SS_T - 1) / SS_T, i0 = tid * per, i1 = min(n, i0 + per);
+  int32_t s = 0;
+  for (int i = i0; i < i1; i++) s += a[i];
+  const int32_t inc = wave_incl_scan(s, lane);
+  if (lane == 63) ws[wid] = inc;
+  __syncthreads();
+  int32_t run = inc - s;
+  for (int w = 0; w < wid; w++) run += ws[w];
+  for (int i = i0; i < i1; i++) {
+    const int32_t v = a[i];
+    a[i] = run;
+    run += v;
+  }
+}
+
 }  // namespace k
 
 // ---------------------------------------------------------------- host wrappers
@@ -330,7 +433,17 @@ hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* 
   return scan_rec<int64_t>(in, out, n, tmp, st);
 }
 hipError_t launch_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t st) {
-  return scan_rec<int32_t>(in, out, n, tmp, st);
+  if (n < ((int64_t)1 << 20) || (((uintptr_t)in | (uintptr_t)out) & 15)) return scan_rec<int32_t>(in, out, n, tmp, st);
+  const int64_t nb = (n + k::SC_TILE - 1) / k::SC_TILE;  // tmp: nb tile sums + the recursion's (< 2 nb / 1024 more)
+  hipLaunchKernelGGL(k::scan_reduce_i32_kernel, dim3((unsigned)nb), dim3(k::SC_T), 0, st, in, n, tmp);
+  if (nb <= k::SS_MAX) {
+    hipLaunchKernelGGL(k::scan_small_i32_kernel, dim3(1), dim3(k::SS_T), 0, st, tmp, (int)nb);
+  } else {
+    const hipError_t e = scan_rec<int32_t>(tmp, tmp, nb, tmp + nb, st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k::scan_apply_i32_kernel, dim3((unsigned)nb), dim3(k::SC_T), 0, st, in, out, n, tmp);
+  return hipGetLastError();
 }
 
 static unsigned grid_for(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
