@@ -4,6 +4,7 @@
 // reference's WindowManager registration (S/WindowManager.java:121-151).
 #include "exact_batch.h"
 #include "exact_engine.h"
+#include "exact_quiet.h"
 #include "host_copy.h"
 #include "keyed_grid.h"
 
@@ -12,6 +13,7 @@
 #include <cmath>
 #include <cstddef>
 #include <cstring>
+#include <queue>
 
 namespace scotty {
 hipError_t launch_replay(const XBatchArgs& a, int vt, hipStream_t st);
@@ -49,6 +51,9 @@ int kg_cells(bool mm);
 hipError_t launch_kg_bounds(const int64_t* ts, int64_t n, const XCfg* cfg, int kmax, int64_t* gpts, int64_t* out,
                             hipStream_t st);
 hipError_t launch_kg_dcount(const uint8_t* mark, int64_t n, int32_t* blk, hipStream_t st);
+hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
+hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
+hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
 hipError_t launch_kg_dgather(const uint32_t* key, const int64_t* ts, const void* val, uint8_t* mark, int64_t n,
                              const int32_t* blk_off, uint32_t* okey, int64_t* ots, void* oval, int vt,
                              hipStream_t st);
@@ -113,6 +118,13 @@ void XEngine::release() {
   dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
   dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
   dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
+  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_rank); dfree(d_xq_flag);
+  for (int k = 0; k < NPART; k++) dfree(d_xq_cpart[k]);
+  dfree(d_xq_eg); dfree(d_xq_epos); dfree(d_xq_meta); dfree(d_xq_cix); dfree(d_xq_cixmeta); dfree(d_xq_ctl);
+  for (auto& e : ev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  ev_pending.clear();
+  ev_pool.clear();
   dfree(d_kgtab); dfree(d_kghist); dfree(d_kgscan); dfree(d_kgblk); dfree(d_kgrec); dfree(d_kgmark); dfree(d_kgctl);
   dfree(d_kgkey); dfree(d_kgts); dfree(d_kgval); dfree(d_kggpts); dfree(d_kgpos); dfree(d_kgpart); dfree(d_kgdflag);
   if (h_kgctl) (void)hipHostFree(h_kgctl);
@@ -239,6 +251,7 @@ int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>&
   c.cf_a = d_cf_a;
   c.cf_b = d_cf_b;
   cfg = c;
+  xq_need_grid = true;  // the union edge grid follows the registered windows
   XCHK(hipMemcpyAsync(d_cfg, &cfg, sizeof(XCfg), hipMemcpyHostToDevice, stream));
   if (nctx > ctx_alloc) {  // session windows registered (possibly mid-stream): widen the per-op session table
     int rc = grow_caps(sc, sesscap, nctx);
@@ -496,6 +509,27 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
   int64_t pos0 = 0;
   last_events = 0;
   last_segments = 0;
+  last_quiet = 0;
+  if (n > 0 && quiet_eligible()) {
+    int32_t res = XQ_NONE;
+    int rc = push_quiet(d_ts, d_val, n, &res);
+    if (rc) return rc;
+    last_quiet = res;
+    if (res == XQ_COMMITTED) {
+      quiet_commits++;
+      return SCOTTY_OK;
+    }
+    quiet_fallbacks++;
+  }
+  TEv tx;
+  int rct = tbegin(tx, SCOTTY_TIME_PUSH_OTHER);
+  if (rct) return rct;
+  struct TEnd {  // the event-exact path's device time (class PUSH_OTHER), also on early returns
+    XEngine* e;
+    TEv* t;
+    int64_t n;
+    ~TEnd() { (void)e->tend(*t, n); }
+  } tend_guard{this, &tx, n};
   for (int64_t round = 0; pos0 < n; round++) {
     int64_t stop = -1;
     int rc = push_round(d_ts + pos0, (const unsigned char*)d_val + pos0 * vb, n - pos0, round > 0, &stop);
@@ -514,6 +548,243 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
       return SCOTTY_ERR_STATE;
     }
   }
+  return SCOTTY_OK;
+}
+
+
+// ---------------------------------------------------------------- one-pass quiet path (exact_quiet.hip)
+// Eligible configurations: non-keyed, time measure, Eager slices (no count windows, maxLateness > 0), and partials the
+// grid ingest computes bit-identically (an int32 stream's sums wrap mod 2^32 there: SUM_I32 only).
+bool XEngine::quiet_eligible() const {
+  if (keyed || quiet_off || use_serial() || cfg.lazy || cfg.has_count || !cfg.has_time) return false;
+  for (int i = 0; i < cfg.n_aggs; i++) {
+    const int k = cfg.agg_kind[i] & 0xFFFF;
+    if (vt == VT_I32 && (k == SCOTTY_AGG_SUM_I64 || k == SCOTTY_AGG_SUM_F64)) return false;
+  }
+  return true;
+}
+
+int XEngine::tbegin(TEv& e, int cls) {
+  e.cls = cls;
+  e.a = e.b = nullptr;
+  if (!timing) return SCOTTY_OK;
+  if (!ev_pool.empty()) {
+    e.a = ev_pool.back().a;
+    e.b = ev_pool.back().b;
+    ev_pool.pop_back();
+  } else {
+    XCHK(hipEventCreate(&e.a));
+    XCHK(hipEventCreate(&e.b));
+  }
+  XCHK(hipEventRecord(e.a, stream));
+  return SCOTTY_OK;
+}
+int XEngine::tend(TEv& e, int64_t n) {
+  if (!timing || !e.a) return SCOTTY_OK;
+  XCHK(hipEventRecord(e.b, stream));
+  e.n = n;
+  ev_pending.push_back(e);
+  e.a = nullptr;
+  return SCOTTY_OK;
+}
+// after a synchronisation: completed intervals into their classes
+int XEngine::collect_timing() {
+  std::vector<TEv> keep;
+  for (auto& e : ev_pending) {
+    if (hipEventQuery(e.b) == hipErrorNotReady) {
+      keep.push_back(e);
+      continue;
+    }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess && e.cls >= 0 && e.cls < 4) {
+      t_ms[e.cls] += ms;
+      t_cnt[e.cls]++;
+      if (e.cls == SCOTTY_TIME_INGEST) t_tuples += e.n;
+    }
+    ev_pool.push_back(e);
+  }
+  ev_pending.swap(keep);
+  return SCOTTY_OK;
+}
+
+// Union edge grid of the context-free time windows from the pending edge N (first entry) up to a horizon: the
+// points nextGrid visits (S/StreamSlicer.java:103-116; TumblingWindow.java:29-31, SlidingWindow.java:41-43,
+// FixedBandWindow.java:37-48), a k-way merge of arithmetic progressions.  Built on the host at synchronisation
+// points only (the first push, a stale grid, a horizon running short).
+int XEngine::xq_rebuild_grid() {
+  XState s{};
+  XCHK(hipMemcpyAsync(&s, d_st, sizeof(XState), hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  xq_hgrid.clear();
+  if (!cfg.has_fixed) {
+    xq_need_grid = false;
+    return SCOTTY_OK;
+  }
+  const int64_t N = s.nextEdgeTs;
+  if (N < 0 || !s.started) return SCOTTY_OK;  // not yet: the event-exact path runs, the grid is built later
+  if (xq_gcap == 0) xq_gcap = 1 << 20;
+  auto next_start = [](const XWinDef& w, int64_t t) -> int64_t {
+    auto jadd_ = [](int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); };
+    if (w.kind == SCOTTY_WIN_TUMBLING) return jadd_(t, w.a) - (w.a == -1 ? 0 : t % w.a);
+    if (w.kind == SCOTTY_WIN_SLIDING) return jadd_(t, w.b) - (w.b == -1 ? 0 : t % w.b);
+    if (t == INT64_MAX || t < w.a) return w.a;
+    if (t >= w.a && t < jadd_(w.a, w.b)) return jadd_(w.a, w.b);
+    return INT64_MAX;
+  };
+  const int64_t span = std::max<int64_t>(xq_span, 1);
+  const int64_t front = std::max<int64_t>(s.maxEventTime, 0);
+  const int64_t horizon = front > INT64_MAX / 2 ? INT64_MAX : front + std::max<int64_t>(64 * span, 600000);
+  xq_hgrid.push_back(N);
+  using Item = std::pair<int64_t, int>;
+  std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+  bool infinite = false;
+  for (int i = 0; i < (int)h_wins.size(); i++) {
+    const XWinDef& w = h_wins[i];
+    if (w.kind == SCOTTY_WIN_SESSION || w.measure != SCOTTY_MEASURE_TIME) continue;
+    if (w.kind == SCOTTY_WIN_FIXED_BAND) {
+      if (w.a > N) pq.push({w.a, -1});
+      const int64_t e = (int64_t)((uint64_t)w.a + (uint64_t)w.b);
+      if (e > N) pq.push({e, -1});
+    } else {
+      infinite = true;
+      pq.push({next_start(w, N), i});
+    }
+  }
+  while (!pq.empty() && (int64_t)xq_hgrid.size() < xq_gcap - 1) {
+    const Item it = pq.top();
+    pq.pop();
+    if (it.first > xq_hgrid.back()) {
+      if (it.first > horizon && infinite) break;
+      xq_hgrid.push_back(it.first);
+    }
+    if (it.second >= 0) {
+      const int64_t nx = next_start(h_wins[it.second], it.first);
+      if (nx > it.first) pq.push({nx, it.second});
+    }
+  }
+  if (!infinite && pq.empty()) xq_hgrid.push_back(INT64_MAX);
+  if (!d_xq_grid) XCHK(dalloc(&d_xq_grid, xq_gcap));
+  XCHK(hipMemcpyAsync(d_xq_grid, xq_hgrid.data(), xq_hgrid.size() * 8, hipMemcpyHostToDevice, stream));
+  XCHK(hipStreamSynchronize(stream));
+  xq_need_grid = false;
+  return SCOTTY_OK;
+}
+
+int XEngine::xq_ensure(int64_t n) {
+  if (xq_gcap == 0) xq_gcap = 1 << 20;
+  if (!d_xq_meta) {
+    XCHK(dalloc((unsigned char**)&d_xq_meta, sizeof(DevMeta)));
+    XCHK(dalloc((unsigned char**)&d_xq_ctl, sizeof(XQCtl)));
+    XCHK(dalloc(&d_xq_cix, CIX_CAP));
+    XCHK(dalloc(&d_xq_cixmeta, 8));
+    XCHK(dalloc(&d_xq_rank, xq_gcap));
+    XCHK(dalloc(&d_xq_flag, xq_gcap));
+    XCHK(dalloc(&d_xq_eg, xq_gcap));
+    XCHK(dalloc(&d_xq_epos, 2 * xq_gcap));
+    if (!d_xq_grid) XCHK(dalloc(&d_xq_grid, xq_gcap));
+  }
+  if (xq_ccap < (int64_t)sc + xq_gcap) {  // cells: retained slices ++ grid cells, identity between batches
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_xq_ccnt); dfree(d_xq_ctmax);
+    for (int k = 0; k < NPART; k++) dfree(d_xq_cpart[k]);
+    xq_ccap = (int64_t)sc + xq_gcap;
+    XCHK(dalloc(&d_xq_ccnt, xq_ccap));
+    XCHK(dalloc(&d_xq_ctmax, xq_ccap));
+    for (int k = 0; k < NPART; k++) XCHK(dalloc(&d_xq_cpart[k], xq_ccap));
+    XCHK(launch_fill_u64(d_xq_ccnt, xq_ccap, 0, stream));
+    XCHK(launch_fill_u64((unsigned long long*)d_xq_ctmax, xq_ccap, (unsigned long long)INT64_MIN, stream));
+    XCHK(launch_fill_u64(d_xq_cpart[0], xq_ccap, 0, stream));
+    XCHK(launch_fill_u64(d_xq_cpart[1], xq_ccap, (unsigned long long)INT64_MAX, stream));
+    XCHK(launch_fill_u64(d_xq_cpart[2], xq_ccap, (unsigned long long)INT64_MIN, stream));
+  }
+  const int64_t nt = (n + TILE_MIN - 1) / TILE_MIN + 1;
+  if (nt > xq_tcap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_xq_tilemax);
+    xq_tcap = std::max<int64_t>(nt, 1024);
+    XCHK(dalloc(&d_xq_tilemax, xq_tcap));
+  }
+  return SCOTTY_OK;
+}
+
+// One HBM pass over the batch (grid ingest into cells), then the quiet verdict and commit on the device; one host
+// synchronisation reads the verdict.  Nothing of the operator changes unless *result == XQ_COMMITTED.
+int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32_t* result) {
+  *result = XQ_NONE;
+  if (xq_need_grid) {
+    int rc = xq_rebuild_grid();
+    if (rc) return rc;
+    if (xq_need_grid) {  // the stream has not reached a pending edge yet
+      *result = XQ_GRID;
+      return SCOTTY_OK;
+    }
+  }
+  int rc = xq_ensure(n);
+  if (rc) return rc;
+  int64_t tile = TILE_MIN;
+  while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
+  const int64_t target_blocks = 1024;  // ~4 workgroups per CU, a tile-aligned contiguous range per wave
+  int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
+  per_wave = std::max(((per_wave + tile - 1) / tile) * tile, tile);
+  const int64_t nblocks = (n + per_wave * 4 - 1) / (per_wave * 4);
+  IngestArgs ia{};
+  ia.ts = d_ts;
+  ia.val = d_val;
+  ia.n = n;
+  ia.s_tstart = sl.ts;  // op 0
+  ia.grid = d_xq_grid;
+  ia.c_cnt = d_xq_ccnt;
+  ia.c_tmax = d_xq_ctmax;
+  for (int k = 0; k < NPART; k++) ia.c_part[k] = d_xq_cpart[k];
+  ia.tilemax = d_xq_tilemax;
+  ia.meta = d_xq_meta;
+  ia.per_wave = per_wave;
+  ia.tile = tile;
+  ia.cix = d_xq_cix;
+  ia.cix_meta = d_xq_cixmeta;
+  ia.cix_margin = std::max<int64_t>(4 * xq_span, 4000);
+  XQArgs q{};
+  q.ts = d_ts;
+  q.n = n;
+  q.tile = tile;
+  q.cfg = d_cfg;
+  q.st = d_st;
+  q.sl = sl;
+  q.ss = ss;
+  q.grid = d_xq_grid;
+  q.gcount = (int64_t)xq_hgrid.size();
+  q.meta = d_xq_meta;
+  q.c_cnt = d_xq_ccnt;
+  q.c_tmax = d_xq_ctmax;
+  for (int k = 0; k < NPART; k++) q.c_part[k] = d_xq_cpart[k];
+  q.tilemax = d_xq_tilemax;
+  q.rank = d_xq_rank;
+  q.flag = d_xq_flag;
+  q.eg = d_xq_eg;
+  q.epos = d_xq_epos;
+  q.ctl = (XQCtl*)d_xq_ctl;
+  q.margin = std::max<int64_t>(16 * xq_span, 60000);
+  TEv t0, t1, t2;
+  if ((rc = tbegin(t0, SCOTTY_TIME_PUSH_OTHER))) return rc;
+  XCHK(launch_xq_prep(q, stream));
+  XCHK(launch_cix_build(ia, stream));
+  if ((rc = tend(t0, 0))) return rc;
+  if ((rc = tbegin(t1, SCOTTY_TIME_INGEST))) return rc;
+  XCHK(launch_ingest(ia, vt, cfg.need, nblocks, stream, -1));
+  if ((rc = tend(t1, n))) return rc;
+  if ((rc = tbegin(t2, SCOTTY_TIME_PUSH_OTHER))) return rc;
+  XCHK(launch_xq_commit(q, stream));
+  static_assert(sizeof(XQCtl) <= 16 * sizeof(int64_t), "XQCtl fits the mapped control block");
+  XCHK(launch_copy_to_host(d_xq_ctl, h_misc_dev, sizeof(XQCtl), stream));
+  if ((rc = tend(t2, 0))) return rc;
+  XCHK(hipStreamSynchronize(stream));
+  XQCtl c;
+  std::memcpy(&c, h_misc, sizeof(XQCtl));
+  *result = c.result;
+  last_quiet_why = c.why;
+  if (c.result == XQ_COMMITTED && c.batch_max > c.p_start) xq_span = std::max<int64_t>(c.batch_max - c.p_start, 1);
+  if (c.result == XQ_GRID || (c.result == XQ_COMMITTED && c.rebuild)) xq_need_grid = true;
+  if (timing) collect_timing();
   return SCOTTY_OK;
 }
 
@@ -1014,12 +1285,16 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     }
     return finish_rows((int64_t)h_misc[3], r, to_host, false);
   }
+  TEv tw1;
+  int rct = tbegin(tw1, SCOTTY_TIME_WATERMARK);
+  if (rct) return rct;
   XCHK(hipMemsetAsync(d_misc, 0, 3 * 8, stream));
   XCHK(lane_mode() ? launch_lane_wm_count(a, stream) : launch_wm_count(a, stream));
   XCHK(launch_scan_i64(d_wcount, d_woff, n_ops, d_scan64, stream));
   XCHK(launch_copy_to_host(d_misc, h_misc_dev, 3 * 8, stream));
   XCHK(launch_copy_to_host(d_woff + n_ops - 1, h_misc_dev + 3, 8, stream));
   XCHK(launch_copy_to_host(d_wcount + n_ops - 1, h_misc_dev + 4, 8, stream));
+  if ((rct = tend(tw1, 0))) return rct;
   XCHK(hipStreamSynchronize(stream));
   r.dropped = (uint64_t)h_misc[1];
   int rc = op_error((int32_t)h_misc[2]);
@@ -1040,6 +1315,8 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
   a.w_key = d_w_key;
   a.n_rows = rows;
+  TEv tw2;
+  if ((rct = tbegin(tw2, SCOTTY_TIME_WATERMARK))) return rct;
   if (lane_mode()) {
     XCHK(launch_lane_wm_emit(a, prefix_agg, stream));
     if (prefix_agg) prefix_stale = false;
@@ -1047,9 +1324,12 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     XCHK(launch_wm_emit(a, stream));
   }
   if (!prefix_agg) XCHK(launch_wm_agg(a, stream, keyed ? 16 : 64));
+  if ((rct = tend(tw2, 0))) return rct;
   have_wm = true;
   last_wm = wm;
-  return finish_rows(rows, r, to_host, true);
+  rc = finish_rows(rows, r, to_host, true);
+  if (timing) collect_timing();
+  return rc;
 }
 
 // Fatal per-operator errors recorded by the kernels (OR of 1 << XState.err over the ops).
@@ -1103,6 +1383,9 @@ int XEngine::finish_rows(int64_t rows, XResult& r, bool to_host, bool check) {
   r.d_key = d_w_key;
   r.d_has = d_has;
   for (int k = 0; k < cfg.n_aggs; k++) r.d_vals[k] = d_vals[k];
+  TEv tc;
+  int rct = tbegin(tc, SCOTTY_TIME_RESULT_COPY);
+  if (rct) return rct;
   if (to_host && rows > 0) {
     r.start.resize(rows); r.end.resize(rows); r.meas.resize(rows); r.has.resize(rows); r.key.resize(rows);
     r.vals.assign(cfg.n_aggs, std::vector<int64_t>(rows));
@@ -1114,6 +1397,7 @@ int XEngine::finish_rows(int64_t rows, XResult& r, bool to_host, bool check) {
     for (int k = 0; k < cfg.n_aggs; k++)
       XCHK(hipMemcpyAsync(r.vals[k].data(), d_vals[k], rows * 8, hipMemcpyDeviceToHost, stream));
   }
+  if ((rct = tend(tc, 0))) return rct;
   if (!check) {
     if (to_host && rows > 0) XCHK(hipStreamSynchronize(stream));
     return SCOTTY_OK;

@@ -43,6 +43,25 @@ class XEngine {
   int push(const int64_t* d_ts, const void* d_val, int64_t n);
   int push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n);
   int push_batch(const int64_t* d_ts, const void* d_val, int64_t n);  // non-keyed, batch-parallel
+  // non-keyed one-pass path (exact_quiet.hip): *result = XQ_COMMITTED, or why the batch needs the event-exact path
+  int push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32_t* result);
+  bool quiet_eligible() const;
+  bool quiet_off = false;      // A/B: every non-keyed batch through the event-exact path
+  int64_t quiet_commits = 0, quiet_fallbacks = 0;
+  int32_t last_quiet = 0;      // XQ_* verdict of the last non-keyed push (0: not attempted)
+  int64_t last_quiet_why = 0;  // XQCtl.why of the last verdict
+  // device time of the last pushes by class (HIP events; scotty_device_timing): 0 quiet ingest, 1 other push work
+  bool timing = false;
+  struct TEv {
+    hipEvent_t a = nullptr, b = nullptr;
+    int cls = 0;
+    int64_t n = 0;
+  };
+  std::vector<TEv> ev_pending, ev_pool;
+  double t_ms[4] = {0, 0, 0, 0};
+  int64_t t_cnt[4] = {0, 0, 0, 0};
+  int64_t t_tuples = 0;
+  int collect_timing();
   int push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool resume, int64_t* stop_at);
   int64_t last_events = 0, last_segments = 0;                          // statistics of the last push
   int watermark(int64_t wm, XResult& r, bool to_host);
@@ -176,6 +195,26 @@ class XEngine {
   int32_t* xb_eptail = nullptr;
   int64_t* xb_sufmin = nullptr;
   int64_t xb_sufcap = 0;
+  // one-pass quiet path (exact_quiet.hip): union edge grid, per-batch cells, ingest view of the store
+  int xq_rebuild_grid();
+  int xq_ensure(int64_t n);
+  int tbegin(TEv& e, int cls);
+  int tend(TEv& e, int64_t n);
+  std::vector<int64_t> xq_hgrid;
+  int64_t xq_gcap = 0, xq_ccap = 0, xq_tcap = 0;
+  int64_t* d_xq_grid = nullptr;
+  unsigned long long* d_xq_ccnt = nullptr;
+  long long* d_xq_ctmax = nullptr;
+  unsigned long long* d_xq_cpart[NPART] = {};
+  long long* d_xq_tilemax = nullptr;
+  int32_t *d_xq_rank = nullptr, *d_xq_flag = nullptr;
+  int64_t *d_xq_eg = nullptr, *d_xq_epos = nullptr;
+  DevMeta* d_xq_meta = nullptr;
+  uint32_t* d_xq_cix = nullptr;
+  int64_t* d_xq_cixmeta = nullptr;
+  void* d_xq_ctl = nullptr;
+  int64_t xq_span = 1000;       // event-time span of the last committed batch (grid horizon and cell-index sizing)
+  bool xq_need_grid = true;     // (re)build the grid from the pending edge at the next push
 };
 
 }  // namespace scotty

@@ -153,6 +153,7 @@ struct scotty_op {
   CEngine* c = nullptr;  // mode 3: count-window path (count_engine.h)
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
+  bool x_quiet_off = false;  // exact engine: no one-pass quiet path (A/B)
   bool x_lane_off = false;
   bool x_kg_off = false;
   int64_t x_kg_chunk = -1;
@@ -914,6 +915,7 @@ static int decide_mode(scotty_op* op) {
   op->x->sc_override = op->x_sc;
   op->x->sess_override = op->x_sess;
   op->x->serial = op->x_serial;
+  op->x->quiet_off = op->x_quiet_off;
   op->x->lane_off = op->x_lane_off;
   op->x->kg_off = op->x_kg_off;
   if (op->x_kg_chunk >= 0) op->x->kg_min_chunk = op->x_kg_chunk;
@@ -1394,6 +1396,14 @@ int64_t scotty_slice_count(scotty_op* op) {
 int scotty_enable_timing(scotty_op* op, int on) {
   if (!op) return SCOTTY_ERR_ARG;
   op->timing = on != 0;
+  if (op->x) {  // exact engine: its own HIP-event classes (quiet ingest, other push work, watermark, result copy)
+    op->x->timing = on != 0;
+    for (int k = 0; k < 4; k++) {
+      op->x->t_ms[k] = 0.0;
+      op->x->t_cnt[k] = 0;
+    }
+    op->x->t_tuples = 0;
+  }
   op->t_ms = 0.0;
   op->t_launches = 0;
   op->t_tuples = 0;
@@ -1406,6 +1416,12 @@ int scotty_enable_timing(scotty_op* op, int on) {
 
 int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* intervals) {
   if (!op || cls < 0 || cls >= NTCLS) return SCOTTY_ERR_ARG;
+  if (op->mode == 2 && op->x) {
+    (void)op->x->collect_timing();
+    if (total_ms) *total_ms = op->x->t_ms[cls];
+    if (intervals) *intervals = op->x->t_cnt[cls];
+    return SCOTTY_OK;
+  }
   if (total_ms) *total_ms = op->t_cls_ms[cls];
   if (intervals) *intervals = op->t_cls_n[cls];
   return SCOTTY_OK;
@@ -1439,6 +1455,11 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   if (std::strcmp(key, "exact_serial") == 0) {
     if (op->mode != 0) return SCOTTY_ERR_ARG;
     op->x_serial = value != 0;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "exact_quiet") == 0) {  // 0: non-keyed exact batches skip the one-pass quiet path (A/B)
+    op->x_quiet_off = value == 0;
+    if (op->x) op->x->quiet_off = op->x_quiet_off;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "shard_count_cells") == 0) {  // cells per rank record of the count path's exchange
@@ -1522,6 +1543,10 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 2: return op->x->last_kg;
     case 3: return op->x->last_kg_deferred;
     case 4: return op->x->last_kg_keys;
+    case 8: return op->x->last_quiet;       // XQ_* verdict of the last non-keyed push (exact_quiet.h)
+    case 9: return op->x->quiet_commits;
+    case 10: return op->x->quiet_fallbacks;
+    case 11: return op->x->last_quiet_why;
     default: return -1;
   }
 }

@@ -199,6 +199,97 @@ def test_batch_parallel_path_equals_serial_replay(pkg, seed):
             assert ops[0].droppedCount() == ops[1].droppedCount()
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_quiet_path_equals_event_exact_path_and_replay(pkg, seed):
+    """The one-pass quiet path (exact_quiet.hip: grid ingest into cells + device verdict) must leave exactly the
+    windows of the event-exact batch path (exact_batch.hip) and of the single-wavefront replay, on session streams
+    whose pauses and out-of-order tuples make some batches quiet and others not; both verdicts must occur."""
+    rng = np.random.default_rng(8800 + seed)
+    vt = ["i32", "i32", "i64", "f64"][seed % 4]
+    cfg = _session_cfg(rng, vt)
+    n = 300_000
+    gaps = _gaps(rng, n, int(rng.integers(20_000, 80_000)), 100, 3000)
+    ts, vals = product().workloads.stream(n, [2, 10, 40][seed % 3], t0=500, ooo_frac=[0.05, 0.2][seed % 2],
+                                          max_delay=int(rng.integers(10, 600)), seed=seed, value_type=vt, gaps=gaps)
+    vtc = {"i32": pkg.VALUE_I32, "i64": pkg.VALUE_I64, "f64": pkg.VALUE_F64}[vt]
+    ops = []
+    for knob, val in (("exact_quiet", 1), ("exact_quiet", 0), ("exact_serial", 1)):
+        op = pkg.SlicingWindowOperator(device=0, value_type=vtc)
+        op.tune(knob, val)
+        for a in cfg["aggs"]:
+            op.addWindowFunction(a)
+        op.setMaxLateness(cfg["lateness"])
+        for w in cfg["windows"]:
+            op.addWindowAssigner(w)
+        ops.append(op)
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
+    sched = interval_schedule(ts, 12, lag=300, pushes_per_interval=3)
+    from helpers import same_windows
+    quiet, event, why = 0, 0, []
+    for step in sched:
+        if step[0] == "push":
+            for op in ops:
+                op.processElements(ts[step[1]:step[2]], vals[step[1]:step[2]])
+            v = ops[0]._debug_stat(8)
+            quiet += v == 1
+            event += v > 1
+            why.append((v, ops[0]._debug_stat(11)))
+        else:
+            a, b, c = (op.processWatermark(step[1]) for op in ops)
+            same_windows(a, b, f64_cols=f64_cols)
+            same_windows(a, c, f64_cols=f64_cols)
+            assert ops[0].droppedCount() == ops[2].droppedCount()
+    assert quiet > 0, ("no batch took the quiet path", cfg, why)
+    assert event > 0, ("no batch needed the event-exact path", why)
+
+
+def test_config3_full_size_quiet_path_equals_replay(pkg):
+    """BASELINE configs[2] (C3) at the benchmark's batch size class: SlidingWindow(60 s, 60 ms) + SessionWindow(1 s),
+    MIN/MAX, 20 % out-of-order by U[1,500] ms, a 1.5 s pause every 4th step, 2^24 tuples per step, generated on the
+    device like bench.py's C3 leg.  Quiet path (default) == event-exact batch path == single-wavefront replay, window
+    by window, every step; the pause steps go through the event-exact path, the others commit in one pass."""
+    import torch
+    dev = torch.device("cuda", 0)
+    batch = 1 << 24
+    rate = batch // 1000
+    g = torch.Generator(device=dev)
+    g.manual_seed(17)
+    ops = []
+    for knob, val in (("exact_quiet", 1), ("exact_quiet", 0), ("exact_serial", 1)):
+        op = pkg.SlicingWindowOperator(device=0)
+        op.tune(knob, val)
+        op.addWindowFunction(MIN)
+        op.addWindowFunction(MAX)
+        op.addWindowFunction(COUNT)
+        op.setMaxLateness(1000)
+        op.addWindowAssigner(Sliding(Time, 60_000, 60))
+        op.addWindowAssigner(Session(Time, 1000))
+        ops.append(op)
+    from helpers import same_windows
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    quiet, event, rows = 0, 0, 0
+    for s in range(10):
+        t_begin = s * 1000 + 1000 + (s // 4) * 1500
+        ts = base + t_begin
+        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        d = torch.randint(1, 501, (batch,), device=dev, generator=g)
+        ts = torch.where(late, torch.clamp(ts - d, min=t_begin - 500), ts).contiguous()
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        for op in ops:
+            op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        verdict = ops[0]._debug_stat(8)
+        quiet += verdict == 1
+        event += verdict > 1
+        wm = t_begin + (batch - 1) // rate - 500
+        a, b, c = (op.processWatermark(wm) for op in ops)
+        same_windows(a, b)
+        same_windows(a, c)
+        rows += len(a)
+    assert quiet >= 5 and event >= 1, (quiet, event)
+    assert rows > 0
+
+
 def test_session_tumbling_mixed_config3_reduced():
     """BASELINE configs[2] at reduced size: sliding + session, 20 % out-of-order (TimeStampGenerator-like,
     delay U[1,500]), MIN/MAX; session silences every ~10 s of event time."""
