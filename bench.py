@@ -93,6 +93,45 @@ def _cpu_nonkeyed(setup, gen_step, wm_of, steps_range, budget_s, chunk, warm=Non
                       "SlicingWindowOperator, 1 thread" % (done, n_wm, sample)}
 
 
+def host_cores():
+    """Host threads this process may run on (sched_getaffinity) and the cgroup CPU quota, if one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return n, quota
+
+
+C1_PUBLISHED = 1.56e6  # README.md:50-54, benchmark/configurations/sliding_benchmark_Scotty.json:22 (Flink + Scotty)
+
+
+def cpu_c1(rate):
+    """C1 (BASELINE configs[0]) on the oracle, 1 thread: the reference benchmark's sliding 60 s / 1 s SUM over
+    Random(43).nextInt() values, in-order, maxLateness 1; sparse 60 s warm-up (1 tuple/ms) then full-rate steps."""
+    pkg = importlib.import_module("scotty-window-processor_amd")
+    jr = pkg.workloads.JavaRandomInts(43)
+
+    def setup(op):
+        op.addWindowFunction(0)
+        op.setMaxLateness(1)
+        op.addWindowAssigner(1, 0, 60_000, 1_000)
+    warm_ts = np.arange(0, 60_000, dtype=np.int64)
+    warm = [(warm_ts, jr.next_ints(len(warm_ts)).astype(np.int64), 59_999)]
+
+    def gen(s):
+        ts = 60_000 + s * 1000 + np.arange(rate * 1000, dtype=np.int64) // rate
+        return ts, jr.next_ints(len(ts)).astype(np.int64)
+    r = _cpu_nonkeyed(setup, gen, lambda s, lt, partial=False: lt, range(1000), CPU_BUDGET_S, 1 << 22, warm,
+                      "C1 at %d tuples/ms after a 60 s sparse warm-up (1 tuple/ms), Random(43).nextInt() values" % rate)
+    r["published_reference_flink_scotty"] = {"value": C1_PUBLISHED, "unit": "events/s",
+                                             "source": "README.md:50-54 (Flink + Scotty, sliding 60 s / 1 s)"}
+    return r
+
+
 def cpu_c2(sizes, rate):
     def setup(op):
         op.addWindowFunction(0)
@@ -157,12 +196,12 @@ def cpu_c3(rate):
     rng = np.random.default_rng(13)
     warm = []
     for s in range(61):  # sparse warm-up with the same session pauses
-        t_begin = s * 1000 + 1000 + (s // 10) * 1500
+        t_begin = s * 1000 + 1000 + (s // 10) * 2000
         ts = t_begin + np.arange(0, 1000, dtype=np.int64)
         warm.append((ts, np.zeros(len(ts), np.int64), t_begin + 999 - 500 if s % 10 == 9 or s == 60 else None))
 
     def gen(s):
-        t_begin = s * 1000 + 1000 + (s // 10) * 1500
+        t_begin = s * 1000 + 1000 + (s // 10) * 2000
         ts = t_begin + np.arange(rate * 1000, dtype=np.int64) // rate
         late = rng.random(len(ts)) < 0.2
         d = rng.integers(1, 501, size=len(ts))
@@ -170,7 +209,7 @@ def cpu_c3(rate):
         return ts, rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64)
 
     def wm(s, lt, partial=False):
-        return s * 1000 + 1000 + (s // 10) * 1500 + 999 - 500 if not partial else lt - 500
+        return s * 1000 + 1000 + (s // 10) * 2000 + 999 - 500 if not partial else lt - 500
     return _cpu_nonkeyed(setup, gen, wm, range(61, 2000), CPU_BUDGET_S, 1 << 20, warm,
                          "C3 at %d tuples/ms, 20%% late, after a 61 s sparse warm-up with the session pauses" % rate)
 
@@ -239,17 +278,68 @@ def cpu_c4(keys, batch, threads):
         steps += 1
         if t_proc > CPU_BUDGET_S:
             break
+    _, quota = host_cores()
     return {"value": done / t_proc, "unit": "tuples/s", "cores": threads, "kind": "port",
+            "cgroup_cpu_quota": quota,
             "sample": "%d steps of %d tuples (%d uniform keys, 1 s of event time each, one watermark per step) after a "
-                      "60 s sparse warm-up; oracle/ KeyedScottyWindowOperator restatement, %d threads (key %% %d "
-                      "partitions)" % (steps, batch, keys, threads, threads)}
+                      "60 s sparse warm-up; oracle/ KeyedScottyWindowOperator restatement, %d threads = every host "
+                      "thread this process may run on (sched_getaffinity; key %% %d partitions)"
+                      % (steps, batch, keys, threads, threads)}
 
 
 # ----------------------------------------------------------------------------------------------- GPU legs
+def extra_c1(pkg, dev, batch, steps):
+    """BASELINE configs[0] (C1), the reference benchmark's own workload at GPU batch size: SlidingWindow(Time,
+    60000, 1000), SUM_I32 of java.util.Random(43).nextInt() values (restated exactly, generated on the host before
+    the timed region), in-order ts = i // rate, maxLateness 1 (Flink connector default), one key; grid path.  A sparse
+    60 s warm-up (1 tuple/ms, the same Random(43) sequence) so every step emits its window; then `steps` wall-clock
+    steps and as many HIP-event steps (roofline).  Published: Flink + Scotty ~1.56 M events/s (README.md:50-54)."""
+    import torch
+    rate = max(1, batch // 1000)
+    jr = pkg.workloads.JavaRandomInts(43)
+    op = pkg.SlicingWindowOperator(device=dev.index)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.setMaxLateness(1)
+    op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
+    wts = torch.arange(0, 60_000, dtype=torch.int64, device=dev)
+    wv = torch.from_numpy(jr.next_ints(60_000)).to(dev)
+    torch.cuda.synchronize(dev)
+    op.processElementsDevice(wts.data_ptr(), wv.data_ptr(), 60_000)
+    op.processWatermarkRaw(59_999)
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    inputs = []
+    for s in range(2 * steps):
+        inputs.append((base + 60_000 + s * 1000, torch.from_numpy(jr.next_ints(batch)).to(dev)))
+    torch.cuda.synchronize(dev)
+    rows = 0
+    t0 = time.perf_counter()
+    for s in range(steps):
+        ts, v = inputs[s]
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkRaw(60_000 + s * 1000 + (batch - 1) // rate)
+        rows += n
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    op.enableTiming(True)
+    for s in range(steps, 2 * steps):
+        ts, v = inputs[s]
+        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+        op.processWatermarkRaw(60_000 + s * 1000 + (batch - 1) // rate)
+    torch.cuda.synchronize(dev)
+    return {"workload": "C1: SlidingWindow(Time,60000,1000), SUM_I32 of Random(43).nextInt(), in-order, "
+                        "maxLateness=1, one key (the reference benchmark's sliding workload)",
+            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * elapsed / steps,
+            "value": batch * steps / elapsed, "unit": "tuples/s", "windows_emitted": rows,
+            "published_reference_flink_scotty": {"value": C1_PUBLISHED, "unit": "events/s",
+                                                 "source": "README.md:50-54"},
+            "roofline": device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")}
+
+
 def extra_c3(pkg, dev, batch, steps=10, warm=61):
     """BASELINE configs[2] (C3): SlidingWindow(60 s, 60 ms) + SessionWindow(1 s gap), MIN_I32 + MAX_I32, 20 %
     out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; exact engine.  Every 10 s of
-    event time the stream pauses for 1.5 s, so sessions close (BenchmarkRunner.generateSessionGaps-like).  61 s of
+    event time the stream pauses for 2 s (SURVEY: 1-2 s silences), so sessions close: tuples up to 500 ms late leave
+    a 1.5 s silence, more than the 1 s gap (a 1.5 s pause leaves exactly the gap, and the sessions merge again).  61 s of
     warm-up: every timed step emits its sliding windows.  The timed steps cover whole 10-step session periods, so
     the pause step (new session, out-of-order session edits: the event-exact path, exact_batch.hip) is counted
     beside the quiet steps (one pass, exact_quiet.hip) in its true proportion.  Inputs resident in HBM; results
@@ -269,7 +359,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
     for s in range(warm + 2 * steps):
         if s == warm + steps:
             op.enableTiming(True)  # instrumented steps: after the wall-clock ones
-        t_begin = s * 1000 + 1000 + (s // 10) * 1500
+        t_begin = s * 1000 + 1000 + (s // 10) * 2000
         ts = base + t_begin
         late = torch.rand(batch, device=dev, generator=g) < 0.2
         d = torch.randint(1, 501, (batch,), device=dev, generator=g)
@@ -286,7 +376,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
             verdicts.append(op._debug_stat(8))
     roof = device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_MIN|NEED_MAX> (quiet path)")
     return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
-                        "(delay U[1,500] ms), lag 500 ms, 1.5 s pause every 10 s, non-keyed, exact engine",
+                        "(delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, non-keyed, exact engine",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
             "ms_per_step_each": [round(1e3 * t, 4) for t in times],
             "quiet_steps": sum(1 for x in verdicts if x == 1), "event_exact_steps": sum(1 for x in verdicts if x != 1),
@@ -391,8 +481,8 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
         if dist is not None and s == warm:
             dist.barrier()
         t0 = time.perf_counter()
-        if G > 1:
-            op.processChunk(ts.data_ptr(), v.data_ptr(), batch, 0, n_before=rank * batch, n_total=G * batch)
+        if G > 1:  # the real bounds exchange: an all-gather of {n, first ts, last ts} per chunk, timed
+            op.processChunk(ts.data_ptr(), v.data_ptr(), batch, 0)
             n, _ = op.processWatermarkDevice(s * 1000 + (G * batch - 1) // rate)
         else:
             op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
@@ -447,9 +537,8 @@ def extra_c5t(pkg, dev, batch, steps, warm=3, rank=0, world=1, dist=None):
             dist.barrier()
         t0 = time.perf_counter()
         wm = (s + 1) * G * batch - 1
-        if G > 1:
-            op.processChunk(ts.data_ptr(), v.data_ptr(), batch, 0, n_before=rank * batch, n_total=G * batch,
-                            ts_before=s * G * batch + rank * batch - 1 if s * G + rank > 0 else -2**63, ts_last=wm)
+        if G > 1:  # the real bounds exchange ({n, first ts, last ts} all-gather per chunk), timed
+            op.processChunk(ts.data_ptr(), v.data_ptr(), batch, 0)
         else:
             op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
         n, _ = op.processWatermarkDevice(wm)
@@ -472,6 +561,63 @@ def extra_c5t(pkg, dev, batch, steps, warm=3, rank=0, world=1, dist=None):
             "scaling": "weak", "windows_emitted": rows,
             "roofline_wall": {"achieved": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9,
                               "frac": batch * BYTES_PER_TUPLE * len(times) / elapsed / 1e9 / HBM_PEAK_GBS}}
+
+
+def c4_routing(pkg, dev, batch, keys, steps, rank, world, dist, seed=4242):
+    """The keyBy in front of the keyed operator at G > 1, timed on its own (BENCH field `routing`): each rank holds an
+    arrival slice of the global keyed stream (uniform keys), splits it on the device by the owner rank of every key
+    (the product router's key-group assignment, KeyedShardRouter / scotty_key_shard, as a device lookup table) with a
+    stable sort, and exchanges the parts with one all-to-all of 16-byte records (RCCL over xGMI for "nccl"; host
+    staged for "gloo") after an all-to-all of the part sizes.  Reported per step: split ms, exchange ms, and the
+    routed tuples/s; the operator legs consume rank-owned batches (what an upstream keyBy delivers)."""
+    import torch
+    allk = np.arange(keys, dtype=np.uint32)
+    parts = pkg.KeyedShardRouter(world).route(allk, allk.astype(np.int64), allk.astype(np.int32))
+    owner = np.zeros(keys, dtype=np.int64)
+    for r, (k, _, _) in enumerate(parts):
+        owner[k] = r
+    owner_d = torch.from_numpy(owner).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + rank)
+    staged = dist.get_backend() != "nccl"
+    rate = max(1, batch // 1000)
+    t_split = t_x = 0.0
+    got = 0
+    for s in range(steps + 1):
+        k = torch.randint(0, keys, (batch,), device=dev, dtype=torch.int64, generator=g)
+        ts = torch.arange(batch, device=dev, dtype=torch.int64) // rate + s * 1000
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int64, generator=g)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        own = owner_d[k]
+        order = torch.sort(own, stable=True).indices
+        rec = torch.stack([ts[order], (k[order] << 32) | (v[order] & 0xFFFFFFFF)], dim=1).contiguous()
+        cnt = torch.bincount(own, minlength=world)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        cin = cnt.cpu() if staged else cnt
+        cout = torch.empty_like(cin)
+        dist.all_to_all_single(cout, cin)
+        ins, outs = cin.tolist(), cout.tolist()
+        src = rec.cpu() if staged else rec
+        dst = torch.empty((sum(outs), 2), dtype=torch.int64, device=src.device)
+        dist.all_to_all_single(dst, src, output_split_sizes=outs, input_split_sizes=ins)
+        if not staged:
+            torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        if s > 0:
+            t_split += t1 - t0
+            t_x += t2 - t1
+            got += int(dst.shape[0])
+    t = torch.tensor([t_split, t_x], dtype=torch.float64, device=dev if not staged else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_split, t_x = (float(x) for x in t.tolist())
+    return {"what": "device split by owner rank (stable sort) + all-to-all of 16-B records, per rank per step",
+            "tuples_per_step_per_gpu": batch, "steps": steps, "split_ms_per_step": 1e3 * t_split / steps,
+            "exchange_ms_per_step": 1e3 * t_x / steps,
+            "routed_tuples_per_s": batch * world * steps / (t_split + t_x),
+            "received_tuples_rank0_per_step": got / steps, "backend": dist.get_backend()}
 
 
 def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None):
@@ -589,7 +735,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
-    ap.add_argument("--only", default="", help="comma list of extra legs to run (c2s,c3,c4,c5,c5t,pcie); default all")
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c5,c5t,pcie); default all")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
@@ -713,13 +859,16 @@ def main():
                                        % world) if sharded else "single GPU"},
             "roofline": roof,
         }
-    legs = set(x for x in args.only.split(",") if x) or {"c2s", "c3", "c4", "c5", "c5t", "pcie"}
+    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c5", "c5t", "pcie"}
     extra = {}
     if not args.no_extra:
         del batches
         del op
         torch.cuda.empty_cache()
         if world == 1:
+            if "c1" in legs:
+                extra["c1"] = extra_c1(pkg, dev, 1 << 26, 5)
+                log("bench: C1 done")
             if "c2s" in legs:
                 extra["c2s"] = extra_c2s(pkg, dev, 1 << 27, 5)
                 log("bench: C2s done")
@@ -742,6 +891,7 @@ def main():
             extra = {"c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, rank=rank, world=world, dist=dist),
                      "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist),
                      "c5t": extra_c5t(pkg, dev, 1 << 26, 5, rank=rank, world=world, dist=dist)}
+            extra["c4"]["routing"] = c4_routing(pkg, dev, C4_BATCH, 1 << 20, 3, rank, world, dist)
     if rank == 0:
         if extra:
             res["extra"] = extra
@@ -749,8 +899,10 @@ def main():
             # CPU baselines on this box's host cores, rank 0, N=1 only (bounded samples of the same streams)
             res["cpu_baseline"] = cpu_c2(sizes, rate)
             log("bench: CPU C2 done")
-            threads = min(16, os.cpu_count() or 1)  # the box's CPU share for one GPU
-            cb = {"c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
+            threads, quota = host_cores()  # T = the host threads this process may use
+            log("bench: host cores: %d usable threads, cgroup quota %s" % (threads, quota))
+            cb = {"c1": lambda: cpu_c1((1 << 26) // 1000),
+                  "c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
                   "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000),
                   "c5t": lambda: cpu_c5t(1 << 20)}
             for name, fn in cb.items():

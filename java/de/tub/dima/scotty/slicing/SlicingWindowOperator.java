@@ -11,161 +11,154 @@ import de.tub.dima.scotty.core.windowType.Window;
 import de.tub.dima.scotty.core.windowType.WindowMeasure;
 import de.tub.dima.scotty.state.StateFactory;
 
-import java.lang.foreign.Arena;
-import java.lang.foreign.FunctionDescriptor;
-import java.lang.foreign.Linker;
-import java.lang.foreign.MemorySegment;
-import java.lang.foreign.SymbolLookup;
-import java.lang.invoke.MethodHandle;
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
 import java.util.ArrayList;
 import java.util.List;
-
-import static java.lang.foreign.ValueLayout.ADDRESS;
-import static java.lang.foreign.ValueLayout.JAVA_BYTE;
-import static java.lang.foreign.ValueLayout.JAVA_DOUBLE;
-import static java.lang.foreign.ValueLayout.JAVA_INT;
-import static java.lang.foreign.ValueLayout.JAVA_LONG;
 
 /**
  * Drop-in for the reference's {@code de.tub.dima.scotty.slicing.SlicingWindowOperator}
  * (slicing/src/main/java/de/tub/dima/scotty/slicing/SlicingWindowOperator.java:20-70), backed by
- * {@code libscotty_mi355x.so} through the Java 22 Foreign Function and Memory API: one native operator per
- * instance, the C-ABI of {@code include/scotty_mi355x.h}.  Put this class ahead of the reference's slicing jar
- * on the classpath; the connectors' {@code new SlicingWindowOperator<>(stateFactory)} then binds here.
+ * {@code libscotty_mi355x.so} (C-ABI: include/scotty_mi355x.h) through {@link NativeApi}: the Java 22 FFM API, or
+ * JNI on older JDKs.  Put this class ahead of the reference's slicing jar on the classpath; the connectors'
+ * {@code new SlicingWindowOperator<>(stateFactory)} then binds here, unchanged.
  *
- * <p>processElement buffers the tuple off-heap (no native call); the buffer goes to the GPU as one micro-batch
- * (scotty_process_elements) before the next processWatermark or configuration call, which is where the reference's
- * per-tuple work becomes observable.  Window results come back as SoA columns (scotty_windows) and are boxed into
- * {@link NativeAggregateWindow}s in the reference's emission order.
- *
- * <p>Only aggregations with a GPU kind run ({@link NativeValues#kindOf}); anything else is rejected with
- * UnsupportedOperationException at addAggregation -- there is no CPU fallback.
+ * <p>Two modes, chosen at construction:
+ * <ul>
+ *   <li>a stand-alone operator (GlobalScottyWindowOperator, direct users): one native operator; processElement
+ *       appends to an off-heap buffer (no native call) which goes to the GPU as one micro-batch
+ *       (scotty_process_elements) before the next processWatermark or configuration call;</li>
+ *   <li>a per-key operator of a keyed connector ({@link KeyedEngine#sharedForCaller}): the instance is one key of
+ *       its thread's shared keyed native operator ({@link KeyedEngine}): one push and one native watermark per
+ *       watermark round for all keys.</li>
+ * </ul>
+ * Window results come back as SoA columns, in the reference's emission order, and are rebuilt into
+ * {@link NativeAggregateWindow}s whose values are the objects the functions' lower() returns
+ * ({@link NativeFunctions.Binding#rebuild}).  Only functions with a GPU binding run ({@link NativeFunctions#bind});
+ * anything else is rejected with UnsupportedOperationException at addAggregation -- there is no CPU fallback.
  */
 public class SlicingWindowOperator<InputType> implements WindowOperator<InputType> {
 
-    private static final Linker LINKER = Linker.nativeLinker();
-    private static final SymbolLookup LIB = SymbolLookup.libraryLookup(
-            System.getProperty("scotty.native.lib", "libscotty_mi355x.so"), Arena.global());
+    // SCOTTY_WIN_* / SCOTTY_FLAG_KEYED / error codes of include/scotty_mi355x.h
+    static final int WIN_TUMBLING = 0, WIN_SLIDING = 1, WIN_SESSION = 2, WIN_FIXED_BAND = 3;
+    static final int FLAG_KEYED = 1;
+    static final int ERR_INDEX = -5;
 
-    private static MethodHandle handle(String name, FunctionDescriptor d) {
-        return LINKER.downcallHandle(LIB.find(name).orElseThrow(() -> new UnsatisfiedLinkError(name)), d);
-    }
-
-    // include/scotty_mi355x.h
-    private static final MethodHandle CREATE = handle("scotty_create",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_INT));
-    private static final MethodHandle DESTROY = handle("scotty_destroy", FunctionDescriptor.ofVoid(ADDRESS));
-    private static final MethodHandle LAST_ERROR = handle("scotty_last_error", FunctionDescriptor.of(ADDRESS, ADDRESS));
-    private static final MethodHandle ADD_WINDOW = handle("scotty_add_window",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, JAVA_INT, JAVA_LONG, JAVA_LONG));
-    private static final MethodHandle ADD_AGGREGATION = handle("scotty_add_aggregation",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
-    private static final MethodHandle SET_MAX_LATENESS = handle("scotty_set_max_lateness",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG));
-    private static final MethodHandle PROCESS_ELEMENTS = handle("scotty_process_elements",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG));
-    private static final MethodHandle PROCESS_WATERMARK = handle("scotty_process_watermark",
-            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
-
-    // SCOTTY_WIN_* / SCOTTY_MEASURE_* / SCOTTY_VALUE_* / error codes
-    private static final int WIN_TUMBLING = 0, WIN_SLIDING = 1, WIN_SESSION = 2, WIN_FIXED_BAND = 3;
-    private static final int ERR_INDEX = -5;
-
-    // scotty_windows: size_t n_windows; int32 n_aggs (+4 pad); start, end, measure, has_value; values[8]; key
-    private static final long RES_BYTES = 120, OFF_N = 0, OFF_START = 16, OFF_END = 24, OFF_MEASURE = 32,
-            OFF_HAS = 40, OFF_VALUES = 48;
-
-    // native state: created in the constructor on the task that runs the operator (connectors build operators in
-    // open(), not by deserialization), so it is not part of the serialized form
-    private final transient Arena arena = Arena.ofShared();
-    private final transient MemorySegment op;
-    private final int valueType;
-    private final NativeValues.Extractor<InputType> extractor;
-    private final List<Integer> kinds = new ArrayList<>();
-    private transient MemorySegment tsBuf, valBuf;
+    private final transient NativeApi api = NativeApi.get();
+    private final int valueType, width;
+    private final NativeValues.Extractor<InputType> extractor;  // null: the functions' bindings read the value
+    private final List<NativeFunctions.Binding> bindings = new ArrayList<>();
+    private final List<long[]> windows = new ArrayList<>();      // {kind, measure, a, b} in registration order
+    private long maxLateness = 1000;                              // S/WindowManager.java:24
+    private boolean latenessSet = false;
+    private final boolean keyed;
+    // stand-alone mode: the native operator and the off-heap micro-batch (created in the constructor on the task
+    // that runs the operator: connectors build operators in open(), not by deserialization)
+    private transient long op;
+    private transient ByteBuffer tsBuf, valBuf;
     private long buffered = 0;
+    // keyed mode: the shared engine and this instance's key
+    private transient KeyedEngine engine;
+    private int id = -1;
 
     /** S/SlicingWindowOperator.java:30-37: the state factory is not used (slices live in HBM). */
     public SlicingWindowOperator(StateFactory stateFactory) {
-        this(stateFactory, NativeValues.VALUE_I32, NativeValues.defaultExtractor());
+        this(stateFactory, NativeValues.VALUE_I32, null);
     }
 
-    /** valueType: NativeValues.VALUE_I32 / VALUE_I64 / VALUE_F64; extractor: the numeric value of a tuple. */
+    /**
+     * valueType: NativeValues.VALUE_I32 / VALUE_I64 / VALUE_F64; extractor: the numeric value of a tuple (null: the
+     * registered functions' bindings read it).
+     */
     public SlicingWindowOperator(StateFactory stateFactory, int valueType, NativeValues.Extractor<InputType> extractor) {
         this.valueType = valueType;
+        this.width = valueType == NativeValues.VALUE_I32 ? 4 : 8;
         this.extractor = extractor;
-        MemorySegment out = arena.allocate(ADDRESS);
-        check(callInt(CREATE, out, 0, valueType, 0));
-        this.op = out.get(ADDRESS, 0);
-        allocate(1 << 16);
+        this.keyed = KeyedEngine.sharedForCaller();
+        if (!keyed) {
+            this.op = api.create(0, valueType, 0);
+            allocate(1 << 16);
+        }
     }
 
     @Override
     public void processElement(InputType element, long ts) {
-        if (buffered == tsBuf.byteSize() / 8) allocate(2 * buffered);
-        tsBuf.setAtIndex(JAVA_LONG, buffered, ts);
-        if (valueType == NativeValues.VALUE_I32) valBuf.setAtIndex(JAVA_INT, buffered, (int) extractor.value(element));
-        else if (valueType == NativeValues.VALUE_I64) valBuf.setAtIndex(JAVA_LONG, buffered, extractor.value(element));
-        else valBuf.setAtIndex(JAVA_DOUBLE, buffered, extractor.doubleValue(element));
+        Number v = value(element);
+        if (keyed) {
+            bindEngine();
+            engine.add(id, ts, v);
+            return;
+        }
+        if (buffered == tsBuf.capacity() / 8) allocate(2 * buffered);
+        tsBuf.putLong((int) (8 * buffered), ts);
+        if (valueType == NativeValues.VALUE_I32) valBuf.putInt((int) (4 * buffered), v.intValue());
+        else if (valueType == NativeValues.VALUE_I64) valBuf.putLong((int) (8 * buffered), v.longValue());
+        else valBuf.putDouble((int) (8 * buffered), v.doubleValue());
         buffered++;
     }
 
     /** S/SlicingWindowOperator.java:46-49 (WindowManager.processWatermark, S/WindowManager.java:38-61). */
     @Override
     public List<AggregateWindow> processWatermark(long watermarkTs) {
-        flush();
-        MemorySegment res = arena.allocate(RES_BYTES, 8);
-        check(callInt(PROCESS_WATERMARK, op, watermarkTs, res));
-        long n = res.get(JAVA_LONG, OFF_N);
-        List<AggregateWindow> windows = new ArrayList<>((int) n);
-        if (n == 0) return windows;
-        MemorySegment start = res.get(ADDRESS, OFF_START).reinterpret(8 * n);
-        MemorySegment end = res.get(ADDRESS, OFF_END).reinterpret(8 * n);
-        MemorySegment measure = res.get(ADDRESS, OFF_MEASURE).reinterpret(4 * n);
-        MemorySegment has = res.get(ADDRESS, OFF_HAS).reinterpret(n);
-        MemorySegment[] values = new MemorySegment[kinds.size()];
-        for (int k = 0; k < values.length; k++) values[k] = res.get(ADDRESS, OFF_VALUES + 8L * k).reinterpret(8 * n);
-        for (long i = 0; i < n; i++) {
-            List<Object> agg = new ArrayList<>(values.length);
-            boolean hasValue = has.get(JAVA_BYTE, i) != 0;
-            if (hasValue)
-                for (int k = 0; k < values.length; k++)
-                    agg.add(NativeValues.box(kinds.get(k), values[k].getAtIndex(JAVA_LONG, i)));
-            windows.add(new NativeAggregateWindow(
-                    measure.getAtIndex(JAVA_INT, i) == 0 ? WindowMeasure.Time : WindowMeasure.Count,
-                    start.getAtIndex(JAVA_LONG, i), end.getAtIndex(JAVA_LONG, i), hasValue, agg));
+        if (keyed) {
+            bindEngine();
+            List<KeyedEngine.Row> rows = engine.watermark(id, watermarkTs);
+            List<AggregateWindow> out = new ArrayList<>(rows.size());
+            for (KeyedEngine.Row r : rows) out.add(window(r.start(), r.end(), r.measure(), r.has(), r.words()));
+            return out;
         }
-        return windows;
+        flush();
+        NativeApi.Windows w = new NativeApi.Windows();
+        check(api.processWatermark(op, watermarkTs, w));
+        List<AggregateWindow> out = new ArrayList<>(w.n);
+        for (int i = 0; i < w.n; i++) {
+            long[] words = new long[w.values.length];
+            for (int k = 0; k < words.length; k++) words[k] = w.values[k][i];
+            out.add(window(w.start[i], w.end[i], w.measure[i], w.has[i] != 0, words));
+        }
+        return out;
+    }
+
+    private AggregateWindow window(long start, long end, int measure, boolean has, long[] words) {
+        List<Object> agg = new ArrayList<>(words.length);
+        if (has)
+            for (int k = 0; k < words.length; k++) agg.add(bindings.get(k).rebuild(words[k]));
+        return new NativeAggregateWindow(measure == 0 ? WindowMeasure.Time : WindowMeasure.Count, start, end, has, agg);
     }
 
     /** WindowManager.addWindowAssigner (S/WindowManager.java:121-147). */
     @Override
     public void addWindowAssigner(Window window) {
-        flush();
-        int m = window.getWindowMeasure() == WindowMeasure.Time ? 0 : 1;
-        if (window instanceof TumblingWindow t) {
-            check(callInt(ADD_WINDOW, op, WIN_TUMBLING, m, t.getSize(), 0L));
-        } else if (window instanceof SlidingWindow s) {
-            check(callInt(ADD_WINDOW, op, WIN_SLIDING, m, s.getSize(), s.getSlide()));
-        } else if (window instanceof SessionWindow s) {
-            check(callInt(ADD_WINDOW, op, WIN_SESSION, m, s.getGap(), 0L));
-        } else if (window instanceof FixedBandWindow f) {
-            check(callInt(ADD_WINDOW, op, WIN_FIXED_BAND, m, f.getStart(), f.getSize()));
-        } else {
-            throw new UnsupportedOperationException("window type without a GPU kind: " + window);
+        long[] w = describe(window);
+        windows.add(w);
+        if (keyed) {
+            configuredAfterUse();
+            return;
         }
+        flush();
+        check(api.addWindow(op, (int) w[0], (int) w[1], w[2], w[3]));
+    }
+
+    private static long[] describe(Window window) {
+        int m = window.getWindowMeasure() == WindowMeasure.Time ? 0 : 1;
+        if (window instanceof TumblingWindow t) return new long[]{WIN_TUMBLING, m, t.getSize(), 0L};
+        if (window instanceof SlidingWindow s) return new long[]{WIN_SLIDING, m, s.getSize(), s.getSlide()};
+        if (window instanceof SessionWindow s) return new long[]{WIN_SESSION, m, s.getGap(), 0L};
+        if (window instanceof FixedBandWindow f) return new long[]{WIN_FIXED_BAND, m, f.getStart(), f.getSize()};
+        throw new UnsupportedOperationException("window type without a GPU kind: " + window);
     }
 
     /** WindowManager.addAggregation (S/WindowManager.java:196-198). */
     @Override
     public <OutputType> void addAggregation(AggregateFunction<InputType, ?, OutputType> windowFunction) {
+        NativeFunctions.Binding b = NativeFunctions.bind(windowFunction, valueType);
+        bindings.add(b);
+        if (keyed) {
+            configuredAfterUse();
+            return;
+        }
         flush();
-        int kind = NativeValues.kindOf(windowFunction, valueType);
-        if (kind < 0)
-            throw new UnsupportedOperationException("AggregateFunction without a GPU kind (user lambdas cannot run on "
-                    + "the GPU): " + windowFunction.getClass().getName());
-        check(callInt(ADD_AGGREGATION, op, kind));
-        kinds.add(kind & 0xFFFF);
+        check(api.addAggregation(op, b.kind));
     }
 
     /** S/SlicingWindowOperator.java:57-63. */
@@ -175,32 +168,75 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
 
     @Override
     public void setMaxLateness(long maxLateness) {
+        this.maxLateness = maxLateness;
+        this.latenessSet = true;
+        if (keyed) {
+            configuredAfterUse();
+            return;
+        }
         flush();
-        check(callInt(SET_MAX_LATENESS, op, maxLateness));
+        check(api.setMaxLateness(op, maxLateness));
     }
 
-    /** Frees the native operator (the reference's operator is garbage collected; here HBM is released). */
+    /** Frees the native operator (stand-alone mode; a keyed engine lives as long as its thread). */
     public void close() {
-        try {
-            DESTROY.invokeExact(op);
-        } catch (Throwable t) {
-            throw new RuntimeException(t);
+        if (!keyed && op != 0) {
+            api.destroy(op);
+            op = 0;
         }
-        arena.close();
+    }
+
+    // ---- value of a tuple: the explicit extractor, else the first value-reading binding (all must agree)
+    private Number value(InputType element) {
+        if (extractor != null) {
+            for (NativeFunctions.Binding b : bindings) b.value(element);  // exemplars / key checks
+            return valueType == NativeValues.VALUE_F64 ? (Number) extractor.doubleValue(element)
+                    : (Number) extractor.value(element);
+        }
+        Number v = null;
+        for (NativeFunctions.Binding b : bindings) {
+            Number x = b.value(element);
+            if ((b.kind & 0xFFFF) == NativeValues.AGG_COUNT) continue;
+            if (v == null) v = x;
+            else if (!v.equals(x))
+                throw new UnsupportedOperationException("the operator's functions read different values from one "
+                        + "tuple; the GPU operator keeps one value per tuple");
+        }
+        return v != null ? v : 0;
+    }
+
+    private void bindEngine() {
+        if (engine != null) return;
+        List<Integer> kinds = new ArrayList<>();
+        StringBuilder sig = new StringBuilder().append(valueType).append('|').append(latenessSet ? maxLateness : "d");
+        for (long[] w : windows) sig.append("|w").append(w[0]).append(',').append(w[1]).append(',').append(w[2])
+                .append(',').append(w[3]);
+        for (NativeFunctions.Binding b : bindings) {
+            kinds.add(b.kind);
+            sig.append("|f").append(b.kind);
+        }
+        engine = KeyedEngine.forThread(sig.toString(), valueType, windows, kinds, maxLateness, latenessSet);
+        id = engine.newId();
+    }
+
+    private void configuredAfterUse() {
+        if (engine != null)
+            throw new UnsupportedOperationException("a per-key operator of a keyed connector was reconfigured after "
+                    + "its first tuple: the shared keyed engine holds one configuration for all keys");
     }
 
     private void flush() {
         if (buffered == 0) return;
-        check(callInt(PROCESS_ELEMENTS, op, tsBuf, valBuf, buffered));
+        check(api.processElements(op, tsBuf, valBuf, buffered));
         buffered = 0;
     }
 
     private void allocate(long capacity) {
-        long width = valueType == NativeValues.VALUE_I32 ? 4 : 8;
-        MemorySegment ts = arena.allocate(8 * capacity, 8), vals = arena.allocate(width * capacity, 8);
+        ByteBuffer ts = ByteBuffer.allocateDirect((int) (8 * capacity)).order(ByteOrder.nativeOrder());
+        ByteBuffer vals = ByteBuffer.allocateDirect((int) (width * capacity)).order(ByteOrder.nativeOrder());
         if (buffered > 0) {
-            MemorySegment.copy(tsBuf, 0, ts, 0, 8 * buffered);
-            MemorySegment.copy(valBuf, 0, vals, 0, width * buffered);
+            ts.put(0, tsBuf, 0, (int) (8 * buffered));
+            vals.put(0, valBuf, 0, (int) (width * buffered));
         }
         tsBuf = ts;
         valBuf = vals;
@@ -208,21 +244,8 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
 
     private void check(int rc) {
         if (rc >= 0) return;  // 1 = SCOTTY_WARN_LATE_DROPPED: tuples the reference drops too
-        String msg;
-        try {
-            msg = ((MemorySegment) LAST_ERROR.invoke(op)).reinterpret(4096).getString(0);
-        } catch (Throwable t) {
-            msg = "scotty error " + rc;
-        }
+        String msg = api.lastError(op);
         if (rc == ERR_INDEX) throw new IndexOutOfBoundsException(msg);  // the reference's exception type
         throw new UnsupportedOperationException(msg);
-    }
-
-    private static int callInt(MethodHandle mh, Object... args) {
-        try {
-            return (int) mh.invokeWithArguments(args);
-        } catch (Throwable t) {
-            throw new RuntimeException(t);
-        }
     }
 }

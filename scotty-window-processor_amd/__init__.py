@@ -547,8 +547,10 @@ class ShardedSlicingWindowOperator:
         self.world = dist.get_world_size(group)
         self.dev = torch.device("cuda", device)
         self.staged = dist.get_backend(group) != "nccl"
-        if not self.staged:  # RCCL: the all-gather's stream is ordered after the push by events, no host sync
-            self.op.tune("shard_async", 1)
+        # No cross-stream event ordering: torch ships its own HIP runtime (torch/lib/libamdhip64.so) beside the one
+        # the library links (/opt/rocm), and an event or stream of one runtime means nothing to the other.  The
+        # push returns after its own stream has finished (shard_async off), and the commit waits for torch's
+        # stream to finish the collective.
         self._xb = None
         self._assigned = []
         self._measures = set()
@@ -595,7 +597,7 @@ class ShardedSlicingWindowOperator:
             mine = t.tensor([n, first, last], dtype=t.int64, device=self.dev if not self.staged else "cpu")
             allv = t.empty(3 * self.world, dtype=t.int64, device=mine.device)
             self.dist.all_gather_into_tensor(allv, mine, group=self.group)
-            g = allv.view(self.world, 3).tolist()
+            g = allv.view(self.world, 3).tolist()  # .tolist() waits for the collective on torch's stream
             r = self.dist.get_rank(self.group)
             n_before, n_total = int(sum(x[0] for x in g[:r])), int(sum(x[0] for x in g))
             lasts = [x[2] for x in g if x[0] > 0]
@@ -616,10 +618,9 @@ class ShardedSlicingWindowOperator:
             gb.copy_(self._hg)
             self.torch.cuda.synchronize(self.dev)
         else:
-            cur = self.torch.cuda.current_stream(self.dev).cuda_stream
-            self.op.streamOrder(cur, False)  # the record is complete before the collective reads it
+            # the record is complete: the push synchronised the library's stream before returning
             self.dist.all_gather_into_tensor(gb, xb, group=self.group)
-            self.op.streamOrder(cur, True)  # the gathered records have landed before the commit reads them
+            self.torch.cuda.current_stream(self.dev).synchronize()  # the gathered records have landed
         self.op.shardCommit(gb.data_ptr(), self.world)
 
 

@@ -39,6 +39,35 @@ class JavaRandom:
         return ((self.next(26) << 27) + self.next(27)) * (1.0 / (1 << 53))
 
 
+class JavaRandomInts:
+    """java.util.Random.nextInt() as numpy int32 blocks (C1: Random(43).nextInt() values).  The
+    48-bit LCG seed_{k+1} = a*seed_k + c jumps k steps as seed_k = A_k*seed_0 + C_k (mod 2^48); uint64 arithmetic
+    wraps mod 2^64, which 2^48 divides, so the masked products are exact."""
+
+    _B = 1 << 16
+
+    def __init__(self, seed):
+        self.seed = np.uint64((seed ^ _MULT) & _MASK)
+        a = np.zeros(self._B, np.uint64)
+        c = np.zeros(self._B, np.uint64)
+        x, y = 1, 0
+        for k in range(self._B):  # A_{k+1}, C_{k+1}: k+1 steps from seed_0
+            x, y = (x * _MULT) & _MASK, (y * _MULT + 0xB) & _MASK
+            a[k], c[k] = x, y
+        self._a, self._c = a, c
+
+    def next_ints(self, n):
+        out = np.empty(n, np.int32)
+        m = np.uint64(_MASK)
+        with np.errstate(over="ignore"):
+            for b0 in range(0, n, self._B):
+                k = min(self._B, n - b0)
+                seeds = (self._a[:k] * self.seed + self._c[:k]) & m
+                out[b0:b0 + k] = (seeds >> np.uint64(16)).astype(np.uint32).view(np.int32)
+                self.seed = seeds[k - 1]
+        return out
+
+
 def random_tumbling_sizes(n=1000, lo=1, hi=20, seed=10):
     """BenchmarkRunner.getAssigner("randomTumbling(n,lo,hi)"): sizes in ms, Random(10)."""
     r = JavaRandom(seed)

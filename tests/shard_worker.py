@@ -1,5 +1,8 @@
 """One rank of a sharded non-keyed run (launched by tests/test_gpu_shard.py through torch.distributed.run).
-Every rank feeds its arrival chunk of each global micro-batch; rank 0 writes the windows of every watermark."""
+Every rank feeds its arrival chunk of each global micro-batch and writes the windows of every watermark to
+<out>.rank<r> (every rank holds the same slice store, so every rank's rows are checked).  RCCL ("nccl"): no
+synchronisation by the test between chunks; the exchange buffer is poisoned on torch's stream before each chunk, so
+a commit that read it before the collective landed would fold garbage and fail the oracle comparison."""
 import json
 import os
 import sys
@@ -40,8 +43,12 @@ def main():
             a, b = int(cuts[rank]), int(cuts[rank + 1])
             t = torch.tensor(ts[a:b], dtype=torch.int64, device=dev)
             v = torch.tensor(vals[a:b], dtype=torch.int32, device=dev)
+            if backend == "nccl":
+                _, gb = op._bufs()
+                gb.fill_(-0x5A5A5A5A5A5A5A5A)  # poison: overwritten by the all-gather before the commit may read it
             op.processChunk(t.data_ptr(), v.data_ptr(), b - a, int(ts[0]))
-            torch.cuda.synchronize(dev)
+            if backend != "nccl":
+                torch.cuda.synchronize(dev)
         else:
             try:
                 ws = op.processWatermark(st[1])
@@ -51,8 +58,7 @@ def main():
                 res.append([["index_error"]])
                 continue
             res.append([list(w.key()[:4]) + [list(w.key()[4])] for w in ws] + [["dropped", op.droppedCount()]])
-    if rank == 0:
-        json.dump(res, open(out, "w"))
+    json.dump(res, open("%s.rank%d" % (out, rank), "w"))
     dist.barrier()
     dist.destroy_process_group()
 

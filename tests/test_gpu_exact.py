@@ -245,9 +245,10 @@ def test_quiet_path_equals_event_exact_path_and_replay(pkg, seed):
 
 def test_config3_full_size_quiet_path_equals_replay(pkg):
     """BASELINE configs[2] (C3) at the benchmark's batch size class: SlidingWindow(60 s, 60 ms) + SessionWindow(1 s),
-    MIN/MAX, 20 % out-of-order by U[1,500] ms, a 1.5 s pause every 4th step, 2^24 tuples per step, generated on the
-    device like bench.py's C3 leg.  Quiet path (default) == event-exact batch path == single-wavefront replay, window
-    by window, every step; the pause steps go through the event-exact path, the others commit in one pass."""
+    MIN/MAX, 20 % out-of-order by U[1,500] ms, 2^24 tuples per step, a 2 s pause before step 3 (the session closes:
+    the silence left by tuples up to 500 ms late exceeds the gap), generated on the device like bench.py's C3 leg.
+    Quiet path (default) == event-exact batch path == single-wavefront replay (~23 s per step), window by window,
+    every step; the pause step goes through the event-exact path, the steps after the first commit in one pass."""
     import torch
     dev = torch.device("cuda", 0)
     batch = 1 << 24
@@ -268,17 +269,23 @@ def test_config3_full_size_quiet_path_equals_replay(pkg):
     from helpers import same_windows
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     quiet, event, rows = 0, 0, 0
-    for s in range(10):
-        t_begin = s * 1000 + 1000 + (s // 4) * 1500
+    import time
+    for s in range(4):
+        t_begin = s * 1000 + 1000 + (s // 3) * 2000
         ts = base + t_begin
         late = torch.rand(batch, device=dev, generator=g) < 0.2
         d = torch.randint(1, 501, (batch,), device=dev, generator=g)
         ts = torch.where(late, torch.clamp(ts - d, min=t_begin - 500), ts).contiguous()
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         torch.cuda.synchronize(dev)
+        tt = []
         for op in ops:
+            t0 = time.perf_counter()
             op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+            op.sync()
+            tt.append(round(time.perf_counter() - t0, 3))
         verdict = ops[0]._debug_stat(8)
+        print("C3 full-size step %d: verdict %d, push s (quiet, event, serial) %s" % (s, verdict, tt), flush=True)
         quiet += verdict == 1
         event += verdict > 1
         wm = t_begin + (batch - 1) // rate - 500
@@ -286,7 +293,7 @@ def test_config3_full_size_quiet_path_equals_replay(pkg):
         same_windows(a, b)
         same_windows(a, c)
         rows += len(a)
-    assert quiet >= 5 and event >= 1, (quiet, event)
+    assert quiet >= 2 and event >= 1, (quiet, event)
     assert rows > 0
 
 

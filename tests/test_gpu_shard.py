@@ -30,23 +30,26 @@ def _run_sharded(tmp_path, cid, nproc, backend):
 
 @pytest.mark.parametrize("cid", [0, 4, 6])
 def test_rccl_exchange_single_rank_matches_oracle(tmp_path, cid):
-    """The RCCL ("nccl") exchange path -- device all-gather ordered against the operator's stream by events
-    (scotty_stream_order, shard_async), no host synchronisation -- on one rank of this one-GPU box: time windows,
-    count windows, count + time windows."""
+    """The RCCL ("nccl") exchange path -- device all-gather on torch's stream between the push (the library's
+    stream, synchronised) and the commit (after torch's stream is synchronised) -- on one rank of this one-GPU box:
+    time windows, count windows, count + time windows; the exchange buffer is poisoned before every chunk."""
     r, out = _run_sharded(tmp_path, cid, 1, "nccl")
-    _check(r, out, cid)
+    _check(r, out, cid, 1)
 
 
 @pytest.mark.parametrize("cid", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_two_rank_sharded_stream_matches_oracle(tmp_path, cid):
     r, out = _run_sharded(tmp_path, cid, 2, "gloo")
-    _check(r, out, cid)
+    _check(r, out, cid, 2)
 
 
-def _check(r, out, cid):
+def _check(r, out, cid, nproc):
     tb = r.stderr.find("Traceback")
     assert r.returncode == 0, r.stderr[tb:tb + 3000] if tb >= 0 else r.stderr[-3000:]
-    got = json.load(open(out))
+    outs = [json.load(open("%s.rank%d" % (out, k))) for k in range(nproc)]
+    for k in range(1, nproc):  # every rank emits the same rows (replicated slice store)
+        assert outs[k] == outs[0], ("rank %d differs from rank 0" % k)
+    got = outs[0]
     cfg, ts, vals, sched = case(cid)
     _, ora = build_ops(cfg)
     k = 0

@@ -9,10 +9,12 @@ import csv
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
+    ap.add_argument("--marker", default="xq_prep_kernel", help="kernel that starts a step (xb_prep_kernel: the "
+                    "event-exact path's round)")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "at::native" not in r["Kernel_Name"]]
-    starts = [i for i, r in enumerate(rows) if "xb_prep_kernel" in r["Kernel_Name"]] + [len(rows)]
+    starts = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]] + [len(rows)]
     steps = []
     for a, b in zip(starts[:-1], starts[1:]):
         per = collections.defaultdict(float)
@@ -23,7 +25,7 @@ def main():
     order = sorted(range(len(steps)), key=lambda i: sum(steps[i].values()))
     for label, i in (("median", order[len(order) // 2]), ("largest", order[-1])):
         p = steps[i]
-        print("C3 %s round of %d: device %.1f us" % (label, len(steps), sum(p.values())))
+        print("C3 %s step of %d: device %.1f us" % (label, len(steps), sum(p.values())))
         for name in sorted(p, key=lambda x: -p[x])[:14]:
             print("  %-60s %8.1f us" % (name, p[name]))
 
