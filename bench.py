@@ -645,7 +645,9 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
     own = pkg.KeyedShardRouter(world).route(allk, allk.astype(np.int64), allk.astype(np.int32))[rank][0]
     own = torch.from_numpy(own.astype(np.int32)).to(dev)
     times, rows, elapsed = [], 0, 0.0
-    for s in range(warm + steps):
+    for s in range(warm + 2 * steps):
+        if s == warm + steps:
+            op.enableTiming(True)  # instrumented steps (HIP events per launch class) after the wall-clock ones
         k = own[torch.randint(0, len(own), (batch,), device=dev, dtype=torch.int64, generator=g)]
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         ts = base + s * 1000
@@ -656,9 +658,13 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
         op.processElementsDevice(k.data_ptr(), ts.data_ptr(), v.data_ptr(), batch)
         n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
         torch.cuda.synchronize(dev)
-        if s >= warm:
+        if warm <= s < warm + steps:
             times.append(time.perf_counter() - t0)
             rows += n
+        if dist is not None and s == warm + steps - 1:
+            dist.barrier()
+    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
+                           "keyed data pass: kg_hist + scan + kg_scatter + kg_bucket (class ingest)")
     elapsed = sum(times)
     if dist is not None:
         t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
@@ -671,7 +677,7 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
             "tuples_per_step": batch * world, "tuples_per_step_per_gpu": batch, "steps": steps,
             "keys_per_gpu": op.keyCount(), "ms_per_step": 1e3 * elapsed / len(times),
             "value": batch * world * len(times) / elapsed, "unit": "tuples/s", "scaling": "weak",
-            "windows_emitted_rank0": rows,
+            "windows_emitted_rank0": rows, "roofline": roof,
             "roofline_wall": {"achieved": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9,
                               "frac": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9 / HBM_PEAK_GBS}}
 

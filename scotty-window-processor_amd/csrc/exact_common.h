@@ -114,63 +114,74 @@ struct XSlices {
   // op's slice positions 0..i (positions below head keep their values until a compaction), valid for positions
   // below XState.pvalid -- a window's COUNT / SUM is then two reads instead of a scan of its slices
   unsigned long long *pc, *ps;
-  // lane path for COUNT / integer SUM functions: the store kept as records instead (XSliceRec, the columns above
-  // unused) -- a key's commit or watermark then touches a few 128-B lines, not one line per column
-  struct XSliceRec* rec;
+  // lane path for COUNT / integer SUM functions: the store kept key-interleaved instead (XKView, the columns above
+  // unused): word (op, slice position i, field f) at kw[((i * XK_NF + f) << kc_sh) + op], so the lanes of a
+  // wavefront -- consecutive keys -- touching the same field of the same slice position read or write one
+  // contiguous 512-B run instead of 64 scattered lines.  Keys advance in lockstep in a steady stream (one slice per
+  // grid interval each, compacted at the same batch), so their positions coincide.  sc and the key capacity are
+  // powers of two (sc_sh, kc_sh their logs).
+  unsigned long long* kw;
+  int32_t sc_sh, kc_sh;
 };
 
-// One slice of the lane path's record store: every field of one slice in one 128-B line.
-struct XSliceRec {
-  int64_t ts, te, tl, tf, cs, cl;
-  unsigned long long cnt, p[NPART];
-  unsigned long long pc, ps;
-  int32_t ty, pad0;
-  int64_t pad1[3];
-};
-static_assert(sizeof(XSliceRec) == 128 && offsetof(XSliceRec, p) == 56 && offsetof(XSliceRec, pc) == 80 &&
-                  offsetof(XSliceRec, ty) == 96,
-              "one cache line per slice; XRecView offsets");
+// Fields of the key-interleaved store (XSlices.kw), one 8-byte word each (ty in the low half of its word)
+enum : int { XK_TS, XK_TE, XK_TL, XK_TF, XK_CS, XK_CL, XK_CNT, XK_P0, XK_P1, XK_P2, XK_PC, XK_PS, XK_TY, XK_NF };
 
-// Column views of the record store with the syntax of XSlices' columns (q.ts[j], q.p[k][j], q.ts + base), so one
-// kernel body serves both layouts (template parameter V = XSlices or XRecView).
-template <typename T, int OFF>
-struct XRecCol {
-  XSliceRec* r;
-  __host__ __device__ T& operator[](int64_t j) const { return *(T*)((unsigned char*)(r + j) + OFF); }
-  __host__ __device__ XRecCol operator+(int64_t j) const { return XRecCol{r + j}; }
+// Column views of the key-interleaved store with the syntax of XSlices' columns (q.ts[j], q.p[k][j], q.ts + base
+// with j = op * sc + i), so one kernel body serves both layouts (template parameter V = XSlices or XKView).
+struct XKCol0 {
+  unsigned long long* w;
+  int64_t off;
+  int32_t sc_sh, kc_sh;
+  int32_t f;
+  __host__ __device__ unsigned long long* addr(int64_t j) const {
+    j += off;
+    const int64_t op = j >> sc_sh, i = j & ((((int64_t)1) << sc_sh) - 1);
+    return w + (((i * XK_NF + f) << kc_sh) + op);
+  }
 };
-struct XRecPart {
-  XSliceRec* r;
-  int k;
-  __host__ __device__ unsigned long long& operator[](int64_t j) const { return r[j].p[k]; }
-  __host__ __device__ XRecPart operator+(int64_t j) const { return XRecPart{r + j, k}; }
+template <typename T>
+struct XKCol : XKCol0 {
+  __host__ __device__ T& operator[](int64_t j) const { return *(T*)addr(j); }
+  __host__ __device__ XKCol operator+(int64_t j) const {
+    XKCol c = *this;
+    c.off += j;
+    return c;
+  }
 };
-struct XRecParts {
-  XSliceRec* r;
-  __host__ __device__ XRecPart operator[](int k) const { return XRecPart{r, k}; }
+struct XKParts {
+  XKCol0 c;
+  __host__ __device__ XKCol<unsigned long long> operator[](int k) const {
+    XKCol<unsigned long long> r;
+    static_cast<XKCol0&>(r) = c;
+    r.f = XK_P0 + k;
+    return r;
+  }
 };
-struct XRecView {
-  XRecCol<int64_t, 0> ts;
-  XRecCol<int64_t, 8> te;
-  XRecCol<int64_t, 16> tl;
-  XRecCol<int64_t, 24> tf;
-  XRecCol<int64_t, 32> cs;
-  XRecCol<int64_t, 40> cl;
-  XRecCol<unsigned long long, 48> cnt;
-  XRecParts p;
-  XRecCol<unsigned long long, 80> pc;
-  XRecCol<unsigned long long, 88> ps;
-  XRecCol<int32_t, 96> ty;
-  __host__ __device__ XRecView() : XRecView(nullptr) {}
-  __host__ __device__ explicit XRecView(XSliceRec* r)
-      : ts{r}, te{r}, tl{r}, tf{r}, cs{r}, cl{r}, cnt{r}, p{r}, pc{r}, ps{r}, ty{r} {}
+struct XKView {
+  XKCol<int64_t> ts, te, tl, tf, cs, cl;
+  XKCol<unsigned long long> cnt;
+  XKParts p;
+  XKCol<unsigned long long> pc, ps;
+  XKCol<int32_t> ty;
+  __host__ __device__ XKView() {}
+  __host__ __device__ explicit XKView(const XSlices& s) {
+    XKCol0 b{s.kw, 0, s.sc_sh, s.kc_sh, 0};
+    auto col = [&](auto& c, int f) {
+      static_cast<XKCol0&>(c) = b;
+      c.f = f;
+    };
+    col(ts, XK_TS); col(te, XK_TE); col(tl, XK_TL); col(tf, XK_TF); col(cs, XK_CS); col(cl, XK_CL);
+    col(cnt, XK_CNT); col(pc, XK_PC); col(ps, XK_PS); col(ty, XK_TY);
+    p.c = b;
+  }
 };
 template <typename V>
 __host__ __device__ inline V xview(const XSlices& s);
 template <>
 __host__ __device__ inline XSlices xview<XSlices>(const XSlices& s) { return s; }
 template <>
-__host__ __device__ inline XRecView xview<XRecView>(const XSlices& s) { return XRecView(s.rec); }
+__host__ __device__ inline XKView xview<XKView>(const XSlices& s) { return XKView(s); }
 
 struct XSess {
   int64_t *start, *end;

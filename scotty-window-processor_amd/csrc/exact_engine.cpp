@@ -44,7 +44,7 @@ hipError_t launch_kg_build(const uint32_t* slot_key, int64_t n_ops, unsigned lon
                            hipStream_t st);
 hipError_t launch_kg_partition(const KgArgs& a, int vt, hipStream_t st);
 hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st);
-hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hipStream_t st);
+hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hipStream_t st, int which);
 hipError_t launch_kg_mark_deferred(const KgArgs& a, hipStream_t st);
 int kg_tile(int vt, int64_t nbk, int variant);
 int kg_cells(bool mm);
@@ -103,7 +103,7 @@ void XEngine::release() {
   dfree(d_cfg); dfree(d_cf_kind); dfree(d_cf_meas); dfree(d_cf_a); dfree(d_cf_b);
   dfree(d_st);
   dfree(sl.ts); dfree(sl.te); dfree(sl.tl); dfree(sl.tf); dfree(sl.cs); dfree(sl.cl); dfree(sl.ty); dfree(sl.cnt);
-  dfree(sl.pc); dfree(sl.ps); dfree(sl.rec);
+  dfree(sl.pc); dfree(sl.ps); dfree(sl.kw);
   for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
   dfree(sl.rlo); dfree(sl.rhi); dfree(sl.nn); dfree(sl.rts); dfree(sl.rv);
   dfree(ss.start); dfree(ss.end);
@@ -212,7 +212,9 @@ int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>&
     if (!keyed) {
       sc = sc_override > 0 ? sc_override : (1 << 20);
     } else if (sc_override > 0) {
-      sc = sc_override;
+      int64_t p = 1;  // keyed stores index slice positions with shifts (XKView): a power of two
+      while (p < sc_override) p <<= 1;
+      sc = (int32_t)p;
     } else {
       int64_t min_step = INT64_MAX;
       for (const XWinDef& w : wins) {
@@ -230,6 +232,8 @@ int XEngine::configure(const std::vector<XWinDef>& wins, const std::vector<int>&
   if (sesscap == 0) sesscap = sess_override > 0 ? sess_override : (keyed ? 64 : 4096);
   if (records && rcap_ == 0) rcap_ = keyed ? 256 : (1 << 20);
   c.sc = sc;
+  sl.sc_sh = 0;
+  while (((int64_t)1 << sl.sc_sh) < sc) sl.sc_sh++;
   c.sesscap = sesscap;
   c.ctx_alloc = ctx_alloc;
   c.rcap = rcap_;
@@ -295,8 +299,19 @@ int XEngine::grow_ops(int64_t need) {
   if (ops_cap == 0)  // the store's layout is fixed with the first allocation
     aos = keyed && lane_mode() && vt != VT_F64 && !(cfg.need & (NEED_MIN | NEED_MAX));
   XCHK(grow(&d_st, 1));
-  if (aos) {
-    XCHK(grow(&sl.rec, sc));
+  if (aos) {  // key-interleaved store: rows (position, field) of cap words, re-strided from the old key capacity
+    unsigned long long* nw = nullptr;
+    const int64_t rows = (int64_t)sc * XK_NF;
+    XCHK(dalloc(&nw, (size_t)(rows * cap)));
+    XCHK(hipMemsetAsync(nw, 0, (size_t)(rows * cap) * 8, stream));
+    if (sl.kw && n_ops > 0)
+      XCHK(hipMemcpy2DAsync(nw, cap * 8, sl.kw, ops_cap * 8, n_ops * 8, rows, hipMemcpyDeviceToDevice, stream));
+    XCHK(hipStreamSynchronize(stream));
+    dfree(sl.kw);
+    sl.kw = nw;
+    int sh = 0;
+    while (((int64_t)1 << sh) < cap) sh++;
+    sl.kc_sh = sh;
   } else {
     XCHK(grow(&sl.ts, sc)); XCHK(grow(&sl.te, sc)); XCHK(grow(&sl.tl, sc)); XCHK(grow(&sl.tf, sc));
     XCHK(grow(&sl.cs, sc)); XCHK(grow(&sl.cl, sc)); XCHK(grow(&sl.ty, sc)); XCHK(grow(&sl.cnt, sc));
@@ -368,7 +383,15 @@ int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx, int
     *p = np;
     return hipSuccess;
   };
-  if (nsc != sc && sl.rec) XCHK(relayout(&sl.rec, sc, nsc, rows, n_ops));
+  if (nsc != sc && sl.kw) {  // key-interleaved: positions are the outer index, the old store is a prefix
+    unsigned long long* nw = nullptr;
+    XCHK(dalloc(&nw, (size_t)(nsc * XK_NF * rows)));
+    XCHK(hipMemsetAsync(nw, 0, (size_t)(nsc * XK_NF * rows) * 8, stream));
+    XCHK(hipMemcpyAsync(nw, sl.kw, (size_t)(sc * XK_NF * rows) * 8, hipMemcpyDeviceToDevice, stream));
+    XCHK(hipStreamSynchronize(stream));
+    dfree(sl.kw);
+    sl.kw = nw;
+  }
   if (nsc != sc && sl.ts) {
     XCHK(relayout(&sl.ts, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.te, sc, nsc, rows, n_ops));
     XCHK(relayout(&sl.tl, sc, nsc, rows, n_ops)); XCHK(relayout(&sl.tf, sc, nsc, rows, n_ops));
@@ -409,6 +432,8 @@ int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx, int
     ss.end = ns_end;
   }
   sc = (int32_t)nsc;
+  sl.sc_sh = 0;
+  while (((int64_t)1 << sl.sc_sh) < sc) sl.sc_sh++;
   sesscap = (int32_t)nss;
   ctx_alloc = nctx;
   rcap_ = nrc;
@@ -1010,14 +1035,24 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
   a.cfg = d_cfg;
   a.st = d_st;
   a.sl = sl;
+  // device time: the data pass over the tuples (class INGEST: histogram, scan, partition, per-(key, cell) fold),
+  // then the per-key commit (PUSH_OTHER)
+  TEv t0, t1;
+  int rc = tbegin(t0, SCOTTY_TIME_INGEST);
+  if (rc) return rc;
   XCHK(launch_kg_partition(a, vt, stream));
   XCHK(launch_scan_i32(d_kghist, d_kghist, nbk * ntiles, d_kgscan, stream));
   XCHK(launch_kg_scatter(a, vt, stream));
-  XCHK(launch_kg_bucket(a, vt, mm, n_ops, stream));
+  XCHK(launch_kg_bucket(a, vt, mm, n_ops, stream, 1));
+  if ((rc = tend(t0, n))) return rc;
+  if ((rc = tbegin(t1, SCOTTY_TIME_PUSH_OTHER))) return rc;
+  XCHK(launch_kg_bucket(a, vt, mm, n_ops, stream, 2));
   KgCtl* hc = (KgCtl*)h_kgctl;
   static_assert(sizeof(KgCtl) % 4 == 0, "KgCtl copied in words");
   XCHK(launch_copy_to_host(d_kgctl, h_kgctl_dev, sizeof(KgCtl), stream));
+  if ((rc = tend(t1, 0))) return rc;
   XCHK(hipStreamSynchronize(stream));
+  if (timing) collect_timing();
   (void)vb;
   *flag_out = hc->flag;
   if (hc->flag) return SCOTTY_OK;
@@ -1269,9 +1304,14 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     a.has_value = d_has;
     for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
     a.w_key = d_w_key;
+    TEv tw;
+    int rct = tbegin(tw, SCOTTY_TIME_WATERMARK);
+    if (rct) return rct;
     XCHK(launch_lane_wm_emit(a, true, stream));
     XCHK(launch_copy_to_host(d_misc, h_misc_dev, 4 * 8, stream));
+    if ((rct = tend(tw, 0))) return rct;
     XCHK(hipStreamSynchronize(stream));
+    if (timing) collect_timing();
     prefix_stale = false;
     have_wm = true;
     last_wm = wm;
@@ -1443,15 +1483,17 @@ int XEngine::debug_dump(int64_t op, std::vector<int64_t>& out) {
     out.insert(out.end(), tmp.begin(), tmp.begin() + S);
     return SCOTTY_OK;
   };
-  if (S > 0 && sl.rec) {  // record store: the same columns, unpacked
-    std::vector<XSliceRec> rr(S);
-    XCHK(hipMemcpy(rr.data(), sl.rec + b, S * sizeof(XSliceRec), hipMemcpyDeviceToHost));
-    for (auto f : {&XSliceRec::ts, &XSliceRec::te, &XSliceRec::tl})
-      for (int64_t i = 0; i < S; i++) out.push_back(rr[i].*f);
-    for (int64_t i = 0; i < S; i++) out.push_back((int64_t)rr[i].cnt);
-    for (auto f : {&XSliceRec::cs, &XSliceRec::cl})
-      for (int64_t i = 0; i < S; i++) out.push_back(rr[i].*f);
-    for (int64_t i = 0; i < S; i++) out.push_back(rr[i].ty);
+  if (S > 0 && sl.kw) {  // key-interleaved store: the same columns, gathered (one word per position and field)
+    const int64_t kc = (int64_t)1 << sl.kc_sh;
+    auto kcol = [&](int f, bool ty32) -> int {
+      XCHK(hipMemcpy2D(tmp.data(), 8, sl.kw + ((s.head * (int64_t)XK_NF + f) << sl.kc_sh) + op, XK_NF * kc * 8, 8, S,
+                       hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < S; i++) out.push_back(ty32 ? (int64_t)(int32_t)tmp[i] : tmp[i]);
+      return SCOTTY_OK;
+    };
+    for (int f : {XK_TS, XK_TE, XK_TL, XK_CNT, XK_CS, XK_CL})
+      if (kcol(f, false)) return SCOTTY_ERR_HIP;
+    if (kcol(XK_TY, true)) return SCOTTY_ERR_HIP;
   } else if (S > 0) {
     if (col(sl.ts) || col(sl.te) || col(sl.tl) || col(sl.cnt) || col(sl.cs) || col(sl.cl)) return SCOTTY_ERR_HIP;
     XCHK(hipMemcpy(ty.data(), sl.ty + b, S * 4, hipMemcpyDeviceToHost));

@@ -866,28 +866,30 @@ hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hipStream_t st) {
+// which: 1 the bucket kernel, 2 the commit kernel (3 both, in that order)
+hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hipStream_t st, int which) {
   const dim3 grid((unsigned)a.nbk), block(1024);
   const dim3 cgrid((unsigned)((n_ops + 255) / 256)), cblock(256);
-  if (a.sl.rec) {  // record store: COUNT / integer SUM only
+  const bool B = (which & 1) != 0, C = (which & 2) != 0;
+  if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM only
     if (vt == VT_I32) {
-      hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false>), grid, block, 0, st, a);
-      hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, false, XRecView>), cgrid, cblock, 0, st, a, n_ops);
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false>), grid, block, 0, st, a);
+      if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, false, XKView>), cgrid, cblock, 0, st, a, n_ops);
     } else {
-      hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I64, false>), grid, block, 0, st, a);
-      hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I64, false, XRecView>), cgrid, cblock, 0, st, a, n_ops);
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I64, false>), grid, block, 0, st, a);
+      if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I64, false, XKView>), cgrid, cblock, 0, st, a, n_ops);
     }
     return hipGetLastError();
   }
-#define SCOTTY_KG(V)                                                                              \
-  do {                                                                                            \
-    if (mm) {                                                                                     \
-      hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<V, true>), grid, block, 0, st, a);             \
-      hipLaunchKernelGGL((kg::kg_commit_kernel<V, true, XSlices>), cgrid, cblock, 0, st, a, n_ops);  \
-    } else {                                                                                      \
-      hipLaunchKernelGGL((kg::kg_bucket_kernel<V, false>), grid, block, 0, st, a);               \
-      hipLaunchKernelGGL((kg::kg_commit_kernel<V, false, XSlices>), cgrid, cblock, 0, st, a, n_ops); \
-    }                                                                                             \
+#define SCOTTY_KG(V)                                                                                   \
+  do {                                                                                                 \
+    if (mm) {                                                                                          \
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<V, true>), grid, block, 0, st, a);           \
+      if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<V, true, XSlices>), cgrid, cblock, 0, st, a, n_ops);  \
+    } else {                                                                                           \
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<V, false>), grid, block, 0, st, a);             \
+      if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<V, false, XSlices>), cgrid, cblock, 0, st, a, n_ops); \
+    }                                                                                                  \
   } while (0)
   if (vt == VT_I32) SCOTTY_KG(VT_I32);
   else if (vt == VT_I64) SCOTTY_KG(VT_I64);

@@ -551,9 +551,9 @@ hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStre
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
   const bool mm = (host_cfg.need & (NEED_MIN | NEED_MAX)) != 0;
   const int vt = host_cfg.vt;
-  if (a.sl.rec) {  // record store: COUNT / integer SUM only (no MIN / MAX, no f64)
-    if (vt == VT_I32) hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I32, false, XRecView>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I64, false, XRecView>), grid, block, 0, st, a);
+  if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM only (no MIN / MAX, no f64)
+    if (vt == VT_I32) hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I32, false, XKView>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I64, false, XKView>), grid, block, 0, st, a);
     return hipGetLastError();
   }
 #define SCOTTY_LANE(V, M) hipLaunchKernelGGL((ln::lane_replay_kernel<V, M, XSlices>), grid, block, 0, st, a)
@@ -566,14 +566,14 @@ hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStre
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
-  if (a.sl.rec) hipLaunchKernelGGL(ln::lane_wm_count_kernel<XRecView>, grid, block, 0, st, a);
+  if (a.sl.kw) hipLaunchKernelGGL(ln::lane_wm_count_kernel<XKView>, grid, block, 0, st, a);
   else hipLaunchKernelGGL(ln::lane_wm_count_kernel<XSlices>, grid, block, 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
   const dim3 grid((unsigned)((a.n_ops + ln::EMIT_T - 1) / ln::EMIT_T)), block(ln::EMIT_T);
-  if (a.sl.rec) hipLaunchKernelGGL((ln::lane_wm_emit_kernel<true, XRecView>), grid, block, 0, st, a);
+  if (a.sl.kw) hipLaunchKernelGGL((ln::lane_wm_emit_kernel<true, XKView>), grid, block, 0, st, a);
   else if (agg) hipLaunchKernelGGL((ln::lane_wm_emit_kernel<true, XSlices>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((ln::lane_wm_emit_kernel<false, XSlices>), grid, block, 0, st, a);
   return hipGetLastError();
