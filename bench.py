@@ -380,6 +380,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
             "ms_per_step_each": [round(1e3 * t, 4) for t in times],
             "quiet_steps": sum(1 for x in verdicts if x == 1), "event_exact_steps": sum(1 for x in verdicts if x != 1),
+            "event_prefix_then_quiet_steps": op._debug_stat(12),
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
             "roofline": roof,
             "roofline_wall": {"achieved": batch * BYTES_PER_TUPLE * len(times) / sum(times) / 1e9,

@@ -118,7 +118,7 @@ void XEngine::release() {
   dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
   dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
   dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
-  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_rank); dfree(d_xq_flag);
+  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_stepmax); dfree(d_xq_rank); dfree(d_xq_flag);
   for (int k = 0; k < NPART; k++) dfree(d_xq_cpart[k]);
   dfree(d_xq_eg); dfree(d_xq_epos); dfree(d_xq_meta); dfree(d_xq_cix); dfree(d_xq_cixmeta); dfree(d_xq_ctl);
   for (auto& e : ev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -531,21 +531,48 @@ int XEngine::push(const int64_t* d_ts, const void* d_val, int64_t n) {
 // is then classified again against the updated operator (rounds are rare: record-breaking session growth).
 int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
   const size_t vb = vt == VT_I32 ? 4 : 8;
-  int64_t pos0 = 0;
   last_events = 0;
   last_segments = 0;
   last_quiet = 0;
-  if (n > 0 && quiet_eligible()) {
-    int32_t res = XQ_NONE;
-    int rc = push_quiet(d_ts, d_val, n, &res);
-    if (rc) return rc;
-    last_quiet = res;
-    if (res == XQ_COMMITTED) {
-      quiet_commits++;
-      return SCOTTY_OK;
+  // The batch is processed in consecutive pieces, which the sequential reference cannot tell from one batch: the
+  // quiet path takes the rest of the batch in one pass when it can; when it cannot, the event-exact path takes a
+  // prefix and the quiet path is tried again on what follows.  A batch whose session structure changes only near its
+  // start (the stream resuming after a silence: a new session whose start moves down with the first out-of-order
+  // tuples) costs one short event-exact prefix, not rounds over the whole batch.  The prefix grows 4x with every
+  // further refusal, so a batch that is not quiet anywhere reaches the event-exact path for all of it quickly.
+  int64_t pos0 = 0;
+  int64_t chunk = std::max<int64_t>(n / 32, (int64_t)1 << 20);
+  chunk = (chunk + 4095) & ~(int64_t)4095;  // pieces start 16-byte aligned (the ingest's vector loads)
+  while (pos0 < n) {
+    const int64_t rest = n - pos0;
+    const unsigned char* val0 = (const unsigned char*)d_val + pos0 * vb;
+    if (quiet_eligible()) {
+      int32_t res = XQ_NONE;
+      int rc = push_quiet(d_ts + pos0, val0, rest, &res);
+      if (rc) return rc;
+      if (pos0 == 0) last_quiet = res;  // the batch's own verdict (a committed remainder is counted below)
+      else if (res == XQ_COMMITTED) quiet_tail_commits++;
+      if (res == XQ_COMMITTED) {
+        quiet_commits++;
+        return SCOTTY_OK;
+      }
+      quiet_fallbacks++;
     }
-    quiet_fallbacks++;
+    const int64_t w = quiet_eligible() && chunk < rest ? chunk : rest;
+    int rc = push_exact(d_ts + pos0, val0, w);
+    if (rc) return rc;
+    pos0 += w;
+    chunk *= 4;
   }
+  return SCOTTY_OK;
+}
+
+// Event-exact batch path over [0, n): classify (all CUs) -> compacted events (one wave, exact) -> apply (all CUs).  A
+// round ends at the first out-of-order event that may modify sessions / older slices; the rest is then classified
+// again against the updated operator (rounds are rare: record-breaking session growth).
+int XEngine::push_exact(const int64_t* d_ts, const void* d_val, int64_t n) {
+  const size_t vb = vt == VT_I32 ? 4 : 8;
+  int64_t pos0 = 0;
   TEv tx;
   int rct = tbegin(tx, SCOTTY_TIME_PUSH_OTHER);
   if (rct) return rct;
@@ -561,11 +588,6 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
     if (rc) return rc;
     last_segments++;
     if (stop < 0) break;
-    if (stop == 0 && round > 0 && false) {
-      err = "event pass made no progress";
-      failed = true;
-      return SCOTTY_ERR_STATE;
-    }
     pos0 += stop;
     if (round > 4 * n + 16) {
       err = "event pass made no progress";
@@ -729,6 +751,13 @@ int XEngine::xq_ensure(int64_t n) {
     xq_tcap = std::max<int64_t>(nt, 1024);
     XCHK(dalloc(&d_xq_tilemax, xq_tcap));
   }
+  const int64_t ns = n / 256 + 2;
+  if (ns > xq_scap) {
+    XCHK(hipStreamSynchronize(stream));
+    dfree(d_xq_stepmax);
+    xq_scap = std::max<int64_t>(ns, 4096);
+    XCHK(dalloc(&d_xq_stepmax, xq_scap));
+  }
   return SCOTTY_OK;
 }
 
@@ -762,6 +791,7 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   ia.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) ia.c_part[k] = d_xq_cpart[k];
   ia.tilemax = d_xq_tilemax;
+  ia.stepmax = d_xq_stepmax;
   ia.meta = d_xq_meta;
   ia.per_wave = per_wave;
   ia.tile = tile;
@@ -783,12 +813,17 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   q.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) q.c_part[k] = d_xq_cpart[k];
   q.tilemax = d_xq_tilemax;
+  q.stepmax = d_xq_stepmax;
   q.rank = d_xq_rank;
   q.flag = d_xq_flag;
   q.eg = d_xq_eg;
   q.epos = d_xq_epos;
   q.ctl = (XQCtl*)d_xq_ctl;
   q.margin = std::max<int64_t>(16 * xq_span, 60000);
+  static long long* d_xq_dbg = nullptr;
+  const bool prof = getenv("SCOTTY_XQ_PROF") != nullptr;
+  if (prof && !d_xq_dbg) XCHK(hipMalloc(&d_xq_dbg, 16 * 8));
+  q.dbg = prof ? d_xq_dbg : nullptr;
   TEv t0, t1, t2;
   if ((rc = tbegin(t0, SCOTTY_TIME_PUSH_OTHER))) return rc;
   XCHK(launch_xq_prep(q, stream));
@@ -803,6 +838,13 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   XCHK(launch_copy_to_host(d_xq_ctl, h_misc_dev, sizeof(XQCtl), stream));
   if ((rc = tend(t2, 0))) return rc;
   XCHK(hipStreamSynchronize(stream));
+  if (prof) {  // debugging aid: s_memtime deltas between the commit's phases
+    long long h[16];
+    XCHK(hipMemcpy(h, d_xq_dbg, sizeof(h), hipMemcpyDeviceToHost));
+    fprintf(stderr, "xq commit phase ticks:");
+    for (int i = 1; i <= 7; i++) fprintf(stderr, " %lld", h[i] - h[i - 1]);
+    fprintf(stderr, "\n");
+  }
   XQCtl c;
   std::memcpy(&c, h_misc, sizeof(XQCtl));
   *result = c.result;

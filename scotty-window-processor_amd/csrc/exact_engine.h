@@ -43,11 +43,12 @@ class XEngine {
   int push(const int64_t* d_ts, const void* d_val, int64_t n);
   int push_keyed(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n);
   int push_batch(const int64_t* d_ts, const void* d_val, int64_t n);  // non-keyed, batch-parallel
+  int push_exact(const int64_t* d_ts, const void* d_val, int64_t n);  // event-exact rounds over [0, n)
   // non-keyed one-pass path (exact_quiet.hip): *result = XQ_COMMITTED, or why the batch needs the event-exact path
   int push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32_t* result);
   bool quiet_eligible() const;
   bool quiet_off = false;      // A/B: every non-keyed batch through the event-exact path
-  int64_t quiet_commits = 0, quiet_fallbacks = 0;
+  int64_t quiet_commits = 0, quiet_fallbacks = 0, quiet_tail_commits = 0;
   int32_t last_quiet = 0;      // XQ_* verdict of the last non-keyed push (0: not attempted)
   int64_t last_quiet_why = 0;  // XQCtl.why of the last verdict
   // device time of the last pushes by class (HIP events; scotty_device_timing): 0 quiet ingest, 1 other push work
@@ -201,12 +202,13 @@ class XEngine {
   int tbegin(TEv& e, int cls);
   int tend(TEv& e, int64_t n);
   std::vector<int64_t> xq_hgrid;
-  int64_t xq_gcap = 0, xq_ccap = 0, xq_tcap = 0;
+  int64_t xq_gcap = 0, xq_ccap = 0, xq_tcap = 0, xq_scap = 0;
   int64_t* d_xq_grid = nullptr;
   unsigned long long* d_xq_ccnt = nullptr;
   long long* d_xq_ctmax = nullptr;
   unsigned long long* d_xq_cpart[NPART] = {};
   long long* d_xq_tilemax = nullptr;
+  long long* d_xq_stepmax = nullptr;  // the quiet ingest's 256-tuple step maxima (candidate first crossings)
   int32_t *d_xq_rank = nullptr, *d_xq_flag = nullptr;
   int64_t *d_xq_eg = nullptr, *d_xq_epos = nullptr;
   DevMeta* d_xq_meta = nullptr;

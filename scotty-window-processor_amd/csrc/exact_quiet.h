@@ -62,12 +62,14 @@ struct XQArgs {
   long long* c_tmax;
   unsigned long long* c_part[NPART];
   long long* tilemax;
+  long long* stepmax;    // max ts of every 256-tuple arrival step, written by the ingest
   int32_t* rank;         // scratch [gcap]
   int32_t* flag;         // scratch [gcap]
   int64_t* eg;           // scratch [gcap]: emitted edges by rank
   int64_t* epos;         // scratch [gcap]: arrival index of the tuple that appends each emitted edge
   XQCtl* ctl;
   int64_t margin;        // grid horizon margin (ms past the stream front) below which a rebuild is requested
+  long long* dbg;        // nullable: clock stamps of the commit's phases (SCOTTY_XQ_PROF, a debugging aid)
 };
 
 hipError_t launch_xq_prep(const XQArgs& a, hipStream_t st);

@@ -116,6 +116,23 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
       why |= 1024;
     }
   }
+  if (res == XQ_NONE && c->n_ctx > 0 && a.n > 0) {
+    // fast refusal: one of the first 64 tuples jumps its running max by a session gap (a new session: the stream
+    // resumes after a silence) -- the batch is not quiet, and the ingest pass is skipped
+    const int64_t v = lane < a.n ? a.ts[lane] : JMIN;
+    int64_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+      if (lane >= o) inc = max(inc, u);
+    }
+    int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
+    ex = lane == 0 ? P : max(P, ex);
+    if (__ballot(lane < a.n && v != JMIN && !(ex <= JMAX - min_gap && v < ex + min_gap)) != 0) {
+      res = XQ_NOT_QUIET;
+      why |= 4;
+    }
+  }
   if (lane == 0) {
     DevMeta m{};
     m.head = h0;
@@ -176,6 +193,10 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
   __shared__ long long s_w[32];
   __shared__ int64_t sc[8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto stamp = [&](int k) {
+    if (a.dbg && tid == 0) a.dbg[k] = (long long)__builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   const XQCtl q = *a.ctl;
   if (q.result != XQ_NONE) return;  // refused by the prep kernel: no cell was touched
   const XCfg* cfg = a.cfg;
@@ -211,6 +232,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
   }
   __syncthreads();
   const int64_t batch_max = max(P, nT > 0 ? (int64_t)s_p[nT - 1] : JMIN);
+  stamp(1);
 
   // ---- quiet verdict
   bool fail = false;
@@ -234,9 +256,15 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     // no in-order jump by a gap: items after a tile's first are below max(carry, first) + gap; the first is below
     // carry + gap (carry = running max before the tile).  A tile failing this bound (a slow stream: the tile spans
     // more than a gap of event time) is checked item by item below.
+    int64_t t0s[NT_MAX / 1024];  // every tile start loaded before the checks: one round trip, not one per tile
+#pragma unroll
+    for (int j = 0; j < NT_MAX / 1024; j++) {
+      const int64_t t = tid + (int64_t)j * 1024;
+      t0s[j] = t < nT ? a.ts[t * tile] : JMIN;
+    }
     for (int64_t t = tid; t < nT; t += 1024) {
       const int64_t carry = t > 0 ? max(P, (int64_t)s_p[t - 1]) : P;
-      const int64_t t0 = a.ts[t * tile], tm = a.tilemax[t];
+      const int64_t t0 = t0s[(t - tid) >> 10], tm = a.tilemax[t];
       if (!lt_plus(t0, carry, q.min_gap)) {
         fail = true;
         atomicOr(&s_why, 4);
@@ -282,6 +310,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     fail = __syncthreads_or(fail);
   }
 
+  stamp(2);
   // ---- candidates: grid points g[k] <= batch_max (k < kc)
   if (wid == 0) {
     int64_t lo = 0, hi = fail ? 0 : kc;  // first k with g[k] > batch_max
@@ -311,6 +340,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
   }
   __syncthreads();
   const int64_t ncand = sc[0];
+  stamp(3);
 
   // ---- edge decision (StreamSlicer.determineSlices, S/StreamSlicer.java:55-84; see commit_kernel): a grid point g
   //      first reached by the in-order tuple e (running max m before it) becomes an edge iff g == nextGrid(m) or
@@ -320,7 +350,23 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     const int64_t gk = g[k];
     const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
     int64_t r = ts_ > 0 ? max(P, (int64_t)s_p[ts_ - 1]) : P;
-    const int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
+    int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
+    {  // narrow to the tile's first 256-tuple arrival step holding a tuple >= gk (the ingest's step maxima)
+      const int64_t s0 = e0 >> 8, s1 = (e1 + 255) >> 8;
+      for (int64_t sb = s0; sb < s1; sb += 64) {
+        const int64_t si = sb + lane;
+        const int64_t v = si < s1 ? (int64_t)a.stepmax[si] : JMIN;
+        const unsigned long long hit = __ballot(v >= gk);
+        if (hit) {
+          const int f = __ffsll((long long)hit) - 1;
+          r = max(r, wmax(lane < f ? v : JMIN));
+          e0 = (sb + f) << 8;
+          e1 = min(a.n, e0 + 256);
+          break;
+        }
+        r = max(r, wmax(v));
+      }
+    }
     int64_t e = JMIN, mm = JMIN, pos = -1;
     constexpr int B = 16;
     for (int64_t base = e0; base < e1 && pos < 0; base += 64 * B) {
@@ -361,6 +407,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
   }
   __syncthreads();
 
+  stamp(4);
   // ---- rank = inclusive prefix count of emitted edges
   int64_t n_emit = 0;
   {
@@ -391,6 +438,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     n_emit = base_cnt;
   }
   int32_t result = XQ_COMMITTED;
+  stamp(5);
   if (fail) result = XQ_NOT_QUIET;
   else if (tail + n_emit > cfg->sc) result = XQ_CAPACITY;
   __syncthreads();
@@ -438,6 +486,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     sl.ty[pv] = XTYPE_FIXED | (sl.ty[pv] & XTYPE_LAZY);
   }
   __syncthreads();
+  stamp(6);
   // ---- cells into slices (AbstractSlice.addElement + AggregateState.addElement), cells back to identity
   for (int64_t c = cfirst + tid; c < ncell; c += 1024) {
     const unsigned long long cnt = a.c_cnt[c];
@@ -464,6 +513,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     a.c_part[1][c] = (unsigned long long)ID_MIN;
     a.c_part[2][c] = (unsigned long long)ID_MAX;
   }
+  stamp(7);
   // ---- scalars: StreamSlicer.maxEventTime / min_next_edge_ts, WindowManager.currentCount, and the last session of
   //      every context extended to the batch max (every in-order tuple is within a gap of it: shiftEnd)
   if (tid == 0) {

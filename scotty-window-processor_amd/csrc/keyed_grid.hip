@@ -336,6 +336,136 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   }
 }
 
+// The same scatter as a persistent, software-pipelined kernel (variant 4): one workgroup per CU walks its tiles
+// with the NEXT tile's loads (keys, timestamps, values, run bases) in flight in a second register set while the
+// current tile goes through its LDS phases (rank, scan, stage, write-out).  The one-tile-per-workgroup form leaves
+// the CU's memory pipe idle during those phases (one workgroup fits a CU: its 120 KB of LDS).  Plain loads survive
+// __syncthreads (no LDS-DMA in flight), so the prefetch spans the barriers.  Tiles of an XCD are consecutive: the
+// 32 workgroups of an XCD write adjacent runs of every bucket at the same time, which meet in its L2.
+template <int IT>
+struct KTile {  // one tile's inputs in registers
+  uint32_t k[IT];
+  int64_t t[IT];
+  uint32_t v[IT];
+};
+template <int T, int NBS, int ST>
+__global__ __launch_bounds__(ST) void kg_scatter_pipe_kernel(KgArgs a) {
+  constexpr int IT = T / ST;
+  constexpr int PER = NBS / ST;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[T * 3];
+  __shared__ int32_t cnt[NBS + 1], tst[NBS], base[NBS];
+  __shared__ int32_t wsum[ST / 64];
+  __shared__ long long g_first[T / 64], g_last[T / 64];  // first / last ts of each 64-tuple group (order check)
+  if (a.ctl->flag) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t f = a.ctl->ts_first;
+  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
+  const int64_t per = (a.ntiles + 7) >> 3;
+  const int64_t t_end = min((int64_t)a.ntiles, (xcd + 1) * per);
+  auto load = [&](KTile<IT>& x, int32_t (&bs)[PER], int64_t tile) {
+    const int64_t i0 = tile * T;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      const int64_t i = i0 + j * ST + tid;
+      const int64_t ic = i < a.n ? i : a.n - 1;
+      x.k[j] = __builtin_nontemporal_load(a.key + ic);
+      x.t[j] = a.ts[ic];
+      x.v[j] = (uint32_t)((const int32_t*)a.val)[ic];
+    }
+#pragma unroll
+    for (int p = 0; p < PER; p++) {
+      const int b = tid * PER + p;
+      bs[p] = a.hist[(int64_t)(b < a.nbk ? b : 0) * a.ntiles + tile];
+    }
+  };
+  auto process = [&](const KTile<IT>& x, const int32_t (&bs)[PER], int64_t tile) {
+    const int64_t i0 = tile * T;
+    __syncthreads();  // the previous tile's write-out has read stage / tst / base
+#pragma unroll
+    for (int p = 0; p < PER; p++) {
+      const int b = tid * PER + p;
+      if (b < a.nbk) {
+        cnt[b] = 0;
+        base[b] = bs[p];
+      }
+    }
+    __syncthreads();
+    int32_t bk[IT], rk[IT];
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      const int64_t i = i0 + j * ST + tid;
+      const bool in = i < a.n;
+      // order inside the 64-tuple group from the neighbour lane; across groups through LDS below
+      const int64_t prev = (int64_t)__shfl_up((long long)x.t[j], 1);
+      bad |= in && lane > 0 && prev > x.t[j];
+      if (lane == 0) g_first[j * (ST / 64) + wid] = in ? x.t[j] : JMAX;
+      if (lane == 63) g_last[j * (ST / 64) + wid] = x.t[j];
+      bk[j] = in ? (int32_t)bucket_of(x.k[j], a.kmask) : NBS;
+      rk[j] = atomicAdd(&cnt[bk[j]], 1);
+    }
+    __syncthreads();
+    // group g + 1 follows group g in arrival order; the tile's first tuple follows the tuple before the tile
+    if (tid < T / 64) {
+      const int64_t pl = tid > 0 ? (int64_t)g_last[tid - 1] : (i0 > 0 ? a.ts[i0 - 1] : JMIN);
+      bad |= pl > (int64_t)g_first[tid];
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(&a.ctl->flag, KG_UNSORTED);
+    int32_t loc[PER], s = 0;
+#pragma unroll
+    for (int p = 0; p < PER; p++) {
+      const int idx = tid * PER + p;
+      loc[p] = s;
+      s += idx < a.nbk ? cnt[idx] : 0;
+    }
+    int32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int32_t ex = inc - s;
+    for (int w = 0; w < wid; w++) ex += wsum[w];
+#pragma unroll
+    for (int p = 0; p < PER; p++) {
+      const int idx = tid * PER + p;
+      if (idx < a.nbk) tst[idx] = ex + loc[p];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IT; j++)
+      if (bk[j] < NBS) {
+        const KRec<4> r{x.k[j], (uint32_t)(x.t[j] - f), x.v[j]};
+        r.store_lds(stage, tst[bk[j]] + rk[j]);
+      }
+    __syncthreads();
+    const int nt = (int)min((int64_t)T, a.n - i0);
+    for (int i = tid; i < nt; i += ST) {
+      const KRec<4> r = KRec<4>::load_lds(stage, i);
+      const uint32_t b = bucket_of(r.key(), a.kmask);
+      r.store(a.rec, (int64_t)base[b] + (i - tst[b]));
+    }
+  };
+  int64_t t0 = xcd * per + q;
+  if (t0 >= t_end) return;
+  KTile<IT> A, B;
+  int32_t ba[PER], bb[PER];
+  load(A, ba, t0);
+  for (;;) {
+    const int64_t t1 = t0 + nq;
+    if (t1 < t_end) load(B, bb, t1);
+    process(A, ba, t0);
+    if (t1 >= t_end) break;
+    const int64_t t2 = t1 + nq;
+    if (t2 < t_end) load(A, ba, t2);
+    process(B, bb, t1);
+    if (t2 >= t_end) break;
+    t0 = t2;
+  }
+}
+
 // The same scatter in 72 KB of LDS (two workgroups per CU): one bucket array serves as the rank counters, then
 // (scanned in place) as the tile-local run starts, then as each run's global start minus its tile-local start.
 template <int T, int NBS, int ST>
@@ -437,18 +567,19 @@ __device__ __forceinline__ unsigned long long add_sum(unsigned long long acc, un
 // One workgroup per bucket: probe the bucket's slice of the key table in LDS, fold the bucket's records into
 // per-(key, cell) partials with LDS atomics, write the partials of every touched key to its slot (KPart).
 // Records whose key is not in the table (new keys, or probed past the spill) are marked for the replay path.
-template <int VT, bool MM>
+template <int VT, bool MM, int U>
 __device__ __forceinline__ void kg_bucket_body(const KgArgs& a);
 // COUNT / SUM: 74 KB of LDS and <= 64 VGPRs, two workgroups per CU; MIN / MAX: one (87 KB)
-template <int VT, bool MM>
+template <int VT, bool MM, int U = 2>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void kg_bucket_kernel(KgArgs a) {
-  kg_bucket_body<VT, MM>(a);
+  kg_bucket_body<VT, MM, U>(a);
 }
 template <int VT, bool MM>
 __global__ __launch_bounds__(1024) void kg_bucket_mm_kernel(KgArgs a) {
-  kg_bucket_body<VT, MM>(a);
+  kg_bucket_body<VT, MM, 2>(a);
 }
-template <int VT, bool MM>
+// U: records loaded per round before they are folded (U loads in flight per lane)
+template <int VT, bool MM, int U>
 __device__ __forceinline__ void kg_bucket_body(const KgArgs& a) {
   constexpr int CM = MM ? 2 : 3;
   constexpr int VB = VT == VT_I32 ? 4 : 8;
@@ -503,7 +634,6 @@ __device__ __forceinline__ void kg_bucket_body(const KgArgs& a) {
       atomicMax(&L.vmax[q], (long long)mx);
     }
   };
-  constexpr int U = 2;  // records loaded per round before they are folded: 2 loads in flight per lane
   int64_t r = r0 + tid;
   for (; r + (U - 1) * nt < r1; r += U * nt) {
     KRec<VB> rc[U];
@@ -853,6 +983,10 @@ hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st) {
     hipLaunchKernelGGL((kg::kg_scatter2_kernel<5632, 2048, 512>), dim3(grid), dim3(512), 0, st, a);
     return hipGetLastError();
   }
+  if (vt == VT_I32 && a.tile == 8192 && a.variant >= 4) {  // persistent: one workgroup per CU (256 CUs)
+    hipLaunchKernelGGL((kg::kg_scatter_pipe_kernel<8192, 2048, 1024>), dim3(256), dim3(1024), 0, st, a);
+    return hipGetLastError();
+  }
   if (vt == VT_I32) {
     if (a.tile == 8192 && a.variant == 1)
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 1024>), dim3(grid), dim3(1024), 0, st, a);
@@ -873,7 +1007,9 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
   const bool B = (which & 1) != 0, C = (which & 2) != 0;
   if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM only
     if (vt == VT_I32) {
-      if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false>), grid, block, 0, st, a);
+      if (B && a.variant == 5) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 4>), grid, block, 0, st, a);
+      else if (B && a.variant == 6) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 8>), grid, block, 0, st, a);
+      else if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false>), grid, block, 0, st, a);
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, false, XKView>), cgrid, cblock, 0, st, a, n_ops);
     } else {
       if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I64, false>), grid, block, 0, st, a);

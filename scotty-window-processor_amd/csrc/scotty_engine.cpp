@@ -1485,7 +1485,7 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only)
-    if (op->mode != 0 || value < 0 || value > 3) return SCOTTY_ERR_ARG;
+    if (op->mode != 0 || value < 0 || value > 6) return SCOTTY_ERR_ARG;
     op->x_kg_variant = (int32_t)value;
     if (op->x) op->x->kg_variant = op->x_kg_variant;
     return SCOTTY_OK;
@@ -1547,6 +1547,7 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 9: return op->x->quiet_commits;
     case 10: return op->x->quiet_fallbacks;
     case 11: return op->x->last_quiet_why;
+    case 12: return op->x->quiet_tail_commits;  // batches whose remainder committed after an event-exact prefix
     default: return -1;
   }
 }

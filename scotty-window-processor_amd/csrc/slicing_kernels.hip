@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "device_common.h"
@@ -446,7 +447,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   acc.reset();
   int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
   uint32_t n_late = 0, n_ovf = 0, n_glb = 0;
-  int64_t tile_max = INT64_MIN;
+  int64_t tile_max = INT64_MIN, step_max = INT64_MIN;
   int64_t cmin = INT64_MAX;  // lowest cell this wave added to outside the LDS window (commit folds from there)
   int qn = 0;                // deferred queue fill (wave-uniform)
 
@@ -472,11 +473,24 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     acc.reset();
   };
 
+  // one tuple into a window cell.  tmax / min / max only move one way, so the atomic is skipped when a plain LDS
+  // read already holds a value at least as good (a stale read only costs a redundant atomic): out-of-order tuples
+  // concentrate on the few cells behind the stream front, where same-address LDS atomics serialise lane by lane
   auto lds_one = [&](int64_t l, int64_t t, V v) {
     Acc<VT, NEED> one;
     one.reset();
     one.add(t, v);
-    lds_add<VT, NEED>(w, l, 1u, t, one.sum_word(), one.sum_f(), one.mn, one.mx);
+    atomicAdd(&w.cnt[l], 1u);
+    if (t > (int64_t)w.tmax[l]) atomicMax(&w.tmax[l], (long long)t);
+    if constexpr ((NEED & NEED_SUM) != 0) {
+      if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[l], one.sum_f());
+      else if constexpr (VT == VT_I32) atomicAdd(&w.sum[l], (uint32_t)one.sum_word());
+      else atomicAdd(&w.sum[l], (unsigned long long)one.sum_word());
+    }
+    if constexpr ((NEED & NEED_MIN) != 0)
+      if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (long long)one.mn);
+    if constexpr ((NEED & NEED_MAX) != 0)
+      if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (long long)one.mx);
   };
 
   auto slow = [&](int64_t t, V v) {
@@ -497,11 +511,50 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     }
   };
 
-  // fold the deferred queue: 64 entries per pass, every lane one lookup + one set of LDS atomics
+  // fold the deferred queue: 64 entries per pass, every lane one lookup + one set of LDS atomics.  MODE bit 3: the
+  // counts of lanes that hit the same cell are added by one atomic per cell (up to 8 cells per pass, the rest per lane):
+  // out-of-order tuples behind a stream of wide cells fall on a few cells, where per-lane same-address atomics
+  // serialise
+  constexpr bool GROUP = (MODE & 8) != 0;
   auto drain = [&]() {
     for (int b = 0; b < qn; b += 64) {
       const int e = b + lane;
-      if (e < qn) {
+      const bool valid = e < qn;
+      if constexpr (GROUP) {
+        int64_t t = 0, l = -1;
+        V v{};
+        if (valid) {
+          t = tw0 + (int64_t)q_t[e];
+          v = q_v[e];
+          l = wfind(t);
+        }
+        unsigned long long pending = __ballot(valid);
+        bool counted = false;
+        for (int it = 0; it < 8 && pending; it++) {
+          const int lead = __ffsll((long long)pending) - 1;
+          const int64_t lc = rl64(l, lead);
+          const unsigned long long same = __ballot(valid && l == lc) & pending;
+          if (lane == lead) atomicAdd(&w.cnt[lc], (uint32_t)__popcll(same));
+          counted |= ((same >> lane) & 1) != 0;
+          pending &= ~same;
+        }
+        if (valid) {
+          Acc<VT, NEED> one;
+          one.reset();
+          one.add(t, v);
+          if (!counted) atomicAdd(&w.cnt[l], 1u);
+          if (t > (int64_t)w.tmax[l]) atomicMax(&w.tmax[l], (long long)t);
+          if constexpr ((NEED & NEED_SUM) != 0) {
+            if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[l], one.sum_f());
+            else if constexpr (VT == VT_I32) atomicAdd(&w.sum[l], (uint32_t)one.sum_word());
+            else atomicAdd(&w.sum[l], (unsigned long long)one.sum_word());
+          }
+          if constexpr ((NEED & NEED_MIN) != 0)
+            if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (long long)one.mn);
+          if constexpr ((NEED & NEED_MAX) != 0)
+            if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (long long)one.mx);
+        }
+      } else if (valid) {
         const int64_t t = tw0 + (int64_t)q_t[e];
         lds_one(wfind(t), t, q_v[e]);
       }
@@ -571,7 +624,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     uint32_t sm = 0;  // tuples outside the wave's current cell take the slow path, one code copy for all four
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      tile_max = max(tile_max, t[j]);
+      step_max = max(step_max, t[j]);
       if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
       else sm |= 1u << j;
     }
@@ -600,7 +653,13 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       slow(tj, vj);
     }
   };
-  auto tile_done = [&](int64_t s) {
+  auto tile_done = [&](int64_t s) {  // end of the step at s: step and tile maxima
+    if (a.stepmax) {
+      const int64_t sm_ = wmax64(step_max);
+      if (lane == 0) a.stepmax[s >> 8] = sm_;
+    }
+    tile_max = max(tile_max, step_max);
+    step_max = INT64_MIN;
     const int64_t done = s + 256;
     if (((done - w0) & (a.tile - 1)) == 0 || done >= w1) {
       int64_t tm = wmax64(tile_max);
@@ -662,7 +721,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       if (idx[j] < w1) {
         int64_t tj = a.ts[idx[j]];
         V vj = vp[idx[j]];
-        tile_max = max(tile_max, tj);
+        step_max = max(step_max, tj);
         if (tj >= lo && tj < hi) acc.add(tj, vj);
         else slow(tj, vj);
       }
@@ -1303,6 +1362,18 @@ hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode) {
+  static const int env_mode = [] {  // A/B of ingest variants on any int32 SUM or MIN|MAX configuration
+    const char* e = getenv("SCOTTY_INGEST_MODE");
+    return e ? atoi(e) : -1;
+  }();
+  if (mode < 0 && env_mode >= 0 && vt == VT_I32 && need == (NEED_MIN | NEED_MAX)) {
+    switch (env_mode) {
+      case 2: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 2>(a, nblocks, st);
+      case 14: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 14>(a, nblocks, st);
+      default: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 6>(a, nblocks, st);
+    }
+  }
+  if (mode < 0 && env_mode >= 0 && vt == VT_I32 && need == NEED_SUM) mode = env_mode;
   if (mode >= 0 && vt == VT_I32 && need == NEED_SUM) {
     switch (mode) {
       case 0: return launch_ingest_t<VT_I32, NEED_SUM, 0>(a, nblocks, st);
@@ -1310,6 +1381,7 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
       case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
       case 3: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
       case 7: return launch_ingest_t<VT_I32, NEED_SUM, 7>(a, nblocks, st);
+      case 14: return launch_ingest_t<VT_I32, NEED_SUM, 14>(a, nblocks, st);
       default: return launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st);
     }
   }

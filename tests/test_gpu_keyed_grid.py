@@ -7,6 +7,8 @@ lane replay, batches it cannot take go there entirely.  Every test compares it w
 window bounds, hasValue and integer aggregates bit-exact, f64 sums within 1e-6 relative (north_star).
 Reference: flink-connector/.../KeyedScottyWindowOperator.java:56-86, S/StreamSlicer.java:36-116,
 S/SliceManager.java:27-87."""
+import os
+
 import numpy as np
 import pytest
 
@@ -37,6 +39,8 @@ def _make(pkg, vt, wins, aggs, lateness, kg):
     op = pkg.KeyedSlicingWindowOperator(device=0, value_type=vtc)
     op.tune("keyed_grid", 1 if kg else 0)
     op.tune("keyed_grid_chunk", 0)  # chunk many-cell pushes however small (the default leaves small ones to replay)
+    if kg and os.environ.get("SCOTTY_TEST_KG_VARIANT"):  # run the suite against a kernel variant (A/B candidates)
+        op.tune("keyed_grid_variant", int(os.environ["SCOTTY_TEST_KG_VARIANT"]))
     for a in aggs:
         op.addWindowFunction(a)
     op.setMaxLateness(lateness)
