@@ -66,7 +66,6 @@ struct IngestArgs {
   uint32_t* cix;
   int64_t* cix_meta;         // [base, shift, n, cells indexed, ts end of the indexed range]
   int64_t cix_margin;        // ms past the stream front (prev_max) the index covers
-  long long* stepmax;        // nullable: max ts of every 256-tuple arrival step (step s at [s >> 8])
 };
 
 struct CommitArgs {

@@ -73,6 +73,7 @@ namespace scotty {
   } while (0)
 
 namespace {
+// device allocation, zero-filled: no kernel may read a previous owner's bytes from reused memory
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
   *p = nullptr;
@@ -751,13 +752,6 @@ int XEngine::xq_ensure(int64_t n) {
     xq_tcap = std::max<int64_t>(nt, 1024);
     XCHK(dalloc(&d_xq_tilemax, xq_tcap));
   }
-  const int64_t ns = n / 256 + 2;
-  if (ns > xq_scap) {
-    XCHK(hipStreamSynchronize(stream));
-    dfree(d_xq_stepmax);
-    xq_scap = std::max<int64_t>(ns, 4096);
-    XCHK(dalloc(&d_xq_stepmax, xq_scap));
-  }
   return SCOTTY_OK;
 }
 
@@ -791,7 +785,6 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   ia.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) ia.c_part[k] = d_xq_cpart[k];
   ia.tilemax = d_xq_tilemax;
-  ia.stepmax = d_xq_stepmax;
   ia.meta = d_xq_meta;
   ia.per_wave = per_wave;
   ia.tile = tile;
@@ -813,7 +806,6 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   q.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) q.c_part[k] = d_xq_cpart[k];
   q.tilemax = d_xq_tilemax;
-  q.stepmax = d_xq_stepmax;
   q.rank = d_xq_rank;
   q.flag = d_xq_flag;
   q.eg = d_xq_eg;

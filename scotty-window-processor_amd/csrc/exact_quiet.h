@@ -62,7 +62,6 @@ struct XQArgs {
   long long* c_tmax;
   unsigned long long* c_part[NPART];
   long long* tilemax;
-  long long* stepmax;    // max ts of every 256-tuple arrival step, written by the ingest
   int32_t* rank;         // scratch [gcap]
   int32_t* flag;         // scratch [gcap]
   int64_t* eg;           // scratch [gcap]: emitted edges by rank

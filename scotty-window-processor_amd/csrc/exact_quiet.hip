@@ -256,15 +256,9 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     // no in-order jump by a gap: items after a tile's first are below max(carry, first) + gap; the first is below
     // carry + gap (carry = running max before the tile).  A tile failing this bound (a slow stream: the tile spans
     // more than a gap of event time) is checked item by item below.
-    int64_t t0s[NT_MAX / 1024];  // every tile start loaded before the checks: one round trip, not one per tile
-#pragma unroll
-    for (int j = 0; j < NT_MAX / 1024; j++) {
-      const int64_t t = tid + (int64_t)j * 1024;
-      t0s[j] = t < nT ? a.ts[t * tile] : JMIN;
-    }
     for (int64_t t = tid; t < nT; t += 1024) {
       const int64_t carry = t > 0 ? max(P, (int64_t)s_p[t - 1]) : P;
-      const int64_t t0 = t0s[(t - tid) >> 10], tm = a.tilemax[t];
+      const int64_t t0 = a.ts[t * tile], tm = a.tilemax[t];
       if (!lt_plus(t0, carry, q.min_gap)) {
         fail = true;
         atomicOr(&s_why, 4);
@@ -350,23 +344,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     const int64_t gk = g[k];
     const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
     int64_t r = ts_ > 0 ? max(P, (int64_t)s_p[ts_ - 1]) : P;
-    int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
-    {  // narrow to the tile's first 256-tuple arrival step holding a tuple >= gk (the ingest's step maxima)
-      const int64_t s0 = e0 >> 8, s1 = (e1 + 255) >> 8;
-      for (int64_t sb = s0; sb < s1; sb += 64) {
-        const int64_t si = sb + lane;
-        const int64_t v = si < s1 ? (int64_t)a.stepmax[si] : JMIN;
-        const unsigned long long hit = __ballot(v >= gk);
-        if (hit) {
-          const int f = __ffsll((long long)hit) - 1;
-          r = max(r, wmax(lane < f ? v : JMIN));
-          e0 = (sb + f) << 8;
-          e1 = min(a.n, e0 + 256);
-          break;
-        }
-        r = max(r, wmax(v));
-      }
-    }
+    const int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
     int64_t e = JMIN, mm = JMIN, pos = -1;
     constexpr int B = 16;
     for (int64_t base = e0; base < e1 && pos < 0; base += 64 * B) {

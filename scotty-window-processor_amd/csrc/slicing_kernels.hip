@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   acc.reset();
   int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
   uint32_t n_late = 0, n_ovf = 0, n_glb = 0;
-  int64_t tile_max = INT64_MIN, step_max = INT64_MIN;
+  int64_t tile_max = INT64_MIN;
   int64_t cmin = INT64_MAX;  // lowest cell this wave added to outside the LDS window (commit folds from there)
   int qn = 0;                // deferred queue fill (wave-uniform)
 
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     uint32_t sm = 0;  // tuples outside the wave's current cell take the slow path, one code copy for all four
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      step_max = max(step_max, t[j]);
+      tile_max = max(tile_max, t[j]);
       if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
       else sm |= 1u << j;
     }
@@ -653,13 +653,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       slow(tj, vj);
     }
   };
-  auto tile_done = [&](int64_t s) {  // end of the step at s: step and tile maxima
-    if (a.stepmax) {
-      const int64_t sm_ = wmax64(step_max);
-      if (lane == 0) a.stepmax[s >> 8] = sm_;
-    }
-    tile_max = max(tile_max, step_max);
-    step_max = INT64_MIN;
+  auto tile_done = [&](int64_t s) {
     const int64_t done = s + 256;
     if (((done - w0) & (a.tile - 1)) == 0 || done >= w1) {
       int64_t tm = wmax64(tile_max);
@@ -721,7 +715,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       if (idx[j] < w1) {
         int64_t tj = a.ts[idx[j]];
         V vj = vp[idx[j]];
-        step_max = max(step_max, tj);
+        tile_max = max(tile_max, tj);
         if (tj >= lo && tj < hi) acc.add(tj, vj);
         else slow(tj, vj);
       }

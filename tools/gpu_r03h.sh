@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out/r03h
 timeout -k 10 900 python -u -m pytest tests/test_gpu_exact.py tests/test_gpu_parity.py -x -v -s --timeout 300 --timeout-method thread \
-  > gpurun_out/r03h/tests.log 2>&1 || { tail -60 gpurun_out/r03h/tests.log; exit 1; }
+  > gpurun_out/r03h/tests.log 2>&1 || { tail -30 gpurun_out/r03h/tests.log; exit 1; }
 tail -2 gpurun_out/r03h/tests.log
 SCOTTY_TEST_KG_VARIANT=4 timeout -k 10 400 python -u -m pytest tests/test_gpu_keyed_grid.py -x -v --timeout 300 --timeout-method thread \
   > gpurun_out/r03h/keyed_grid_v4.log 2>&1 || { tail -40 gpurun_out/r03h/keyed_grid_v4.log; exit 1; }
