@@ -53,6 +53,7 @@ hipError_t launch_kg_bounds(const int64_t* ts, int64_t n, const XCfg* cfg, int k
 hipError_t launch_kg_dcount(const uint8_t* mark, int64_t n, int32_t* blk, hipStream_t st);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
+int ingest_wgs_per_cu(int vt, int need);
 hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
 hipError_t launch_kg_dgather(const uint32_t* key, const int64_t* ts, const void* val, uint8_t* mark, int64_t n,
                              const int32_t* blk_off, uint32_t* okey, int64_t* ots, void* oval, int vt,
@@ -771,7 +772,7 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   if (rc) return rc;
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
-  const int64_t target_blocks = 1024;  // ~4 workgroups per CU, a tile-aligned contiguous range per wave
+  const int64_t target_blocks = 256 * ingest_wgs_per_cu(vt, cfg.need);  // one round of resident workgroups
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
   per_wave = std::max(((per_wave + tile - 1) / tile) * tile, tile);
   const int64_t nblocks = (n + per_wave * 4 - 1) / (per_wave * 4);

@@ -23,6 +23,7 @@
 
 namespace scotty {
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
+int ingest_wgs_per_cu(int vt, int need);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_wm(const WmArgs& a, hipStream_t st);
@@ -142,7 +143,7 @@ struct scotty_op {
   uint64_t dropped = 0, processed = 0;
 
   int ingest_mode = -1;  // tuning knob (scotty_tune), -1 = default variant
-  int64_t ingest_blocks = 1024;  // tuning knob: target workgroups of the ingest launch (~4 per CU)
+  int64_t ingest_blocks = 0;  // tuning knob: target workgroups of the ingest launch (0: one round of resident ones)
 
   // ---- engine selection: the grid path (context-free time windows, non-keyed) or the exact engine
   //      (keyed ops, session windows, count windows); decided at the first push
@@ -536,7 +537,8 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
   // ~4 workgroups per CU on 256 CUs; each wave streams a tile-aligned contiguous range
-  const int64_t target_blocks = op->ingest_blocks;
+  // one round of resident workgroups (a tune value overrides)
+  const int64_t target_blocks = op->ingest_blocks > 0 ? op->ingest_blocks : 256 * ingest_wgs_per_cu(op->vt, op->need);
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
   per_wave = ((per_wave + tile - 1) / tile) * tile;
   if (per_wave < tile) per_wave = tile;

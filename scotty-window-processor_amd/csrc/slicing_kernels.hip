@@ -1335,18 +1335,48 @@ static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStrea
 // profiles/r02/)
 constexpr int DEFAULT_MODE = 6;
 
+// MIN / MAX partials: software-pipelined as well (MM_MODE = 7; A/B r03m on C3: 0.258 -> 0.227 ms per 2^26 tuples).  Their
+// larger LDS window leaves 3 workgroups per CU instead of 4, and two steps in flight per wave make up the bytes in
+// flight; SUM / COUNT configurations measured equal with it (r02c) and keep the plain loop
+constexpr int MM_MODE = 7;
 template <int VT>
 static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
   switch (need) {
     case 0: return launch_ingest_t<VT, 0, DEFAULT_MODE>(a, nblocks, st);
     case 1: return launch_ingest_t<VT, 1, DEFAULT_MODE>(a, nblocks, st);
-    case 2: return launch_ingest_t<VT, 2, DEFAULT_MODE>(a, nblocks, st);
-    case 3: return launch_ingest_t<VT, 3, DEFAULT_MODE>(a, nblocks, st);
-    case 4: return launch_ingest_t<VT, 4, DEFAULT_MODE>(a, nblocks, st);
-    case 5: return launch_ingest_t<VT, 5, DEFAULT_MODE>(a, nblocks, st);
-    case 6: return launch_ingest_t<VT, 6, DEFAULT_MODE>(a, nblocks, st);
-    default: return launch_ingest_t<VT, 7, DEFAULT_MODE>(a, nblocks, st);
+    case 2: return launch_ingest_t<VT, 2, MM_MODE>(a, nblocks, st);
+    case 3: return launch_ingest_t<VT, 3, MM_MODE>(a, nblocks, st);
+    case 4: return launch_ingest_t<VT, 4, MM_MODE>(a, nblocks, st);
+    case 5: return launch_ingest_t<VT, 5, MM_MODE>(a, nblocks, st);
+    case 6: return launch_ingest_t<VT, 6, MM_MODE>(a, nblocks, st);
+    default: return launch_ingest_t<VT, 7, MM_MODE>(a, nblocks, st);
   }
+}
+
+// Ingest workgroups one CU holds at once (the LDS window bounds it: 160 KB per CU on gfx950, 4 waves per
+// workgroup, at most 4 workgroups): the launch is sized to exactly one round of them, so no second partial round of
+// workgroups trails the first (a config whose window takes 51 KB fits 3 per CU: 1024 workgroups ran in 1.33 rounds)
+int ingest_wgs_per_cu(int vt, int need) {
+  size_t lds;
+  const int nd = need & (NEED_SUM | NEED_MIN | NEED_MAX);
+  auto pick = [&](auto vtag) {
+    constexpr int V = decltype(vtag)::value;
+    switch (nd) {
+      case 0: return ingest_lds_bytes<V, 0, DEFAULT_MODE>();
+      case 1: return ingest_lds_bytes<V, 1, DEFAULT_MODE>();
+      case 2: return ingest_lds_bytes<V, 2, DEFAULT_MODE>();
+      case 3: return ingest_lds_bytes<V, 3, DEFAULT_MODE>();
+      case 4: return ingest_lds_bytes<V, 4, DEFAULT_MODE>();
+      case 5: return ingest_lds_bytes<V, 5, DEFAULT_MODE>();
+      case 6: return ingest_lds_bytes<V, 6, DEFAULT_MODE>();
+      default: return ingest_lds_bytes<V, 7, DEFAULT_MODE>();
+    }
+  };
+  if (vt == VT_I32) lds = pick(std::integral_constant<int, VT_I32>{});
+  else if (vt == VT_I64) lds = pick(std::integral_constant<int, VT_I64>{});
+  else lds = pick(std::integral_constant<int, VT_F64>{});
+  const int k = (int)((160 * 1024) / lds);
+  return k < 1 ? 1 : (k > 4 ? 4 : k);
 }
 
 // mode < 0: default; mode 0..3 selects a variant for the (int32, SUM) configuration (A/B tuning)
@@ -1364,7 +1394,9 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
     switch (env_mode) {
       case 2: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 2>(a, nblocks, st);
       case 14: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 14>(a, nblocks, st);
-      default: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 6>(a, nblocks, st);
+      case 7: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 7>(a, nblocks, st);
+      case 6: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 6>(a, nblocks, st);
+      default: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, MM_MODE>(a, nblocks, st);
     }
   }
   if (mode < 0 && env_mode >= 0 && vt == VT_I32 && need == NEED_SUM) mode = env_mode;
