@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <limits>
 #include <type_traits>
 
 #include "device_common.h"
@@ -252,29 +253,39 @@ struct LdsSum {
   using T = typename std::conditional<VT == VT_I32, uint32_t, unsigned long long>::type;
 };
 
-// LDS cell window of a workgroup
+// LDS min / max word of a cell: int32 values keep 4-byte partials (the window then leaves room for a 4th workgroup per
+// CU with MIN / MAX functions); int64 / double keep 8 bytes
+template <int VT>
+struct LdsMM {
+  using T = typename std::conditional<VT == VT_I32, int32_t, long long>::type;
+};
+
+// LDS cell window of a workgroup.  tmax is kept as a 32-bit offset from the window's first cell start (tbase): the
+// window is cut so that every cell of it ends within 2^32 - 1 of tbase (cells beyond take the global path)
 template <int VT>
 struct LdsWin {
   int64_t* tw;                // [WCAP+1] cell starts
   uint32_t* cnt;              // [WCAP]
-  long long* tmax;            // [WCAP]
+  uint32_t* tmax;             // [WCAP] max ts - tbase
   typename LdsSum<VT>::T* sum;  // [WCAP] (NEED_SUM)
-  long long* mn;              // [WCAP] (NEED_MIN)
-  long long* mx;              // [WCAP] (NEED_MAX)
+  typename LdsMM<VT>::T* mn;    // [WCAP] (NEED_MIN)
+  typename LdsMM<VT>::T* mx;    // [WCAP] (NEED_MAX)
+  int64_t tbase;
 };
 
 template <int VT, int NEED>
 __device__ __forceinline__ void lds_add(const LdsWin<VT>& w, int64_t i, uint32_t cnt, int64_t tmax, uint64_t sumw,
                                         double sumf, int64_t mn, int64_t mx) {
+  using M = typename LdsMM<VT>::T;
   atomicAdd(&w.cnt[i], cnt);
-  atomicMax(&w.tmax[i], (long long)tmax);
+  atomicMax(&w.tmax[i], (uint32_t)(tmax - w.tbase));
   if constexpr ((NEED & NEED_SUM) != 0) {
     if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[i], sumf);
     else if constexpr (VT == VT_I32) atomicAdd(&w.sum[i], (uint32_t)sumw);
     else atomicAdd(&w.sum[i], (unsigned long long)sumw);
   }
-  if constexpr ((NEED & NEED_MIN) != 0) atomicMin(&w.mn[i], (long long)mn);
-  if constexpr ((NEED & NEED_MAX) != 0) atomicMax(&w.mx[i], (long long)mx);
+  if constexpr ((NEED & NEED_MIN) != 0) atomicMin(&w.mn[i], (M)mn);
+  if constexpr ((NEED & NEED_MAX) != 0) atomicMax(&w.mx[i], (M)mx);
 }
 
 template <int VT, int NEED>
@@ -293,10 +304,10 @@ __device__ __forceinline__ void glb_add(const IngestArgs& a, int64_t c, uint64_t
 // LDS bytes of one ingest workgroup (host launch and kernel carve the same layout)
 template <int VT, int NEED, int MODE>
 __host__ __device__ constexpr size_t ingest_lds_bytes() {
-  size_t b = 8 * ING_SC + 8 * (WCAP + 2) + 4 * WCAP + 8 * WCAP;
+  size_t b = 8 * ING_SC + 8 * (WCAP + 2) + 4 * WCAP + 4 * WCAP;
   if (NEED & NEED_SUM) b += (VT == VT_I32 ? 4 : 8) * WCAP;
-  if (NEED & NEED_MIN) b += 8 * WCAP;
-  if (NEED & NEED_MAX) b += 8 * WCAP;
+  if (NEED & NEED_MIN) b += (VT == VT_I32 ? 4 : 8) * WCAP;
+  if (NEED & NEED_MAX) b += (VT == VT_I32 ? 4 : 8) * WCAP;
   b += 2 * LCIX;
   if (MODE & 4) b += 4 * DEFER_CAP * (4 + (VT == VT_I32 ? 4 : 8));
   return (b + 15) & ~(size_t)15;
@@ -319,17 +330,18 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   unsigned char* p = smem + 8 * ING_SC;
   w.tw = (int64_t*)p;
   p += 8 * (WCAP + 2);
-  w.tmax = (long long*)p;
-  p += 8 * WCAP;
+  using MMT = typename LdsMM<VT>::T;
+  w.tmax = (uint32_t*)p;
+  p += 4 * WCAP;
   w.mn = nullptr;
   w.mx = nullptr;
   if (NEED & NEED_MIN) {
-    w.mn = (long long*)p;
-    p += 8 * WCAP;
+    w.mn = (MMT*)p;
+    p += sizeof(MMT) * WCAP;
   }
   if (NEED & NEED_MAX) {
-    w.mx = (long long*)p;
-    p += 8 * WCAP;
+    w.mx = (MMT*)p;
+    p += sizeof(MMT) * WCAP;
   }
   w.sum = nullptr;
   if (NEED & NEED_SUM) {
@@ -379,6 +391,15 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     else chi = cx0.find(cv, x);
     int64_t wbase = max((int64_t)0, chi + 16 - WCAP);
     int64_t wn = min((int64_t)WCAP, ctot - wbase);
+    {  // every window cell ends within 2^32 - 1 of the window's first start (the LDS keeps 32-bit tmax offsets)
+      const int64_t tws = cv.start(wbase);
+      int64_t l_ = 0, h_ = wn;  // largest w <= wn with start(wbase + w) - tws <= 2^32 - 1 (starts increase)
+      while (l_ < h_) {
+        const int64_t mid = (l_ + h_ + 1) >> 1;
+        if ((uint64_t)(cv.start(wbase + mid) - tws) <= 0xFFFFFFFFull) l_ = mid; else h_ = mid - 1;
+      }
+      wn = l_;
+    }
     sc[0] = m.overflow;
     sc[1] = head; sc[2] = tail; sc[3] = j0; sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
     sc[7] = wbase; sc[8] = wn;
@@ -418,13 +439,14 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   }
   for (int64_t i = tid; i < wn; i += 256) {
     w.cnt[i] = 0;
-    w.tmax[i] = INT64_MIN;
+    w.tmax[i] = 0;
     if (NEED & NEED_SUM) w.sum[i] = 0;
-    if (NEED & NEED_MIN) w.mn[i] = PART_ID_MIN;
-    if (NEED & NEED_MAX) w.mx[i] = PART_ID_MAX;
+    if (NEED & NEED_MIN) w.mn[i] = std::numeric_limits<MMT>::max();
+    if (NEED & NEED_MAX) w.mx[i] = std::numeric_limits<MMT>::min();
   }
   __syncthreads();
   const int64_t tw0 = uni64(w.tw[0]), twn = uni64(w.tw[wn]);
+  w.tbase = tw0;
   // window cell of t (tw0 <= t < twn): staged cell index, else binary search over the window's starts
   auto wfind = [&](int64_t t) -> int64_t {
     int64_t l = 0, h = wn;
@@ -481,16 +503,17 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     one.reset();
     one.add(t, v);
     atomicAdd(&w.cnt[l], 1u);
-    if (t > (int64_t)w.tmax[l]) atomicMax(&w.tmax[l], (long long)t);
+    const uint32_t to = (uint32_t)(t - w.tbase);
+    if (to > w.tmax[l]) atomicMax(&w.tmax[l], to);
     if constexpr ((NEED & NEED_SUM) != 0) {
       if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[l], one.sum_f());
       else if constexpr (VT == VT_I32) atomicAdd(&w.sum[l], (uint32_t)one.sum_word());
       else atomicAdd(&w.sum[l], (unsigned long long)one.sum_word());
     }
     if constexpr ((NEED & NEED_MIN) != 0)
-      if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (long long)one.mn);
+      if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (MMT)one.mn);
     if constexpr ((NEED & NEED_MAX) != 0)
-      if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (long long)one.mx);
+      if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (MMT)one.mx);
   };
 
   auto slow = [&](int64_t t, V v) {
@@ -543,16 +566,17 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
           one.reset();
           one.add(t, v);
           if (!counted) atomicAdd(&w.cnt[l], 1u);
-          if (t > (int64_t)w.tmax[l]) atomicMax(&w.tmax[l], (long long)t);
+          const uint32_t to = (uint32_t)(t - w.tbase);
+          if (to > w.tmax[l]) atomicMax(&w.tmax[l], to);
           if constexpr ((NEED & NEED_SUM) != 0) {
             if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[l], one.sum_f());
             else if constexpr (VT == VT_I32) atomicAdd(&w.sum[l], (uint32_t)one.sum_word());
             else atomicAdd(&w.sum[l], (unsigned long long)one.sum_word());
           }
           if constexpr ((NEED & NEED_MIN) != 0)
-            if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (long long)one.mn);
+            if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (MMT)one.mn);
           if constexpr ((NEED & NEED_MAX) != 0)
-            if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (long long)one.mx);
+            if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (MMT)one.mx);
         }
       } else if (valid) {
         const int64_t t = tw0 + (int64_t)q_t[e];
@@ -741,7 +765,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     if (c) {
       uint64_t sw = (NEED & NEED_SUM) ? (uint64_t)w.sum[i] : 0;
       double sf = (NEED & NEED_SUM) ? __longlong_as_double((long long)sw) : 0.0;
-      glb_add<VT, NEED>(a, wbase + i, c, w.tmax[i], sw, sf, (NEED & NEED_MIN) ? (int64_t)w.mn[i] : 0,
+      glb_add<VT, NEED>(a, wbase + i, c, w.tbase + (int64_t)w.tmax[i], sw, sf, (NEED & NEED_MIN) ? (int64_t)w.mn[i] : 0,
                         (NEED & NEED_MAX) ? (int64_t)w.mx[i] : 0);
       bmin = min(bmin, wbase + i);
     }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 3: ingest grid = one round of resident workgroups; quiet/grid parity, then C3 modes 6/7 and C2s, C1
+# round 3: compact LDS window (32-bit tmax offsets, int32 min/max): parity, C3 modes, C2s, C1
 export TMPDIR=/tmp
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out/r03m
