@@ -543,7 +543,12 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
   // tuples) costs one short event-exact prefix, not rounds over the whole batch.  The prefix grows 4x with every
   // further refusal, so a batch that is not quiet anywhere reaches the event-exact path for all of it quickly.
   int64_t pos0 = 0;
-  int64_t chunk = std::max<int64_t>(n / 32, (int64_t)1 << 20);
+  static const int64_t chunk_min = [] {  // A/B of the first event-exact prefix (SCOTTY_XQ_CHUNK tuples)
+    const char* e = getenv("SCOTTY_XQ_CHUNK");
+    return e ? std::max<int64_t>(4096, atoll(e)) : (int64_t)1 << 20;
+  }();
+  int64_t chunk = std::max<int64_t>(n / 32, chunk_min);
+  if (getenv("SCOTTY_XQ_CHUNK")) chunk = chunk_min;
   chunk = (chunk + 4095) & ~(int64_t)4095;  // pieces start 16-byte aligned (the ingest's vector loads)
   while (pos0 < n) {
     const int64_t rest = n - pos0;
