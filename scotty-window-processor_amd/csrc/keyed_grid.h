@@ -26,7 +26,7 @@ enum : int32_t {
 struct KgCtl {
   int32_t flag, ncell;
   unsigned long long deferred;     // tuples left to the replay path (keys new / not eligible this batch)
-  unsigned long long kg_keys;      // (unused: keys_shard holds the committed keys)
+  int32_t compact, pad0;           // the partition writes 8-byte records this batch (see KgArgs.allow_compact)
   unsigned long long defer_keys;   // known keys deferred
   int64_t ts_first, ts_last;
   int64_t bg[KG_MAXCELL];          // bg[c] (c >= 1): lower bound of batch cell c (a grid point); bg[0] = ts_first
@@ -52,6 +52,8 @@ struct KgArgs {
   int32_t cmax;                    // cells the bucket kernel variant keeps
   int32_t tile;                    // tuples per partition tile
   int32_t variant;                 // kernel variant (A/B, scotty_tune "keyed_grid_variant")
+  int32_t allow_compact;           // int32 values, default kernels: 8-byte records when the batch's ts span fits the
+                                   // bits the key leaves (key hash bits outside the bucket, ts offset, value)
   int32_t* hist;                   // [nbk][ntiles], scanned in place (exclusive)
   void* rec;                       // bucket-ordered records
   uint8_t* mark;                   // [n] tuple deferred to the replay path (reset by the gather)

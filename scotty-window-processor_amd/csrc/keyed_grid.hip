@@ -46,6 +46,31 @@ __device__ __forceinline__ uint32_t khash(uint32_t x) {  // murmur3 finaliser (t
   return x;
 }
 
+__device__ __forceinline__ uint32_t khash_inv(uint32_t x) {  // inverse of khash (the murmur3 finaliser is a bijection)
+  x ^= x >> 16;
+  x *= 0x7ed1b41du;
+  x ^= x >> 13;
+  x ^= x >> 26;
+  x *= 0xa5cb9243u;
+  x ^= x >> 16;
+  return x;
+}
+
+// 8-byte records (KgCtl.compact): word 0 = the key's hash bits outside the bucket field | ts offset << (32 - bb),
+// word 1 = the int32 value; bb = log2(buckets).  The bucket kernel knows the bucket of every record it reads, so the
+// full hash -- and through khash_inv the key -- is recovered exactly.
+__device__ __forceinline__ uint32_t compact_word(uint32_t key, uint32_t toff, int bb) {
+  const uint32_t h = khash(key);
+  const uint32_t lo = h & ((1u << KG_RB) - 1), hi = h >> (KG_RB + bb);
+  return lo | (hi << KG_RB) | (toff << (32 - bb));
+}
+__device__ __forceinline__ void compact_decode(uint32_t w, uint32_t bk, int bb, uint32_t& key, uint32_t& toff) {
+  toff = w >> (32 - bb);
+  const uint32_t rest = w & ((1u << (32 - bb)) - 1);
+  const uint32_t h = ((rest >> KG_RB) << (KG_RB + bb)) | (bk << KG_RB) | (rest & ((1u << KG_RB) - 1));
+  key = khash_inv(h);
+}
+
 __device__ __forceinline__ int64_t f64_key(double d) {
   const int64_t b = __double_as_longlong(d);
   return b ^ ((b >> 63) & 0x7FFFFFFFFFFFFFFFLL);
@@ -120,7 +145,11 @@ __global__ void kg_prep_kernel(KgArgs a) {
   c.ts_first = f;
   c.ts_last = l;
   c.deferred = 0;
-  c.kg_keys = 0;
+  {
+    const int bb = 31 - __clz(a.nbk);
+    c.compact = (a.allow_compact && !flag && (a.nbk & (a.nbk - 1)) == 0 && bb >= 1 && bb <= 16 &&
+                 (uint64_t)l - (uint64_t)f < ((uint64_t)1 << bb)) ? 1 : 0;
+  }
   c.defer_keys = 0;
   for (int i = 0; i < KG_SHARDS; i++) c.keys_shard[i] = 0;
 }
@@ -324,11 +353,29 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
     if (idx < a.nbk) tst[idx] = ex + loc[q];
   }
   __syncthreads();
+  const int nt = (int)min((int64_t)T, a.n - i0);
+  if (VB == 4 && a.ctl->compact) {  // 8-byte records: staged with their bucket, 8 bytes written
+    const int bb = 31 - __clz(a.nbk);
+#pragma unroll
+    for (int j = 0; j < IT; j++)
+      if (bk[j] < NBS) {
+        const int q = tst[bk[j]] + rk[j];
+        const KRec<4>& r4 = reinterpret_cast<const KRec<4>&>(rec[j]);
+        stage[3 * q] = compact_word(r4.x, r4.y, bb);
+        stage[3 * q + 1] = r4.z;
+        stage[3 * q + 2] = (uint32_t)bk[j];
+      }
+    __syncthreads();
+    for (int i = tid; i < nt; i += ST) {
+      const uint32_t w0 = stage[3 * i], w1 = stage[3 * i + 1], b = stage[3 * i + 2];
+      ((uint2*)a.rec)[(int64_t)base[b] + (i - tst[b])] = make_uint2(w0, w1);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < IT; j++)
     if (bk[j] < NBS) rec[j].store_lds(stage, tst[bk[j]] + rk[j]);
   __syncthreads();
-  const int nt = (int)min((int64_t)T, a.n - i0);
   for (int i = tid; i < nt; i += ST) {
     const KRec<VB> r = KRec<VB>::load_lds(stage, i);
     const uint32_t b = bucket_of(r.key(), a.kmask);
@@ -635,14 +682,34 @@ __device__ __forceinline__ void kg_bucket_body(const KgArgs& a) {
     }
   };
   int64_t r = r0 + tid;
-  for (; r + (U - 1) * nt < r1; r += U * nt) {
-    KRec<VB> rc[U];
+  if (VB == 4 && a.ctl->compact) {  // 8-byte records: key and ts offset decoded from the hash word and the bucket
+    const int bb = 31 - __clz(a.nbk);
+    const uint2* cr = (const uint2*)a.rec;
+    auto fold_c = [&](uint2 w) {
+      uint32_t key, toff;
+      compact_decode(w.x, bk, bb, key, toff);
+      KRec<VB> rec;
+      reinterpret_cast<KRec<4>&>(rec) = KRec<4>{key, toff, w.y};
+      fold(rec);
+    };
+    for (; r + (U - 1) * nt < r1; r += U * nt) {
+      uint2 w[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) rc[u] = KRec<VB>::load(a.rec, r + u * nt);
+      for (int u = 0; u < U; u++) w[u] = cr[r + u * nt];
 #pragma unroll
-    for (int u = 0; u < U; u++) fold(rc[u]);
+      for (int u = 0; u < U; u++) fold_c(w[u]);
+    }
+    for (; r < r1; r += nt) fold_c(cr[r]);
+  } else {
+    for (; r + (U - 1) * nt < r1; r += U * nt) {
+      KRec<VB> rc[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) rc[u] = KRec<VB>::load(a.rec, r + u * nt);
+#pragma unroll
+      for (int u = 0; u < U; u++) fold(rc[u]);
+    }
+    for (; r < r1; r += nt) fold(KRec<VB>::load(a.rec, r));
   }
-  for (; r < r1; r += nt) fold(KRec<VB>::load(a.rec, r));
   if (miss) atomicAdd(&s_miss, (unsigned long long)miss);
   __syncthreads();
   for (int p = tid; p < KG_RP; p += nt) {
