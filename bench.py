@@ -355,7 +355,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 60))
     op.addWindowAssigner(pkg.SessionWindow(pkg.WindowMeasure.Time, 1000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
-    times, rows, verdicts = [], 0, []
+    times, rows, verdicts, rounds = [], 0, [], []
     for s in range(warm + 2 * steps):
         if s == warm + steps:
             op.enableTiming(True)  # instrumented steps: after the wall-clock ones
@@ -374,6 +374,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
             times.append(time.perf_counter() - t0)
             rows += n
             verdicts.append(op._debug_stat(8))
+            rounds.append((op._debug_stat(0), op._debug_stat(1)))  # events, event-exact rounds of the batch
     roof = device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_MIN|NEED_MAX> (quiet path)")
     return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
                         "(delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, non-keyed, exact engine",
@@ -381,6 +382,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
             "ms_per_step_each": [round(1e3 * t, 4) for t in times],
             "quiet_steps": sum(1 for x in verdicts if x == 1), "event_exact_steps": sum(1 for x in verdicts if x != 1),
             "event_prefix_then_quiet_steps": op._debug_stat(12),
+            "events_rounds_each": rounds,
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
             "roofline": roof,
             "roofline_wall": {"achieved": batch * BYTES_PER_TUPLE * len(times) / sum(times) / 1e9,

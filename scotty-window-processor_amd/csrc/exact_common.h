@@ -230,7 +230,8 @@ struct XWmArgs {
   const uint32_t* slot_key;            // nullable
   int64_t n_rows;
   int32_t prefix_reset;                // lane path: recompute every op's slice prefixes from position 0
-  unsigned long long* row_count;       // lane path: rows reserved by the emit kernel itself (n_rows = capacity)
+  unsigned long long* row_count;       // lane path / single mode: rows written by the emit kernel (n_rows = capacity)
+  int32_t single;                      // one operator: wm_emit_kernel counts, checks and emits (no count pass)
 };
 
 }  // namespace scotty

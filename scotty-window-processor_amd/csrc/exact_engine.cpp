@@ -75,11 +75,17 @@ namespace scotty {
 
 namespace {
 // device allocation, zero-filled: no kernel may read a previous owner's bytes from reused memory
+// (the fill runs on the null stream and the host waits for it, so it is complete before the operator's non-blocking
+// stream can touch the buffer)
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
   *p = nullptr;
   if (count == 0) count = 1;
-  return hipMalloc((void**)p, count * sizeof(T));
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(*p, 0, count * sizeof(T), nullptr);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(nullptr);
 }
 void dfree(void* p) {
   if (p) (void)hipFree(p);
@@ -120,7 +126,7 @@ void XEngine::release() {
   dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
   dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
   dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
-  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_stepmax); dfree(d_xq_rank); dfree(d_xq_flag);
+  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_pmax); dfree(d_xq_rank); dfree(d_xq_flag);
   for (int k = 0; k < NPART; k++) dfree(d_xq_cpart[k]);
   dfree(d_xq_eg); dfree(d_xq_epos); dfree(d_xq_meta); dfree(d_xq_cix); dfree(d_xq_cixmeta); dfree(d_xq_ctl);
   for (auto& e : ev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -550,6 +556,9 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
   int64_t chunk = std::max<int64_t>(n / 32, chunk_min);
   if (getenv("SCOTTY_XQ_CHUNK")) chunk = chunk_min;
   chunk = (chunk + 4095) & ~(int64_t)4095;  // pieces start 16-byte aligned (the ingest's vector loads)
+  // event-exact piece behind a located jump: the stream resuming after a silence opens a session whose start settles
+  // within the first tuples (out-of-order tuples reach at most maxDelay below it), then the batch is quiet again
+  int64_t chunk_jump = (int64_t)1 << 18;
   while (pos0 < n) {
     const int64_t rest = n - pos0;
     const unsigned char* val0 = (const unsigned char*)d_val + pos0 * vb;
@@ -564,6 +573,27 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
         return SCOTTY_OK;
       }
       quiet_fallbacks++;
+      // the verdict failed only on session-gap jumps and located the first one: everything before its arrival tile
+      // is quiet (the verdict's other conditions held for the whole rest) -- commit that prefix in one pass, then the
+      // event-exact path from the jump on
+      const int64_t J = res == XQ_NOT_QUIET && (last_quiet_why & ~(int64_t)12) == 0 ? last_quiet_jump : 0;
+      if (J > 0 && J < rest) {
+        res = XQ_NONE;
+        rc = push_quiet(d_ts + pos0, val0, J, &res);
+        if (rc) return rc;
+        if (res == XQ_COMMITTED) {
+          quiet_commits++;
+          quiet_split_commits++;
+          pos0 += J;
+          const int64_t w = std::min(chunk_jump, n - pos0);
+          rc = push_exact(d_ts + pos0, (const unsigned char*)d_val + pos0 * vb, w);
+          if (rc) return rc;
+          pos0 += w;
+          chunk_jump *= 4;
+          continue;
+        }
+        quiet_fallbacks++;
+      }
     }
     const int64_t w = quiet_eligible() && chunk < rest ? chunk : rest;
     int rc = push_exact(d_ts + pos0, val0, w);
@@ -735,6 +765,7 @@ int XEngine::xq_ensure(int64_t n) {
     XCHK(dalloc(&d_xq_flag, xq_gcap));
     XCHK(dalloc(&d_xq_eg, xq_gcap));
     XCHK(dalloc(&d_xq_epos, 2 * xq_gcap));
+    XCHK(dalloc(&d_xq_pmax, NT_MAX));
     if (!d_xq_grid) XCHK(dalloc(&d_xq_grid, xq_gcap));
   }
   if (xq_ccap < (int64_t)sc + xq_gcap) {  // cells: retained slices ++ grid cells, identity between batches
@@ -812,6 +843,7 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   q.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) q.c_part[k] = d_xq_cpart[k];
   q.tilemax = d_xq_tilemax;
+  q.pmax = d_xq_pmax;
   q.rank = d_xq_rank;
   q.flag = d_xq_flag;
   q.eg = d_xq_eg;
@@ -840,13 +872,14 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
     long long h[16];
     XCHK(hipMemcpy(h, d_xq_dbg, sizeof(h), hipMemcpyDeviceToHost));
     fprintf(stderr, "xq commit phase ticks:");
-    for (int i = 1; i <= 7; i++) fprintf(stderr, " %lld", h[i] - h[i - 1]);
+    for (int i = 1; i <= 3; i++) fprintf(stderr, " %lld", h[i] - h[i - 1]);
     fprintf(stderr, "\n");
   }
   XQCtl c;
   std::memcpy(&c, h_misc, sizeof(XQCtl));
   *result = c.result;
   last_quiet_why = c.why;
+  last_quiet_jump = c.result == XQ_NOT_QUIET && c.jump_tile > 0 && c.jump_tile < (n + tile - 1) / tile ? c.jump_tile * tile : 0;
   if (c.result == XQ_COMMITTED && c.batch_max > c.p_start) xq_span = std::max<int64_t>(c.batch_max - c.p_start, 1);
   if (c.result == XQ_GRID || (c.result == XQ_COMMITTED && c.rebuild)) xq_need_grid = true;
   if (timing) collect_timing();
@@ -1367,6 +1400,54 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     }
     return finish_rows((int64_t)h_misc[3], r, to_host, false);
   }
+  const int64_t sbound = !keyed && n_ops == 1 && !lane_mode() ? single_row_bound(wm) : -1;
+  if (sbound >= 0) {  // one operator: no count pass -- the emit kernel checks, emits and counts (rows from a bound)
+    int rc = ensure_rows(std::max<int64_t>(sbound, 1));
+    if (rc) return rc;
+    a.single = 1;
+    a.row_count = (unsigned long long*)(d_misc + 3);
+    a.n_rows = sbound;
+    a.w_start = d_w_start;
+    a.w_end = d_w_end;
+    a.w_meas = d_w_meas;
+    a.w_op = d_w_op;
+    a.has_value = d_has;
+    for (int k = 0; k < cfg.n_aggs; k++) a.values[k] = d_vals[k];
+    a.w_key = d_w_key;
+    TEv tw;
+    int rct = tbegin(tw, SCOTTY_TIME_WATERMARK);
+    if (rct) return rct;
+    XCHK(hipMemsetAsync(d_misc, 0, 4 * 8, stream));
+    XCHK(launch_wm_emit(a, stream));
+    XCHK(launch_wm_agg(a, stream, 64));
+    XCHK(launch_copy_to_host(d_misc, h_misc_dev, 4 * 8, stream));
+    if ((rct = tend(tw, 0))) return rct;
+    XCHK(hipStreamSynchronize(stream));
+    r.dropped = (uint64_t)h_misc[1];
+    rc = op_error((int32_t)h_misc[2]);
+    if (rc) return rc;
+    const int32_t ef = (int32_t)h_misc[0];
+    if (ef & 1) {
+      err = "processWatermark threw IndexOutOfBoundsException (empty session context / count trigger before the "
+            "oldest slice, S/WindowManager.java:98-118)";
+      return SCOTTY_ERR_INDEX;
+    }
+    if (ef & 4) {
+      err = "internal: watermark rows exceeded the host bound";
+      failed = true;
+      return SCOTTY_ERR_STATE;
+    }
+    have_wm = true;
+    last_wm = wm;
+    rc = finish_rows((int64_t)h_misc[3], r, to_host, false);
+    if (rc) return rc;
+    if (ef & 2) {
+      err = "processWatermark threw IndexOutOfBoundsException in LazyAggregateStore.aggregate (getSlice(-1))";
+      return SCOTTY_ERR_INDEX;
+    }
+    if (timing) collect_timing();
+    return SCOTTY_OK;
+  }
   TEv tw1;
   int rct = tbegin(tw1, SCOTTY_TIME_WATERMARK);
   if (rct) return rct;
@@ -1456,6 +1537,25 @@ int64_t XEngine::lane_row_bound(int64_t wm) const {
   return rows > 2e9 ? -1 : (int64_t)rows;
 }
 
+// Upper bound of the rows one watermark of the single (non-keyed) operator emits: context-free time windows by the
+// lane bound's arithmetic (the operator's lastWatermark is at least the bound's l0), every session of every context
+// (at most the session capacity); -1 (count windows): use the count pass.
+int64_t XEngine::single_row_bound(int64_t wm) const {
+  if (cfg.has_count) return -1;
+  const double lo = std::max(0.0, (double)wm - (double)cfg.max_lateness);
+  const double l0 = have_wm ? std::min(lo, (double)last_wm) : lo;
+  const double span = std::max(0.0, (double)wm + 1.0 - l0);
+  double rows = 0;
+  for (const XWinDef& w : h_wins) {
+    if (w.kind == SCOTTY_WIN_SESSION) rows += (double)sesscap;
+    else if (w.kind == SCOTTY_WIN_TUMBLING && w.a > 0) rows += std::floor(span / (double)w.a) + 2;
+    else if (w.kind == SCOTTY_WIN_SLIDING && w.b > 0) rows += std::floor(span / (double)w.b) + 2;
+    else if (w.kind == SCOTTY_WIN_FIXED_BAND) rows += 1;
+    else return -1;
+  }
+  return rows > 1e6 ? -1 : (int64_t)rows;
+}
+
 // check: a kernel may have flagged LazyAggregateStore.aggregate's getSlice(-1) (err_flag bit 1)
 int XEngine::finish_rows(int64_t rows, XResult& r, bool to_host, bool check) {
   r.n = rows;
@@ -1495,6 +1595,8 @@ int XEngine::finish_rows(int64_t rows, XResult& r, bool to_host, bool check) {
 
 int XEngine::set_last_watermark(int64_t lw) {
   if (n_ops < 1) return SCOTTY_OK;
+  last_wm = lw;  // the row bounds start from it
+  have_wm = true;
   XCHK(hipMemcpyAsync((unsigned char*)d_st + offsetof(XState, lastWatermark), &lw, 8, hipMemcpyHostToDevice, stream));
   XCHK(hipStreamSynchronize(stream));
   return SCOTTY_OK;

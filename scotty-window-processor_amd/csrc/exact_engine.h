@@ -51,6 +51,8 @@ class XEngine {
   int64_t quiet_commits = 0, quiet_fallbacks = 0, quiet_tail_commits = 0;
   int32_t last_quiet = 0;      // XQ_* verdict of the last non-keyed push (0: not attempted)
   int64_t last_quiet_why = 0;  // XQCtl.why of the last verdict
+  int64_t last_quiet_jump = 0;   // first tuple of the arrival tile holding the verdict's first session-gap jump (0: none)
+  int64_t quiet_split_commits = 0;  // quiet prefixes committed up to a located jump
   // device time of the last pushes by class (HIP events; scotty_device_timing): 0 quiet ingest, 1 other push work
   bool timing = false;
   struct TEv {
@@ -106,6 +108,7 @@ class XEngine {
   int ensure_rows(int64_t rows);
   int op_error(int32_t op_err);
   int64_t lane_row_bound(int64_t wm) const;
+  int64_t single_row_bound(int64_t wm) const;
   int finish_rows(int64_t rows, XResult& r, bool to_host, bool check);
   int push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n);
   int push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_val, int64_t n, int64_t* deferred,
@@ -202,13 +205,13 @@ class XEngine {
   int tbegin(TEv& e, int cls);
   int tend(TEv& e, int64_t n);
   std::vector<int64_t> xq_hgrid;
-  int64_t xq_gcap = 0, xq_ccap = 0, xq_tcap = 0, xq_scap = 0;
+  int64_t xq_gcap = 0, xq_ccap = 0, xq_tcap = 0;
   int64_t* d_xq_grid = nullptr;
   unsigned long long* d_xq_ccnt = nullptr;
   long long* d_xq_ctmax = nullptr;
   unsigned long long* d_xq_cpart[NPART] = {};
   long long* d_xq_tilemax = nullptr;
-  long long* d_xq_stepmax = nullptr;  // the quiet ingest's 256-tuple step maxima (candidate first crossings)
+  long long* d_xq_pmax = nullptr;     // prefix maxima of the tile maxima (quiet scan -> edge kernel)
   int32_t *d_xq_rank = nullptr, *d_xq_flag = nullptr;
   int64_t *d_xq_eg = nullptr, *d_xq_epos = nullptr;
   DevMeta* d_xq_meta = nullptr;

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "exact_op.h"
 
 namespace scotty {
@@ -410,6 +412,10 @@ __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
   o.bind(a.cfg, a.sl, a.ss, op, lane);
   o.s = a.st[op];
   const XCfg* cfg = a.cfg;
+  if (a.single && lane == 0) {  // the count pass's accounting (single mode has none)
+    if (o.s.dropped) atomicAdd(a.dropped_total, (unsigned long long)o.s.dropped);
+    if (o.s.err) atomicOr(a.op_err, 1 << o.s.err);
+  }
   if (o.s.err) return;
   if (o.s.tail <= o.s.head) {  // empty store: lastWatermark := wm (:43-49)
     wm_prologue(o, a.wm);
@@ -420,8 +426,16 @@ __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
   wm_prologue(o, a.wm);
   const int64_t oldest = o.ts[o.s.head];
   if (o.s.lastWatermark < oldest) o.s.lastWatermark = oldest;
-  const int64_t off = a.woff[op];
+  if (a.single) {  // the count pass's checks, before any state changes: an exception leaves the operator as it was
+    const int64_t kd = wm_triggers<true>(o, a.wm, nullptr, nullptr, nullptr, nullptr, 0, 0);
+    if (o.exc || kd > a.n_rows) {
+      if (lane == 0) atomicOr(a.err_flag, o.exc ? 1 : 4);
+      return;
+    }
+  }
+  const int64_t off = a.single ? 0 : a.woff[op];
   const int64_t k = wm_triggers<false>(o, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, off, (int32_t)op);
+  if (a.single && lane == 0) *a.row_count = (unsigned long long)k;
   // aggregate range of LazyAggregateStore.aggregate (:83-90)
   int64_t minTs = JMAX, maxTs = 0, minCount = o.s.currentCount, maxCount = 0;
   __threadfence_block();
@@ -476,11 +490,48 @@ __device__ __forceinline__ T greduce(T v, F f) {
   for (int o = G / 2; o > 0; o >>= 1) v = f(v, (T)__shfl_xor(v, o));
   return v;
 }
+// first m in [lo, hi) with pred(m) (pred monotone false -> true), hi if none: G-ary search by a group of G lanes
+// (lane = index in the group; every lane of the group runs it with the same arguments)
+template <int G, typename P>
+__device__ __forceinline__ int64_t group_first(int64_t lo, int64_t hi, int lane, P pred) {
+  const int gsh = (int)(__lane_id() & (64 - G));  // the group's first bit in the wave's ballot
+  auto gbal = [&](bool b) -> unsigned long long {
+    const unsigned long long m = __ballot(b);
+    return G == 64 ? m : (m >> gsh) & ((1ull << G) - 1);
+  };
+  while (hi - lo > G) {
+    const int64_t stride = (hi - lo + G - 1) / G;
+    const int64_t p = lo + (int64_t)lane * stride;
+    const unsigned long long bal = gbal(p < hi && pred(p));
+    if (bal == 0) {
+      lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
+    } else {
+      const int f = __ffsll((long long)bal) - 1;
+      if (f == 0) return lo;
+      const int64_t pf = lo + (int64_t)f * stride;
+      lo = pf - stride + 1;
+      hi = pf;
+    }
+  }
+  const int64_t p = lo + lane;
+  const unsigned long long bal = gbal(p < hi && pred(p));
+  return bal ? lo + __ffsll((long long)bal) - 1 : hi;
+}
+
+template <int G>
+__device__ __forceinline__ void agg_row(const XWmArgs& a, int64_t wi, int lane);
+
+// rows: n_rows, or (single mode) the count the emit kernel wrote; groups stride over them
 template <int G>
 __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   const int lane = threadIdx.x & (G - 1);
-  const int64_t wi = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  if (wi >= a.n_rows) return;
+  const int64_t nrows = a.single ? (int64_t)*a.row_count : a.n_rows;
+  const int64_t stride = (int64_t)gridDim.x * (256 / G);
+  for (int64_t wi = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G; wi < nrows; wi += stride) agg_row<G>(a, wi, lane);
+}
+
+template <int G>
+__device__ __forceinline__ void agg_row(const XWmArgs& a, int64_t wi, int lane) {
   const int64_t op = a.w_op[wi];
   const XState& st = a.st[op];
   const int64_t base = op * (int64_t)a.cfg->sc;
@@ -489,25 +540,13 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   int64_t lo = st.wlo, hi = st.whi;
   if (lo < 0) lo = 0;
   const int64_t* key = tmeas ? a.sl.ts + base : a.sl.cs + base;
-  // narrow to start keys in [ws, we] (contained slices satisfy it); a range of a few group widths is
-  // cheaper to scan than to bisect (the bisection is a chain of dependent loads)
+  // narrow to start keys in [ws, we] (contained slices satisfy it) by a G-ary search of the group (one probe per
+  // lane per round; a bisection is a chain of dependent loads); a range of a few group widths is scanned as is
   if ((!(st.unsorted & 3) || !tmeas) && hi - lo > 4 * G) {
-    int64_t l = lo, h = hi;
-    while (l < h) {
-      int64_t m = (l + h) >> 1;
-      if (key[m] < ws) l = m + 1; else h = m;
-    }
-    const int64_t nlo = l;
-    l = nlo; h = hi;
+    const int64_t nlo = group_first<G>(lo, hi, lane, [&](int64_t m) { return key[m] >= ws; });
     // contained slices start no later than the window's end -- except with LazySlice record moves, which can
     // leave a slice's tLast (cLast) below its tStart (cStart): then only the lower bound narrows
-    if (!a.cfg->records) {
-      while (l < h) {
-        int64_t m = (l + h) >> 1;
-        if (key[m] <= we) l = m + 1; else h = m;
-      }
-      hi = l;
-    }
+    if (!a.cfg->records) hi = group_first<G>(nlo, hi, lane, [&](int64_t m) { return key[m] > we; });
     lo = nlo;
   }
   const int need = a.cfg->need, vt = a.cfg->vt;
@@ -515,21 +554,32 @@ __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
   uint64_t cnt = 0, sw = 0, present = 0;
   double sf = 0.0;
   int64_t mn = ID_MIN, mx = ID_MAX;
-  for (int64_t i = lo + lane; i < hi; i += G) {
-    const int64_t s = base + i;
-    const bool contains = tmeas ? (ws <= a.sl.ts[s] && we > a.sl.tl[s]) : (ws <= a.sl.cs[s] && we >= a.sl.cl[s]);
-    if (!contains) continue;
-    const uint64_t c = a.sl.cnt[s];
-    // a partial is present when non-null: count > 0, or (records mode) kept after liftAndInvert
-    if (recs ? a.sl.nn[s] == 0 : c == 0) continue;
-    present = 1;
-    cnt += c;
-    if (need & NEED_SUM) {
-      if (vt == VT_F64) sf += __longlong_as_double((long long)a.sl.p[0][s]);
-      else sw += a.sl.p[0][s];
+  // two slices per lane per round, every load issued before the containment tests (no early continue)
+  for (int64_t i0 = lo + lane; i0 < hi; i0 += 2 * G) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int64_t i = i0 + u * G;
+      const bool in = i < hi;
+      const int64_t s = base + (in ? i : lo);
+      const int64_t k0 = tmeas ? a.sl.ts[s] : a.sl.cs[s];
+      const int64_t k1 = tmeas ? a.sl.tl[s] : a.sl.cl[s];
+      const uint64_t c = a.sl.cnt[s];
+      const bool nonnull = recs ? a.sl.nn[s] != 0 : c != 0;
+      const uint64_t p0 = (need & NEED_SUM) ? a.sl.p[0][s] : 0;
+      const int64_t p1 = (need & NEED_MIN) ? (int64_t)a.sl.p[1][s] : ID_MIN;
+      const int64_t p2 = (need & NEED_MAX) ? (int64_t)a.sl.p[2][s] : ID_MAX;
+      const bool contains = tmeas ? (ws <= k0 && we > k1) : (ws <= k0 && we >= k1);
+      // a partial is present when non-null: count > 0, or (records mode) kept after liftAndInvert
+      if (!(in && contains && nonnull)) continue;
+      present = 1;
+      cnt += c;
+      if (need & NEED_SUM) {
+        if (vt == VT_F64) sf += __longlong_as_double((long long)p0);
+        else sw += p0;
+      }
+      if (need & NEED_MIN) mn = min(mn, p1);
+      if (need & NEED_MAX) mx = max(mx, p2);
     }
-    if (need & NEED_MIN) mn = min(mn, (int64_t)a.sl.p[1][s]);
-    if (need & NEED_MAX) mx = max(mx, (int64_t)a.sl.p[2][s]);
   }
   auto add_u = [](unsigned long long x, unsigned long long y) { return x + y; };
   auto min_i = [](long long x, long long y) { return x < y ? x : y; };
@@ -593,10 +643,12 @@ hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint3
 }
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group) {
   if (a.n_rows <= 0) return hipSuccess;
+  // single mode: n_rows is the capacity (the device holds the count): at most 256 workgroups stride over the rows
+  const int64_t cap = a.single ? 256 : INT32_MAX;
   if (group == 16)
-    hipLaunchKernelGGL(x::wm_agg_kernel<16>, dim3((unsigned)((a.n_rows + 15) / 16)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(x::wm_agg_kernel<16>, dim3((unsigned)std::min<int64_t>((a.n_rows + 15) / 16, cap)), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(x::wm_agg_kernel<64>, dim3((unsigned)((a.n_rows + 3) / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(x::wm_agg_kernel<64>, dim3((unsigned)std::min<int64_t>((a.n_rows + 3) / 4, cap)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

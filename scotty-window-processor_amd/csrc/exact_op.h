@@ -152,6 +152,49 @@ struct Mod {  // C/windowType/windowContext/{Shift,Delete,Add}Modification.java
 
 // ======================================================================== one operator, wave-uniform
 #define LANE_ID ((int)__lane_id())
+
+// Slice-list searches run by a whole wavefront (wave-uniform arguments and result).
+// wave_first: first i in [lo, hi) with pred(i), for pred false...false true...true over the range; hi if none.  A
+// 64-ary search, one probe per lane per round (two rounds for up to 4096 slices) instead of a chain of ~12 dependent
+// loads.
+template <typename P>
+__device__ __forceinline__ int wave_first(int lo, int hi, P pred) {
+  const int lane = LANE_ID;
+  while (hi - lo > 64) {
+    const int stride = (hi - lo + 63) >> 6;
+    const int p = lo + lane * stride;
+    const unsigned long long bal = __ballot(p < hi && pred(p));
+    if (bal == 0) {
+      lo = lo + ((hi - 1 - lo) / stride) * stride + 1;  // past the last probe
+    } else {
+      const int f = __ffsll((long long)bal) - 1;
+      if (f == 0) return lo;
+      const int pf = lo + f * stride;  // answer in (pf - stride, pf]
+      lo = pf - stride + 1;
+      hi = pf;
+    }
+  }
+  const int p = lo + lane;
+  const unsigned long long bal = __ballot(p < hi && pred(p));
+  return bal ? lo + __ffsll((long long)bal) - 1 : hi;
+}
+// wave_last: last i in [lo, hi) with pred(i), -1 if none (no order assumed): a backward scan, four 64-slice chunks per
+// round so their loads are in flight together
+template <typename P>
+__device__ __forceinline__ int wave_last(int lo, int hi, P pred) {
+  for (int b = hi - 1; b >= lo; b -= 256) {
+    unsigned long long m[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = b - j * 64 - LANE_ID;
+      m[j] = __ballot(i >= lo && pred(i));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (m[j]) return b - j * 64 - (__ffsll((long long)m[j]) - 1);
+  }
+  return -1;
+}
 struct Op {
   const XCfg* cfg;
   // slice arrays of this op (already offset by op * sc)
@@ -302,41 +345,19 @@ struct Op {
   // LazyAggregateStore.findSliceIndexByTimestamp (:29-37): last slice with tStart <= t, -1 if none
   __device__ int find_ts(int64_t t) {
     if (s.tail <= s.head) return -1;
-    if (!(s.unsorted & 1)) {
-      int lo = s.head, hi = s.tail;  // count of tStart <= t in [head, tail)
-      while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (ts[mid] <= t) lo = mid + 1; else hi = mid;
-      }
+    if (!(s.unsorted & 1)) {  // count of tStart <= t in [head, tail)
+      const int lo = wave_first(s.head, s.tail, [&](int i) { return ts[i] > t; });
       return lo - 1 >= s.head ? lo - 1 : -1;
     }
-    for (int b = s.tail - 1; b >= s.head; b -= 64) {
-      const int i = b - LANE_ID;
-      const bool hit = i >= s.head && ts[i] <= t;
-      const unsigned long long m = __ballot(hit);
-      if (m) return b - (__ffsll((long long)m) - 1);
-    }
-    return -1;
+    return wave_last(s.head, s.tail, [&](int i) { return ts[i] <= t; });
   }
   // LazyAggregateStore.findSliceIndexByCount (:41-49)
   __device__ int find_count(int64_t c) {
-    for (int b = s.tail - 1; b >= s.head; b -= 64) {
-      const int i = b - LANE_ID;
-      const bool hit = i >= s.head && cs[i] <= c;
-      const unsigned long long m = __ballot(hit);
-      if (m) return b - (__ffsll((long long)m) - 1);
-    }
-    return -1;
+    return wave_last(s.head, s.tail, [&](int i) { return cs[i] <= c; });
   }
   // LazyAggregateStore.findSliceByEnd (:127-135)
   __device__ int find_end(int64_t e) {
-    for (int b = s.tail - 1; b >= s.head; b -= 64) {
-      const int i = b - LANE_ID;
-      const bool hit = i >= s.head && te[i] == e;
-      const unsigned long long m = __ballot(hit);
-      if (m) return b - (__ffsll((long long)m) - 1);
-    }
-    return -1;
+    return wave_last(s.head, s.tail, [&](int i) { return te[i] == e; });
   }
 
   // AbstractSlice.addElement + AggregateState.addElement (one tuple, exact)

@@ -13,7 +13,8 @@
 // change is the last one's end moving to the batch max (shiftEnd, SessionWindow.java:72-74).  The batch is therefore
 // ingested ONCE with the grid path's ingest kernel into per-cell partials (cells = retained slices ++ grid cells above
 // the pending edge), and a one-workgroup commit verifies the quiet conditions from the ingest's per-tile maxima and
-// counters and either commits (edges, slices, state, sessions) or returns every cell to identity so the host runs
+// counters (the per-tile and per-edge scans of the batch spread over many workgroups, exact_quiet.hip) and either
+// commits (edges, slices, state, sessions) or returns every cell to identity so the host runs
 // the event-exact batch path (exact_batch.hip) on the same batch.  No state is written before the verdict.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -45,6 +46,8 @@ struct XQCtl {
   int64_t h_end;        // grid horizon end
   int64_t batch_max;    // maxEventTime after the committed batch
   int64_t why;          // XQ_NOT_QUIET: 1 late / past the horizon, 2 below lo_bound, 4 tile start jump, 8 item jump, 16 range
+  int64_t ncand;        // grid points <= batch_max (scan kernel -> edge and commit kernels)
+  int64_t jump_tile;    // XQ_NOT_QUIET: first arrival tile holding a session-gap jump (JMAX: none located)
 };
 
 struct XQArgs {
@@ -62,6 +65,7 @@ struct XQArgs {
   long long* c_tmax;
   unsigned long long* c_part[NPART];
   long long* tilemax;
+  long long* pmax;       // scratch [NT_MAX]: prefix maxima of the tile maxima (arrival order)
   int32_t* rank;         // scratch [gcap]
   int32_t* flag;         // scratch [gcap]
   int64_t* eg;           // scratch [gcap]: emitted edges by rank
@@ -72,6 +76,8 @@ struct XQArgs {
 };
 
 hipError_t launch_xq_prep(const XQArgs& a, hipStream_t st);
+// after the ingest: xq_scan_kernel (1 workgroup: prefix maxima, batch max, candidates), xq_edges_kernel (many
+// workgroups: the gap checks of every tile and one arrival tile per candidate edge), xq_commit_kernel (1 workgroup)
 hipError_t launch_xq_commit(const XQArgs& a, hipStream_t st);
 
 }  // namespace scotty

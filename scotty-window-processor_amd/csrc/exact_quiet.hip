@@ -152,20 +152,12 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
     q.pending = s.nextEdgeTs;
     q.h_end = h_end;
     q.why = why;
+    q.jump_tile = (why & 4) ? 0 : JMAX;
     *a.ctl = q;
   }
 }
 
-__device__ __forceinline__ int64_t lower_bound_lds(const long long* p, int64_t n, int64_t x) {  // first p[i] >= x
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (p[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// block-wide (1024 threads) inclusive max scan; wtot: LDS [16]
+// block-wide (1024 threads) inclusive max scan; wtot: LDS [16] (wtot[15] = the block's max on return)
 __device__ __forceinline__ int64_t block_incl_max(int64_t v, long long* wtot, int lane, int wid) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -188,32 +180,21 @@ __device__ __forceinline__ int64_t block_incl_max(int64_t v, long long* wtot, in
   return v;
 }
 
-__global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
-  __shared__ long long s_p[NT_MAX];  // tile maxima -> prefix maxima (arrival order)
+// ---- scan (1 workgroup): prefix maxima of the ingest's tile maxima, batch max, the candidate grid points
+//      g[k] <= batch_max, and the verdict parts that need no pass over the batch
+__global__ __launch_bounds__(1024) void xq_scan_kernel(XQArgs a) {
   __shared__ long long s_w[32];
-  __shared__ int64_t sc[8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  auto stamp = [&](int k) {
-    if (a.dbg && tid == 0) a.dbg[k] = (long long)__builtin_amdgcn_s_memtime();
-  };
-  stamp(0);
   const XQCtl q = *a.ctl;
   if (q.result != XQ_NONE) return;  // refused by the prep kernel: no cell was touched
-  const XCfg* cfg = a.cfg;
   const DevMeta& m = *a.meta;
-  const int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount, cmin = m.cmin;
+  const int64_t j0 = m.j0, gcount = m.gcount;
   const int64_t P = q.p_start;
-  const int64_t c_old = tail - head;
   int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
   if (kc < 0) kc = 0;
-  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : JMAX;
   const int64_t* g = a.grid + j0;
-  const int64_t L = cfg->max_lateness;
-  const int64_t tile = a.tile;
-  const int64_t nT = (a.n + tile - 1) / tile;
-  const int need = cfg->need, vt = cfg->vt;
-
-  // ---- prefix max over the tile maxima (8 consecutive tiles per thread)
+  const int64_t nT = (a.n + a.tile - 1) / a.tile;
+  // prefix max over the tile maxima (8 consecutive tiles per thread)
   int64_t loc[8];
   int64_t run = JMIN;
 #pragma unroll
@@ -228,169 +209,252 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const int64_t t = (int64_t)tid * 8 + j;
-    if (t < nT) s_p[t] = max(carry0, loc[j]);
+    if (t < nT) a.pmax[t] = max(carry0, loc[j]);
   }
-  __syncthreads();
-  const int64_t batch_max = max(P, nT > 0 ? (int64_t)s_p[nT - 1] : JMIN);
-  stamp(1);
-
-  // ---- quiet verdict
-  bool fail = false;
-  __shared__ int s_why;
-  if (tid == 0) {
-    int why = 0;
+  const int64_t batch_max = max(P, (int64_t)s_w[15]);
+  if (wid != 0) return;
+  // candidates: grid points g[k] <= batch_max (k < kc), a 64-ary search
+  int64_t lo = 0, hi = kc;  // first k with g[k] > batch_max
+  while (hi - lo > 64) {
+    const int64_t stride = (hi - lo + 63) >> 6;
+    const int64_t p = lo + (int64_t)lane * stride;
+    const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
+    if (bal == 0) {
+      lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
+    } else {
+      const int f = __ffsll((long long)bal) - 1;
+      if (f == 0) {
+        hi = lo;
+        break;
+      }
+      const int64_t pf = lo + (int64_t)f * stride;
+      lo = pf - stride + 1;
+      hi = pf;
+    }
+  }
+  if (hi > lo) {
+    const int64_t p = lo + lane;
+    const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
+    lo = bal ? lo + __ffsll((long long)bal) - 1 : hi;
+  }
+  if (lane == 0) {
+    int64_t why = 0;
     if (m.late_push != 0 || m.overflow_push != 0) why |= 1;  // a too-late tuple, or one past the grid horizon
+    const int64_t cmin = m.cmin, c_old = m.tail - m.head;
     if (cmin != INT64_MAX) {  // the lowest cell any tuple landed in must start at or above lo_bound
-      const int64_t cs0 = cmin < c_old ? a.sl.ts[head + cmin] : (cmin - c_old < kc ? g[cmin - c_old] : h_end);
+      const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : JMAX;
+      const int64_t cs0 = cmin < c_old ? a.sl.ts[m.head + cmin] : (cmin - c_old < kc ? g[cmin - c_old] : h_end);
       if (cs0 < q.lo_bound) why |= 2;
     }
     if (batch_max > SAFE) why |= 16;
-    s_why = why;
-    fail = why != 0;
+    XQCtl* o = a.ctl;
+    o->batch_max = batch_max;
+    o->ncand = lo;
+    o->why = why;
   }
-  __shared__ int s_nscan;
-  __shared__ int s_scan[64];
-  if (tid == 0) s_nscan = 0;
-  __syncthreads();
-  if (cfg->n_ctx > 0) {
-    // no in-order jump by a gap: items after a tile's first are below max(carry, first) + gap; the first is below
-    // carry + gap (carry = running max before the tile).  A tile failing this bound (a slow stream: the tile spans
-    // more than a gap of event time) is checked item by item below.
-    for (int64_t t = tid; t < nT; t += 1024) {
-      const int64_t carry = t > 0 ? max(P, (int64_t)s_p[t - 1]) : P;
-      const int64_t t0 = a.ts[t * tile], tm = a.tilemax[t];
-      if (!lt_plus(t0, carry, q.min_gap)) {
-        fail = true;
-        atomicOr(&s_why, 4);
-      } else if (!lt_plus(tm, max(carry, t0), q.min_gap)) {
-        const int i = atomicAdd(&s_nscan, 1);
-        if (i < 64) s_scan[i] = (int)t;
-        else {
-          fail = true;
-          atomicOr(&s_why, 8);
-        }
-      }
-    }
-  }
-  fail = __syncthreads_or(fail);
-  if (!fail && s_nscan > 0) {
-    // exact test of the listed tiles: every item below (running max before it) + gap, one wave per tile
-    const int nscan = s_nscan;
-    for (int i = wid; i < nscan; i += 16) {
-      const int64_t t = s_scan[i];
-      int64_t run_ = t > 0 ? max(P, (int64_t)s_p[t - 1]) : P;
-      const int64_t e0 = t * tile, e1 = min(a.n, e0 + tile);
-      bool bad = false;
-      for (int64_t base = e0; base < e1 && !bad; base += 64) {
-        const int64_t idx = base + lane;
-        const int64_t v = idx < e1 ? a.ts[idx] : JMIN;
-        int64_t inc = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int64_t u = (int64_t)__shfl_up((long long)inc, o);
-          if (lane >= o) inc = max(inc, u);
-        }
-        int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
-        if (lane == 0) ex = JMIN;
-        ex = max(ex, run_);
-        bad = __ballot(idx < e1 && !lt_plus(v, ex, q.min_gap)) != 0;
-        run_ = max(run_, rl64(inc, 63));
-      }
-      if (bad) {
-        fail = true;
-        atomicOr(&s_why, 8);
-      }
-    }
-    fail = __syncthreads_or(fail);
-  }
+}
 
-  stamp(2);
-  // ---- candidates: grid points g[k] <= batch_max (k < kc)
-  if (wid == 0) {
-    int64_t lo = 0, hi = fail ? 0 : kc;  // first k with g[k] > batch_max
-    while (hi - lo > 64) {
-      const int64_t stride = (hi - lo + 63) >> 6;
-      const int64_t p = lo + (int64_t)lane * stride;
-      const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
-      if (bal == 0) {
-        lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
-      } else {
-        const int f = __ffsll((long long)bal) - 1;
-        if (f == 0) {
-          hi = lo;
+constexpr int XE_T = 256;                  // threads per edge workgroup
+constexpr int XE_PER = 32;                 // consecutive tuples per thread per chunk
+constexpr int XE_CHUNK = XE_T * XE_PER;    // 8192 tuples: one tile of a 2^26-tuple batch in one round of loads
+constexpr int XE_GRID = 256;               // edge workgroups
+constexpr int XE_LIST = 64;                // slow tiles a workgroup can list (>= its share of NT_MAX tiles)
+static_assert((NT_MAX + XE_GRID - 1) / XE_GRID <= XE_LIST, "every tile of a workgroup's share fits its list");
+
+// exclusive max over the threads before this one in a 256-thread block; total = the block's max.  s4: LDS [4]
+__device__ __forceinline__ int64_t blk_excl_max(int64_t v, long long* s4, int lane, int wid, int64_t& total) {
+  int64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = (int64_t)__shfl_up((long long)inc, o);
+    if (lane >= o) inc = max(inc, u);
+  }
+  if (lane == 63) s4[wid] = inc;
+  __syncthreads();
+  int64_t before = JMIN;
+  total = JMIN;
+#pragma unroll
+  for (int w = 0; w < XE_T / 64; w++) {
+    const int64_t x = s4[w];
+    if (w < wid) before = max(before, x);
+    total = max(total, x);
+  }
+  int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
+  if (lane == 0) ex = JMIN;
+  __syncthreads();  // s4 free again
+  return max(before, ex);
+}
+
+// this thread's XE_PER consecutive tuples of the chunk at base (JMIN at and past e1)
+__device__ __forceinline__ void xe_load(const int64_t* ts, int64_t base, int64_t e1, int tid, int64_t (&v)[XE_PER]) {
+  const int64_t i0 = base + (int64_t)tid * XE_PER;
+  if (i0 + XE_PER <= e1) {
+#pragma unroll
+    for (int j = 0; j < XE_PER; j++) v[j] = ts[i0 + j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < XE_PER; j++) v[j] = i0 + j < e1 ? ts[i0 + j] : JMIN;
+  }
+}
+
+// ---- edges (XE_GRID workgroups): (1) no in-order jump by a session gap -- items after a tile's first are below
+//      max(carry, first) + gap, the first below carry + gap (carry = running max before the tile); a tile failing
+//      the bound (a slow stream: it spans more than a gap of event time) is checked item by item;
+//      (2) per candidate grid point g[k], StreamSlicer.determineSlices (S/StreamSlicer.java:55-84; see commit_kernel
+//      of slicing_kernels.hip): the in-order tuple e that first reaches g[k] (running max m before it) makes g[k]
+//      an edge iff g[k] == nextGrid(m) or e - g[k] < maxLateness; its arrival index is the new slice's cStart /
+//      cLast (WindowManager.getCurrentCount at appendSlice, S/SliceManager.java:36).  One workgroup per candidate
+//      reads the candidate's arrival tile in one round of loads (spread over the chip instead of one workgroup's
+//      chain of loads per candidate).
+__global__ __launch_bounds__(XE_T) void xq_edges_kernel(XQArgs a) {
+  __shared__ long long s4[XE_T / 64];
+  __shared__ int s_list[XE_LIST];
+  __shared__ int s_nl;
+  __shared__ int s_i[XE_T / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const XQCtl q = *a.ctl;
+  if (q.result != XQ_NONE) return;
+  const XCfg* cfg = a.cfg;
+  const int64_t P = q.p_start, tile = a.tile, nT = (a.n + tile - 1) / tile;
+  const int64_t* g = a.grid + a.meta->j0;
+  if (cfg->n_ctx > 0) {
+    const int64_t gap = q.min_gap;
+    const int64_t per = (nT + gridDim.x - 1) / gridDim.x;
+    const int64_t t0 = (int64_t)blockIdx.x * per, t1 = min(nT, t0 + per);
+    if (tid == 0) s_nl = 0;
+    __syncthreads();
+    bool bad = false;
+    for (int64_t t = t0 + tid; t < t1; t += XE_T) {
+      const int64_t carry = t > 0 ? max(P, (int64_t)a.pmax[t - 1]) : P;
+      const int64_t f0 = a.ts[t * tile], tm = a.tilemax[t];
+      if (!lt_plus(f0, carry, gap)) {
+        if (!bad) atomicMin((long long*)&a.ctl->jump_tile, (long long)t);  // t ascends: the thread's first
+        bad = true;
+      } else if (!lt_plus(tm, max(carry, f0), gap)) {
+        s_list[atomicAdd(&s_nl, 1)] = (int)t;
+      }
+    }
+    if (bad) atomicOr((unsigned long long*)&a.ctl->why, 4ull);
+    __syncthreads();
+    const int nl = s_nl;
+    for (int li = 0; li < nl; li++) {
+      const int64_t t = s_list[li];
+      int64_t r = t > 0 ? max(P, (int64_t)a.pmax[t - 1]) : P;
+      const int64_t e1 = min(a.n, (t + 1) * tile);
+      bool badi = false;
+      for (int64_t base = t * tile; base < e1; base += XE_CHUNK) {
+        int64_t v[XE_PER];
+        xe_load(a.ts, base, e1, tid, v);
+        int64_t tmx = JMIN;
+#pragma unroll
+        for (int j = 0; j < XE_PER; j++) tmx = max(tmx, v[j]);
+        int64_t total;
+        int64_t run = max(r, blk_excl_max(tmx, s4, lane, wid, total));
+        const int64_t i0 = base + (int64_t)tid * XE_PER;
+#pragma unroll
+        for (int j = 0; j < XE_PER; j++) {
+          if (i0 + j < e1 && !lt_plus(v[j], run, gap)) badi = true;
+          run = max(run, v[j]);
+        }
+        r = max(r, total);
+      }
+      if (__syncthreads_or(badi) && tid == 0) {
+        atomicOr((unsigned long long*)&a.ctl->why, 8ull);
+        atomicMin((long long*)&a.ctl->jump_tile, (long long)t);
+      }
+    }
+  }
+  const int64_t ncand = a.ctl->ncand;
+  const int64_t L = cfg->max_lateness;
+  for (int64_t k = blockIdx.x; k < ncand; k += gridDim.x) {
+    const int64_t gk = g[k];
+    // arrival tile of the first tuple >= gk: the number of tiles whose prefix max is below gk
+    int cb = 0;
+#pragma unroll 8
+    for (int64_t t = tid; t < nT; t += XE_T) cb += a.pmax[t] < gk ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cb += __shfl_xor(cb, o);
+    if (lane == 0) s_i[wid] = cb;
+    __syncthreads();
+    int64_t tk = 0;
+#pragma unroll
+    for (int w = 0; w < XE_T / 64; w++) tk += s_i[w];
+    __syncthreads();
+    bool found = false;
+    if (tk < nT) {
+      int64_t r = tk > 0 ? max(P, (int64_t)a.pmax[tk - 1]) : P;
+      const int64_t e1 = min(a.n, (tk + 1) * tile);
+      for (int64_t base = tk * tile; base < e1; base += XE_CHUNK) {
+        int64_t v[XE_PER];
+        xe_load(a.ts, base, e1, tid, v);
+        int hit = -1;
+        int64_t hv = JMIN, before = JMIN, tmx = JMIN;
+#pragma unroll
+        for (int j = 0; j < XE_PER; j++) {
+          if (hit < 0 && v[j] >= gk) {
+            hit = j;
+            hv = v[j];
+            before = tmx;
+          }
+          tmx = max(tmx, v[j]);
+        }
+        int64_t total;
+        const int64_t ex = blk_excl_max(tmx, s4, lane, wid, total);
+        const unsigned long long bal = __ballot(hit >= 0);
+        if (lane == 0) s_i[wid] = bal ? wid * 64 + __ffsll((long long)bal) - 1 : XE_T;
+        __syncthreads();
+        int win = XE_T;
+#pragma unroll
+        for (int w = 0; w < XE_T / 64; w++) win = min(win, s_i[w]);
+        __syncthreads();
+        if (win < XE_T) {
+          if (tid == win) {
+            const int64_t mm = max(max(r, ex), before);
+            const bool emit = k == 0 || g[k - 1] <= mm || (int64_t)((uint64_t)hv - (uint64_t)gk) < L;
+            a.flag[k] = emit ? 1 : 0;
+            a.epos[k] = base + (int64_t)tid * XE_PER + hit;
+          }
+          found = true;
           break;
         }
-        const int64_t pf = lo + (int64_t)f * stride;
-        lo = pf - stride + 1;
-        hi = pf;
+        r = max(r, total);
       }
     }
-    if (hi > lo) {
-      const int64_t p = lo + lane;
-      const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
-      lo = bal ? lo + __ffsll((long long)bal) - 1 : hi;
-    }
-    if (lane == 0) sc[0] = lo;
-  }
-  __syncthreads();
-  const int64_t ncand = sc[0];
-  stamp(3);
-
-  // ---- edge decision (StreamSlicer.determineSlices, S/StreamSlicer.java:55-84; see commit_kernel): a grid point g
-  //      first reached by the in-order tuple e (running max m before it) becomes an edge iff g == nextGrid(m) or
-  //      e - g < maxLateness.  Every candidate's first-reaching tuple is located in its tile by one wave (its arrival
-  //      index is the new slice's cStart / cLast: WindowManager.getCurrentCount at appendSlice, S/SliceManager.java:36).
-  for (int64_t k = wid; k < ncand; k += 16) {
-    const int64_t gk = g[k];
-    const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
-    int64_t r = ts_ > 0 ? max(P, (int64_t)s_p[ts_ - 1]) : P;
-    const int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
-    int64_t e = JMIN, mm = JMIN, pos = -1;
-    constexpr int B = 16;
-    for (int64_t base = e0; base < e1 && pos < 0; base += 64 * B) {
-      int64_t v[B];
-#pragma unroll
-      for (int j = 0; j < B; j++) {
-        const int64_t i = base + j * 64 + lane;
-        v[j] = i < e1 ? a.ts[i] : JMIN;
-      }
-      int jf = -1;  // first of the B rows holding a tuple >= gk (wave-uniform)
-      unsigned long long hf = 0;
-      int64_t vf = JMIN;
-#pragma unroll
-      for (int j = 0; j < B; j++) {
-        const unsigned long long hit = __ballot(v[j] >= gk);
-        if (jf < 0) {
-          if (hit) {
-            jf = j;
-            hf = hit;
-            vf = v[j];
-          } else {
-            r = max(r, wmax(v[j]));
-          }
-        }
-      }
-      if (jf >= 0) {
-        const int f = __ffsll((long long)hf) - 1;
-        e = rl64(vf, f);
-        mm = max(r, wmax(lane < f ? vf : JMIN));
-        pos = base + jf * 64 + f;
-      }
-    }
-    if (lane == 0) {
-      const bool emit = k == 0 || g[k - 1] <= mm || (int64_t)((uint64_t)e - (uint64_t)gk) < L;
-      a.flag[k] = emit ? 1 : 0;
-      a.epos[k] = pos;
+    if (!found && tid == 0) {  // unreachable: g[k] <= batch_max is reached inside the batch
+      a.flag[k] = k == 0 ? 1 : 0;
+      a.epos[k] = -1;
     }
   }
-  __syncthreads();
+}
 
-  stamp(4);
+// ---- commit (1 workgroup): verdict, slice appends, cell fold, operator scalars
+__global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
+  __shared__ long long s_w[32];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto stamp = [&](int k) {
+    if (a.dbg && tid == 0) a.dbg[k] = (long long)__builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  const XQCtl q = *a.ctl;
+  if (q.result != XQ_NONE) return;  // refused by the prep kernel: no cell was touched
+  const XCfg* cfg = a.cfg;
+  const DevMeta& m = *a.meta;
+  const int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount, cmin = m.cmin;
+  const int64_t c_old = tail - head;
+  int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+  if (kc < 0) kc = 0;
+  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : JMAX;
+  const int64_t* g = a.grid + j0;
+  const int need = cfg->need, vt = cfg->vt;
+  const int64_t batch_max = q.batch_max;
+  const int64_t ncand = q.ncand;
+  const bool fail = q.why != 0;
+
   // ---- rank = inclusive prefix count of emitted edges
   int64_t n_emit = 0;
   {
     int64_t base_cnt = 0;
-    for (int64_t base = 0; base < ncand; base += 1024) {
+    for (int64_t base = 0; base < (fail ? 0 : ncand); base += 1024) {
       const int64_t k = base + tid;
       const bool f = k < ncand && a.flag[k] == 1;
       const unsigned long long bal = __ballot(f);
@@ -416,7 +480,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     n_emit = base_cnt;
   }
   int32_t result = XQ_COMMITTED;
-  stamp(5);
+  stamp(1);
   if (fail) result = XQ_NOT_QUIET;
   else if (tail + n_emit > cfg->sc) result = XQ_CAPACITY;
   __syncthreads();
@@ -433,10 +497,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
       a.c_part[1][c] = (unsigned long long)ID_MIN;
       a.c_part[2][c] = (unsigned long long)ID_MAX;
     }
-    if (tid == 0) {
-      a.ctl->result = result;
-      a.ctl->why = s_why;
-    }
+    if (tid == 0) a.ctl->result = result;
     return;
   }
 
@@ -464,7 +525,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     sl.ty[pv] = XTYPE_FIXED | (sl.ty[pv] & XTYPE_LAZY);
   }
   __syncthreads();
-  stamp(6);
+  stamp(2);
   // ---- cells into slices (AbstractSlice.addElement + AggregateState.addElement), cells back to identity
   for (int64_t c = cfirst + tid; c < ncell; c += 1024) {
     const unsigned long long cnt = a.c_cnt[c];
@@ -491,7 +552,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     a.c_part[1][c] = (unsigned long long)ID_MIN;
     a.c_part[2][c] = (unsigned long long)ID_MAX;
   }
-  stamp(7);
+  stamp(3);
   // ---- scalars: StreamSlicer.maxEventTime / min_next_edge_ts, WindowManager.currentCount, and the last session of
   //      every context extended to the batch max (every in-order tuple is within a gap of it: shiftEnd)
   if (tid == 0) {
@@ -508,7 +569,6 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     }
     XQCtl* o = a.ctl;
     o->n_emit = n_emit;
-    o->batch_max = batch_max;
     o->rebuild = cfg->has_fixed && (kc - ncand < 1024 || (h_end != JMAX && h_end - batch_max < a.margin)) ? 1 : 0;
     o->result = XQ_COMMITTED;
   }
@@ -521,6 +581,9 @@ hipError_t launch_xq_prep(const XQArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_xq_commit(const XQArgs& a, hipStream_t st) {
+  if ((a.n + a.tile - 1) / a.tile > NT_MAX) return hipErrorInvalidValue;  // the scan holds 8 tiles per thread
+  hipLaunchKernelGGL(xq::xq_scan_kernel, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(xq::xq_edges_kernel, dim3(xq::XE_GRID), dim3(xq::XE_T), 0, st, a);
   hipLaunchKernelGGL(xq::xq_commit_kernel, dim3(1), dim3(1024), 0, st, a);
   return hipGetLastError();
 }

@@ -1550,6 +1550,7 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 10: return op->x->quiet_fallbacks;
     case 11: return op->x->last_quiet_why;
     case 12: return op->x->quiet_tail_commits;  // batches whose remainder committed after an event-exact prefix
+    case 13: return op->x->quiet_split_commits;  // quiet prefixes committed up to a located session-gap jump
     default: return -1;
   }
 }

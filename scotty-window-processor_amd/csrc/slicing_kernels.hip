@@ -163,8 +163,9 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
   // thread per cell: cell c owns the buckets whose point first + (k << shift) lies in [start(c), start(c+1));
   // cells are sorted, so the block stops at its first cell starting at or beyond span_end.  A cell owning more
   // than CIX_RUN buckets (cells of seconds at one bucket per ms) is queued in LDS and written by the whole block,
-  // not by its one thread bucket after bucket.
-  constexpr int CIX_RUN = 16;
+  // not by its one thread bucket after bucket.  (CIX_RUN 16 queued every 60-ms cell of a 60 s window: 256 serial
+  // block rounds, 30 us; a thread's run of up to 128 stores issues without waiting.)
+  constexpr int CIX_RUN = 128;
   __shared__ int64_t l_k0[256], l_k1[256];
   __shared__ uint32_t l_c[256];
   __shared__ int l_n;
