@@ -456,10 +456,20 @@ __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
   if (k > 0) {
     const int S = o.s.tail - o.s.head;
     auto rel = [&](int i) { return i < 0 ? -1 : i - o.s.head; };
+    // min(si, findSliceIndexByCount(minCount)) and max(ei, findSliceIndexByCount(maxCount)) look only where the last
+    // slice with cStart <= x can change the bound: a hit at or after si leaves si (searched first, from the tail), a
+    // hit at or before ei leaves ei (only (ei, tail) is searched) -- not the whole list from the tail
     int si = max(rel(o.find_ts(minTs)), 0);
-    si = min(si, rel(o.find_count(minCount)));
+    {
+      const int h = o.s.head + si;
+      if (wave_last(h, o.s.tail, [&](int i) { return o.cs[i] <= minCount; }) < 0)
+        si = min(si, rel(wave_last(o.s.head, h, [&](int i) { return o.cs[i] <= minCount; })));
+    }
     int ei = min(S - 1, rel(o.find_ts(maxTs)));
-    ei = max(ei, rel(o.find_count(maxCount)));
+    {
+      const int j = wave_last(o.s.head + ei + 1, o.s.tail, [&](int i) { return o.cs[i] <= maxCount; });
+      if (j >= 0) ei = max(ei, rel(j));
+    }
     if (si < 0 && si <= ei) {  // getSlice(-1): IndexOutOfBoundsException in the reference
       if (lane == 0) atomicOr(a.err_flag, 2);
       si = 0;

@@ -43,10 +43,30 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
       res = XQ_STATE;
       why |= 512;
     } else {
-      int64_t lo = 0, hi = a.gcount;  // first grid entry >= N
-      while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a.grid[mid] < N) lo = mid + 1; else hi = mid;
+      // first grid entry >= N: a 64-ary search (3-4 rounds of one probe per lane over up to 2^20 entries instead of
+      // a chain of 20 dependent loads)
+      int64_t lo = 0, hi = a.gcount;
+      while (hi - lo > 64) {
+        const int64_t stride = (hi - lo + 63) >> 6;
+        const int64_t p = lo + (int64_t)lane * stride;
+        const unsigned long long bal = __ballot(p < hi && a.grid[p] >= N);
+        if (bal == 0) {
+          lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
+        } else {
+          const int f = __ffsll((long long)bal) - 1;
+          if (f == 0) {
+            hi = lo;
+            break;
+          }
+          const int64_t pf = lo + (int64_t)f * stride;
+          lo = pf - stride + 1;
+          hi = pf;
+        }
+      }
+      if (hi > lo) {
+        const int64_t p = lo + lane;
+        const unsigned long long bal = __ballot(p < hi && a.grid[p] >= N);
+        lo = bal ? lo + __ffsll((long long)bal) - 1 : hi;
       }
       if (lo + 1 >= a.gcount || a.grid[lo] != N) {
         res = XQ_GRID;

@@ -15,19 +15,25 @@ def main():
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
     rows = [r for r in rows if "at::native" not in r["Kernel_Name"]]
     starts = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]] + [len(rows)]
-    steps = []
+    steps, spans, calls = [], [], []
     for a, b in zip(starts[:-1], starts[1:]):
         per = collections.defaultdict(float)
+        cnt = collections.Counter()
         for r in rows[a:b]:
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-            per[r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scotty::", "")[:60]] += d
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("scotty::", "")[:60]
+            per[k] += d
+            cnt[k] += 1
         steps.append(per)
+        calls.append(cnt)
+        spans.append((int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3)
     order = sorted(range(len(steps)), key=lambda i: sum(steps[i].values()))
     for label, i in (("median", order[len(order) // 2]), ("largest", order[-1])):
         p = steps[i]
-        print("C3 %s step of %d: device %.1f us" % (label, len(steps), sum(p.values())))
+        print("C3 %s step of %d: device %.1f us, first start to last end %.1f us, %d launches" %
+              (label, len(steps), sum(p.values()), spans[i], sum(calls[i].values())))
         for name in sorted(p, key=lambda x: -p[x])[:14]:
-            print("  %-60s %8.1f us" % (name, p[name]))
+            print("  %-60s %8.1f us  %4d calls" % (name, p[name], calls[i][name]))
 
 
 if __name__ == "__main__":
