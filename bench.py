@@ -298,7 +298,8 @@ def extra_c1(pkg, dev, batch, steps):
     rate = max(1, batch // 1000)
     jr = pkg.workloads.JavaRandomInts(43)
     op = pkg.SlicingWindowOperator(device=dev.index)
-    op.addWindowFunction(pkg.AGG_SUM_I32)
+    for agg in aggs or (pkg.AGG_SUM_I32,):  # aggs: A/B of the watermark's assembly (tools/c4_run.py minmax)
+        op.addWindowFunction(agg)
     op.setMaxLateness(1)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
     wts = torch.arange(0, 60_000, dtype=torch.int64, device=dev)
@@ -623,7 +624,7 @@ def c4_routing(pkg, dev, batch, keys, steps, rank, world, dist, seed=4242):
             "received_tuples_rank0_per_step": got / steps, "backend": dist.get_backend()}
 
 
-def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None):
+def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None, aggs=None):
     """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
     connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
     with no collective -- rank r owns the keys KeyedShardRouter(world) assigns it (what an upstream keyBy delivers), `keys`
@@ -638,7 +639,8 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
         op.tune("keyed_lane", 0)
     for k, v in (tune or {}).items():
         op.tune(k, v)
-    op.addWindowFunction(pkg.AGG_SUM_I32)
+    for agg in aggs or (pkg.AGG_SUM_I32,):  # aggs: A/B of the watermark's assembly (tools/c4_run.py minmax)
+        op.addWindowFunction(agg)
     op.setMaxLateness(1)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate

@@ -13,7 +13,10 @@ def main():
     bench = importlib.import_module("bench")
     pkg = importlib.import_module("scotty-window-processor_amd")
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 6
-    r = bench.extra_c4(pkg, torch.device("cuda", 0), bench.C4_BATCH, 1 << 20, steps)
+    aggs = None
+    if len(sys.argv) > 2 and sys.argv[2] == "minmax":  # the keyed watermark's MIN/MAX assembly vs the SUM prefix path
+        aggs = (pkg.AGG_MIN_I32, pkg.AGG_MAX_I32)
+    r = bench.extra_c4(pkg, torch.device("cuda", 0), bench.C4_BATCH, 1 << 20, steps, aggs=aggs)
     print(json.dumps(r), flush=True)
 
 
