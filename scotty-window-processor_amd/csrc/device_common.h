@@ -124,6 +124,7 @@ struct WmArgs {
   int64_t n_windows;               // row capacity of the packed output (an upper bound of the triggered windows,
                                    // computed on the host in O(#definitions)); the device writes the true count
   unsigned char* out;              // packed output (device): header, start[n], end[n], values[n_aggs][n], has[n]
+  unsigned char* hout;             // nullable: the same layout in host-mapped memory, written directly (no publish copy)
   int32_t n_aggs;
   int32_t agg_kind[8];
   int need;

@@ -1282,6 +1282,7 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     wa.remove_from = remove_from;
     wa.n_windows = cap;
     wa.out = op->d_out;
+    wa.hout = (unsigned char*)op->h_out_dev;  // rows written straight into host-mapped memory: no publish copy
     wa.n_aggs = (int32_t)op->aggs.size();
     for (size_t k = 0; k < op->aggs.size(); k++) wa.agg_kind[k] = op->aggs[k];
     wa.need = op->need;
@@ -1293,12 +1294,14 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
       if (rc) return rc;
       HIPCHK(launch_wm(wa, op->stream));
       rc = tend(op, tw);
-      if (!rc) rc = tbegin(op, tc, SCOTTY_TIME_RESULT_COPY);
       if (rc) return rc;
-      if (op->h_out_dev) HIPCHK(launch_wm_publish(op->d_out, op->h_out_dev, L.total, op->stream));
-      else HIPCHK(hipMemcpyAsync(op->h_out, op->d_out, L.total, hipMemcpyDeviceToHost, op->stream));
-      rc = tend(op, tc);
-      if (rc) return rc;
+      if (!op->h_out_dev) {  // no host-mapped result buffer: one DMA transfer (class RESULT_COPY)
+        rc = tbegin(op, tc, SCOTTY_TIME_RESULT_COPY);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(op->h_out, op->d_out, L.total, hipMemcpyDeviceToHost, op->stream));
+        rc = tend(op, tc);
+        if (rc) return rc;
+      }
       // the next micro-batch's cell index is built while the host handles this result
       if (!op->wm_ev) HIPCHK(hipEventCreateWithFlags(&op->wm_ev, hipEventDisableTiming));
       HIPCHK(hipEventRecord(op->wm_ev, op->stream));

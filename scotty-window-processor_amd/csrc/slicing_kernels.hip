@@ -892,6 +892,13 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   // in-order tuple e(g) that first reaches g appends {N} U {g' : max(N, e - maxLateness) < g' <= e};
   // hence g becomes an edge iff g == nextGrid(m(g)) or e(g) - g < maxLateness, where m(g) is the
   // running max before e(g).  e(g), m(g) come from the tile prefix maxima; ambiguous cases scan the tile.
+  // ambiguous candidates are listed in LDS, so the exact pass below visits only them (a wave walking every 16th
+  // candidate's flag in global memory was a chain of dependent loads, ~10 us for C2's ~180 candidates)
+  constexpr int AMB_CAP = 256;
+  __shared__ int32_t s_amb[AMB_CAP];
+  __shared__ int s_namb;
+  if (tid == 0) s_namb = 0;
+  __syncthreads();
   if (!ovf) {
     for (int64_t k = tid; k < ncand; k += 1024) {
       const int64_t gk = g[k];
@@ -902,12 +909,19 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       if (k == 0 || g[k - 1] <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < L) f = 1;
       else f = 2;
       a.flag[k] = f;
+      if (f == 2) {
+        const int i = atomicAdd(&s_namb, 1);
+        if (i < AMB_CAP) s_amb[i] = (int32_t)k;
+      }
     }
   }
   __syncthreads();
+  const int namb = s_namb;
   if (!ovf) {
-    for (int64_t k = wid; k < ncand; k += 16) {
-      if (a.flag[k] != 2) continue;
+    const int64_t kn = namb <= AMB_CAP ? namb : ncand;  // list overflow: every candidate, flag checked
+    for (int64_t j = wid; j < kn; j += 16) {
+      const int64_t k = namb <= AMB_CAP ? (int64_t)s_amb[j] : j;
+      if (namb > AMB_CAP && a.flag[k] != 2) continue;
       const int64_t gk = g[k];
       const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
       int64_t r = ts_ > 0 ? max(prev_max, (int64_t)s_p[ts_ - 1]) : prev_max;

@@ -164,6 +164,10 @@ __global__ __launch_bounds__(1024) void wm_prep_kernel(WmArgs a) {
     if (tid == 0) {
       *(DevMeta*)a.out = *meta;
       *(int64_t*)(a.out + WM_HDR_N) = -1;
+      if (a.hout) {
+        *(DevMeta*)a.hout = *meta;
+        *(int64_t*)(a.hout + WM_HDR_N) = -1;
+      }
     }
     return;
   }
@@ -287,6 +291,10 @@ __global__ __launch_bounds__(1024) void wm_prep_kernel(WmArgs a) {
     meta->dirty_from = tail;
     *(DevMeta*)a.out = *meta;
     *(int64_t*)(a.out + WM_HDR_N) = (int64_t)emitted;
+    if (a.hout) {
+      *(DevMeta*)a.hout = *meta;
+      *(int64_t*)(a.hout + WM_HDR_N) = (int64_t)emitted;
+    }
   }
 }
 
@@ -322,6 +330,10 @@ __global__ __launch_bounds__(256) void wm_windows_kernel(WmArgs a) {
   const int64_t head = meta->whead, tail = meta->tail;
   const int64_t ws = ((const int64_t*)(a.out + L.start))[wi];
   const int64_t we = ((const int64_t*)(a.out + L.end))[wi];
+  if (a.hout && lane == 0) {  // the row straight into host-mapped memory
+    ((int64_t*)(a.hout + L.start))[wi] = ws;
+    ((int64_t*)(a.hout + L.end))[wi] = we;
+  }
   const int64_t sa = wave_lower_bound(a.s_tstart, head, tail, ws, lane);
   const int64_t sb = wave_lower_bound(a.s_tlast, head, tail, we, lane);
   const bool need_min = (a.need & NEED_MIN) != 0, need_max = (a.need & NEED_MAX) != 0;
@@ -379,11 +391,12 @@ __global__ __launch_bounds__(256) void wm_windows_kernel(WmArgs a) {
   if (need_max) mx = wmax64(mx);
   if (f64 && need_sum) sw = (uint64_t)__double_as_longlong(sf);
   const bool has = cnt != 0;
+  unsigned char* const o = a.hout ? a.hout : a.out;  // values and flags are read by the host only
   if (lane < a.n_aggs) {
     const int64_t v = has ? lower_value(a.agg_kind[lane], cnt, sw, mn, mx) : 0;
-    ((int64_t*)(a.out + L.vals))[(int64_t)lane * a.n_windows + wi] = v;
+    ((int64_t*)(o + L.vals))[(int64_t)lane * a.n_windows + wi] = v;
   }
-  if (lane == 0) a.out[L.has + wi] = has ? 1 : 0;
+  if (lane == 0) o[L.has + wi] = has ? 1 : 0;
 }
 
 // The packed result into host-mapped pinned memory: one small kernel (16-byte stores over PCIe) instead of a DMA
