@@ -298,8 +298,7 @@ def extra_c1(pkg, dev, batch, steps):
     rate = max(1, batch // 1000)
     jr = pkg.workloads.JavaRandomInts(43)
     op = pkg.SlicingWindowOperator(device=dev.index)
-    for agg in aggs or (pkg.AGG_SUM_I32,):  # aggs: A/B of the watermark's assembly (tools/c4_run.py minmax)
-        op.addWindowFunction(agg)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
     op.setMaxLateness(1)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
     wts = torch.arange(0, 60_000, dtype=torch.int64, device=dev)

@@ -967,10 +967,8 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
     a.ep_tail = xb_eptail;
     a.ep_cap = xb_evcap + 4;
     XCHK(hipMemsetAsync(xb_ctl, 0, xb_ctl_bytes(), stream));
-    if (resume) {
-      const int32_t one = 1;
-      XCHK(hipMemcpyAsync((unsigned char*)xb_ctl + 48, &one, 4, hipMemcpyHostToDevice, stream));  // XBCtl.resume
-    }
+    // XBCtl.resume: a device-side fill (a pageable 4-byte host copy went through a staging buffer every round)
+    if (resume) XCHK(hipMemsetD32Async((hipDeviceptr_t)((unsigned char*)xb_ctl + 48), 1, 1, stream));
     XCHK(xb_classify_phase(a, 0, stream));
     XCHK(xb_classify_phase(a, 1, stream));
     XCHK(xb_classify_phase(a, 2, stream));
@@ -989,8 +987,8 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
     }
     XCHK(xb_apply(a, stream));
     static_assert(sizeof(int64_t) * 9 >= 68, "XBCtl layout");
-    XCHK(launch_copy_to_host(xb_ctl, h_misc_dev, 72, stream));
-    if (cfg.n_ctx > 0) XCHK(launch_copy_to_host(xb_nstot, h_misc_dev + 9, 8 * cfg.n_ctx, stream));
+    XCHK(launch_copy2_to_host(xb_ctl, h_misc_dev, 72, xb_nstot, h_misc_dev + 9, cfg.n_ctx > 0 ? 8 * cfg.n_ctx : 0,
+                              stream));
     XCHK(hipStreamSynchronize(stream));
     const int64_t nev = h_misc[0];
     const int32_t retry = ((const int32_t*)(h_misc + 8))[0];

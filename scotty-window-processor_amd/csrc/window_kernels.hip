@@ -411,6 +411,21 @@ __global__ __launch_bounds__(64) void copy_words_kernel(const uint32_t* src, uin
 
 }  // namespace wk
 
+namespace wk {
+__global__ __launch_bounds__(64) void copy2_words_kernel(const uint32_t* s1, uint32_t* d1, int64_t n1, const uint32_t* s2,
+                                                         uint32_t* d2, int64_t n2) {
+  for (int64_t i = threadIdx.x; i < n1; i += 64) d1[i] = s1[i];
+  for (int64_t i = threadIdx.x; i < n2; i += 64) d2[i] = s2[i];
+}
+}  // namespace wk
+
+hipError_t launch_copy2_to_host(const void* d_src1, void* h_dst1_dev, size_t bytes1, const void* d_src2, void* h_dst2_dev,
+                                size_t bytes2, hipStream_t st) {
+  hipLaunchKernelGGL(wk::copy2_words_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)d_src1, (uint32_t*)h_dst1_dev,
+                     (int64_t)(bytes1 / 4), (const uint32_t*)d_src2, (uint32_t*)h_dst2_dev, (int64_t)(bytes2 / 4));
+  return hipGetLastError();
+}
+
 hipError_t launch_copy_to_host(const void* d_src, void* h_dst_dev, size_t bytes, hipStream_t st) {
   hipLaunchKernelGGL(wk::copy_words_kernel, dim3(1), dim3(64), 0, st, (const uint32_t*)d_src, (uint32_t*)h_dst_dev,
                      (int64_t)(bytes / 4));
