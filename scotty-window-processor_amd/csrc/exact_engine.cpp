@@ -1359,7 +1359,8 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.op_err = (int32_t*)(d_misc + 2);
   a.slot_key = keyed ? d_slot_key : nullptr;
   // lane path: COUNT / integer SUM windows straight from the slice prefixes in the emit kernel; MIN / MAX / f64
-  // sums scan the slices (wm_agg)
+  // sums scan the slices (wm_agg).  (MIN / MAX by a lane-per-key scan of each window's contained run inside the emit
+  // kernel measured 2.46 ms per C4 watermark against 1.18 ms this way: the lanes walk 64 different lines per load.)
   const bool prefix_agg = lane_mode() && !(cfg.need & (NEED_MIN | NEED_MAX)) &&
                           !((cfg.need & NEED_SUM) && vt == VT_F64);
   a.prefix_reset = prefix_stale ? 1 : 0;
