@@ -262,9 +262,12 @@ def test_device_timing_classes(pkg):
         op.processElements(ts[lo:lo + 50_000], vals[lo:lo + 50_000])
         op.processWatermark(int(ts[lo + 49_999]))
     t = op.deviceTiming()
-    assert t["ingest"][1] == 4 and t["watermark"][1] == 4 and t["result_copy"][1] == 4
+    assert t["ingest"][1] == 4 and t["watermark"][1] == 4
+    # the watermark writes its rows straight into host-mapped memory: a result-copy interval exists only where the
+    # library fell back to a DMA transfer (no device address for the pinned buffer)
+    assert t["result_copy"][1] in (0, 4), t
     assert t["push_other"][1] == 8
-    assert all(v[0] > 0 for v in t.values()), t
+    assert all(v[0] > 0 for v in t.values() if v[1] > 0), t
 
 
 def test_f64_sum_at_bench_scale(pkg):
