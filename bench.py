@@ -94,7 +94,8 @@ def _cpu_nonkeyed(setup, gen_step, wm_of, steps_range, budget_s, chunk, warm=Non
 
 
 def host_cores():
-    """Host threads this process may run on (sched_getaffinity) and the cgroup CPU quota, if one is set."""
+    """(effective cores, affinity threads, cgroup CPU quota or None).  Effective = min(the threads this process may
+    run on (sched_getaffinity), the cgroup's CPU quota): more threads than the quota only time-slice the same CPUs."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     quota = None
     try:
@@ -103,7 +104,8 @@ def host_cores():
             quota = float(q) / float(period)
     except (OSError, ValueError):
         pass
-    return n, quota
+    eff = n if quota is None else max(1, min(n, int(quota)))
+    return eff, n, quota
 
 
 C1_PUBLISHED = 1.56e6  # README.md:50-54, benchmark/configurations/sliding_benchmark_Scotty.json:22 (Flink + Scotty)
@@ -278,13 +280,13 @@ def cpu_c4(keys, batch, threads):
         steps += 1
         if t_proc > CPU_BUDGET_S:
             break
-    _, quota = host_cores()
+    eff, affinity, quota = host_cores()
     return {"value": done / t_proc, "unit": "tuples/s", "cores": threads, "kind": "port",
-            "cgroup_cpu_quota": quota,
+            "affinity_threads": affinity, "cgroup_cpu_quota": quota,
             "sample": "%d steps of %d tuples (%d uniform keys, 1 s of event time each, one watermark per step) after a "
-                      "60 s sparse warm-up; oracle/ KeyedScottyWindowOperator restatement, %d threads = every host "
-                      "thread this process may run on (sched_getaffinity; key %% %d partitions)"
-                      % (steps, batch, keys, threads, threads)}
+                      "60 s sparse warm-up; oracle/ KeyedScottyWindowOperator restatement on %d threads = the effective "
+                      "host cores of this process, min(sched_getaffinity %d, cgroup quota %s); key %% %d partitions"
+                      % (steps, batch, keys, threads, affinity, quota, threads)}
 
 
 # ----------------------------------------------------------------------------------------------- GPU legs
@@ -909,8 +911,8 @@ def main():
             # CPU baselines on this box's host cores, rank 0, N=1 only (bounded samples of the same streams)
             res["cpu_baseline"] = cpu_c2(sizes, rate)
             log("bench: CPU C2 done")
-            threads, quota = host_cores()  # T = the host threads this process may use
-            log("bench: host cores: %d usable threads, cgroup quota %s" % (threads, quota))
+            threads, affinity, quota = host_cores()  # T = the host cores this process may use
+            log("bench: host cores: %d effective (%d affinity threads, cgroup quota %s)" % (threads, affinity, quota))
             cb = {"c1": lambda: cpu_c1((1 << 26) // 1000),
                   "c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
                   "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000),

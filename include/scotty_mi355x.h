@@ -180,7 +180,10 @@ int scotty_route_keyed(const uint32_t* key, const int64_t* ts, const void* val, 
  * op_waits == 0: `stream` waits for the work queued on the op's stream so far (the exchange record of a shard push
  * is complete before the all-gather reads it); op_waits != 0: the op's stream waits for the work queued on `stream`
  * (the gathered records have landed before scotty_shard_commit reads them).  With scotty_tune("shard_async", 1) the
- * shard pushes then return without a host synchronisation.  `stream` is a hipStream_t (NULL: the default stream). */
+ * shard pushes then return without a host synchronisation.  `stream` is a hipStream_t (NULL: the default stream) of
+ * the HIP runtime this library links: a caller with its own copy of the runtime (PyTorch wheels ship one) cannot
+ * share streams or events with it, and host-synchronises both sides instead (the Python ShardedSlicingWindowOperator
+ * does; shard_async stays off there). */
 int scotty_stream_order(scotty_op* op, void* stream, int op_waits);
 
 /* Number of keys (operators) of a keyed op. */
@@ -217,7 +220,9 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
  * promise they run on the exact engine, which keeps the record sets), "ingest_blocks", "shard_cells" / "shard_cands" (cells /
  * edge candidates per rank record of the time-window exchange), "shard_count_cells" (count cells per rank record
  * of the count-window exchange), "shard_async" 1 (shard pushes return without a host synchronisation: the caller
- * orders its collective's stream with scotty_stream_order). */
+ * orders its collective's stream with scotty_stream_order -- same HIP runtime only, see there), "exact_prefix" n
+ * (exact engine, non-keyed: the first event-exact piece of a batch the one-pass quiet path refused, in tuples;
+ * 0 = max(batch / 32, 2^20); later pieces grow 4x; the split is invisible in the results). */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */

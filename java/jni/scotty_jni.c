@@ -1,9 +1,10 @@
-/* scotty_jni.c -- JNI fallback of the Java shim (java/de/tub/dima/scotty/slicing/JniApi.java) for JDKs without the
- * Foreign Function and Memory API.  Each native method forwards to one entry point of include/scotty_mi355x.h.
+/* scotty_jni.c -- JNI binding of the Java shim (java/main/de/tub/dima/scotty/slicing/JniApi.java), the default on
+ * every JDK from 8 on.  Each native method forwards to one entry point of include/scotty_mi355x.h.
  * Tuple buffers arrive as direct ByteBuffers (GetDirectBufferAddress: the library reads the off-heap memory the
  * shim filled, no copy); a watermark's SoA result columns are copied into fresh Java arrays.
  *
- * Build (JDK 8+; no JDK exists in this repository's build container, so this file is reviewed, not compiled here):
+ * Build (JDK 8+; no JDK exists in this repository's build container: tests/test_java_shim_cpu.py compiles this file
+ * with -fsyntax-only against a type-check stub of jni.h, tests/jni_stub/jni.h, and links nothing):
  *   gcc -O2 -shared -fPIC -I"$JAVA_HOME/include" -I"$JAVA_HOME/include/linux" -Iinclude \
  *       java/jni/scotty_jni.c -Lscotty-window-processor_amd -lscotty_mi355x -Wl,-rpath,'$ORIGIN' \
  *       -o libscotty_jni.so

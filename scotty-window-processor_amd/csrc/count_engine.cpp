@@ -40,7 +40,7 @@ int64_t jsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b)
 int64_t jmod(int64_t a, int64_t b) { return b == -1 ? 0 : a % b; }
 template <typename T>
 hipError_t dalloc(T** p, int64_t n) {
-  return hipMalloc((void**)p, (size_t)std::max<int64_t>(n, 1) * sizeof(T));
+  return dev_malloc((void**)p, (size_t)std::max<int64_t>(n, 1) * sizeof(T));  // poisoned under SCOTTY_ALLOC_POISON
 }
 void dfree(void* p) {
   if (p) (void)hipFree(p);
@@ -101,10 +101,10 @@ int CEngine::init(int dev, hipStream_t st, int vt_, std::string& e) {
   device = dev;
   stream = st;
   vt = vt_;
-  if (hipMalloc((void**)&d_meta, sizeof(CMeta)) != hipSuccess ||
+  if (dev_malloc((void**)&d_meta, sizeof(CMeta)) != hipSuccess ||
       mapped_host_alloc((void**)&h_meta, (void**)&h_meta_dev, sizeof(CMeta)) != hipSuccess ||
       hipHostMalloc((void**)&h_tmp, 8 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess ||
-      hipMalloc((void**)&d_nte, sizeof(unsigned long long)) != hipSuccess) {
+      dev_malloc((void**)&d_nte, sizeof(unsigned long long)) != hipSuccess) {
     e = "count engine: out of memory";
     return SCOTTY_ERR_NOMEM;
   }
@@ -650,7 +650,7 @@ bool CEngine::trigger_segs(int64_t last_c, int64_t cur_c, int64_t last_t, int64_
     d_segbuf = nullptr;
     segcap = 2 * nseg + 64;
     if (hipHostMalloc((void**)&h_segs, segcap * sizeof(CRowSeg), hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&d_segbuf, segcap * sizeof(CRowSeg)) != hipSuccess) {
+        dev_malloc(&d_segbuf, segcap * sizeof(CRowSeg)) != hipSuccess) {
       segcap = 0;
       return false;
     }

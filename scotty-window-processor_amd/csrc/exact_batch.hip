@@ -1071,6 +1071,9 @@ __global__ __launch_bounds__(256) void xb_apply_kernel(XBArgs a) {
   const XState& st = *a.st;
   const int head = st.head;
   const int64_t nep = ctl.ep_count;
+  // the event pass writes at least the segment's opening epoch entry; it writes none when it returned at once (an
+  // operator already failed): nothing to apply, and ep_tail holds nothing of this round
+  if (nep <= 0) return;
   const int wtop = a.ep_tail[nep - 1];
   const int wbase = max(head, wtop - XW);
   const int64_t* sk = (st.unsorted & 1) ? a.sufmin : a.sl.ts;

@@ -4,6 +4,7 @@
 // reference's WindowManager registration (S/WindowManager.java:121-151).
 #include "exact_batch.h"
 #include "exact_engine.h"
+#include "dev_alloc.h"
 #include "exact_quiet.h"
 #include "host_copy.h"
 #include "keyed_grid.h"
@@ -74,18 +75,17 @@ namespace scotty {
   } while (0)
 
 namespace {
-// device allocation, zero-filled: no kernel may read a previous owner's bytes from reused memory
-// (the fill runs on the null stream and the host waits for it, so it is complete before the operator's non-blocking
-// stream can touch the buffer)
+// device allocation.  Every buffer is written by the engine before any kernel reads it (state explicitly
+// initialised, scratch written by the producing kernel of the same launch chain); the zero fill is defence in
+// depth only.  SCOTTY_ALLOC_POISON (dev_alloc.h) replaces it by a poison byte to check exactly that.
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
   *p = nullptr;
   if (count == 0) count = 1;
   hipError_t e = hipMalloc((void**)p, count * sizeof(T));
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(*p, 0, count * sizeof(T), nullptr);
-  if (e != hipSuccess) return e;
-  return hipStreamSynchronize(nullptr);
+  const int pb = alloc_poison();
+  return dev_fill_sync(*p, pb >= 0 ? pb : 0, count * sizeof(T));
 }
 void dfree(void* p) {
   if (p) (void)hipFree(p);
@@ -129,6 +129,8 @@ void XEngine::release() {
   dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_pmax); dfree(d_xq_rank); dfree(d_xq_flag);
   for (int k = 0; k < NPART; k++) dfree(d_xq_cpart[k]);
   dfree(d_xq_eg); dfree(d_xq_epos); dfree(d_xq_meta); dfree(d_xq_cix); dfree(d_xq_cixmeta); dfree(d_xq_ctl);
+  dfree(d_dbg);
+  d_dbg = nullptr;
   for (auto& e : ev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   ev_pending.clear();
@@ -549,30 +551,49 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
   // tuples) costs one short event-exact prefix, not rounds over the whole batch.  The prefix grows 4x with every
   // further refusal, so a batch that is not quiet anywhere reaches the event-exact path for all of it quickly.
   int64_t pos0 = 0;
-  static const int64_t chunk_min = [] {  // A/B of the first event-exact prefix (SCOTTY_XQ_CHUNK tuples)
-    const char* e = getenv("SCOTTY_XQ_CHUNK");
-    return e ? std::max<int64_t>(4096, atoll(e)) : (int64_t)1 << 20;
-  }();
-  int64_t chunk = std::max<int64_t>(n / 32, chunk_min);
-  if (getenv("SCOTTY_XQ_CHUNK")) chunk = chunk_min;
+  xq_trace.clear();
+  int64_t chunk = xq_prefix > 0 ? xq_prefix : std::max<int64_t>(n / 32, (int64_t)1 << 20);
   chunk = (chunk + 4095) & ~(int64_t)4095;  // pieces start 16-byte aligned (the ingest's vector loads)
   // event-exact piece behind a located jump: the stream resuming after a silence opens a session whose start settles
   // within the first tuples (out-of-order tuples reach at most maxDelay below it), then the batch is quiet again
   int64_t chunk_jump = (int64_t)1 << 18;
+  bool try_quiet = quiet_eligible();
+  if (try_quiet && xq_skip > 0) {  // backed off after consecutive refusals the batch itself caused (see below)
+    xq_skip--;
+    quiet_skipped++;
+    try_quiet = false;
+  }
   while (pos0 < n) {
     const int64_t rest = n - pos0;
     const unsigned char* val0 = (const unsigned char*)d_val + pos0 * vb;
-    if (quiet_eligible()) {
+    if (try_quiet) {
       int32_t res = XQ_NONE;
       int rc = push_quiet(d_ts + pos0, val0, rest, &res);
       if (rc) return rc;
+      xq_trace.push_back((int64_t)res | (last_quiet_why & 0xFFFF) << 8 | pos0 << 24);
       if (pos0 == 0) last_quiet = res;  // the batch's own verdict (a committed remainder is counted below)
       else if (res == XQ_COMMITTED) quiet_tail_commits++;
       if (res == XQ_COMMITTED) {
         quiet_commits++;
+        xq_refused_run = 0;
         return SCOTTY_OK;
       }
       quiet_fallbacks++;
+      if (res == XQ_NOT_QUIET && (last_quiet_why & 3) != 0) {
+        // tuples below the cell view or the last session's start (why 1 / 2).  Within a batch such a refusal is often
+        // transient -- a resumed stream's new session settles within its first tuples (C3's pause step), and until
+        // it has, the view of an unsorted slice list starts above the tuples still to come -- so the event-exact
+        // prefix keeps growing 4x and the quiet path is tried on what follows (at most ~log4(n / prefix) attempts;
+        // stopping at the first why-1 refusal sent 2^26 - 4096 tuples of C3's pause step through event-exact rounds,
+        // profiles/r04/r04b_c3_quiet_attempts.txt).  Batches whose own verdict fails that way back the quiet path off
+        // across batches (after two in a row: the next 1, 2, 4 .. 16 batches go straight to the event-exact path).
+        if (pos0 == 0) {
+          xq_refused_run++;
+          if (xq_refused_run >= 2) xq_skip = std::min(1 << std::min(xq_refused_run - 2, 4), 16);
+        }
+      } else if (pos0 == 0) {
+        xq_refused_run = 0;
+      }
       // the verdict failed only on session-gap jumps and located the first one: everything before its arrival tile
       // is quiet (the verdict's other conditions held for the whole rest) -- commit that prefix in one pass, then the
       // event-exact path from the jump on
@@ -595,7 +616,7 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
         quiet_fallbacks++;
       }
     }
-    const int64_t w = quiet_eligible() && chunk < rest ? chunk : rest;
+    const int64_t w = try_quiet && chunk < rest ? chunk : rest;
     int rc = push_exact(d_ts + pos0, val0, w);
     if (rc) return rc;
     pos0 += w;
@@ -796,6 +817,8 @@ int XEngine::xq_ensure(int64_t n) {
 // synchronisation reads the verdict.  Nothing of the operator changes unless *result == XQ_COMMITTED.
 int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32_t* result) {
   *result = XQ_NONE;
+  last_quiet_why = 0;
+  last_quiet_jump = 0;
   if (xq_need_grid) {
     int rc = xq_rebuild_grid();
     if (rc) return rc;
@@ -850,10 +873,9 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   q.epos = d_xq_epos;
   q.ctl = (XQCtl*)d_xq_ctl;
   q.margin = std::max<int64_t>(16 * xq_span, 60000);
-  static long long* d_xq_dbg = nullptr;
   const bool prof = getenv("SCOTTY_XQ_PROF") != nullptr;
-  if (prof && !d_xq_dbg) XCHK(hipMalloc(&d_xq_dbg, 16 * 8));
-  q.dbg = prof ? d_xq_dbg : nullptr;
+  if (prof && !d_dbg) XCHK(dalloc(&d_dbg, 256));
+  q.dbg = prof ? d_dbg : nullptr;
   TEv t0, t1, t2;
   if ((rc = tbegin(t0, SCOTTY_TIME_PUSH_OTHER))) return rc;
   XCHK(launch_xq_prep(q, stream));
@@ -870,7 +892,7 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   XCHK(hipStreamSynchronize(stream));
   if (prof) {  // debugging aid: s_memtime deltas between the commit's phases
     long long h[16];
-    XCHK(hipMemcpy(h, d_xq_dbg, sizeof(h), hipMemcpyDeviceToHost));
+    XCHK(hipMemcpy(h, d_dbg, sizeof(h), hipMemcpyDeviceToHost));
     fprintf(stderr, "xq commit phase ticks:");
     for (int i = 1; i <= 3; i++) fprintf(stderr, " %lld", h[i] - h[i - 1]);
     fprintf(stderr, "\n");
@@ -972,9 +994,8 @@ int XEngine::push_round(const int64_t* d_ts, const void* d_val, int64_t n, bool 
     XCHK(xb_classify_phase(a, 0, stream));
     XCHK(xb_classify_phase(a, 1, stream));
     XCHK(xb_classify_phase(a, 2, stream));
-    static long long* d_dbg = nullptr;
     const bool prof = getenv("SCOTTY_XB_PROF") != nullptr;
-    if (prof && !d_dbg) XCHK(hipMalloc(&d_dbg, 256 * 8));
+    if (prof && !d_dbg) XCHK(dalloc(&d_dbg, 256));
     a.dbg = prof ? d_dbg : nullptr;
     XCHK(xb_events(a, stream));
     if (prof) {  // debugging aid: clock stamps of the event pass (100 MHz-ish s_memtime ticks, see MI355X guide)

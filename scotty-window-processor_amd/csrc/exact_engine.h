@@ -53,6 +53,15 @@ class XEngine {
   int64_t last_quiet_why = 0;  // XQCtl.why of the last verdict
   int64_t last_quiet_jump = 0;   // first tuple of the arrival tile holding the verdict's first session-gap jump (0: none)
   int64_t quiet_split_commits = 0;  // quiet prefixes committed up to a located jump
+  // first event-exact piece of a refused quiet batch, in tuples (scotty_tune "exact_prefix"; 0: max(n / 32, 2^20))
+  int64_t xq_prefix = 0;
+  // batches whose own quiet verdict fails on their tuples (below the cell view / too late / past the grid horizon:
+  // XQCtl.why bit 1; below the last session's start: bit 2) back the quiet path off: after two such batches in a row,
+  // the next 1, 2, 4 .. 16 batches go straight to the event-exact path
+  int32_t xq_refused_run = 0, xq_skip = 0;
+  int64_t quiet_skipped = 0;        // batches that went to the event-exact path under that back-off
+  // verdicts of the last batch's quiet attempts, in order: XQ_* | why << 8 | (attempt's first tuple) << 24 (debugging)
+  std::vector<int64_t> xq_trace;
   // device time of the last pushes by class (HIP events; scotty_device_timing): 0 quiet ingest, 1 other push work
   bool timing = false;
   struct TEv {
@@ -218,6 +227,7 @@ class XEngine {
   uint32_t* d_xq_cix = nullptr;
   int64_t* d_xq_cixmeta = nullptr;
   void* d_xq_ctl = nullptr;
+  long long* d_dbg = nullptr;   // debugging aid (SCOTTY_XQ_PROF / SCOTTY_XB_PROF): clock stamps, this engine's device
   int64_t xq_span = 1000;       // event-time span of the last committed batch (grid horizon and cell-index sizing)
   bool xq_need_grid = true;     // (re)build the grid from the pending edge at the next push
 };

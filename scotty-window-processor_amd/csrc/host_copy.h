@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include "dev_alloc.h"  // mapped_host_alloc
+
 namespace scotty {
 
 // copy `bytes` (a multiple of 4) from device memory to the device address of a host-mapped buffer
@@ -15,12 +17,5 @@ hipError_t launch_copy_to_host(const void* d_src, void* h_dst_dev, size_t bytes,
 // two ranges in one launch (bytes2 may be 0)
 hipError_t launch_copy2_to_host(const void* d_src1, void* h_dst1_dev, size_t bytes1, const void* d_src2, void* h_dst2_dev,
                                 size_t bytes2, hipStream_t st);
-
-// pinned, host-mapped allocation: *h host address, *d its device address
-inline hipError_t mapped_host_alloc(void** h, void** d, size_t bytes) {
-  hipError_t e = hipHostMalloc(h, bytes, hipHostMallocMapped);
-  if (e != hipSuccess) return e;
-  return hipHostGetDevicePointer(d, *h, 0);
-}
 
 }  // namespace scotty

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <queue>
@@ -16,6 +18,7 @@
 #include <vector>
 
 #include "../../include/scotty_mi355x.h"
+#include "dev_alloc.h"
 #include "device_common.h"
 #include "count_engine.h"
 #include "exact_engine.h"
@@ -32,6 +35,15 @@ hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long 
 hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st);
 hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st);
 hipError_t launch_shard_commit(const ShardArgs& a, hipStream_t st);
+}  // namespace scotty
+
+// Allocation poison (dev_alloc.h): -1 off, else the byte every new engine allocation is filled with.
+namespace scotty {
+static std::atomic<int> g_alloc_poison{[] {
+  const char* e = getenv("SCOTTY_ALLOC_POISON");
+  return (e && *e) ? (int)(strtol(e, nullptr, 0) & 0xFF) : -1;
+}()};
+int alloc_poison() { return g_alloc_poison.load(std::memory_order_relaxed); }
 }  // namespace scotty
 
 using namespace scotty;
@@ -158,6 +170,7 @@ struct scotty_op {
   bool x_lane_off = false;
   bool x_kg_off = false;
   int64_t x_kg_chunk = -1;
+  int64_t x_prefix = 0;      // exact engine: first event-exact prefix of a refused quiet batch (0: default)
   int32_t x_kg_variant = -1;
   int64_t shard_count_total = 0;
   int64_t count_shard_cap = 1 << 16;
@@ -340,20 +353,20 @@ int alloc_all(scotty_op* op) {
   HIPCHK(hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking));
   op->ingest = new HostIngest();
   if (op->ingest->init(op->device, op->stream)) return fail(op, SCOTTY_ERR_HIP, "host ingest: stream / event creation");
-  HIPCHK(hipMalloc(&op->d_meta, sizeof(DevMeta)));
+  HIPCHK(dev_malloc(&op->d_meta, sizeof(DevMeta)));
   HIPCHK(hipHostMalloc(&op->h_snap, sizeof(DevMeta), hipHostMallocDefault));
   HIPCHK(hipMemset(op->d_meta, 0, sizeof(DevMeta)));
-  HIPCHK(hipMalloc(&op->d_tstart, op->scap * 8));
-  HIPCHK(hipMalloc(&op->d_tlast, op->scap * 8));
-  HIPCHK(hipMalloc(&op->d_scnt, op->scap * 8));
-  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_spart[k], op->scap * 8));
-  HIPCHK(hipMalloc(&op->d_grid, op->gcap * 8));
-  HIPCHK(hipMalloc(&op->d_ccnt, op->ccap * 8));
-  HIPCHK(hipMalloc(&op->d_ctmax, op->ccap * 8));
-  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_cpart[k], op->ccap * 8));
-  HIPCHK(hipMalloc(&op->d_rank, op->gcap * 4));
-  HIPCHK(hipMalloc(&op->d_flag, op->gcap * 4));
-  HIPCHK(hipMalloc(&op->d_scratch, 64));
+  HIPCHK(dev_malloc(&op->d_tstart, op->scap * 8));
+  HIPCHK(dev_malloc(&op->d_tlast, op->scap * 8));
+  HIPCHK(dev_malloc(&op->d_scnt, op->scap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(dev_malloc(&op->d_spart[k], op->scap * 8));
+  HIPCHK(dev_malloc(&op->d_grid, op->gcap * 8));
+  HIPCHK(dev_malloc(&op->d_ccnt, op->ccap * 8));
+  HIPCHK(dev_malloc(&op->d_ctmax, op->ccap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(dev_malloc(&op->d_cpart[k], op->ccap * 8));
+  HIPCHK(dev_malloc(&op->d_rank, op->gcap * 4));
+  HIPCHK(dev_malloc(&op->d_flag, op->gcap * 4));
+  HIPCHK(dev_malloc(&op->d_scratch, 64));
   HIPCHK(launch_fill_u64(op->d_ccnt, op->ccap, 0, op->stream));
   HIPCHK(launch_fill_u64((unsigned long long*)op->d_ctmax, op->ccap, (unsigned long long)INT64_MIN, op->stream));
   HIPCHK(launch_fill_u64(op->d_cpart[0], op->ccap, 0, op->stream));
@@ -370,8 +383,8 @@ int ensure_tiles(scotty_op* op, int64_t n) {
   if (op->d_tilemax) HIPCHK(hipFree(op->d_tilemax));
   if (op->d_pmax) HIPCHK(hipFree(op->d_pmax));
   op->tcap = std::max(nt, (int64_t)1024);
-  HIPCHK(hipMalloc(&op->d_tilemax, op->tcap * 8));
-  HIPCHK(hipMalloc(&op->d_pmax, op->tcap * 8));
+  HIPCHK(dev_malloc(&op->d_tilemax, op->tcap * 8));
+  HIPCHK(dev_malloc(&op->d_pmax, op->tcap * 8));
   return SCOTTY_OK;
 }
 
@@ -379,12 +392,12 @@ int ensure_tiles(scotty_op* op, int64_t n) {
 int alloc_blocks(scotty_op* op) {
   if (op->d_bcnt) return SCOTTY_OK;
   op->nbcap = op->scap / SBLK + 1;
-  HIPCHK(hipMalloc(&op->d_bcnt, op->nbcap * 8));
-  for (int k = 0; k < NPART; k++) HIPCHK(hipMalloc(&op->d_bpart[k], op->nbcap * 8));
-  HIPCHK(hipMalloc(&op->d_pcnt, op->nbcap * 8));
-  HIPCHK(hipMalloc(&op->d_psum, op->nbcap * 8));
-  HIPCHK(hipMalloc(&op->d_stmin, (size_t)ST_LEVELS * op->nbcap * 8));
-  HIPCHK(hipMalloc(&op->d_stmax, (size_t)ST_LEVELS * op->nbcap * 8));
+  HIPCHK(dev_malloc(&op->d_bcnt, op->nbcap * 8));
+  for (int k = 0; k < NPART; k++) HIPCHK(dev_malloc(&op->d_bpart[k], op->nbcap * 8));
+  HIPCHK(dev_malloc(&op->d_pcnt, op->nbcap * 8));
+  HIPCHK(dev_malloc(&op->d_psum, op->nbcap * 8));
+  HIPCHK(dev_malloc(&op->d_stmin, (size_t)ST_LEVELS * op->nbcap * 8));
+  HIPCHK(dev_malloc(&op->d_stmax, (size_t)ST_LEVELS * op->nbcap * 8));
   return SCOTTY_OK;
 }
 
@@ -398,7 +411,7 @@ int ensure_wm_out(scotty_op* op, int64_t bytes) {
   op->h_out = nullptr;
   op->out_cap = std::max<int64_t>(bytes + bytes / 2, 1 << 16);
   op->out_cap = (op->out_cap + 15) & ~(int64_t)15;
-  HIPCHK(hipMalloc(&op->d_out, op->out_cap));
+  HIPCHK(dev_malloc(&op->d_out, op->out_cap));
   HIPCHK(hipHostMalloc(&op->h_out, op->out_cap, hipHostMallocMapped));
   op->h_out_dev = nullptr;
   if (hipHostGetDevicePointer(&op->h_out_dev, op->h_out, 0) != hipSuccess) op->h_out_dev = nullptr;
@@ -413,7 +426,7 @@ int upload_wdefs(scotty_op* op) {
     HIPCHK(hipStreamSynchronize(op->stream));
     if (op->d_wdef) HIPCHK(hipFree(op->d_wdef));
     op->wdef_cap = std::max<int64_t>(n, 64);
-    HIPCHK(hipMalloc(&op->d_wdef, op->wdef_cap * 3 * 8));
+    HIPCHK(dev_malloc(&op->d_wdef, op->wdef_cap * 3 * 8));
   }
   std::vector<int64_t> v;
   for (const CFWin& w : op->windows) {
@@ -460,7 +473,7 @@ int compact_if_needed(scotty_op* op) {
   op->cix_ready = false;  // slices move
   const int64_t live = m.tail - m.head;
   int64_t* tmp = nullptr;
-  HIPCHK(hipMalloc(&tmp, std::max<int64_t>(live, 1) * 8));
+  HIPCHK(dev_malloc(&tmp, std::max<int64_t>(live, 1) * 8));
   int64_t* arrs[3 + NPART] = {op->d_tstart, op->d_tlast, (int64_t*)op->d_scnt, (int64_t*)op->d_spart[0],
                              (int64_t*)op->d_spart[1], (int64_t*)op->d_spart[2]};
   for (int64_t* a : arrs) {
@@ -489,8 +502,8 @@ int sync_snapshot(scotty_op* op) {
 // so the grid watermark enqueues it behind the result transfer for the next micro-batch.
 int enqueue_cix(scotty_op* op) {
   if (!op->d_cix) {
-    HIPCHK(hipMalloc(&op->d_cix, CIX_CAP * 4));
-    HIPCHK(hipMalloc(&op->d_cixmeta, 8 * 8));
+    HIPCHK(dev_malloc(&op->d_cix, CIX_CAP * 4));
+    HIPCHK(dev_malloc(&op->d_cixmeta, 8 * 8));
   }
   IngestArgs ia{};
   ia.s_tstart = op->d_tstart;
@@ -522,8 +535,8 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   ia.tilemax = op->d_tilemax;
   ia.meta = op->d_meta;
   if (!op->d_cix) {
-    HIPCHK(hipMalloc(&op->d_cix, CIX_CAP * 4));
-    HIPCHK(hipMalloc(&op->d_cixmeta, 8 * 8));
+    HIPCHK(dev_malloc(&op->d_cix, CIX_CAP * 4));
+    HIPCHK(dev_malloc(&op->d_cixmeta, 8 * 8));
   }
   ia.cix = op->d_cix;
   ia.cix_meta = op->d_cixmeta;
@@ -922,6 +935,8 @@ static int decide_mode(scotty_op* op) {
   op->x->kg_off = op->x_kg_off;
   if (op->x_kg_chunk >= 0) op->x->kg_min_chunk = op->x_kg_chunk;
   if (op->x_kg_variant >= 0) op->x->kg_variant = op->x_kg_variant;
+  op->x->xq_prefix = op->x_prefix;
+  op->x->timing = op->timing;  // scotty_enable_timing before the first push (the natural order) reaches the engine
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
   if (!rc) rc = op->x->configure(op->xwins, op->aggs, op->max_lateness, op->agg_inv);
@@ -1147,8 +1162,8 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
     return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs context-free time windows or count windows only");
   if (!op->has_fixed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs at least one context-free window");
   if (!op->d_shrank) {
-    HIPCHK(hipMalloc(&op->d_shrank, op->shard_kg * 4));
-    HIPCHK(hipMalloc(&op->d_shflag, op->shard_kg * 4));
+    HIPCHK(dev_malloc(&op->d_shrank, op->shard_kg * 4));
+    HIPCHK(dev_malloc(&op->d_shflag, op->shard_kg * 4));
   }
   if (!op->started) {
     rc = start_stream(op, ts0);
@@ -1467,6 +1482,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->x) op->x->quiet_off = op->x_quiet_off;
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "exact_prefix") == 0) {  // first event-exact piece of a refused quiet batch (tuples, >= 4096)
+    if (value != 0 && (value < 4096 || value > ((int64_t)1 << 40))) return SCOTTY_ERR_ARG;
+    op->x_prefix = value;
+    if (op->x) op->x->xq_prefix = value;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "shard_count_cells") == 0) {  // cells per rank record of the count path's exchange
     if (op->mode != 0 || value < 16 || value > (1 << 24)) return SCOTTY_ERR_ARG;
     op->count_shard_cap = value;
@@ -1516,6 +1537,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   return SCOTTY_ERR_ARG;
 }
 
+// Internal (not in the header): allocations made from now on are filled with `byte` (0..255), or left as allocated
+// (exact engine: zero-filled) for byte < 0.  Returns the previous setting.  Tests of never-written reads only.
+int scotty_debug_alloc_poison(int byte) {
+  return scotty::g_alloc_poison.exchange(byte < 0 ? -1 : (byte & 0xFF));
+}
+
 // Internal (not in the header): grid-path statistics (0: tuples added with global atomics since creation).
 int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
   if (!op || op->mode != 1 || !op->d_meta) return -1;
@@ -1554,7 +1581,11 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 11: return op->x->last_quiet_why;
     case 12: return op->x->quiet_tail_commits;  // batches whose remainder committed after an event-exact prefix
     case 13: return op->x->quiet_split_commits;  // quiet prefixes committed up to a located session-gap jump
-    default: return -1;
+    case 14: return op->x->quiet_skipped;        // batches sent to the event-exact path by the quiet back-off
+    case 15: return (int64_t)op->x->xq_trace.size();  // quiet attempts of the last batch; 16 + k: attempt k's trace
+    default:
+      if (which >= 16 && which - 16 < (int)op->x->xq_trace.size()) return op->x->xq_trace[which - 16];
+      return -1;
   }
 }
 

@@ -137,7 +137,16 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
   const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
   const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
   const int64_t ctot = cv.c_old + kc;
-  if (ctot <= 0) return;
+  if (ctot <= 0) {  // no cells: an empty index (every lookup past span_end takes the bisection), never a stale one
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      a.cix_meta[0] = 0;
+      a.cix_meta[1] = 0;
+      a.cix_meta[2] = 0;
+      a.cix_meta[3] = 0;
+      a.cix_meta[4] = INT64_MIN;
+    }
+    return;
+  }
   const int64_t first = cv.start(0);
   const int64_t full_end = h_end != INT64_MAX ? h_end : cv.start(ctot - 1) + 1;
   // the index stops `margin` ms past the stream front (prev_max): the cells of a far horizon cost a pass each
@@ -373,6 +382,12 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     if (tid == 0) sc[15] = x;
   }
   __syncthreads();
+  // An overflowed / refused interval: the cell-index build wrote no index this push (cix_build_kernel returns at
+  // once), so nothing below may look at cix_meta -- a previous push's index (or never-written memory) would send
+  // the window search to an arbitrary cix entry.  Decide the early return before any index read.
+  if (tid == 0) sc[0] = a.meta->overflow;
+  __syncthreads();
+  if (sc[0] != 0) return;  // an earlier push of this interval overflowed: nothing is committed until replay
   if (tid == 0) {
     const DevMeta& m = *a.meta;
     int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
@@ -401,7 +416,6 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       }
       wn = l_;
     }
-    sc[0] = m.overflow;
     sc[1] = head; sc[2] = tail; sc[3] = j0; sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
     sc[7] = wbase; sc[8] = wn;
     const int64_t twa = cv.start(wbase), twb = cv.start(wbase + wn);
@@ -421,7 +435,6 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     sc[18] = (DEFER && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
   }
   __syncthreads();
-  if (sc[0] != 0) return;  // an earlier push of this interval overflowed: nothing is committed until replay
   // block-uniform scalars: readfirstlane keeps them in SGPRs (an LDS load alone yields VGPRs)
   const int64_t head = uni64(sc[1]), tail = uni64(sc[2]), j0 = uni64(sc[3]), kc = uni64(sc[4]);
   const int64_t h_end = uni64(sc[5]), first_start = uni64(sc[6]);

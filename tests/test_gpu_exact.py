@@ -245,11 +245,14 @@ def test_quiet_path_equals_event_exact_path_and_replay(pkg, seed):
 
 def test_config3_full_size_quiet_path_equals_replay(pkg):
     """BASELINE configs[2] (C3) at the benchmark's batch size class: SlidingWindow(60 s, 60 ms) + SessionWindow(1 s),
-    MIN/MAX, 20 % out-of-order by U[1,500] ms, 2^24 tuples per step, a 2 s pause before step 3 (the session closes:
-    the silence left by tuples up to 500 ms late exceeds the gap), generated on the device like bench.py's C3 leg.
-    Quiet path (default) == event-exact batch path == single-wavefront replay (~23 s per step), window by window,
-    every step; the pause step goes through the event-exact path, the steps after the first commit in one pass."""
+    MIN/MAX, 20 % out-of-order by U[1,500] ms, 2^24 tuples per full step, a 2 s pause every 10 s of event time (the
+    session closes: the silence left by tuples up to 500 ms late exceeds the gap), generated on the device like
+    bench.py's C3 leg.  68 s of sparse warm-up (1 tuple per ms) first, so the full steps 68-70 emit the 60 s sliding
+    windows (ws + size <= wm + 1, C/windowType/SlidingWindow.java:50-57) besides the sessions; step 70 resumes after a
+    pause.  Quiet path (default) == event-exact batch path == single-wavefront replay (~23 s per full step), window by
+    window, every step, and all three == the oracle."""
     import torch
+    from oracle.oracle import OracleOperator
     dev = torch.device("cuda", 0)
     batch = 1 << 24
     rate = batch // 1000
@@ -259,42 +262,55 @@ def test_config3_full_size_quiet_path_equals_replay(pkg):
     for knob, val in (("exact_quiet", 1), ("exact_quiet", 0), ("exact_serial", 1)):
         op = pkg.SlicingWindowOperator(device=0)
         op.tune(knob, val)
+        ops.append(op)
+    ora = OracleOperator()
+    for op in ops + [ora]:
         op.addWindowFunction(MIN)
         op.addWindowFunction(MAX)
         op.addWindowFunction(COUNT)
         op.setMaxLateness(1000)
         op.addWindowAssigner(Sliding(Time, 60_000, 60))
         op.addWindowAssigner(Session(Time, 1000))
-        ops.append(op)
     from helpers import same_windows
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
-    quiet, event, rows = 0, 0, 0
+    quiet, event, rows, sliding = 0, 0, 0, 0
     import time
-    for s in range(4):
-        t_begin = s * 1000 + 1000 + (s // 3) * 2000
-        ts = base + t_begin
-        late = torch.rand(batch, device=dev, generator=g) < 0.2
-        d = torch.randint(1, 501, (batch,), device=dev, generator=g)
-        ts = torch.where(late, torch.clamp(ts - d, min=t_begin - 500), ts).contiguous()
-        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+    for s in range(71):
+        t_begin = s * 1000 + 1000 + (s // 10) * 2000
+        if s < 68:
+            ts = torch.arange(1000, device=dev, dtype=torch.int64) + t_begin
+            v = torch.randint(-2**31, 2**31, (1000,), device=dev, dtype=torch.int32, generator=g)
+        else:
+            ts = base + t_begin
+            late = torch.rand(batch, device=dev, generator=g) < 0.2
+            d = torch.randint(1, 501, (batch,), device=dev, generator=g)
+            ts = torch.where(late, torch.clamp(ts - d, min=t_begin - 500), ts).contiguous()
+            v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         torch.cuda.synchronize(dev)
+        n = ts.numel()
         tt = []
         for op in ops:
             t0 = time.perf_counter()
-            op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
+            op.processElementsDevice(ts.data_ptr(), v.data_ptr(), n)
             op.sync()
             tt.append(round(time.perf_counter() - t0, 3))
-        verdict = ops[0]._debug_stat(8)
-        print("C3 full-size step %d: verdict %d, push s (quiet, event, serial) %s" % (s, verdict, tt), flush=True)
-        quiet += verdict == 1
-        event += verdict > 1
-        wm = t_begin + (batch - 1) // rate - 500
+        assert ora.processElements(ts.cpu().numpy(), v.cpu().numpy()) == 0
+        if s >= 68:
+            verdict = ops[0]._debug_stat(8)
+            print("C3 full-size step %d: verdict %d, push s (quiet, event, serial) %s" % (s, verdict, tt), flush=True)
+            quiet += verdict == 1
+            event += verdict > 1
+        wm = t_begin + (n - 1) // (rate if s >= 68 else 1) - 500
         a, b, c = (op.processWatermark(wm) for op in ops)
+        exp = ora.processWatermark(wm)
         same_windows(a, b)
         same_windows(a, c)
-        rows += len(a)
-    assert quiet >= 2 and event >= 1, (quiet, event)
-    assert rows > 0
+        same_windows(a, exp)
+        if s >= 68:
+            rows += len(a)
+            sliding += sum(1 for w in a if w.getEnd() - w.getStart() == 60_000)
+    assert quiet >= 1 and event >= 1, (quiet, event)
+    assert sliding > 30 and rows > sliding, (rows, sliding)
 
 
 def test_session_tumbling_mixed_config3_reduced():
