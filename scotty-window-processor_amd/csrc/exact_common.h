@@ -124,8 +124,17 @@ struct XSlices {
   int32_t sc_sh, kc_sh;
 };
 
-// Fields of the key-interleaved store (XSlices.kw), one 8-byte word each (ty in the low half of its word)
-enum : int { XK_TS, XK_TE, XK_TL, XK_TF, XK_CS, XK_CL, XK_CNT, XK_P0, XK_P1, XK_P2, XK_PC, XK_PS, XK_TY, XK_NF };
+// Fields of the key-interleaved store (XSlices.kw), one 8-byte word each (ty in the low half of its word).
+// MIN / MAX window assembly (keyed_lane.hip, lane_wm_emit_kernel) keeps block summaries of p[1] / p[2] over blocks of
+// XK_MB consecutive slice positions: QN / QX the min / max from the block's first position up to this one (valid below
+// XState.pvalid, like PC / PS), SN / SX from this position to the block's end (kept for complete blocks only: the
+// emit kernel recomputes them for every complete block that holds a position at or above pvalid) -- a window of
+// positions [lo, hi) then reads SN[lo], QN at the end of each whole block and QN[hi - 1], not each of its slices.
+enum : int {
+  XK_TS, XK_TE, XK_TL, XK_TF, XK_CS, XK_CL, XK_CNT, XK_P0, XK_P1, XK_P2, XK_PC, XK_PS,
+  XK_QN, XK_SN, XK_QX, XK_SX, XK_TY, XK_NF
+};
+constexpr int XK_MB = 16;  // slice positions per MIN / MAX summary block
 
 // Column views of the key-interleaved store with the syntax of XSlices' columns (q.ts[j], q.p[k][j], q.ts + base
 // with j = op * sc + i), so one kernel body serves both layouts (template parameter V = XSlices or XKView).
@@ -163,6 +172,7 @@ struct XKView {
   XKCol<unsigned long long> cnt;
   XKParts p;
   XKCol<unsigned long long> pc, ps;
+  XKCol<int64_t> qn, sn, qx, sx;  // MIN / MAX block summaries (XK_QN ...)
   XKCol<int32_t> ty;
   __host__ __device__ XKView() {}
   __host__ __device__ explicit XKView(const XSlices& s) {
@@ -173,6 +183,7 @@ struct XKView {
     };
     col(ts, XK_TS); col(te, XK_TE); col(tl, XK_TL); col(tf, XK_TF); col(cs, XK_CS); col(cl, XK_CL);
     col(cnt, XK_CNT); col(pc, XK_PC); col(ps, XK_PS); col(ty, XK_TY);
+    col(qn, XK_QN); col(sn, XK_SN); col(qx, XK_QX); col(sx, XK_SX);
     p.c = b;
   }
 };

@@ -307,7 +307,7 @@ int XEngine::grow_ops(int64_t need) {
     return hipSuccess;
   };
   if (ops_cap == 0)  // the store's layout is fixed with the first allocation
-    aos = keyed && lane_mode() && vt != VT_F64 && !(cfg.need & (NEED_MIN | NEED_MAX));
+    aos = keyed && lane_mode() && vt != VT_F64;
   XCHK(grow(&d_st, 1));
   if (aos) {  // key-interleaved store: rows (position, field) of cap words, re-strided from the old key capacity
     unsigned long long* nw = nullptr;
@@ -1379,11 +1379,12 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.dropped_total = (unsigned long long*)(d_misc + 1);
   a.op_err = (int32_t*)(d_misc + 2);
   a.slot_key = keyed ? d_slot_key : nullptr;
-  // lane path: COUNT / integer SUM windows straight from the slice prefixes in the emit kernel; MIN / MAX / f64
-  // sums scan the slices (wm_agg).  (MIN / MAX by a lane-per-key scan of each window's contained run inside the emit
-  // kernel measured 2.46 ms per C4 watermark against 1.18 ms this way: the lanes walk 64 different lines per load.)
-  const bool prefix_agg = lane_mode() && !(cfg.need & (NEED_MIN | NEED_MAX)) &&
-                          !((cfg.need & NEED_SUM) && vt == VT_F64);
+  // lane path: COUNT / integer SUM windows straight from the slice prefixes in the emit kernel, integer MIN / MAX from
+  // the key-interleaved store's block summaries (XK_QN ...); f64 (and MIN / MAX outside that store) scan the slices
+  // (wm_agg).  (MIN / MAX by a lane-per-key scan of each window's contained run in the key-major store measured
+  // 2.46 ms per C4 watermark against 1.18 ms with wm_agg: the lanes walk 64 different lines per load.)
+  const bool prefix_agg = lane_mode() && !((cfg.need & NEED_SUM) && vt == VT_F64) &&
+                          (!(cfg.need & (NEED_MIN | NEED_MAX)) || sl.kw != nullptr);
   a.prefix_reset = prefix_stale ? 1 : 0;
   const int64_t bound = prefix_agg ? lane_row_bound(wm) : -1;
   if (bound >= 0) {  // one kernel: count, reserve, emit, aggregate, GC -- rows sized from the bound

@@ -102,7 +102,7 @@ class XEngine {
   // non-keyed: the single-wavefront replay (LazySlice record sets live only there)
   bool use_serial() const { return serial || records; }
   bool records = false;   // LazySlice record sets kept (XCfg.records)
-  // lane path with COUNT / integer SUM functions only: the slice store is kept key-interleaved (XSlices.kw, XKView),
+  // lane path with integer values: the slice store is kept key-interleaved (XSlices.kw, XKView),
   // fixed with the first allocation -- the lane path cannot be switched off afterwards
   bool aos = false;
   bool layout_fixed() const { return aos; }

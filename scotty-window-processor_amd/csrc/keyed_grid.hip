@@ -1072,7 +1072,17 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
   const dim3 grid((unsigned)a.nbk), block(1024);
   const dim3 cgrid((unsigned)((n_ops + 255) / 256)), cblock(256);
   const bool B = (which & 1) != 0, C = (which & 2) != 0;
-  if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM only
+  if (a.sl.kw && mm) {  // key-interleaved store with MIN / MAX (integer values)
+    if (vt == VT_I32) {
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<VT_I32, true>), grid, block, 0, st, a);
+      if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, true, XKView>), cgrid, cblock, 0, st, a, n_ops);
+    } else {
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<VT_I64, true>), grid, block, 0, st, a);
+      if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I64, true, XKView>), cgrid, cblock, 0, st, a, n_ops);
+    }
+    return hipGetLastError();
+  }
+  if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM
     if (vt == VT_I32) {
       // 8 records in flight per lane (A/B r03k: 2 -> 8 cut the data pass 1.14 -> 1.02 ms per 2^26 tuples; variant 5:
       // 4, variant 0: 2)

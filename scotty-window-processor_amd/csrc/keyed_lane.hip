@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "exact_common.h"
 #include "exact_op.h"
 
@@ -491,10 +493,17 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
   }
   if (AGG && k > 0) {
     const bool sums = (c->need & NEED_SUM) != 0;
+    // MIN / MAX (integer values, key-interleaved store only): block summaries instead of a scan of each window's
+    // slices (LazyAggregateStore.aggregate's per-slice AggregateWindowState.addState, :83-111, regrouped: min / max
+    // are associative, and the slices of a window's run are combined in blocks)
+    constexpr bool KW = std::is_same<V, XKView>::value;
+    const bool mmin = KW && (c->need & NEED_MIN) != 0, mmax = KW && (c->need & NEED_MAX) != 0;
     const auto pc = q.pc + base;
     const auto ps = q.ps + base;
     const auto cnt = q.cnt + base;
     const auto p0 = q.p[0] + base;
+    const auto p1 = q.p[1] + base;
+    const auto p2 = q.p[2] + base;
     int pv = a.prefix_reset ? 0 : s.pvalid;
     if (pv < t) {  // extend the prefixes over the slices changed since the last watermark
       unsigned long long rc = pv > 0 ? pc[pv - 1] : 0, rs = pv > 0 && sums ? ps[pv - 1] : 0;
@@ -506,6 +515,29 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
           ps[i] = rs;
         }
       }
+      if constexpr (KW) {
+        if (mmin || mmax) {
+          const auto qn = q.qn + base, sn = q.sn + base, qx = q.qx + base, sx = q.sx + base;
+          // in-block prefixes of the changed positions (a block's first position starts its own)
+          int64_t rn = (pv % XK_MB) ? qn[pv - 1] : ID_MIN, rx = (pv % XK_MB) ? qx[pv - 1] : ID_MAX;
+          for (int i = pv; i < t; i++) {
+            if (i % XK_MB == 0) {
+              rn = ID_MIN;
+              rx = ID_MAX;
+            }
+            if (mmin) qn[i] = rn = min(rn, (int64_t)p1[i]);
+            if (mmax) qx[i] = rx = max(rx, (int64_t)p2[i]);
+          }
+          // in-block suffixes of every complete block that holds a changed position
+          for (int b0 = pv - pv % XK_MB; b0 + XK_MB <= t; b0 += XK_MB) {
+            int64_t un = ID_MIN, ux = ID_MAX;
+            for (int i = b0 + XK_MB - 1; i >= b0; i--) {
+              if (mmin) sn[i] = un = min(un, (int64_t)p1[i]);
+              if (mmax) sx[i] = ux = max(ux, (int64_t)p2[i]);
+            }
+          }
+        }
+      }
       pv = t;
     }
     s.pvalid = pv;
@@ -515,25 +547,48 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
     for (int64_t r = off; r < off + k; r++) {
       const int64_t ws = a.w_start[r], we = a.w_end[r];
       uint64_t cn = 0, sw = 0;
+      int64_t mn = ID_MIN, mx = ID_MAX;
       if (sorted) {  // the contained slices (ws <= tStart, tLast < we) are the run [lo, hi): tLast increases
         const int lo = first_true_up(lo0, hi0, [&](int i) { return ts[i] >= ws; });
         const int hi = first_true_down(lo, hi0, [&](int i) { return tl[i] >= we; });
         if (hi > lo) {
           cn = pc[hi - 1] - (lo > 0 ? pc[lo - 1] : 0ull);
           if (sums) sw = ps[hi - 1] - (lo > 0 ? ps[lo - 1] : 0ull);
+          if constexpr (KW) {
+            if (mmin || mmax) {
+              const auto qn = q.qn + base, sn = q.sn + base, qx = q.qx + base, sx = q.sx + base;
+              const int bl = lo / XK_MB, bh = (hi - 1) / XK_MB;
+              if (bl == bh) {  // within one block: its slices (at most XK_MB)
+                for (int i = lo; i < hi; i++) {
+                  if (mmin) mn = min(mn, (int64_t)p1[i]);
+                  if (mmax) mx = max(mx, (int64_t)p2[i]);
+                }
+              } else {  // suffix of lo's (complete) block, whole blocks, prefix of hi - 1's block
+                if (mmin) mn = min(sn[lo], qn[hi - 1]);
+                if (mmax) mx = max(sx[lo], qx[hi - 1]);
+                for (int b = bl + 1; b < bh; b++) {
+                  const int e = b * XK_MB + XK_MB - 1;
+                  if (mmin) mn = min(mn, (int64_t)qn[e]);
+                  if (mmax) mx = max(mx, (int64_t)qx[e]);
+                }
+              }
+            }
+          }
         }
       } else {
         for (int i = lo0; i < hi0; i++) {
           if (!(ws <= ts[i] && we > tl[i])) continue;
           cn += cnt[i];
           if (sums) sw += p0[i];
+          if (mmin) mn = min(mn, (int64_t)p1[i]);
+          if (mmax) mx = max(mx, (int64_t)p2[i]);
         }
       }
       const bool present = cn != 0;
       a.has_value[r] = present ? 1 : 0;
       if (a.w_key) a.w_key[r] = key;
       for (int q = 0; q < c->n_aggs; q++)
-        a.values[q][r] = present ? x::lower_value(c->agg_kind[q], cn, sw, ID_MIN, ID_MAX) : 0;
+        a.values[q][r] = present ? x::lower_value(c->agg_kind[q], cn, sw, mn, mx) : 0;
     }
   }
   s.lastWatermark = a.wm;
@@ -551,9 +606,14 @@ hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStre
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
   const bool mm = (host_cfg.need & (NEED_MIN | NEED_MAX)) != 0;
   const int vt = host_cfg.vt;
-  if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM only (no MIN / MAX, no f64)
-    if (vt == VT_I32) hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I32, false, XKView>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I64, false, XKView>), grid, block, 0, st, a);
+  if (a.sl.kw) {  // key-interleaved store: integer values (COUNT, SUM, MIN, MAX; no f64)
+    if (vt == VT_I32) {
+      if (mm) hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I32, true, XKView>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I32, false, XKView>), grid, block, 0, st, a);
+    } else {
+      if (mm) hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I64, true, XKView>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((ln::lane_replay_kernel<VT_I64, false, XKView>), grid, block, 0, st, a);
+    }
     return hipGetLastError();
   }
 #define SCOTTY_LANE(V, M) hipLaunchKernelGGL((ln::lane_replay_kernel<V, M, XSlices>), grid, block, 0, st, a)

@@ -821,28 +821,32 @@ __device__ __forceinline__ int64_t block_incl_max(int64_t v, long long* wtot, in
   return v;
 }
 
+// Candidate grid points held in LDS by the commit (a batch reaching more of them takes the global-memory search)
+constexpr int CAND_LDS = 2048;
+
 __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __shared__ long long s_p[NT_MAX];   // tile maxima -> prefix maxima (arrival order)
+  __shared__ long long s_g[CAND_LDS]; // grid points g[0 .. CAND_LDS) above the pending edge's predecessor
+  __shared__ int32_t s_flag[CAND_LDS], s_rank[CAND_LDS];
   __shared__ long long s_w[32];
   __shared__ int64_t sc[16];
   __shared__ long long s_dirty;       // lowest slice whose partials change (watermark block summaries)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // Every thread reads the operator's scalars itself (one line, uniform addresses) and issues the tile-maxima and
+  // grid-window loads at once: the chain of dependent global accesses is what bounds this one-workgroup kernel
+  const DevMeta& m = *a.meta;
+  const int64_t ovf0 = m.overflow, head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount, prev_max = m.prev_max;
+  const int64_t cmin = m.cmin;
+  if (ovf0 != 0) return;
   if (tid == 0) s_dirty = INT64_MAX;
-  if (tid == 0) {
-    const DevMeta& m = *a.meta;
-    sc[0] = m.overflow; sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount; sc[5] = m.prev_max;
-    sc[10] = m.cmin;
-  }
-  __syncthreads();
-  if (sc[0] != 0) return;
-  const int64_t head = sc[1], tail = sc[2], j0 = sc[3], gcount = sc[4], prev_max = sc[5];
   const int64_t c_old = tail - head;
   int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
   if (kc < 0) kc = 0;
-  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
   const int64_t* g = a.grid + j0;
   const int64_t L = a.max_lateness;
   const int64_t tile = a.tile;
+  const int64_t kl = min(kc, (int64_t)CAND_LDS);  // grid points staged in LDS
+  for (int64_t k = tid; k < kl; k += 1024) s_g[k] = g[k];
 
   // ---- (a) prefix max over tile maxima, in LDS: 8 consecutive tiles per thread
   const int64_t nT = (a.n + tile - 1) / tile;
@@ -864,32 +868,45 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   }
   __syncthreads();
   const int64_t batch_max = max(prev_max, nT > 0 ? (int64_t)s_p[nT - 1] : INT64_MIN);
+  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
 
-  // ---- (b) candidates: grid points g[k] <= batch_max (k < kc): wavefront-cooperative search (64 probes per
-  //      round) instead of a 20-step chain of dependent loads on one thread
+  // ---- (b) candidates: grid points g[k] <= batch_max (k < kc).  The staged window answers with one count over LDS;
+  //      a batch that reaches past it searches the grid wavefront-cooperatively (64 probes per round)
+  {
+    int c = 0;
+    for (int64_t k = tid; k < kl; k += 1024) c += s_g[k] <= batch_max ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) s_w[16 + wid] = c;
+  }
+  __syncthreads();
   if (wid == 0) {
-    int64_t lo = 0, hi = kc;  // first k with g[k] > batch_max
-    while (hi - lo > 64) {
-      const int64_t stride = (hi - lo + 63) >> 6;
-      const int64_t p = lo + (int64_t)lane * stride;
-      const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
-      if (bal == 0) {
-        lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
-      } else {
-        const int f = __ffsll((long long)bal) - 1;
-        if (f == 0) {
-          hi = lo;
-          break;
+    int64_t lo = 0;
+    for (int w = 0; w < 16; w++) lo += s_w[16 + w];
+    if (lo == kl && kl < kc) {  // every staged point is reached: the rest of the grid by search
+      int64_t hi = kc;          // first k with g[k] > batch_max
+      while (hi - lo > 64) {
+        const int64_t stride = (hi - lo + 63) >> 6;
+        const int64_t p = lo + (int64_t)lane * stride;
+        const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
+        if (bal == 0) {
+          lo = lo + ((hi - 1 - lo) / stride) * stride + 1;
+        } else {
+          const int f = __ffsll((long long)bal) - 1;
+          if (f == 0) {
+            hi = lo;
+            break;
+          }
+          const int64_t pf = lo + (int64_t)f * stride;
+          lo = pf - stride + 1;
+          hi = pf;
         }
-        const int64_t pf = lo + (int64_t)f * stride;
-        lo = pf - stride + 1;
-        hi = pf;
       }
-    }
-    if (hi > lo) {
-      const int64_t p = lo + lane;
-      const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
-      lo = bal ? lo + __ffsll((long long)bal) - 1 : hi;
+      if (hi > lo) {
+        const int64_t p = lo + lane;
+        const unsigned long long bal = __ballot(p < hi && g[p] > batch_max);
+        lo = bal ? lo + __ffsll((long long)bal) - 1 : hi;
+      }
     }
     if (lane == 0) {
       sc[8] = lo;
@@ -899,6 +916,11 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __syncthreads();
   const int64_t ncand = sc[8];
   int ovf = (int)sc[9];
+  // flags and ranks of the candidates: LDS for the common case, the global scratch arrays beyond it
+  const bool lds = ncand <= CAND_LDS;
+  int32_t* const flag = lds ? s_flag : a.flag;
+  int32_t* const rank = lds ? s_rank : a.rank;
+  auto gk_of = [&](int64_t k) -> int64_t { return k < kl ? (int64_t)s_g[k] : g[k]; };
 
   // ---- (c) edge decision, StreamSlicer.determineSlices (S/StreamSlicer.java:55-84) per candidate.
   // For a grid point g with pending edge N (g in the effective grid above N's predecessor) the
@@ -914,14 +936,14 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __syncthreads();
   if (!ovf) {
     for (int64_t k = tid; k < ncand; k += 1024) {
-      const int64_t gk = g[k];
+      const int64_t gk = gk_of(k);
       const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
       const int64_t pprev = ts_ > 0 ? max(prev_max, (int64_t)s_p[ts_ - 1]) : prev_max;
       const int64_t tm = a.tilemax[ts_];
       int f;
-      if (k == 0 || g[k - 1] <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < L) f = 1;
+      if (k == 0 || gk_of(k - 1) <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < L) f = 1;
       else f = 2;
-      a.flag[k] = f;
+      flag[k] = f;
       if (f == 2) {
         const int i = atomicAdd(&s_namb, 1);
         if (i < AMB_CAP) s_amb[i] = (int32_t)k;
@@ -930,16 +952,16 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   }
   __syncthreads();
   const int namb = s_namb;
-  if (!ovf) {
+  if (!ovf && namb > 0) {
     const int64_t kn = namb <= AMB_CAP ? namb : ncand;  // list overflow: every candidate, flag checked
     for (int64_t j = wid; j < kn; j += 16) {
       const int64_t k = namb <= AMB_CAP ? (int64_t)s_amb[j] : j;
-      if (namb > AMB_CAP && a.flag[k] != 2) continue;
-      const int64_t gk = g[k];
+      if (namb > AMB_CAP && flag[k] != 2) continue;
+      const int64_t gk = gk_of(k);
       const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
       int64_t r = ts_ > 0 ? max(prev_max, (int64_t)s_p[ts_ - 1]) : prev_max;
       const int64_t e0 = ts_ * tile, e1 = min(a.n, e0 + tile);
-      int64_t e = INT64_MIN, m = INT64_MIN;
+      int64_t e = INT64_MIN, mm = INT64_MIN;
       for (int64_t base = e0; base < e1; base += 64) {
         const int64_t i = base + lane;
         const int64_t v = i < e1 ? a.ts[i] : INT64_MIN;
@@ -956,18 +978,18 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
         if (hit) {
           const int f = __ffsll((long long)hit) - 1;
           e = rl64(v, f);
-          m = rl64(ex, f);
+          mm = rl64(ex, f);
           break;
         }
         r = max(r, rl64(inc, 63));
       }
       if (lane == 0) {
-        const bool emit = (int64_t)((uint64_t)e - (uint64_t)gk) < L || g[k - 1] <= m;
-        a.flag[k] = emit ? 1 : 0;
+        const bool emit = (int64_t)((uint64_t)e - (uint64_t)gk) < L || gk_of(k - 1) <= mm;
+        flag[k] = emit ? 1 : 0;
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
 
   // ---- (d) rank = inclusive prefix count of emitted edges (ballot/popcount per wave)
   int64_t n_emit = 0;
@@ -975,7 +997,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     int64_t base_cnt = 0;
     for (int64_t base = 0; base < ncand; base += 1024) {
       const int64_t k = base + tid;
-      const bool f = k < ncand && a.flag[k] == 1;
+      const bool f = k < ncand && flag[k] == 1;
       const unsigned long long bal = __ballot(f);
       const int in_wave = __popcll(bal & ((2ull << lane) - 1));  // inclusive within the wave
       if (lane == 0) s_w[wid] = __popcll(bal);
@@ -984,7 +1006,23 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       for (int w = 0; w < wid; w++) before += s_w[w];
       int64_t tot = 0;
       for (int w = 0; w < 16; w++) tot += s_w[w];
-      if (k < ncand) a.rank[k] = (int32_t)(base_cnt + before + in_wave);
+      const int32_t rk = (int32_t)(base_cnt + before + in_wave);
+      if (k < ncand) rank[k] = rk;
+      // ---- (e) append the new slice of an emitted edge at once (SliceManager.appendSlice: tStart = edge,
+      //      tLast = tStart, empty partial); a capacity overflow is decided after the loop and undoes nothing:
+      //      slices past the capacity are not written, and the tail moves only on success
+      if (f) {
+        const int64_t sl = tail + rk - 1;
+        if (sl < a.scap) {
+          const int64_t gk = gk_of(k);
+          a.s_tstart[sl] = gk;
+          a.s_tlast[sl] = gk;
+          a.s_cnt[sl] = 0;
+          a.s_part[0][sl] = 0;
+          a.s_part[1][sl] = (unsigned long long)PART_ID_MIN;
+          a.s_part[2][sl] = (unsigned long long)PART_ID_MAX;
+        }
+      }
       base_cnt += tot;
       __syncthreads();
     }
@@ -994,23 +1032,10 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __syncthreads();
 
   if (!ovf) {
-    // ---- (e) append new slices (SliceManager.appendSlice: tStart = edge, tLast = tStart, empty partial)
-    for (int64_t k = tid; k < ncand; k += 1024) {
-      if (a.flag[k] == 1) {
-        const int64_t s = tail + a.rank[k] - 1;
-        a.s_tstart[s] = g[k];
-        a.s_tlast[s] = g[k];
-        a.s_cnt[s] = 0;
-        a.s_part[0][s] = 0;
-        a.s_part[1][s] = (unsigned long long)PART_ID_MIN;
-        a.s_part[2][s] = (unsigned long long)PART_ID_MAX;
-      }
-    }
-    __syncthreads();
     // ---- (f) fold cells into slices (AbstractSlice.addElement + AggregateState.merge semantics); cells below
     //      the lowest cell the ingest touched (DevMeta.cmin) are untouched
     const int64_t ncell = c_old + ncand;
-    const int64_t cfirst = min(max(sc[10], (int64_t)0), ncell);
+    const int64_t cfirst = min(max(cmin, (int64_t)0), ncell);
     for (int64_t c = cfirst + tid; c < ncell; c += 1024) {
       const unsigned long long cnt = a.c_cnt[c];
       if (cnt == 0) continue;
@@ -1018,7 +1043,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       if (c < c_old) {
         s = head + c;
       } else {
-        const int32_t r = a.rank[c - c_old];
+        const int32_t r = rank[c - c_old];
         s = r > 0 ? tail + r - 1 : tail - 1;
       }
       atomicMin(&s_dirty, (long long)s);
@@ -1050,23 +1075,23 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   }
   __syncthreads();
   if (tid == 0) {
-    DevMeta& m = *a.meta;
-    m.batch_max = batch_max;
+    DevMeta& mw = *a.meta;
+    mw.batch_max = batch_max;
     if (!ovf) {
-      m.tail = tail + n_emit;
-      m.j0 = j0 + ncand;
-      m.prev_max = batch_max;
-      m.n_emitted = n_emit;
-      m.dirty_from = min(m.dirty_from, min((int64_t)s_dirty, tail));
-      m.late_total += m.late_push;
-      m.processed_total += (uint64_t)a.n - m.late_push;
+      mw.tail = tail + n_emit;
+      mw.j0 = j0 + ncand;
+      mw.prev_max = batch_max;
+      mw.n_emitted = n_emit;
+      mw.dirty_from = min(mw.dirty_from, min((int64_t)s_dirty, tail));
+      mw.late_total += mw.late_push;
+      mw.processed_total += (uint64_t)a.n - mw.late_push;
     } else {
-      m.overflow = ovf;
-      m.failed_push = a.push_seq;
+      mw.overflow = ovf;
+      mw.failed_push = a.push_seq;
     }
-    m.late_push = 0;
-    m.overflow_push = 0;
-    m.cmin = INT64_MAX;
+    mw.late_push = 0;
+    mw.overflow_push = 0;
+    mw.cmin = INT64_MAX;
   }
 }
 
