@@ -216,6 +216,17 @@ struct XBatchArgs {
   unsigned long long* need; // [3] capacity pre-check: max slices / sessions / records an op may need (atomicMax)
 };
 
+// Block summaries of one operator's slices for the watermark (exact_kernels.hip, wm_blocks_kernel): block b covers
+// slice positions [XB_BLK * b, XB_BLK * (b + 1)); a block not wholly inside the scan range [wlo, whi) gets ts_min =
+// INT64_MIN, so no window takes it whole
+constexpr int XB_BLK = 64;
+struct XBlocks {
+  unsigned long long *cnt, *sum;   // COUNT; wrapping integer sum or f64 sum bits
+  long long *mn, *mx;              // MIN / MAX partials (order-preserving keys for f64)
+  long long *ts_min, *tl_max;      // smallest tStart / largest tLast of the block (whole-block containment test)
+  int64_t nbcap;
+};
+
 struct XWmArgs {
   const XCfg* cfg;
   XState* st;
@@ -243,6 +254,9 @@ struct XWmArgs {
   int32_t prefix_reset;                // lane path: recompute every op's slice prefixes from position 0
   unsigned long long* row_count;       // lane path / single mode: rows written by the emit kernel (n_rows = capacity)
   int32_t single;                      // one operator: wm_emit_kernel counts, checks and emits (no count pass)
+  // one operator, Eager slices: 64-slice block summaries over the scan range [wlo, whi) (wm_blocks_kernel), read by
+  // wm_agg_kernel for the blocks a window contains whole; null: every window scans its slices
+  XBlocks blk;
 };
 
 }  // namespace scotty

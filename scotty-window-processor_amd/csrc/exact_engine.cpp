@@ -21,6 +21,7 @@ hipError_t launch_replay(const XBatchArgs& a, int vt, hipStream_t st);
 hipError_t launch_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group);
+hipError_t launch_wm_blocks(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st);
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st);
@@ -131,6 +132,9 @@ void XEngine::release() {
   dfree(d_xq_eg); dfree(d_xq_epos); dfree(d_xq_meta); dfree(d_xq_cix); dfree(d_xq_cixmeta); dfree(d_xq_ctl);
   dfree(d_dbg);
   d_dbg = nullptr;
+  dfree(xblk.cnt); dfree(xblk.sum); dfree(xblk.mn); dfree(xblk.mx); dfree(xblk.ts_min); dfree(xblk.tl_max);
+  xblk = XBlocks{};
+  xblk_cap = 0;
   for (auto& e : ev_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto& e : ev_pool) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   ev_pending.clear();
@@ -1425,6 +1429,18 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   if (sbound >= 0) {  // one operator: no count pass -- the emit kernel checks, emits and counts (rows from a bound)
     int rc = ensure_rows(std::max<int64_t>(sbound, 1));
     if (rc) return rc;
+    if (!cfg.records) {  // 64-slice block summaries of the scan range for the window assembly (wm_blocks_kernel)
+      const int64_t need_b = (int64_t)sc / XB_BLK + 2;
+      if (xblk_cap < need_b) {
+        XCHK(hipStreamSynchronize(stream));
+        dfree(xblk.cnt); dfree(xblk.sum); dfree(xblk.mn); dfree(xblk.mx); dfree(xblk.ts_min); dfree(xblk.tl_max);
+        XCHK(dalloc(&xblk.cnt, need_b)); XCHK(dalloc(&xblk.sum, need_b)); XCHK(dalloc(&xblk.mn, need_b));
+        XCHK(dalloc(&xblk.mx, need_b)); XCHK(dalloc(&xblk.ts_min, need_b)); XCHK(dalloc(&xblk.tl_max, need_b));
+        xblk_cap = need_b;
+      }
+      a.blk = xblk;
+      a.blk.nbcap = xblk_cap;
+    }
     a.single = 1;
     a.row_count = (unsigned long long*)(d_misc + 3);
     a.n_rows = sbound;
@@ -1440,6 +1456,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     if (rct) return rct;
     XCHK(hipMemsetAsync(d_misc, 0, 4 * 8, stream));
     XCHK(launch_wm_emit(a, stream));
+    if (a.blk.cnt) XCHK(launch_wm_blocks(a, stream));
     XCHK(launch_wm_agg(a, stream, 64));
     XCHK(launch_copy_to_host(d_misc, h_misc_dev, 4 * 8, stream));
     if ((rct = tend(tw, 0))) return rct;

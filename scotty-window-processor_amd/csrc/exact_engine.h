@@ -227,7 +227,9 @@ class XEngine {
   uint32_t* d_xq_cix = nullptr;
   int64_t* d_xq_cixmeta = nullptr;
   void* d_xq_ctl = nullptr;
-  long long* d_dbg = nullptr;   // debugging aid (SCOTTY_XQ_PROF / SCOTTY_XB_PROF): clock stamps, this engine's device
+  long long* d_dbg = nullptr;
+  XBlocks xblk{};               // single operator: 64-slice block summaries of the watermark (wm_blocks_kernel)
+  int64_t xblk_cap = 0;   // debugging aid (SCOTTY_XQ_PROF / SCOTTY_XB_PROF): clock stamps, this engine's device
   int64_t xq_span = 1000;       // event-time span of the last committed batch (grid horizon and cell-index sizing)
   bool xq_need_grid = true;     // (re)build the grid from the pending edge at the next push
 };

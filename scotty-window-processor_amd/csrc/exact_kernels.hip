@@ -531,6 +531,59 @@ __device__ __forceinline__ int64_t group_first(int64_t lo, int64_t hi, int lane,
 template <int G>
 __device__ __forceinline__ void agg_row(const XWmArgs& a, int64_t wi, int lane);
 
+// Block summaries of the single operator's scan range (a wavefront per 64-slice block): what a window containing the
+// whole block adds (AggregateWindowState.addState over its slices, S/state/AggregateWindowState.java:33-39), and
+// the block's smallest tStart / largest tLast, so containment (:25-31) of the whole block is one test.
+__global__ __launch_bounds__(256) void wm_blocks_kernel(XWmArgs a) {
+  const int lane = threadIdx.x & 63;
+  const XState& st = a.st[0];
+  if (st.err || (st.unsorted & 3) || a.cfg->records) return;
+  const int64_t wlo = max((int64_t)st.wlo, (int64_t)0), whi = st.whi;
+  if (whi <= wlo) return;
+  const int need = a.cfg->need;
+  const bool f64 = a.cfg->vt == VT_F64;
+  const int64_t b_first = wlo / XB_BLK, b_last = (whi - 1) / XB_BLK;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t b = b_first + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b <= b_last; b += nw) {
+    if (b - b_first >= a.blk.nbcap) break;
+    const int64_t s = b * XB_BLK + lane;
+    const bool in = s >= wlo && s < whi;
+    uint64_t c = 0, sw = 0;
+    double sf = 0.0;
+    int64_t mn = ID_MIN, mx = ID_MAX, t0 = JMAX, t1 = JMIN;
+    if (in) {
+      c = a.sl.cnt[s];
+      t0 = a.sl.ts[s];
+      t1 = a.sl.tl[s];
+      if (need & NEED_SUM) {
+        if (f64) sf = __longlong_as_double((long long)a.sl.p[0][s]);
+        else sw = a.sl.p[0][s];
+      }
+      if (need & NEED_MIN) mn = (int64_t)a.sl.p[1][s];
+      if (need & NEED_MAX) mx = (int64_t)a.sl.p[2][s];
+    }
+    c = greduce<64>((unsigned long long)c, [](unsigned long long x, unsigned long long y) { return x + y; });
+    if (need & NEED_SUM) {
+      if (f64) sf = greduce<64>(sf, [](double x, double y) { return x + y; });
+      else sw = greduce<64>((unsigned long long)sw, [](unsigned long long x, unsigned long long y) { return x + y; });
+    }
+    mn = greduce<64>((long long)mn, [](long long x, long long y) { return x < y ? x : y; });
+    mx = greduce<64>((long long)mx, [](long long x, long long y) { return x > y ? x : y; });
+    t0 = greduce<64>((long long)t0, [](long long x, long long y) { return x < y ? x : y; });
+    t1 = greduce<64>((long long)t1, [](long long x, long long y) { return x > y ? x : y; });
+    const bool whole = b * XB_BLK >= wlo && (b + 1) * XB_BLK <= whi;
+    if (lane == 0) {
+      const int64_t i = b - b_first;  // indexed from the scan range's first block
+      a.blk.cnt[i] = c;
+      a.blk.sum[i] = f64 ? (unsigned long long)__double_as_longlong(sf) : sw;
+      a.blk.mn[i] = mn;
+      a.blk.mx[i] = mx;
+      a.blk.ts_min[i] = whole ? t0 : JMIN;
+      a.blk.tl_max[i] = t1;
+    }
+  }
+}
+
 // rows: n_rows, or (single mode) the count the emit kernel wrote; groups stride over them
 template <int G>
 __global__ __launch_bounds__(256) void wm_agg_kernel(XWmArgs a) {
@@ -564,8 +617,59 @@ __device__ __forceinline__ void agg_row(const XWmArgs& a, int64_t wi, int lane) 
   uint64_t cnt = 0, sw = 0, present = 0;
   double sf = 0.0;
   int64_t mn = ID_MIN, mx = ID_MAX;
+  // one slice: AggregateWindowState.containsSlice + addState (S/state/AggregateWindowState.java:25-39)
+  auto add_slice = [&](int64_t i) {
+    const int64_t s = base + i;
+    const int64_t k0 = tmeas ? a.sl.ts[s] : a.sl.cs[s];
+    const int64_t k1 = tmeas ? a.sl.tl[s] : a.sl.cl[s];
+    const uint64_t c = a.sl.cnt[s];
+    const bool contains = tmeas ? (ws <= k0 && we > k1) : (ws <= k0 && we >= k1);
+    if (!(contains && (recs ? a.sl.nn[s] != 0 : c != 0))) return;
+    present = 1;
+    cnt += c;
+    if (need & NEED_SUM) {
+      if (vt == VT_F64) sf += __longlong_as_double((long long)a.sl.p[0][s]);
+      else sw += a.sl.p[0][s];
+    }
+    if (need & NEED_MIN) mn = min(mn, (int64_t)a.sl.p[1][s]);
+    if (need & NEED_MAX) mx = max(mx, (int64_t)a.sl.p[2][s]);
+  };
+  // One operator with block summaries (wm_blocks_kernel, time windows on a sorted list): a lane per 64-slice block;
+  // a block the window contains whole adds its summary, the others (at most the two at the run's ends, usually) are
+  // scanned slice by slice by the wavefront -- the window costs its blocks, not its slices (north_star: window
+  // assembly from slice summaries; LazyAggregateStore.aggregate, S/aggregationstore/LazyAggregateStore.java:83-111)
+  const bool blocks = G == 64 && a.blk.cnt != nullptr && tmeas && !recs && !(st.unsorted & 3) && hi > lo &&
+                      lo >= st.wlo && hi <= st.whi;
+  if (blocks) {
+    const int64_t bf = st.wlo / XB_BLK;
+    for (int64_t b0 = lo / XB_BLK; b0 <= (hi - 1) / XB_BLK; b0 += G) {
+      const int64_t b = b0 + lane;
+      bool whole = false;
+      if (b <= (hi - 1) / XB_BLK && b - bf < a.blk.nbcap) {
+        const int64_t i = b - bf;
+        whole = a.blk.ts_min[i] >= ws && a.blk.tl_max[i] < we;  // every slice of the block contained
+        if (whole && a.blk.cnt[i] != 0) {
+          present = 1;
+          cnt += a.blk.cnt[i];
+          if (need & NEED_SUM) {
+            if (vt == VT_F64) sf += __longlong_as_double((long long)a.blk.sum[i]);
+            else sw += a.blk.sum[i];
+          }
+          if (need & NEED_MIN) mn = min(mn, (int64_t)a.blk.mn[i]);
+          if (need & NEED_MAX) mx = max(mx, (int64_t)a.blk.mx[i]);
+        }
+      }
+      unsigned long long part = __ballot(b <= (hi - 1) / XB_BLK && !whole);
+      while (part) {  // blocks in part: the wavefront tests each slice
+        const int j = __ffsll((long long)part) - 1;
+        part &= part - 1;
+        const int64_t i = (b0 + j) * XB_BLK + lane;
+        if (i >= lo && i < hi) add_slice(i);
+      }
+    }
+  }
   // two slices per lane per round, every load issued before the containment tests (no early continue)
-  for (int64_t i0 = lo + lane; i0 < hi; i0 += 2 * G) {
+  for (int64_t i0 = lo + lane; !blocks && i0 < hi; i0 += 2 * G) {
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       const int64_t i = i0 + u * G;
@@ -649,6 +753,10 @@ hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint3
   if (to <= from) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((to - from + 255) / 256, 4096);
   hipLaunchKernelGGL(x::xstate_init_kernel, dim3((unsigned)blocks), dim3(256), 0, st, st_, from, to, slot_key);
+  return hipGetLastError();
+}
+hipError_t launch_wm_blocks(const XWmArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(x::wm_blocks_kernel, dim3(64), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group) {

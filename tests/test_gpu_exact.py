@@ -313,6 +313,24 @@ def test_config3_full_size_quiet_path_equals_replay(pkg):
     assert sliding > 30 and rows > sliding, (rows, sliding)
 
 
+@pytest.mark.parametrize("vt", ["i32", "i64", "f64"])
+def test_exact_engine_window_assembly_from_block_summaries(vt):
+    """One operator on the exact engine (a session window beside long sliding windows): windows over hundreds of
+    slices are assembled from 64-slice block summaries (exact_kernels.hip wm_blocks_kernel / agg_row), the blocks at a
+    run's ends slice by slice; out-of-order tuples and session edits change old blocks between watermarks."""
+    aggs = {"i32": [MIN, MAX, SUM, COUNT], "i64": [MAX_I64, SUM_I64, MIN_I64], "f64": [SUM_F64, MIN_F64, MAX_F64, COUNT]}
+    cfg = dict(windows=[Sliding(Time, 9001, 13), Session(Time, 400), Sliding(Time, 2003, 7)], aggs=aggs[vt],
+               lateness=600)
+    n = 400_000
+    gaps = [(i, 900) for i in range(60_000, n, 90_000)]
+    ts, vals = product().workloads.stream(n, 8, t0=100, ooo_frac=0.2, max_delay=300, seed=61, value_type=vt,
+                                          gaps=gaps)
+    gpu, ora = build_ops(cfg, vt)
+    sched = interval_schedule(ts, 30, lag=300, pushes_per_interval=2)
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
+    assert run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols) > 2000
+
+
 def test_session_tumbling_mixed_config3_reduced():
     """BASELINE configs[2] at reduced size: sliding + session, 20 % out-of-order (TimeStampGenerator-like,
     delay U[1,500]), MIN/MAX; session silences every ~10 s of event time."""
