@@ -446,6 +446,8 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
         op.processWatermarkRaw(s * 1000 + 1000 + (batch - 1) // rate - 500)
     torch.cuda.synchronize(dev)
     log("c2s: tuples added with global atomics since creation:", f(op._h, 0))
+    log("c2s: last ingest launch: %d workgroups, streaming variant %d, slow-path tuples of the last push %d"
+        % (f(op._h, 9), f(op._h, 10), f(op._h, 11)))
     log("c2s: cell index base %d shift %d buckets %d full %d span_end %d; slices %d, grid ahead %d, prev_max %d"
         % tuple(f(op._h, k) for k in range(1, 9)))
     return {"workload": "C2s: 1000 concurrent sliding windows, sizes randomTumbling(1000,1,20) Random(10), slide "

@@ -22,6 +22,10 @@ constexpr int ING_SC = 24;        // block scalars of the ingest kernel (int64)
 constexpr int DEFER_CAP = 320;    // per-wave deferred out-of-order queue of the ingest kernel (entries)
 
 enum : int { VT_I32 = 0, VT_I64 = 1, VT_F64 = 2 };
+// launch_ingest's mode for a stream whose last push was in order (DevMeta.slow_last): the software-pipelined loop on
+// fewer, longer waves (r04f A/B on C2: 279 -> 264 us per 2^27 tuples; an out-of-order stream wants the default)
+constexpr int INGEST_STREAMING = -2;
+constexpr int INGEST_STREAMING_WGS_PER_CU = 2;  // x 256 CUs (C2: 448-640 workgroups measured best, 1024 slowest)
 enum : int { NEED_SUM = 1, NEED_MIN = 2, NEED_MAX = 4 };
 
 // Device-resident scalars.  The StreamSlicer state (maxEventTime, min_next_edge_ts) lives here so
@@ -43,6 +47,8 @@ struct DevMeta {
   int64_t cmin;               // lowest cell index the current push's ingest added to (commit folds from there)
   int64_t dirty_from;         // lowest slice index whose partials changed since the last watermark (block summaries)
   int64_t whead;              // head before the last watermark's GC (window assembly reads [whead, tail))
+  uint64_t slow_push;         // tuples of the current push outside their wave's current cell (ingest slow path)
+  uint64_t slow_last, n_last; // the last committed push's slow-path tuples and size (the host picks the next launch)
 };
 
 struct IngestArgs {

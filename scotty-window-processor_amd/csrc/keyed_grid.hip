@@ -383,194 +383,6 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   }
 }
 
-// The same scatter as a persistent, software-pipelined kernel (variant 4): one workgroup per CU walks its tiles
-// with the NEXT tile's loads (keys, timestamps, values, run bases) in flight in a second register set while the
-// current tile goes through its LDS phases (rank, scan, stage, write-out).  The one-tile-per-workgroup form leaves
-// the CU's memory pipe idle during those phases (one workgroup fits a CU: its 120 KB of LDS).  Plain loads survive
-// __syncthreads (no LDS-DMA in flight), so the prefetch spans the barriers.  Tiles of an XCD are consecutive: the
-// 32 workgroups of an XCD write adjacent runs of every bucket at the same time, which meet in its L2.
-template <int IT>
-struct KTile {  // one tile's inputs in registers
-  uint32_t k[IT];
-  int64_t t[IT];
-  uint32_t v[IT];
-};
-template <int T, int NBS, int ST>
-__global__ __launch_bounds__(ST) void kg_scatter_pipe_kernel(KgArgs a) {
-  constexpr int IT = T / ST;
-  constexpr int PER = NBS / ST;
-  __shared__ __attribute__((aligned(16))) uint32_t stage[T * 3];
-  __shared__ int32_t cnt[NBS + 1], tst[NBS], base[NBS];
-  __shared__ int32_t wsum[ST / 64];
-  __shared__ long long g_first[T / 64], g_last[T / 64];  // first / last ts of each 64-tuple group (order check)
-  if (a.ctl->flag) return;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t f = a.ctl->ts_first;
-  const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
-  const int64_t per = (a.ntiles + 7) >> 3;
-  const int64_t t_end = min((int64_t)a.ntiles, (xcd + 1) * per);
-  auto load = [&](KTile<IT>& x, int32_t (&bs)[PER], int64_t tile) {
-    const int64_t i0 = tile * T;
-#pragma unroll
-    for (int j = 0; j < IT; j++) {
-      const int64_t i = i0 + j * ST + tid;
-      const int64_t ic = i < a.n ? i : a.n - 1;
-      x.k[j] = __builtin_nontemporal_load(a.key + ic);
-      x.t[j] = a.ts[ic];
-      x.v[j] = (uint32_t)((const int32_t*)a.val)[ic];
-    }
-#pragma unroll
-    for (int p = 0; p < PER; p++) {
-      const int b = tid * PER + p;
-      bs[p] = a.hist[(int64_t)(b < a.nbk ? b : 0) * a.ntiles + tile];
-    }
-  };
-  auto process = [&](const KTile<IT>& x, const int32_t (&bs)[PER], int64_t tile) {
-    const int64_t i0 = tile * T;
-    __syncthreads();  // the previous tile's write-out has read stage / tst / base
-#pragma unroll
-    for (int p = 0; p < PER; p++) {
-      const int b = tid * PER + p;
-      if (b < a.nbk) {
-        cnt[b] = 0;
-        base[b] = bs[p];
-      }
-    }
-    __syncthreads();
-    int32_t bk[IT], rk[IT];
-    bool bad = false;
-#pragma unroll
-    for (int j = 0; j < IT; j++) {
-      const int64_t i = i0 + j * ST + tid;
-      const bool in = i < a.n;
-      // order inside the 64-tuple group from the neighbour lane; across groups through LDS below
-      const int64_t prev = (int64_t)__shfl_up((long long)x.t[j], 1);
-      bad |= in && lane > 0 && prev > x.t[j];
-      if (lane == 0) g_first[j * (ST / 64) + wid] = in ? x.t[j] : JMAX;
-      if (lane == 63) g_last[j * (ST / 64) + wid] = x.t[j];
-      bk[j] = in ? (int32_t)bucket_of(x.k[j], a.kmask) : NBS;
-      rk[j] = atomicAdd(&cnt[bk[j]], 1);
-    }
-    __syncthreads();
-    // group g + 1 follows group g in arrival order; the tile's first tuple follows the tuple before the tile
-    if (tid < T / 64) {
-      const int64_t pl = tid > 0 ? (int64_t)g_last[tid - 1] : (i0 > 0 ? a.ts[i0 - 1] : JMIN);
-      bad |= pl > (int64_t)g_first[tid];
-    }
-    if (__ballot(bad) && lane == 0) atomicOr(&a.ctl->flag, KG_UNSORTED);
-    int32_t loc[PER], s = 0;
-#pragma unroll
-    for (int p = 0; p < PER; p++) {
-      const int idx = tid * PER + p;
-      loc[p] = s;
-      s += idx < a.nbk ? cnt[idx] : 0;
-    }
-    int32_t inc = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int32_t u = __shfl_up(inc, o);
-      if (lane >= o) inc += u;
-    }
-    if (lane == 63) wsum[wid] = inc;
-    __syncthreads();
-    int32_t ex = inc - s;
-    for (int w = 0; w < wid; w++) ex += wsum[w];
-#pragma unroll
-    for (int p = 0; p < PER; p++) {
-      const int idx = tid * PER + p;
-      if (idx < a.nbk) tst[idx] = ex + loc[p];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < IT; j++)
-      if (bk[j] < NBS) {
-        const KRec<4> r{x.k[j], (uint32_t)(x.t[j] - f), x.v[j]};
-        r.store_lds(stage, tst[bk[j]] + rk[j]);
-      }
-    __syncthreads();
-    const int nt = (int)min((int64_t)T, a.n - i0);
-    for (int i = tid; i < nt; i += ST) {
-      const KRec<4> r = KRec<4>::load_lds(stage, i);
-      const uint32_t b = bucket_of(r.key(), a.kmask);
-      r.store(a.rec, (int64_t)base[b] + (i - tst[b]));
-    }
-  };
-  int64_t t0 = xcd * per + q;
-  if (t0 >= t_end) return;
-  KTile<IT> A, B;
-  int32_t ba[PER], bb[PER];
-  load(A, ba, t0);
-  for (;;) {
-    const int64_t t1 = t0 + nq;
-    if (t1 < t_end) load(B, bb, t1);
-    process(A, ba, t0);
-    if (t1 >= t_end) break;
-    const int64_t t2 = t1 + nq;
-    if (t2 < t_end) load(A, ba, t2);
-    process(B, bb, t1);
-    if (t2 >= t_end) break;
-    t0 = t2;
-  }
-}
-
-// The same scatter in 72 KB of LDS (two workgroups per CU): one bucket array serves as the rank counters, then
-// (scanned in place) as the tile-local run starts, then as each run's global start minus its tile-local start.
-template <int T, int NBS, int ST>
-__global__ __launch_bounds__(ST) void kg_scatter2_kernel(KgArgs a) {
-  constexpr int IT = T / ST;
-  constexpr int PER = NBS / ST;
-  __shared__ __attribute__((aligned(16))) uint32_t stage[T * 3];
-  __shared__ int32_t cnt[NBS + 1];
-  __shared__ int32_t wsum[ST / 64];
-  if (a.ctl->flag) return;
-  const int64_t tile = tile_of(a.ntiles);
-  if (tile >= a.ntiles) return;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int b = tid; b < a.nbk; b += ST) cnt[b] = 0;
-  __syncthreads();
-  const int64_t f = a.ctl->ts_first;
-  const int64_t i0 = tile * T;
-  KRec<4> rec[IT];
-  int32_t bk[IT], rk[IT];
-  const bool bad = tile_records<4, IT, ST, NBS>(a, i0, tid, f, cnt, rec, bk, rk);
-  if (__ballot(bad) && lane == 0) atomicOr(&a.ctl->flag, KG_UNSORTED);
-  __syncthreads();
-  int32_t loc[PER], sacc = 0;
-#pragma unroll
-  for (int q = 0; q < PER; q++) {
-    const int idx = tid * PER + q;
-    loc[q] = sacc;
-    sacc += idx < a.nbk ? cnt[idx] : 0;
-  }
-  int32_t inc = sacc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t u = __shfl_up(inc, o);
-    if (lane >= o) inc += u;
-  }
-  if (lane == 63) wsum[wid] = inc;
-  __syncthreads();
-  int32_t ex = inc - sacc;
-  for (int w = 0; w < wid; w++) ex += wsum[w];
-#pragma unroll
-  for (int q = 0; q < PER; q++) {
-    const int idx = tid * PER + q;
-    if (idx < a.nbk) cnt[idx] = ex + loc[q];  // tile-local run start
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < IT; j++)
-    if (bk[j] < NBS) rec[j].store_lds(stage, cnt[bk[j]] + rk[j]);
-  __syncthreads();
-  for (int b = tid; b < a.nbk; b += ST) cnt[b] = a.hist[(int64_t)b * a.ntiles + tile] - cnt[b];
-  __syncthreads();
-  const int nt = (int)min((int64_t)T, a.n - i0);
-  for (int i = tid; i < nt; i += ST) {
-    const KRec<4> r = KRec<4>::load_lds(stage, i);
-    r.store(a.rec, (int64_t)cnt[bucket_of(r.key(), a.kmask)] + i);
-  }
-}
-
 // ---------------------------------------------------------------- bucket: per-(key, cell) partials in LDS
 template <int CM, bool MM>
 struct KgLds {
@@ -1033,27 +845,17 @@ hipError_t launch_kg_partition(const KgArgs& a, int vt, hipStream_t st) {
   return hipGetLastError();
 }
 
-// tuples per partition tile: the LDS stage holds one tile (16-byte records: 8192 when the bucket counters fit
-// 2048 entries, else 4096; 24-byte records: 4096; variant 2: 4096)
+// tuples per partition tile: the LDS stage holds one tile (int32 values with <= 2048 buckets: 8192 tuples; else 4096).
+// Variant 0 (A/B baseline, scotty_tune "keyed_grid_variant"): 512-thread scatter workgroups and 12-byte records only.
+// (Measured and removed in round 4: a persistent software-pipelined scatter and a 72-KB two-workgroups-per-CU scatter,
+// both equal or slower, profiles/r03/r03k_c4_variant_ab.log.)
 int kg_tile(int vt, int64_t nbk, int variant) {
-  if (vt == VT_I32 && nbk <= 2048 && variant == 3) return 5632;
-  return vt == VT_I32 && nbk <= 2048 && variant != 2 ? 8192 : 4096;
+  (void)variant;
+  return vt == VT_I32 && nbk <= 2048 ? 8192 : 4096;
 }
 
 hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st) {
   const unsigned grid = (unsigned)(((a.ntiles + 7) / 8) * 8);
-  if (vt == VT_I32 && a.tile == 4096 && a.variant == 2) {
-    hipLaunchKernelGGL((kg::kg_scatter2_kernel<4096, 2048, 1024>), dim3(grid), dim3(1024), 0, st, a);
-    return hipGetLastError();
-  }
-  if (vt == VT_I32 && a.tile == 5632 && a.variant == 3) {  // 74 KB of LDS: two workgroups per CU
-    hipLaunchKernelGGL((kg::kg_scatter2_kernel<5632, 2048, 512>), dim3(grid), dim3(512), 0, st, a);
-    return hipGetLastError();
-  }
-  if (vt == VT_I32 && a.tile == 8192 && a.variant >= 4) {  // persistent: one workgroup per CU (256 CUs)
-    hipLaunchKernelGGL((kg::kg_scatter_pipe_kernel<8192, 2048, 1024>), dim3(256), dim3(1024), 0, st, a);
-    return hipGetLastError();
-  }
   if (vt == VT_I32) {
     if (a.tile == 8192 && a.variant == 1)
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 1024>), dim3(grid), dim3(1024), 0, st, a);
@@ -1084,11 +886,8 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
   }
   if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM
     if (vt == VT_I32) {
-      // 8 records in flight per lane (A/B r03k: 2 -> 8 cut the data pass 1.14 -> 1.02 ms per 2^26 tuples; variant 5:
-      // 4, variant 0: 2)
-      if (B && a.variant == 5) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 4>), grid, block, 0, st, a);
-      else if (B && a.variant == 0) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 2>), grid, block, 0, st, a);
-      else if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 8>), grid, block, 0, st, a);
+      // 8 records in flight per lane (A/B r03k: 2 -> 8 cut the data pass 1.14 -> 1.02 ms per 2^26 tuples)
+      if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 8>), grid, block, 0, st, a);
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, false, XKView>), cgrid, cblock, 0, st, a, n_ops);
     } else {
       if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I64, false, 8>), grid, block, 0, st, a);

@@ -156,6 +156,7 @@ struct scotty_op {
 
   int ingest_mode = -1;  // tuning knob (scotty_tune), -1 = default variant
   int64_t ingest_blocks = 0;  // tuning knob: target workgroups of the ingest launch (0: one round of resident ones)
+  int64_t last_ingest_blocks = 0, last_ingest_streaming = 0;  // the last ingest launch (statistics)
 
   // ---- engine selection: the grid path (context-free time windows, non-keyed) or the exact engine
   //      (keyed ops, session windows, count windows); decided at the first push
@@ -549,9 +550,17 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   // tile: power of two >= TILE_MIN with at most NT_MAX tiles (the commit kernel keeps them in LDS)
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
-  // ~4 workgroups per CU on 256 CUs; each wave streams a tile-aligned contiguous range
-  // one round of resident workgroups (a tune value overrides)
-  const int64_t target_blocks = op->ingest_blocks > 0 ? op->ingest_blocks : 256 * ingest_wgs_per_cu(op->vt, op->need);
+  // one round of resident workgroups, each wave streaming a tile-aligned contiguous range (a tune value overrides).
+  // A stream whose last committed push was in order (< 1 % of its tuples outside their wave's current cell) takes the
+  // streaming variant: the software-pipelined loop on fewer, longer waves (fewer concurrent DRAM streams: C2 ingest
+  // 279 -> 264 us per 2^27 tuples, profiles/r04/r04f); out-of-order streams keep more waves to hide their slow paths
+  // (C2s: 314 us with 1024 workgroups, 321 us with 512)
+  const DevMeta& hs = *op->h_snap;
+  const bool streaming = op->ingest_mode < 0 && op->ingest_blocks <= 0 && op->vt == VT_I32 &&
+                         !(op->need & (NEED_MIN | NEED_MAX)) && hs.n_last > 0 && hs.slow_last * 100 < hs.n_last;
+  const int64_t target_blocks = op->ingest_blocks > 0 ? op->ingest_blocks
+                                : streaming          ? 256 * INGEST_STREAMING_WGS_PER_CU
+                                                     : 256 * ingest_wgs_per_cu(op->vt, op->need);
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
   per_wave = ((per_wave + tile - 1) / tile) * tile;
   if (per_wave < tile) per_wave = tile;
@@ -569,7 +578,9 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
     }
     HIPCHK(hipEventRecord(ev.first, op->stream));
   }
-  HIPCHK(launch_ingest(ia, op->vt, op->need, nblocks, op->stream, op->ingest_mode));
+  HIPCHK(launch_ingest(ia, op->vt, op->need, nblocks, op->stream, streaming ? INGEST_STREAMING : op->ingest_mode));
+  op->last_ingest_blocks = nblocks;
+  op->last_ingest_streaming = streaming ? 1 : 0;
   if (op->timing) {
     HIPCHK(hipEventRecord(ev.second, op->stream));
     op->ev_pending.push_back(ev);
@@ -1463,7 +1474,8 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     op->ingest_blocks = value;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "ingest_mode") == 0) {
+  if (std::strcmp(key, "ingest_mode") == 0) {  // int32 SUM / COUNT ingest loop (A/B only): 6 plain, 7 pipelined
+    if (value != -1 && value != 6 && value != 7) return SCOTTY_ERR_ARG;
     op->ingest_mode = (int)value;
     return SCOTTY_OK;
   }
@@ -1510,8 +1522,8 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->c) op->c->shard_async = op->shard_async;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only)
-    if (op->mode != 0 || value < 0 || value > 6) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only: 0 baseline, 1 default)
+    if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;
     op->x_kg_variant = (int32_t)value;
     if (op->x) op->x->kg_variant = op->x_kg_variant;
     return SCOTTY_OK;
@@ -1557,6 +1569,9 @@ int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
   if (which == 6) return m.tail - m.head;
   if (which == 7) return m.gcount - m.j0;
   if (which == 8) return m.prev_max;
+  if (which == 9) return op->last_ingest_blocks;
+  if (which == 10) return op->last_ingest_streaming;
+  if (which == 11) return (int64_t)op->h_snap->slow_last;
   return -1;
 }
 

@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   Acc<VT, NEED> acc;
   acc.reset();
   int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
-  uint32_t n_late = 0, n_ovf = 0, n_glb = 0;
+  uint32_t n_late = 0, n_ovf = 0, n_glb = 0, n_slow = 0;
   int64_t tile_max = INT64_MIN;
   int64_t cmin = INT64_MAX;  // lowest cell this wave added to outside the LDS window (commit folds from there)
   int qn = 0;                // deferred queue fill (wave-uniform)
@@ -548,51 +548,12 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     }
   };
 
-  // fold the deferred queue: 64 entries per pass, every lane one lookup + one set of LDS atomics.  MODE bit 3: the
-  // counts of lanes that hit the same cell are added by one atomic per cell (up to 8 cells per pass, the rest per lane):
-  // out-of-order tuples behind a stream of wide cells fall on a few cells, where per-lane same-address atomics
-  // serialise
-  constexpr bool GROUP = (MODE & 8) != 0;
+  // fold the deferred queue: 64 entries per pass, every lane one lookup + one set of LDS atomics (round 3 measured and
+  // removed a variant that added the counts of lanes hitting the same cell with one atomic: C3 0.315 -> 0.464 ms)
   auto drain = [&]() {
     for (int b = 0; b < qn; b += 64) {
       const int e = b + lane;
-      const bool valid = e < qn;
-      if constexpr (GROUP) {
-        int64_t t = 0, l = -1;
-        V v{};
-        if (valid) {
-          t = tw0 + (int64_t)q_t[e];
-          v = q_v[e];
-          l = wfind(t);
-        }
-        unsigned long long pending = __ballot(valid);
-        bool counted = false;
-        for (int it = 0; it < 8 && pending; it++) {
-          const int lead = __ffsll((long long)pending) - 1;
-          const int64_t lc = rl64(l, lead);
-          const unsigned long long same = __ballot(valid && l == lc) & pending;
-          if (lane == lead) atomicAdd(&w.cnt[lc], (uint32_t)__popcll(same));
-          counted |= ((same >> lane) & 1) != 0;
-          pending &= ~same;
-        }
-        if (valid) {
-          Acc<VT, NEED> one;
-          one.reset();
-          one.add(t, v);
-          if (!counted) atomicAdd(&w.cnt[l], 1u);
-          const uint32_t to = (uint32_t)(t - w.tbase);
-          if (to > w.tmax[l]) atomicMax(&w.tmax[l], to);
-          if constexpr ((NEED & NEED_SUM) != 0) {
-            if constexpr (VT == VT_F64) atomicAdd((double*)&w.sum[l], one.sum_f());
-            else if constexpr (VT == VT_I32) atomicAdd(&w.sum[l], (uint32_t)one.sum_word());
-            else atomicAdd(&w.sum[l], (unsigned long long)one.sum_word());
-          }
-          if constexpr ((NEED & NEED_MIN) != 0)
-            if (one.mn < (int64_t)w.mn[l]) atomicMin(&w.mn[l], (MMT)one.mn);
-          if constexpr ((NEED & NEED_MAX) != 0)
-            if (one.mx > (int64_t)w.mx[l]) atomicMax(&w.mx[l], (MMT)one.mx);
-        }
-      } else if (valid) {
+      if (e < qn) {
         const int64_t t = tw0 + (int64_t)q_t[e];
         lds_one(wfind(t), t, q_v[e]);
       }
@@ -666,8 +627,10 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
       else sm |= 1u << j;
     }
+    n_slow += __popc(sm);
     if constexpr (DEFER) {
-      if (qok) {
+      // (wave-uniform test first: in an in-order stretch no lane has a slow tuple, and the four ballots below are skipped)
+      if (qok && __ballot(sm != 0) != 0) {
         if (qn > DEFER_CAP - 256) drain();
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -762,9 +725,10 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   }
   flush();
   {
-    uint32_t nl = wsum32(n_late), no = wsum32(n_ovf), ng = wsum32(n_glb);
+    uint32_t nl = wsum32(n_late), no = wsum32(n_ovf), ng = wsum32(n_glb), ns = wsum32(n_slow);
     const int64_t cm = wmin64(cmin);
     if (lane == 0 && ng) atomicAdd((unsigned long long*)&a.meta->glb_slow, (unsigned long long)ng);
+    if (lane == 0 && ns) atomicAdd((unsigned long long*)&a.meta->slow_push, (unsigned long long)ns);
     if (lane == 0 && cm != INT64_MAX) atomicMin((long long*)&a.meta->cmin, (long long)cm);
     if (lane == 0 && (nl | no)) {
       if (nl) atomicAdd((unsigned long long*)&a.meta->late_push, (unsigned long long)nl);
@@ -1091,6 +1055,9 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     }
     mw.late_push = 0;
     mw.overflow_push = 0;
+    mw.slow_last = mw.slow_push;
+    mw.n_last = (uint64_t)a.n;
+    mw.slow_push = 0;
     mw.cmin = INT64_MAX;
   }
 }
@@ -1416,11 +1383,14 @@ constexpr int DEFAULT_MODE = 6;
 // larger LDS window leaves 3 workgroups per CU instead of 4, and two steps in flight per wave make up the bytes in
 // flight; SUM / COUNT configurations measured equal with it (r02c) and keep the plain loop
 constexpr int MM_MODE = 7;
+// int32 COUNT / SUM: the software-pipelined loop as well (r04h, same box, C2s: 346 -> 332 us; C2 in order, see
+// INGEST_STREAMING); int64 / double values keep the plain loop (not measured with it)
 template <int VT>
 static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
+  constexpr int SUM_MODE = VT == VT_I32 ? MM_MODE : DEFAULT_MODE;
   switch (need) {
-    case 0: return launch_ingest_t<VT, 0, DEFAULT_MODE>(a, nblocks, st);
-    case 1: return launch_ingest_t<VT, 1, DEFAULT_MODE>(a, nblocks, st);
+    case 0: return launch_ingest_t<VT, 0, SUM_MODE>(a, nblocks, st);
+    case 1: return launch_ingest_t<VT, 1, SUM_MODE>(a, nblocks, st);
     case 2: return launch_ingest_t<VT, 2, MM_MODE>(a, nblocks, st);
     case 3: return launch_ingest_t<VT, 3, MM_MODE>(a, nblocks, st);
     case 4: return launch_ingest_t<VT, 4, MM_MODE>(a, nblocks, st);
@@ -1462,31 +1432,15 @@ hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// mode: -1 the default; INGEST_STREAMING (an in-order stream); 6 / 7 the int32 COUNT / SUM loop (A/B, scotty_tune
+// "ingest_mode": plain / software-pipelined)
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode) {
-  static const int env_mode = [] {  // A/B of ingest variants on any int32 SUM or MIN|MAX configuration
-    const char* e = getenv("SCOTTY_INGEST_MODE");
-    return e ? atoi(e) : -1;
-  }();
-  if (mode < 0 && env_mode >= 0 && vt == VT_I32 && need == (NEED_MIN | NEED_MAX)) {
-    switch (env_mode) {
-      case 2: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 2>(a, nblocks, st);
-      case 14: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 14>(a, nblocks, st);
-      case 7: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 7>(a, nblocks, st);
-      case 6: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, 6>(a, nblocks, st);
-      default: return launch_ingest_t<VT_I32, NEED_MIN | NEED_MAX, MM_MODE>(a, nblocks, st);
-    }
-  }
-  if (mode < 0 && env_mode >= 0 && vt == VT_I32 && need == NEED_SUM) mode = env_mode;
-  if (mode >= 0 && vt == VT_I32 && need == NEED_SUM) {
-    switch (mode) {
-      case 0: return launch_ingest_t<VT_I32, NEED_SUM, 0>(a, nblocks, st);
-      case 1: return launch_ingest_t<VT_I32, NEED_SUM, 1>(a, nblocks, st);
-      case 2: return launch_ingest_t<VT_I32, NEED_SUM, 2>(a, nblocks, st);
-      case 3: return launch_ingest_t<VT_I32, NEED_SUM, 3>(a, nblocks, st);
-      case 7: return launch_ingest_t<VT_I32, NEED_SUM, 7>(a, nblocks, st);
-      case 14: return launch_ingest_t<VT_I32, NEED_SUM, 14>(a, nblocks, st);
-      default: return launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st);
-    }
+  const int nd = need & (NEED_SUM | NEED_MIN | NEED_MAX);
+  if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 6 || mode == 7 || mode == INGEST_STREAMING)) {
+    if (mode == 6) return nd ? launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st)
+                             : launch_ingest_t<VT_I32, 0, 6>(a, nblocks, st);
+    // in order (INGEST_STREAMING) or 7: the software-pipelined loop, two steps of loads in flight
+    return nd ? launch_ingest_t<VT_I32, NEED_SUM, 7>(a, nblocks, st) : launch_ingest_t<VT_I32, 0, 7>(a, nblocks, st);
   }
   if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);
   if (vt == VT_I64) return launch_ingest_vt<VT_I64>(a, need, nblocks, st);
