@@ -673,6 +673,16 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
             dist.barrier()
     roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
                            "keyed data pass: kg_hist + scan + kg_scatter + kg_bucket (class ingest)")
+    roof["traffic"] = None  # HBM bytes of the data pass per step, from separate --pmc passes (tools/keyed_traffic.py)
+    tfile = os.path.join(ROOT, "profiles", "keyed_traffic.json")
+    if os.path.exists(tfile) and world == 1 and aggs is None:
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("batch") == batch and tj.get("keys") == keys:
+                roof["traffic"] = tj.get("hbm_bytes_per_step")
+                roof["traffic_over_algorithmic"] = tj.get("traffic_over_algorithmic")
+        except Exception:
+            pass
     elapsed = sum(times)
     if dist is not None:
         t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
