@@ -384,6 +384,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
             "ms_per_step_each": [round(1e3 * t, 4) for t in times],
             "quiet_steps": sum(1 for x in verdicts if x == 1), "event_exact_steps": sum(1 for x in verdicts if x != 1),
             "event_prefix_then_quiet_steps": op._debug_stat(12),
+            "start_band_moves": op._debug_stat(100), "jump_pieces": op._debug_stat(101),
             "events_rounds_each": rounds,
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
             "roofline": roof,

@@ -222,7 +222,10 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
  * of the count-window exchange), "shard_async" 1 (shard pushes return without a host synchronisation: the caller
  * orders its collective's stream with scotty_stream_order -- same HIP runtime only, see there), "exact_prefix" n
  * (exact engine, non-keyed: the first event-exact piece of a batch the one-pass quiet path refused, in tuples;
- * 0 = max(batch / 32, 2^20); later pieces grow 4x; the split is invisible in the results). */
+ * 0 = max(batch / 32, 2^20); later pieces grow 4x; the split is invisible in the results), "quiet_band" 1 (exact
+ * engine, non-keyed, one session window: one-pass batches may move the last session's start down -- the stream
+ * resuming after a silence then costs one pass instead of event-exact rounds; the results are the same; off by
+ * default). */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */

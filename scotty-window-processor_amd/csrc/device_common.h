@@ -63,8 +63,10 @@ struct IngestArgs {
   unsigned long long* c_cnt;
   long long* c_tmax;
   unsigned long long* c_part[NPART];
-  // tile maxima
+  // tile maxima; tile minima (nullable: only the exact engine's quiet path asks for them -- launch_ingest then runs
+  // the MODE bit-3 instantiation)
   long long* tilemax;
+  long long* tilemin;
   DevMeta* meta;
   int64_t per_wave;          // tuples per wave (multiple of tile)
   int64_t tile;              // tuples per tile (power of two >= TILE_MIN, nT <= NT_MAX)

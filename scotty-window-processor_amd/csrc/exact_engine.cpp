@@ -127,7 +127,7 @@ void XEngine::release() {
   dfree(xb_mcarry); dfree(xb_nscnt); dfree(xb_nstot); dfree(xb_nsstart); dfree(xb_nspb); dfree(xb_evcnt);
   dfree(xb_seghas); dfree(xb_bits); dfree(xb_evpos); dfree(xb_evt); dfree(xb_evv); dfree(xb_eppos);
   dfree(xb_evm); dfree(xb_eptail); dfree(xb_sufmin);
-  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_pmax); dfree(d_xq_rank); dfree(d_xq_flag);
+  dfree(d_xq_grid); dfree(d_xq_ccnt); dfree(d_xq_ctmax); dfree(d_xq_tilemax); dfree(d_xq_tilemin); dfree(d_xq_pmax); dfree(d_xq_rank); dfree(d_xq_flag);
   for (int k = 0; k < NPART; k++) dfree(d_xq_cpart[k]);
   dfree(d_xq_eg); dfree(d_xq_epos); dfree(d_xq_meta); dfree(d_xq_cix); dfree(d_xq_cixmeta); dfree(d_xq_ctl);
   dfree(d_dbg);
@@ -562,6 +562,7 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
   // within the first tuples (out-of-order tuples reach at most maxDelay below it), then the batch is quiet again
   int64_t chunk_jump = (int64_t)1 << 18;
   bool try_quiet = quiet_eligible();
+  int jump_pieces = 0;
   if (try_quiet && xq_skip > 0) {  // backed off after consecutive refusals the batch itself caused (see below)
     xq_skip--;
     quiet_skipped++;
@@ -597,6 +598,20 @@ int XEngine::push_batch(const int64_t* d_ts, const void* d_val, int64_t n) {
         }
       } else if (pos0 == 0) {
         xq_refused_run = 0;
+      }
+      // a session-gap jump among the piece's first 64 tuples (the prep's refusal located it), with the start band: the
+      // event-exact path takes the tuples up to and including the jump (an even count, so the next piece starts
+      // 16-byte aligned) and the quiet path is tried on the rest -- the resumed stream's new session then settles
+      // inside the band in one pass (C3's pause step; exact_quiet.h).  At most two such pieces per batch: a stream
+      // that jumps every few tuples goes on with the growing event-exact prefix below
+      if (res == XQ_NOT_QUIET && last_quiet_why == 4 && last_quiet_jump_pos >= 0 && band_usable() && jump_pieces < 2) {
+        const int64_t w = std::min(rest, (last_quiet_jump_pos + 2) & ~(int64_t)1);
+        rc = push_exact(d_ts + pos0, val0, w);
+        if (rc) return rc;
+        quiet_jump_pieces++;
+        jump_pieces++;
+        pos0 += w;
+        continue;
       }
       // the verdict failed only on session-gap jumps and located the first one: everything before its arrival tile
       // is quiet (the verdict's other conditions held for the whole rest) -- commit that prefix in one pass, then the
@@ -811,8 +826,10 @@ int XEngine::xq_ensure(int64_t n) {
   if (nt > xq_tcap) {
     XCHK(hipStreamSynchronize(stream));
     dfree(d_xq_tilemax);
+    dfree(d_xq_tilemin);
     xq_tcap = std::max<int64_t>(nt, 1024);
     XCHK(dalloc(&d_xq_tilemax, xq_tcap));
+    XCHK(dalloc(&d_xq_tilemin, xq_tcap));
   }
   return SCOTTY_OK;
 }
@@ -823,6 +840,7 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   *result = XQ_NONE;
   last_quiet_why = 0;
   last_quiet_jump = 0;
+  last_quiet_jump_pos = -1;
   if (xq_need_grid) {
     int rc = xq_rebuild_grid();
     if (rc) return rc;
@@ -849,6 +867,8 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   ia.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) ia.c_part[k] = d_xq_cpart[k];
   ia.tilemax = d_xq_tilemax;
+  const bool band = band_usable();
+  ia.tilemin = band ? d_xq_tilemin : nullptr;  // the ingest's per-tile minima (the band's new session start)
   ia.meta = d_xq_meta;
   ia.per_wave = per_wave;
   ia.tile = tile;
@@ -870,6 +890,8 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   q.c_tmax = d_xq_ctmax;
   for (int k = 0; k < NPART; k++) q.c_part[k] = d_xq_cpart[k];
   q.tilemax = d_xq_tilemax;
+  q.tilemin = d_xq_tilemin;
+  q.band = band ? 1 : 0;
   q.pmax = d_xq_pmax;
   q.rank = d_xq_rank;
   q.flag = d_xq_flag;
@@ -903,9 +925,20 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   }
   XQCtl c;
   std::memcpy(&c, h_misc, sizeof(XQCtl));
+  if (getenv("SCOTTY_XQ_DEBUG")) {  // debugging aid: the verdict's inputs
+    DevMeta m;
+    XCHK(hipMemcpy(&m, d_xq_meta, sizeof(DevMeta), hipMemcpyDeviceToHost));
+    fprintf(stderr, "xq n=%lld res=%d why=%lld lo=%lld band_si=%lld band_s=%lld bmin=%lld bmax=%lld head=%lld tail=%lld "
+            "cmin=%lld late=%llu ovf=%llu ncand=%lld\n", (long long)n, c.result, (long long)c.why, (long long)c.lo_bound,
+            (long long)c.band_si, (long long)c.band_s, (long long)c.batch_min, (long long)c.batch_max,
+            (long long)m.head, (long long)m.tail, (long long)m.cmin, (unsigned long long)m.late_push,
+            (unsigned long long)m.overflow_push, (long long)c.ncand);
+  }
   *result = c.result;
   last_quiet_why = c.why;
   last_quiet_jump = c.result == XQ_NOT_QUIET && c.jump_tile > 0 && c.jump_tile < (n + tile - 1) / tile ? c.jump_tile * tile : 0;
+  last_quiet_jump_pos = c.result == XQ_NOT_QUIET ? c.jump_pos : -1;
+  if (c.result == XQ_COMMITTED && c.band_si != -1 && c.batch_min < c.band_s) quiet_band_moves++;
   if (c.result == XQ_COMMITTED && c.batch_max > c.p_start) xq_span = std::max<int64_t>(c.batch_max - c.p_start, 1);
   if (c.result == XQ_GRID || (c.result == XQ_COMMITTED && c.rebuild)) xq_need_grid = true;
   if (timing) collect_timing();
@@ -1123,7 +1156,7 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
   a.tile = tile;
   a.variant = kg_variant;
   static const bool no_compact = getenv("SCOTTY_KG_NO_COMPACT") != nullptr;  // A/B of the 8-byte records
-  a.allow_compact = vt == VT_I32 && kg_variant == 1 && tile == 8192 && !no_compact ? 1 : 0;  // default kernels only
+  a.allow_compact = vt == VT_I32 && kg_variant >= 1 && tile == 8192 && !no_compact ? 1 : 0;  // default kernels only
   a.part = d_kgpart;
   a.dflag = d_kgdflag;
   a.hist = d_kghist;

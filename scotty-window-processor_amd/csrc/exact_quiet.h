@@ -15,7 +15,23 @@
 // the pending edge), and a one-workgroup commit verifies the quiet conditions from the ingest's per-tile maxima and
 // counters (the per-tile and per-edge scans of the batch spread over many workgroups, exact_quiet.hip) and either
 // commits (edges, slices, state, sessions) or returns every cell to identity so the host runs
-// the event-exact batch path (exact_batch.hip) on the same batch.  No state is written before the verdict.
+// the event-exact batch path (exact_batch.hip) on the same batch.  No state is written before the verdict, except the
+// start band's provisional slice start below, which the commit kernel restores on every refusal.
+//
+// Start band (one session context, Eager slices): out-of-order tuples t with max(s - gap, reach) < t < s, where s is
+// the last session's start and reach the latest end + gap of the sessions before it, move that start down one record
+// low at a time in the reference: SessionWindow.java:56-66 shiftStart (getSession :86 returns the last session for them;
+// no merge, since t > reach), and SliceManager.checkSliceEdges (S/SliceManager.java:89-125) moves the edge between the
+// slice si ending at s (findSliceByEnd, searched from the end) and si + 1 to t when si is movable (Flexible(1)).  Every
+// such tuple then lands in si + 1 (the last slice with tStart <= t), and every other tuple where it would have without
+// the band (the moved edge only crosses tuples of the band).  So a batch whose out-of-order tuples reach into the
+// band is still one pass: the prep kernel lets the cell view start at si + 1 with the band's lower end as its start
+// (written provisionally into the slice store, restored or finalised by the commit), the ingest records per-tile
+// minima, and the commit moves the edge and the session start to the batch minimum (and sets the store's order bits as
+// checkSliceEdges' note_order would).  When no slice ends anywhere in [band lower end, s] (the session opened without
+// a flexible edge), every shift's findSliceByEnd misses and is skipped: the band's tuples then land where the plain
+// quiet view puts them and only the session start moves.  C3's pause step: the stream resumes with a new session
+// whose start settles over the next ~500 ms of tuples -- rounds of the event-exact path before, one quiet pass now.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,6 +64,11 @@ struct XQCtl {
   int64_t why;          // XQ_NOT_QUIET: 1 late / past the horizon, 2 below lo_bound, 4 tile start jump, 8 item jump, 16 range
   int64_t ncand;        // grid points <= batch_max (scan kernel -> edge and commit kernels)
   int64_t jump_tile;    // XQ_NOT_QUIET: first arrival tile holding a session-gap jump (JMAX: none located)
+  int64_t jump_pos;     // the prep's refusal: arrival index (< 64) of the first session-gap jump, else -1
+  int64_t band_si;      // start band (see below): the slice ending at the last session's start; -2: no slice ends in
+                        // the band (only the start moves); -1: no band
+  int64_t band_s;       // start band: the last session's start at batch start (slice band_si + 1 starts there)
+  int64_t batch_min;    // start band: the batch's lowest timestamp (scan kernel)
 };
 
 struct XQArgs {
@@ -65,6 +86,7 @@ struct XQArgs {
   long long* c_tmax;
   unsigned long long* c_part[NPART];
   long long* tilemax;
+  long long* tilemin;    // per-tile minima (the ingest's MODE bit 3)
   long long* pmax;       // scratch [NT_MAX]: prefix maxima of the tile maxima (arrival order)
   int32_t* rank;         // scratch [gcap]
   int32_t* flag;         // scratch [gcap]
@@ -73,6 +95,7 @@ struct XQArgs {
   XQCtl* ctl;
   int64_t margin;        // grid horizon margin (ms past the stream front) below which a rebuild is requested
   long long* dbg;        // nullable: clock stamps of the commit's phases (SCOTTY_XQ_PROF, a debugging aid)
+  int32_t band;          // the start band may be used (one session context, Eager slices, tilemin set)
 };
 
 hipError_t launch_xq_prep(const XQArgs& a, hipStream_t st);

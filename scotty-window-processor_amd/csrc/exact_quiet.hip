@@ -79,6 +79,7 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
   }
   int64_t lo_bound = JMIN, min_gap = JMAX;
   int64_t h0 = s.head;  // first slice of the cell view
+  int64_t reach0 = JMIN, s_last0 = JMIN;  // context 0: reach of the earlier sessions, last session's start
   if (res == XQ_NONE) {
     for (int k = 0; k < c->n_ctx && res == XQ_NONE; k++) {
       const int64_t gap = c->gap[k];
@@ -103,9 +104,57 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
       reach = wmax(reach);
       lo_bound = max(lo_bound, st_[ns - 1]);
       if (reach != JMIN) lo_bound = max(lo_bound, reach + 1);
+      if (k == 0) {
+        reach0 = reach;
+        s_last0 = st_[ns - 1];
+      }
     }
   }
-  if (res == XQ_NONE) {
+  constexpr int64_t SCAN_CAP = 16384;
+  constexpr int64_t BAND_NO_EDGE = -2;  // XQCtl.band_si: the start band without a slice edge to move
+  // start band (exact_quiet.h): one session context; si = findSliceByEnd(s) (the last slice ending at the last
+  // session's start, S/SliceManager.java:94) movable and Eager, si + 1 starting at s, the slices from si + 1 on in
+  // tStart order (they become the cell view)
+  int64_t band_si = -1, band_lo = JMIN;
+  if (res == XQ_NONE && a.band && c->n_ctx == 1) {
+    const int64_t S = s_last0, gap = c->gap[0];
+    band_lo = S - gap + 1;  // SessionWindow.java:57: start - gap < t (no wrap: |S|, gap <= SAFE)
+    if (reach0 != JMIN) band_lo = max(band_lo, reach0 + 1);
+    int64_t si = -1;
+    for (int64_t b = (int64_t)s.tail - 1; b >= s.head && b > (int64_t)s.tail - 1 - SCAN_CAP && si < 0; b -= 64) {
+      const int64_t i = b - lane;
+      const unsigned long long hit = __ballot(i >= s.head && a.sl.te[i] == S);
+      if (hit) si = b - (__ffsll((long long)hit) - 1);
+    }
+    const bool lo_ok = band_lo < S && band_lo >= -SAFE;
+    bool ok = si >= 0 && si + 1 < s.tail && lo_ok && ty_movable(a.sl.ty[si]) && !ty_lazy(a.sl.ty[si]) &&
+              a.sl.ts[si + 1] == S && (int64_t)s.tail - si <= SCAN_CAP;
+    for (int64_t i = si + 1 + lane; ok && i + 1 < s.tail; i += 64)
+      if (a.sl.ts[i] > a.sl.ts[i + 1]) ok = false;
+    ok = __ballot(!ok) == 0;
+    if (ok) {
+      band_si = si;
+    } else if (si < 0 && lo_ok && (int64_t)s.tail - s.head <= SCAN_CAP) {
+      // no slice ends at s (StreamSlicer opened the session without a flexible edge: calculateNextFlexEdge compares
+      // with the pending fixed edge, S/StreamSlicer.java:118-130): every shiftStart's findSliceByEnd misses and the
+      // modification is skipped (S/SliceManager.java:94-96) -- as long as no slice ends anywhere in [band_lo, s], the
+      // band's tuples only move the session start, and land where the plain quiet view puts them
+      bool none = true;
+      for (int64_t i = s.head + lane; i < s.tail; i += 64) {
+        const int64_t e = a.sl.te[i];
+        if (e >= band_lo && e <= S) none = false;
+      }
+      if (__ballot(!none) == 0) band_si = BAND_NO_EDGE;
+    }
+  }
+  if (res == XQ_NONE && band_si == BAND_NO_EDGE) lo_bound = band_lo;  // then the plain view below
+  if (res == XQ_NONE && band_si >= 0) {
+    // the view starts at si + 1 with the band's lower end as its start: every tuple >= band_lo lands where the
+    // reference puts it (exact_quiet.h), anything below is refused by the ingest (late) -- which also covers the sorted
+    // list's oldest-slice bound
+    h0 = band_si + 1;
+    lo_bound = band_lo;
+  } else if (res == XQ_NONE) {
     if (!(s.unsorted & 1)) {
       // sorted list: the oldest slice bounds every tuple (an older one throws IndexOutOfBounds; the ingest counts it)
       lo_bound = max(lo_bound, a.sl.ts[s.head]);
@@ -113,7 +162,6 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
       // a list whose tStart order was broken by session edits: every tuple of a quiet batch is >= lo_bound, and
       // findSliceIndexByTimestamp (the LAST slice with tStart <= t, LazyAggregateStore.java:29-37) then lands in the
       // suffix that starts at the last slice with tStart <= lo_bound -- if that suffix is sorted, it is the view
-      constexpr int64_t SCAN_CAP = 16384;
       int64_t i0 = -1;
       for (int64_t b = (int64_t)s.tail - 1; b >= s.head && b > (int64_t)s.tail - 1 - SCAN_CAP && i0 < 0; b -= 64) {
         const int64_t i = b - lane;
@@ -136,6 +184,7 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
       why |= 1024;
     }
   }
+  int64_t jump_pos = -1;
   if (res == XQ_NONE && c->n_ctx > 0 && a.n > 0) {
     // fast refusal: one of the first 64 tuples jumps its running max by a session gap (a new session: the stream
     // resumes after a silence) -- the batch is not quiet, and the ingest pass is skipped
@@ -148,12 +197,18 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
     }
     int64_t ex = (int64_t)__shfl_up((long long)inc, 1);
     ex = lane == 0 ? P : max(P, ex);
-    if (__ballot(lane < a.n && v != JMIN && !(ex <= JMAX - min_gap && v < ex + min_gap)) != 0) {
+    const unsigned long long jb = __ballot(lane < a.n && v != JMIN && !(ex <= JMAX - min_gap && v < ex + min_gap));
+    if (jb != 0) {
       res = XQ_NOT_QUIET;
       why |= 4;
+      jump_pos = __ffsll((long long)jb) - 1;
     }
   }
+  if (res != XQ_NONE) band_si = -1;
   if (lane == 0) {
+    // the band's provisional view start (restored or finalised by the commit kernel, which runs whenever res is
+    // XQ_NONE here)
+    if (band_si >= 0) a.sl.ts[band_si + 1] = band_lo;
     DevMeta m{};
     m.head = h0;
     m.tail = s.tail;
@@ -173,6 +228,10 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
     q.h_end = h_end;
     q.why = why;
     q.jump_tile = (why & 4) ? 0 : JMAX;
+    q.jump_pos = jump_pos;
+    q.band_si = band_si;
+    q.band_s = s_last0;
+    q.batch_min = JMAX;
     *a.ctl = q;
   }
 }
@@ -204,6 +263,7 @@ __device__ __forceinline__ int64_t block_incl_max(int64_t v, long long* wtot, in
 //      g[k] <= batch_max, and the verdict parts that need no pass over the batch
 __global__ __launch_bounds__(1024) void xq_scan_kernel(XQArgs a) {
   __shared__ long long s_w[32];
+  __shared__ long long s_mn[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const XQCtl q = *a.ctl;
   if (q.result != XQ_NONE) return;  // refused by the prep kernel: no cell was touched
@@ -217,13 +277,21 @@ __global__ __launch_bounds__(1024) void xq_scan_kernel(XQArgs a) {
   // prefix max over the tile maxima (8 consecutive tiles per thread)
   int64_t loc[8];
   int64_t run = JMIN;
+  int64_t bmin = JMAX;  // start band: the batch minimum (per-tile minima of the ingest)
+  const bool band = q.band_si != -1;  // >= 0: with the movable edge; -2: no edge
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const int64_t t = (int64_t)tid * 8 + j;
     run = max(run, t < nT ? (int64_t)a.tilemax[t] : JMIN);
     loc[j] = run;
+    if (band && t < nT) bmin = min(bmin, (int64_t)a.tilemin[t]);
   }
-  const int64_t incl = block_incl_max(run, s_w, lane, wid);
+  if (band) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bmin = min(bmin, (int64_t)__shfl_xor((long long)bmin, o));
+    if (lane == 0) s_mn[wid] = bmin;
+  }
+  const int64_t incl = block_incl_max(run, s_w, lane, wid);  // (its barriers publish s_mn)
   const int64_t excl_thread = (int64_t)__shfl_up((long long)incl, 1);
   const int64_t carry0 = lane == 0 ? (wid > 0 ? (int64_t)s_w[wid - 1] : JMIN) : excl_thread;
 #pragma unroll
@@ -271,6 +339,11 @@ __global__ __launch_bounds__(1024) void xq_scan_kernel(XQArgs a) {
     o->batch_max = batch_max;
     o->ncand = lo;
     o->why = why;
+    if (band) {
+      int64_t bm = JMAX;
+      for (int w = 0; w < 16; w++) bm = min(bm, (int64_t)s_mn[w]);
+      o->batch_min = bm;
+    }
   }
 }
 
@@ -517,7 +590,10 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
       a.c_part[1][c] = (unsigned long long)ID_MIN;
       a.c_part[2][c] = (unsigned long long)ID_MAX;
     }
-    if (tid == 0) a.ctl->result = result;
+    if (tid == 0) {
+      if (q.band_si >= 0) a.sl.ts[q.band_si + 1] = q.band_s;  // the band's provisional view start, undone
+      a.ctl->result = result;
+    }
     return;
   }
 
@@ -581,11 +657,30 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
     if (cfg->has_fixed) s.nextEdgeTs = g[ncand];
     s.currentCount = jadd(c0, a.n);
     s.tail = (int32_t)(tail + n_emit);
+    int64_t band_to = JMAX;
+    if (q.band_si >= 0) {
+      // start band: the record-low chain of shiftStart modifications in one step (exact_quiet.h) -- the last session
+      // starts at the batch minimum, the movable edge between si and si + 1 follows (S/SliceManager.java:101-105),
+      // and the order bits as SliceManager.note_order would leave them (exact_op.h check_slice_edges)
+      const int64_t si = q.band_si, bm = q.batch_min;
+      if (bm < q.band_s) {
+        sl.ts[si + 1] = bm;
+        sl.te[si] = bm;
+        s.unsorted |= 2;
+        if (sl.ts[si] > bm) s.unsorted |= 1;
+        band_to = bm;
+      } else {
+        sl.ts[si + 1] = q.band_s;
+      }
+    } else if (q.band_si == -2 && q.batch_min < q.band_s) {
+      band_to = q.batch_min;  // no slice edge at the session start: only the start moves
+    }
     *a.st = s;
     for (int k = 0; k < cfg->n_ctx; k++) {
       const int ns = s.ns(k);
       int64_t* en_ = a.ss.end + (int64_t)k * cfg->sesscap;
       en_[ns - 1] = max(en_[ns - 1], batch_max);
+      if (k == 0 && band_to != JMAX) a.ss.start[ns - 1] = band_to;
     }
     XQCtl* o = a.ctl;
     o->n_emit = n_emit;

@@ -168,6 +168,7 @@ struct scotty_op {
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
   bool x_quiet_off = false;  // exact engine: no one-pass quiet path (A/B)
+  bool x_band_on = false;    // exact engine: quiet batches may move the last session's start (start band)
   bool x_lane_off = false;
   bool x_kg_off = false;
   int64_t x_kg_chunk = -1;
@@ -942,6 +943,7 @@ static int decide_mode(scotty_op* op) {
   op->x->sess_override = op->x_sess;
   op->x->serial = op->x_serial;
   op->x->quiet_off = op->x_quiet_off;
+  op->x->band_on = op->x_band_on;
   op->x->lane_off = op->x_lane_off;
   op->x->kg_off = op->x_kg_off;
   if (op->x_kg_chunk >= 0) op->x->kg_min_chunk = op->x_kg_chunk;
@@ -1494,6 +1496,11 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->x) op->x->quiet_off = op->x_quiet_off;
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "quiet_band") == 0) {  // 1: quiet batches may move the session start (exact_quiet.h)
+    op->x_band_on = value != 0;
+    if (op->x) op->x->band_on = op->x_band_on;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "exact_prefix") == 0) {  // first event-exact piece of a refused quiet batch (tuples, >= 4096)
     if (value != 0 && (value < 4096 || value > ((int64_t)1 << 40))) return SCOTTY_ERR_ARG;
     op->x_prefix = value;
@@ -1522,8 +1529,8 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->c) op->c->shard_async = op->shard_async;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only: 0 baseline, 1 default)
-    if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only: 0 baseline, 1 default, 2 overlapped scatter loads)
+    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;
     op->x_kg_variant = (int32_t)value;
     if (op->x) op->x->kg_variant = op->x_kg_variant;
     return SCOTTY_OK;
@@ -1598,6 +1605,8 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 13: return op->x->quiet_split_commits;  // quiet prefixes committed up to a located session-gap jump
     case 14: return op->x->quiet_skipped;        // batches sent to the event-exact path by the quiet back-off
     case 15: return (int64_t)op->x->xq_trace.size();  // quiet attempts of the last batch; 16 + k: attempt k's trace
+    case 100: return op->x->quiet_band_moves;   // committed quiet batches that moved a session start (start band)
+    case 101: return op->x->quiet_jump_pieces;  // event-exact pieces cut right behind a located session-gap jump
     default:
       if (which >= 16 && which - 16 < (int)op->x->xq_trace.size()) return op->x->xq_trace[which - 16];
       return -1;

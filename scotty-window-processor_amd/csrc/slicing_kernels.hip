@@ -330,10 +330,13 @@ __host__ __device__ constexpr size_t ingest_lds_bytes() {
 //            (out-of-order tuples) are appended to a per-wave LDS queue (ballot + mbcnt, no dependent loads) and
 //            folded 64 at a time with every lane busy, instead of a per-lane loop of dependent lookups whose
 //            iterations run with a fraction of the lanes active
+// MODE bit3: per-tile minima as well (a.tilemin; the exact engine's quiet path: the lowest tuple of a batch is the
+//            new start of a session whose start the batch moves down, exact_quiet.h)
 template <int VT, int NEED, int MODE>
 __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   using V = typename ValT<VT>::T;
   constexpr bool DEFER = (MODE & 4) != 0;
+  constexpr bool TMIN = (MODE & 8) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int64_t* sc = (int64_t*)smem;  // block scalars [ING_SC]
   LdsWin<VT> w;
@@ -484,6 +487,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   int64_t cstar = -1, lo = 1, hi = 0;  // wave-uniform current cell [lo, hi)
   uint32_t n_late = 0, n_ovf = 0, n_glb = 0, n_slow = 0;
   int64_t tile_max = INT64_MIN;
+  int64_t tile_min = INT64_MAX;  // TMIN only
   int64_t cmin = INT64_MAX;  // lowest cell this wave added to outside the LDS window (commit folds from there)
   int qn = 0;                // deferred queue fill (wave-uniform)
 
@@ -624,6 +628,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       tile_max = max(tile_max, t[j]);
+      if constexpr (TMIN) tile_min = min(tile_min, t[j]);
       if (t[j] >= lo && t[j] < hi) acc.add(t[j], v[j]);
       else sm |= 1u << j;
     }
@@ -660,6 +665,11 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       int64_t tm = wmax64(tile_max);
       if (lane == 0) a.tilemax[s / a.tile] = tm;
       tile_max = INT64_MIN;
+      if constexpr (TMIN) {
+        const int64_t tn = wmin64(tile_min);
+        if (lane == 0) a.tilemin[s / a.tile] = tn;
+        tile_min = INT64_MAX;
+      }
     }
   };
   const int64_t w1_full = w0 + ((w1 - w0) / 256) * 256;  // end of the full steps
@@ -717,6 +727,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
         int64_t tj = a.ts[idx[j]];
         V vj = vp[idx[j]];
         tile_max = max(tile_max, tj);
+        if constexpr (TMIN) tile_min = min(tile_min, tj);
         if (tj >= lo && tj < hi) acc.add(tj, vj);
         else slow(tj, vj);
       }
@@ -1385,18 +1396,20 @@ constexpr int DEFAULT_MODE = 6;
 constexpr int MM_MODE = 7;
 // int32 COUNT / SUM: the software-pipelined loop as well (r04h, same box, C2s: 346 -> 332 us; C2 in order, see
 // INGEST_STREAMING); int64 / double values keep the plain loop (not measured with it)
-template <int VT>
+// TM: 8 (per-tile minima, a.tilemin) or 0
+template <int VT, int TM>
 static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
-  constexpr int SUM_MODE = VT == VT_I32 ? MM_MODE : DEFAULT_MODE;
+  constexpr int SUM_MODE = (VT == VT_I32 ? MM_MODE : DEFAULT_MODE) | TM;
+  constexpr int MMM = MM_MODE | TM;
   switch (need) {
     case 0: return launch_ingest_t<VT, 0, SUM_MODE>(a, nblocks, st);
     case 1: return launch_ingest_t<VT, 1, SUM_MODE>(a, nblocks, st);
-    case 2: return launch_ingest_t<VT, 2, MM_MODE>(a, nblocks, st);
-    case 3: return launch_ingest_t<VT, 3, MM_MODE>(a, nblocks, st);
-    case 4: return launch_ingest_t<VT, 4, MM_MODE>(a, nblocks, st);
-    case 5: return launch_ingest_t<VT, 5, MM_MODE>(a, nblocks, st);
-    case 6: return launch_ingest_t<VT, 6, MM_MODE>(a, nblocks, st);
-    default: return launch_ingest_t<VT, 7, MM_MODE>(a, nblocks, st);
+    case 2: return launch_ingest_t<VT, 2, MMM>(a, nblocks, st);
+    case 3: return launch_ingest_t<VT, 3, MMM>(a, nblocks, st);
+    case 4: return launch_ingest_t<VT, 4, MMM>(a, nblocks, st);
+    case 5: return launch_ingest_t<VT, 5, MMM>(a, nblocks, st);
+    case 6: return launch_ingest_t<VT, 6, MMM>(a, nblocks, st);
+    default: return launch_ingest_t<VT, 7, MMM>(a, nblocks, st);
   }
 }
 
@@ -1434,17 +1447,23 @@ hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) {
 
 // mode: -1 the default; INGEST_STREAMING (an in-order stream); 6 / 7 the int32 COUNT / SUM loop (A/B, scotty_tune
 // "ingest_mode": plain / software-pipelined)
+// a.tilemin non-null: the default loop with per-tile minima (mode ignored)
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode) {
   const int nd = need & (NEED_SUM | NEED_MIN | NEED_MAX);
+  if (a.tilemin) {
+    if (vt == VT_I32) return launch_ingest_vt<VT_I32, 8>(a, need, nblocks, st);
+    if (vt == VT_I64) return launch_ingest_vt<VT_I64, 8>(a, need, nblocks, st);
+    return launch_ingest_vt<VT_F64, 8>(a, need, nblocks, st);
+  }
   if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 6 || mode == 7 || mode == INGEST_STREAMING)) {
     if (mode == 6) return nd ? launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st)
                              : launch_ingest_t<VT_I32, 0, 6>(a, nblocks, st);
     // in order (INGEST_STREAMING) or 7: the software-pipelined loop, two steps of loads in flight
     return nd ? launch_ingest_t<VT_I32, NEED_SUM, 7>(a, nblocks, st) : launch_ingest_t<VT_I32, 0, 7>(a, nblocks, st);
   }
-  if (vt == VT_I32) return launch_ingest_vt<VT_I32>(a, need, nblocks, st);
-  if (vt == VT_I64) return launch_ingest_vt<VT_I64>(a, need, nblocks, st);
-  return launch_ingest_vt<VT_F64>(a, need, nblocks, st);
+  if (vt == VT_I32) return launch_ingest_vt<VT_I32, 0>(a, need, nblocks, st);
+  if (vt == VT_I64) return launch_ingest_vt<VT_I64, 0>(a, need, nblocks, st);
+  return launch_ingest_vt<VT_F64, 0>(a, need, nblocks, st);
 }
 
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {

@@ -1,0 +1,118 @@
+"""The exact engine's start band (exact_quiet.h): a one-pass ("quiet") batch whose out-of-order tuples move the last
+session's start down -- the chain of SessionWindow shiftStart modifications (SessionWindow.java:56-66) and the movable
+edge they drag (S/SliceManager.java:89-125) applied in one step -- against the oracle, bit-exactly, at every
+watermark, and against the same operator without the band (scotty_tune("quiet_band", 1) turns it on; without it
+such batches take the event-exact path).
+
+Streams resume after silences (a new session opens with the first tuple of a micro-batch, the prep kernel locates the
+jump, the event-exact path takes the tuples up to it and the quiet path the rest) with late tuples of a bounded delay.
+The cases cover the band's refusals as well: delays beyond the session gap (tuples below start - gap open sessions of
+their own: AddModification, refused as below the band), a silence shorter than two gaps (the band's lower end is the
+previous session's reach: tuples at or below it merge the sessions), two session contexts (no band), tumbling instead
+of sliding windows, and MIN/MAX as well as SUM/COUNT partials."""
+import numpy as np
+import pytest
+
+from helpers import product, build_ops, same_windows
+from specs import Tumbling, Sliding, Session, Time, SUM, COUNT, MIN, MAX
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    return product()
+
+
+def _steps(B, nsteps, seed, period=6, silence=2000, max_delay=500, late_frac=0.2, warm=8):
+    """Step s covers 1000 ms of event time starting at t_begin; every `period` steps the stream pauses for `silence`
+    ms.  The first `warm` steps are sparse (1 tuple per ms), the rest carry B tuples, a `late_frac` share of them late
+    by U[1, max_delay] ms.  Watermark: t_begin + 999 - max_delay."""
+    rng = np.random.default_rng(seed)
+    t0 = 1000
+    for s in range(nsteps):
+        t_begin = t0 + s * 1000 + (s // period) * silence
+        if s < warm:
+            ts = t_begin + np.arange(1000, dtype=np.int64)
+        else:
+            ts = t_begin + np.arange(B, dtype=np.int64) * 1000 // B
+            late = rng.random(B) < late_frac
+            d = rng.integers(1, max_delay + 1, size=B)
+            ts = np.where(late, ts - d, ts)
+        vals = rng.integers(-2**31, 2**31, size=len(ts), dtype=np.int64).astype(np.int32)
+        yield s, ts, vals, t_begin + 999 - max_delay
+
+
+def _run(cfg, steps, tunes):
+    import torch
+    dev = torch.device("cuda", 0)
+    ops, ora = [], None
+    for t in tunes:
+        g, o = build_ops(cfg, tune=t)
+        ops.append(g)
+        ora = ora or o
+    total = 0
+    for s, ts, vals, wm in steps:
+        dts = torch.from_numpy(ts).to(dev)
+        dv = torch.from_numpy(vals).to(dev)
+        torch.cuda.synchronize(dev)
+        for op in ops:
+            op.processElementsDevice(dts.data_ptr(), dv.data_ptr(), len(ts))
+        assert ora.processElements(ts, vals) == 0
+        exp = ora.processWatermark(wm)
+        for op in ops:
+            same_windows(op.processWatermark(wm), exp)
+        total += len(exp)
+        tr = [hex(ops[0]._debug_stat(16 + k)) for k in range(ops[0]._debug_stat(15))]
+        print("step %d: quiet attempts %s, band moves %d" % (s, tr, ops[0]._debug_stat(100)), flush=True)
+        del dts, dv
+    return ops, total
+
+
+CASES = {
+    # C3's shape at reduced size: the band moves the new session's start at every resume
+    "sliding_session_minmax": dict(cfg=dict(windows=[Sliding(Time, 60_000, 60), Session(Time, 1000)],
+                                            aggs=[MIN, MAX], lateness=1000), kw=dict(), moves=True),
+    "tumbling_session_sum": dict(cfg=dict(windows=[Tumbling(Time, 5000), Session(Time, 1000)],
+                                          aggs=[SUM, COUNT], lateness=1000), kw=dict(), moves=True),
+    "session_only_sum_minmax": dict(cfg=dict(windows=[Session(Time, 700)], aggs=[SUM, MIN, MAX], lateness=1000),
+                                    kw=dict(max_delay=300, late_frac=0.3), moves=True),
+    # delays beyond the gap: tuples below start - gap open sessions of their own (refused below the band)
+    "delay_beyond_gap": dict(cfg=dict(windows=[Sliding(Time, 10_000, 100), Session(Time, 400)], aggs=[SUM, COUNT],
+                                      lateness=2000), kw=dict(max_delay=900), moves=None),
+    # a silence shorter than two gaps: the previous session's reach bounds the band (tuples below it merge sessions)
+    "short_silence_reach": dict(cfg=dict(windows=[Sliding(Time, 10_000, 100), Session(Time, 1000)],
+                                         aggs=[MIN, MAX], lateness=2000),
+                                kw=dict(silence=1300, max_delay=500), moves=None),
+    # two session contexts: no band (the verdict is the plain quiet path's)
+    "two_sessions": dict(cfg=dict(windows=[Session(Time, 1000), Session(Time, 1200)], aggs=[SUM, COUNT],
+                                  lateness=1000), kw=dict(), moves=False),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_start_band_matches_oracle_and_band_off(pkg, case):
+    c = CASES[case]
+    steps = _steps(1 << 18, 26, seed=sum(map(ord, case)), **c["kw"])
+    (on, off), total = _run(c["cfg"], steps, [{"quiet_band": 1}, None])
+    moves, pieces = on._debug_stat(100), on._debug_stat(101)
+    print("%s: windows %d, band moves %d, jump pieces %d, quiet commits on/off %d/%d" % (
+        case, total, moves, pieces, on._debug_stat(9), off._debug_stat(9)), flush=True)
+    assert total >= 3  # (session-only streams emit one window per silence)
+    assert off._debug_stat(100) == 0 and off._debug_stat(101) == 0
+    if c["moves"] is True:
+        assert moves >= 2 and pieces >= 2
+        assert on._debug_stat(9) > off._debug_stat(9)  # the resumed batches' rests commit in one pass
+    elif c["moves"] is False:
+        assert moves == 0
+
+
+def test_start_band_every_batch_resumes(pkg):
+    """Every micro-batch starts after a silence (period 1): each one opens a session, cuts an event-exact piece
+    behind its first tuple and commits the rest with the band -- the back-off and the piece limit must not change
+    any window."""
+    cfg = dict(windows=[Sliding(Time, 20_000, 250), Session(Time, 1000)], aggs=[SUM, COUNT, MIN, MAX], lateness=1000)
+    (on, off), total = _run(cfg, _steps(1 << 16, 20, seed=5, period=1, silence=1600), [{"quiet_band": 1}, None])
+    print("windows %d, band moves %d, jump pieces %d" % (total, on._debug_stat(100), on._debug_stat(101)))
+    assert total > 10
+    assert on._debug_stat(100) >= 8
