@@ -776,6 +776,7 @@ int scotty_create(scotty_op** out, int device, int value_type, uint32_t flags) {
   op->device = device;
   op->vt = value_type;
   op->keyed = (flags & SCOTTY_FLAG_KEYED) != 0;
+  if (const char* e = getenv("SCOTTY_QUIET_BAND")) op->x_band_on = atoi(e) != 0;  // the start band's default (A/B)
   int rc = alloc_all(op);
   if (rc) {
     scotty_destroy(op);

@@ -94,7 +94,7 @@ CASES = {
 def test_start_band_matches_oracle_and_band_off(pkg, case):
     c = CASES[case]
     steps = _steps(1 << 18, 26, seed=sum(map(ord, case)), **c["kw"])
-    (on, off), total = _run(c["cfg"], steps, [{"quiet_band": 1}, None])
+    (on, off), total = _run(c["cfg"], steps, [{"quiet_band": 1}, {"quiet_band": 0}])
     moves, pieces = on._debug_stat(100), on._debug_stat(101)
     print("%s: windows %d, band moves %d, jump pieces %d, quiet commits on/off %d/%d" % (
         case, total, moves, pieces, on._debug_stat(9), off._debug_stat(9)), flush=True)
@@ -112,7 +112,8 @@ def test_start_band_every_batch_resumes(pkg):
     behind its first tuple and commits the rest with the band -- the back-off and the piece limit must not change
     any window."""
     cfg = dict(windows=[Sliding(Time, 20_000, 250), Session(Time, 1000)], aggs=[SUM, COUNT, MIN, MAX], lateness=1000)
-    (on, off), total = _run(cfg, _steps(1 << 16, 20, seed=5, period=1, silence=1600), [{"quiet_band": 1}, None])
+    steps = _steps(1 << 16, 20, seed=5, period=1, silence=1600)
+    (on, off), total = _run(cfg, steps, [{"quiet_band": 1}, {"quiet_band": 0}])
     print("windows %d, band moves %d, jump pieces %d" % (total, on._debug_stat(100), on._debug_stat(101)))
     assert total > 10
     assert on._debug_stat(100) >= 8
