@@ -49,6 +49,8 @@ struct DevMeta {
   int64_t whead;              // head before the last watermark's GC (window assembly reads [whead, tail))
   uint64_t slow_push;         // tuples of the current push outside their wave's current cell (ingest slow path)
   uint64_t slow_last, n_last; // the last committed push's slow-path tuples and size (the host picks the next launch)
+  int64_t view_s0_on;         // != 0: cell 0 of the ingest's view starts at view_s0 instead of t_start[head] (the exact
+  int64_t view_s0;            //   engine's start band, exact_quiet.h; the slice store itself is not written before a verdict)
 };
 
 struct IngestArgs {

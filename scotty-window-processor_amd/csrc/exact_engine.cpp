@@ -938,7 +938,10 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   last_quiet_why = c.why;
   last_quiet_jump = c.result == XQ_NOT_QUIET && c.jump_tile > 0 && c.jump_tile < (n + tile - 1) / tile ? c.jump_tile * tile : 0;
   last_quiet_jump_pos = c.result == XQ_NOT_QUIET ? c.jump_pos : -1;
-  if (c.result == XQ_COMMITTED && c.band_si != -1 && c.batch_min < c.band_s) quiet_band_moves++;
+  if (c.result == XQ_COMMITTED && c.band_si != -1 && c.batch_min < c.band_s) {
+    quiet_band_moves++;
+    if (c.band_si == -2) quiet_band_noedge++;
+  }
   if (c.result == XQ_COMMITTED && c.batch_max > c.p_start) xq_span = std::max<int64_t>(c.batch_max - c.p_start, 1);
   if (c.result == XQ_GRID || (c.result == XQ_COMMITTED && c.rebuild)) xq_need_grid = true;
   if (timing) collect_timing();

@@ -53,11 +53,12 @@ class XEngine {
   int64_t last_quiet_why = 0;  // XQCtl.why of the last verdict
   int64_t last_quiet_jump = 0;   // first tuple of the arrival tile holding the verdict's first session-gap jump (0: none)
   int64_t quiet_split_commits = 0;  // quiet prefixes committed up to a located jump
-  // start band (exact_quiet.h): quiet batches may move the last session's start down (scotty_tune "quiet_band" 1;
-  // off by default until its round-4 GPU validation has run)
-  bool band_on = false;
+  // start band (exact_quiet.h): quiet batches may move the last session's start down (scotty_tune "quiet_band", on by
+  // default; 0 sends such batches through the event-exact path)
+  bool band_on = true;
   int64_t last_quiet_jump_pos = -1;  // the prep's refusal: arrival index of the first session-gap jump (< 64), else -1
   int64_t quiet_band_moves = 0;      // committed quiet batches that moved a session start (XQCtl.batch_min < band_s)
+  int64_t quiet_band_noedge = 0;     // of those: no slice ended at the session start (band_si -2, only the start moved)
   int64_t quiet_jump_pieces = 0;     // event-exact pieces cut right behind a located jump (then the quiet path again)
   bool band_usable() const { return band_on && cfg.n_ctx == 1 && !cfg.lazy; }
   // first event-exact piece of a refused quiet batch, in tuples (scotty_tune "exact_prefix"; 0: max(n / 32, 2^20))

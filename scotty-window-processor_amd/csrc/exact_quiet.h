@@ -15,8 +15,8 @@
 // the pending edge), and a one-workgroup commit verifies the quiet conditions from the ingest's per-tile maxima and
 // counters (the per-tile and per-edge scans of the batch spread over many workgroups, exact_quiet.hip) and either
 // commits (edges, slices, state, sessions) or returns every cell to identity so the host runs
-// the event-exact batch path (exact_batch.hip) on the same batch.  No state is written before the verdict, except the
-// start band's provisional slice start below, which the commit kernel restores on every refusal.
+// the event-exact batch path (exact_batch.hip) on the same batch.  No state is written before the verdict (the start
+// band's lowered view start travels in DevMeta.view_s0, not in the slice store).
 //
 // Start band (one session context, Eager slices): out-of-order tuples t with max(s - gap, reach) < t < s, where s is
 // the last session's start and reach the latest end + gap of the sessions before it, move that start down one record
@@ -26,11 +26,12 @@
 // such tuple then lands in si + 1 (the last slice with tStart <= t), and every other tuple where it would have without
 // the band (the moved edge only crosses tuples of the band).  So a batch whose out-of-order tuples reach into the
 // band is still one pass: the prep kernel lets the cell view start at si + 1 with the band's lower end as its start
-// (written provisionally into the slice store, restored or finalised by the commit), the ingest records per-tile
+// (DevMeta.view_s0: the ingest and the cell index see it, the slice store does not), the ingest records per-tile
 // minima, and the commit moves the edge and the session start to the batch minimum (and sets the store's order bits as
 // checkSliceEdges' note_order would).  When no slice ends anywhere in [band lower end, s] (the session opened without
 // a flexible edge), every shift's findSliceByEnd misses and is skipped: the band's tuples then land where the plain
-// quiet view puts them and only the session start moves.  C3's pause step: the stream resumes with a new session
+// quiet view puts them and only the session start moves; the verdict then checks the batch minimum (not the lowest
+// touched cell's start, which lies below the band) against the band's lower end.  C3's pause step: the stream resumes with a new session
 // whose start settles over the next ~500 ms of tuples -- rounds of the event-exact path before, one quiet pass now.
 #pragma once
 #include <hip/hip_runtime.h>

@@ -206,10 +206,11 @@ __global__ __launch_bounds__(64) void xq_prep_kernel(XQArgs a) {
   }
   if (res != XQ_NONE) band_si = -1;
   if (lane == 0) {
-    // the band's provisional view start (restored or finalised by the commit kernel, which runs whenever res is
-    // XQ_NONE here)
-    if (band_si >= 0) a.sl.ts[band_si + 1] = band_lo;
     DevMeta m{};
+    // the band's view: cell 0 (slice band_si + 1) starts at band_lo for the ingest and the cell index; the slice store
+    // keeps its start until the commit kernel moves it (nothing is written before the verdict)
+    m.view_s0_on = band_si >= 0 ? 1 : 0;
+    m.view_s0 = band_si >= 0 ? band_lo : 0;
     m.head = h0;
     m.tail = s.tail;
     m.prev_max = P;
@@ -328,10 +329,18 @@ __global__ __launch_bounds__(1024) void xq_scan_kernel(XQArgs a) {
   if (lane == 0) {
     int64_t why = 0;
     if (m.late_push != 0 || m.overflow_push != 0) why |= 1;  // a too-late tuple, or one past the grid horizon
+    int64_t bm = JMAX;
+    if (band)
+      for (int w = 0; w < 16; w++) bm = min(bm, (int64_t)s_mn[w]);
     const int64_t cmin = m.cmin, c_old = m.tail - m.head;
-    if (cmin != INT64_MAX) {  // the lowest cell any tuple landed in must start at or above lo_bound
+    if (q.band_si == -2) {
+      // the no-edge band: the plain view's cells reach below the band (the session opened inside a slice), so the
+      // tuples themselves must lie at or above its lower end -- the batch minimum from the ingest's tile minima
+      if (bm < q.lo_bound) why |= 2;
+    } else if (cmin != INT64_MAX) {  // the lowest cell any tuple landed in must start at or above lo_bound
       const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : JMAX;
-      const int64_t cs0 = cmin < c_old ? a.sl.ts[m.head + cmin] : (cmin - c_old < kc ? g[cmin - c_old] : h_end);
+      const int64_t cs0 = cmin == 0 && c_old > 0 && m.view_s0_on ? m.view_s0
+                          : cmin < c_old ? a.sl.ts[m.head + cmin] : (cmin - c_old < kc ? g[cmin - c_old] : h_end);
       if (cs0 < q.lo_bound) why |= 2;
     }
     if (batch_max > SAFE) why |= 16;
@@ -339,11 +348,7 @@ __global__ __launch_bounds__(1024) void xq_scan_kernel(XQArgs a) {
     o->batch_max = batch_max;
     o->ncand = lo;
     o->why = why;
-    if (band) {
-      int64_t bm = JMAX;
-      for (int w = 0; w < 16; w++) bm = min(bm, (int64_t)s_mn[w]);
-      o->batch_min = bm;
-    }
+    if (band) o->batch_min = bm;
   }
 }
 
@@ -590,10 +595,7 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
       a.c_part[1][c] = (unsigned long long)ID_MIN;
       a.c_part[2][c] = (unsigned long long)ID_MAX;
     }
-    if (tid == 0) {
-      if (q.band_si >= 0) a.sl.ts[q.band_si + 1] = q.band_s;  // the band's provisional view start, undone
-      a.ctl->result = result;
-    }
+    if (tid == 0) a.ctl->result = result;
     return;
   }
 
@@ -669,8 +671,6 @@ __global__ __launch_bounds__(1024) void xq_commit_kernel(XQArgs a) {
         s.unsorted |= 2;
         if (sl.ts[si] > bm) s.unsorted |= 1;
         band_to = bm;
-      } else {
-        sl.ts[si + 1] = q.band_s;
       }
     } else if (q.band_si == -2 && q.batch_min < q.band_s) {
       band_to = q.batch_min;  // no slice edge at the session start: only the start moves

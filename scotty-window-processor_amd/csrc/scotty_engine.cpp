@@ -168,7 +168,7 @@ struct scotty_op {
   int32_t x_sc = 0, x_sess = 0;       // capacity knobs
   bool x_serial = false;
   bool x_quiet_off = false;  // exact engine: no one-pass quiet path (A/B)
-  bool x_band_on = false;    // exact engine: quiet batches may move the last session's start (start band)
+  bool x_band_on = true;     // exact engine: quiet batches may move the last session's start (start band; scotty_tune)
   bool x_lane_off = false;
   bool x_kg_off = false;
   int64_t x_kg_chunk = -1;
@@ -776,7 +776,6 @@ int scotty_create(scotty_op** out, int device, int value_type, uint32_t flags) {
   op->device = device;
   op->vt = value_type;
   op->keyed = (flags & SCOTTY_FLAG_KEYED) != 0;
-  if (const char* e = getenv("SCOTTY_QUIET_BAND")) op->x_band_on = atoi(e) != 0;  // the start band's default (A/B)
   int rc = alloc_all(op);
   if (rc) {
     scotty_destroy(op);
@@ -1608,6 +1607,7 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 15: return (int64_t)op->x->xq_trace.size();  // quiet attempts of the last batch; 16 + k: attempt k's trace
     case 100: return op->x->quiet_band_moves;   // committed quiet batches that moved a session start (start band)
     case 101: return op->x->quiet_jump_pieces;  // event-exact pieces cut right behind a located session-gap jump
+    case 102: return op->x->quiet_band_noedge;  // of the band moves: sessions opened without a slice edge (start only)
     default:
       if (which >= 16 && which - 16 < (int)op->x->xq_trace.size()) return op->x->xq_trace[which - 16];
       return -1;

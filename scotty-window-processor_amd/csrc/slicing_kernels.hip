@@ -83,8 +83,9 @@ struct CellView {
   const int64_t* tstart;  // + head
   const int64_t* grid;    // + j0
   int64_t c_old, kc, h_end;
+  int64_t s0;             // start of cell 0 when c_old > 0 (t_start[head], or DevMeta.view_s0)
   __device__ __forceinline__ int64_t start(int64_t c) const {
-    return c < c_old ? tstart[c] : (c - c_old < kc ? grid[c - c_old] : h_end);
+    return c < c_old ? (c == 0 ? s0 : tstart[c]) : (c - c_old < kc ? grid[c - c_old] : h_end);
   }
   // largest c with start(c) <= t; requires start(0) <= t < h_end
   __device__ int64_t find(int64_t t) const {
@@ -104,6 +105,12 @@ struct CellView {
     return lo;
   }
 };
+
+__device__ __forceinline__ CellView make_view(const IngestArgs& a, const DevMeta& m, int64_t head, int64_t tail,
+                                              int64_t j0, int64_t kc, int64_t h_end) {
+  const int64_t* t = a.s_tstart + head;
+  return CellView{t, a.grid + j0, tail - head, kc, h_end, tail > head ? (m.view_s0_on ? m.view_s0 : t[0]) : 0};
+}
 
 // Cell index: cix[k] = last cell with start <= base + (k << shift), built once per push (cix_build_kernel) over
 // the cells a push can reach in practice: [first cell start, span_end) with span_end = min(horizon end, stream
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
   int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
   if (kc < 0) kc = 0;
   const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
-  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+  const CellView cv = make_view(a, m, head, tail, j0, kc, h_end);
   const int64_t ctot = cv.c_old + kc;
   if (ctot <= 0) {  // no cells: an empty index (every lookup past span_end takes the bisection), never a stale one
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
     if (kc < 0) kc = 0;
     int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
-    CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+    CellView cv = make_view(a, m, head, tail, j0, kc, h_end);
     int64_t ctot = cv.c_old + kc;
     int64_t first_start = cv.start(0);
     const int64_t cbase = a.cix_meta[0], cshift = a.cix_meta[1], cn = a.cix_meta[2];
@@ -436,13 +443,14 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     sc[17] = span_end;
     // deferred queue: time offsets from the window's first start must fit 32 bits
     sc[18] = (DEFER && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
+    sc[19] = cv.s0;
   }
   __syncthreads();
   // block-uniform scalars: readfirstlane keeps them in SGPRs (an LDS load alone yields VGPRs)
   const int64_t head = uni64(sc[1]), tail = uni64(sc[2]), j0 = uni64(sc[3]), kc = uni64(sc[4]);
   const int64_t h_end = uni64(sc[5]), first_start = uni64(sc[6]);
   const int64_t wbase = uni64(sc[7]), wn = uni64(sc[8]);
-  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end};
+  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end, uni64(sc[19])};
   const CellIndex cx{a.cix, uni64(sc[9]), uni64(sc[11]), uni64(sc[14]), uni64(sc[16]), uni64(sc[17]),
                      (int)uni64(sc[10])};
   const int64_t lk0 = uni64(sc[12]), lcn = uni64(sc[13]);

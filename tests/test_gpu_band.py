@@ -73,8 +73,12 @@ CASES = {
     # C3's shape at reduced size: the band moves the new session's start at every resume
     "sliding_session_minmax": dict(cfg=dict(windows=[Sliding(Time, 60_000, 60), Session(Time, 1000)],
                                             aggs=[MIN, MAX], lateness=1000), kw=dict(), moves=True),
+    # tumbling edges every 5 s: the resume at 17 s opens its session with a flexible edge (the movable-edge band), the
+    # one at 33 s without one (calculateNextFlexEdge compares with the pending fixed edge at 35 s,
+    # S/StreamSlicer.java:118-130: the no-edge band), the one at 25 s on the fixed edge itself (a non-movable slice
+    # ends at the start: shiftStart splits it, S/SliceManager.java:126-135 -- refused, event-exact)
     "tumbling_session_sum": dict(cfg=dict(windows=[Tumbling(Time, 5000), Session(Time, 1000)],
-                                          aggs=[SUM, COUNT], lateness=1000), kw=dict(), moves=True),
+                                          aggs=[SUM, COUNT], lateness=1000), kw=dict(), moves=True, noedge=True),
     "session_only_sum_minmax": dict(cfg=dict(windows=[Session(Time, 700)], aggs=[SUM, MIN, MAX], lateness=1000),
                                     kw=dict(max_delay=300, late_frac=0.3), moves=True),
     # delays beyond the gap: tuples below start - gap open sessions of their own (refused below the band)
@@ -95,9 +99,9 @@ def test_start_band_matches_oracle_and_band_off(pkg, case):
     c = CASES[case]
     steps = _steps(1 << 18, 26, seed=sum(map(ord, case)), **c["kw"])
     (on, off), total = _run(c["cfg"], steps, [{"quiet_band": 1}, {"quiet_band": 0}])
-    moves, pieces = on._debug_stat(100), on._debug_stat(101)
-    print("%s: windows %d, band moves %d, jump pieces %d, quiet commits on/off %d/%d" % (
-        case, total, moves, pieces, on._debug_stat(9), off._debug_stat(9)), flush=True)
+    moves, pieces, noedge = on._debug_stat(100), on._debug_stat(101), on._debug_stat(102)
+    print("%s: windows %d, band moves %d (no-edge %d), jump pieces %d, quiet commits on/off %d/%d" % (
+        case, total, moves, noedge, pieces, on._debug_stat(9), off._debug_stat(9)), flush=True)
     assert total >= 3  # (session-only streams emit one window per silence)
     assert off._debug_stat(100) == 0 and off._debug_stat(101) == 0
     if c["moves"] is True:
@@ -105,6 +109,8 @@ def test_start_band_matches_oracle_and_band_off(pkg, case):
         assert on._debug_stat(9) > off._debug_stat(9)  # the resumed batches' rests commit in one pass
     elif c["moves"] is False:
         assert moves == 0
+    if c.get("noedge"):
+        assert noedge >= 1 and moves - noedge >= 1  # both band variants ran (and matched the oracle above)
 
 
 def test_start_band_every_batch_resumes(pkg):
