@@ -337,7 +337,7 @@ def extra_c1(pkg, dev, batch, steps):
             "roofline": device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")}
 
 
-def extra_c3(pkg, dev, batch, steps=10, warm=61):
+def extra_c3(pkg, dev, batch, steps=10, warm=61, tune=None):
     """BASELINE configs[2] (C3): SlidingWindow(60 s, 60 ms) + SessionWindow(1 s gap), MIN_I32 + MAX_I32, 20 %
     out-of-order tuples late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000; exact engine.  Every 10 s of
     event time the stream pauses for 2 s (SURVEY: 1-2 s silences), so sessions close: tuples up to 500 ms late leave
@@ -345,12 +345,15 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
     warm-up: every timed step emits its sliding windows.  The timed steps cover whole 10-step session periods, so
     the pause step (new session, out-of-order session edits: the event-exact path, exact_batch.hip) is counted
     beside the quiet steps (one pass, exact_quiet.hip) in its true proportion.  Inputs resident in HBM; results
-    stay in HBM (processWatermarkDevice).  A second run of as many steps with HIP events gives the device roofline."""
+    stay in HBM (processWatermarkDevice).  A second run of as many steps with HIP events gives the device roofline.
+    `tune`: scotty_tune knobs (the "c3nb" leg: {"quiet_band": 0}, the start band off, for an A/B in one run)."""
     import torch
     rate = max(1, batch // 1000)
     g = torch.Generator(device=dev)
     g.manual_seed(7)
     op = pkg.SlicingWindowOperator(device=dev.index)
+    for k, v in (tune or {}).items():
+        op.tune(k, v)
     op.addWindowFunction(pkg.AGG_MIN_I32)
     op.addWindowFunction(pkg.AGG_MAX_I32)
     op.setMaxLateness(1000)
@@ -384,7 +387,8 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61):
             "ms_per_step_each": [round(1e3 * t, 4) for t in times],
             "quiet_steps": sum(1 for x in verdicts if x == 1), "event_exact_steps": sum(1 for x in verdicts if x != 1),
             "event_prefix_then_quiet_steps": op._debug_stat(12),
-            "start_band_moves": op._debug_stat(100), "jump_pieces": op._debug_stat(101),
+            "start_band_moves": op._debug_stat(100), "start_band_moves_no_edge": op._debug_stat(102),
+            "jump_pieces": op._debug_stat(101), "tune": tune or {},
             "events_rounds_each": rounds,
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows,
             "roofline": roof,
@@ -760,7 +764,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
-    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c5,c5t,pcie); default all")
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c5,c5t,pcie; c3nb: C3 with the start band "
+                    "off, A/B); default all but c3nb")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
@@ -900,6 +905,9 @@ def main():
             if "c3" in legs:
                 extra["c3"] = extra_c3(pkg, dev, 1 << 26, 10)
                 log("bench: C3 done")
+            if "c3nb" in args.only.split(","):  # A/B only (not in the default legs): C3 with the start band off
+                extra["c3nb"] = extra_c3(pkg, dev, 1 << 26, 10, tune={"quiet_band": 0})
+                log("bench: C3 (band off) done")
             if "c4" in legs:
                 extra["c4"] = extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5)
                 log("bench: C4 done")

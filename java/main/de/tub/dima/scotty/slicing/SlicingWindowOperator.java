@@ -49,8 +49,8 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
     private final transient NativeApi api = NativeApi.get();
     private final int valueType, width;
     private final NativeValues.Extractor<InputType> extractor;  // null: the functions' bindings read the value
-    private final List<NativeFunctions.Binding> bindings = new ArrayList<AggregateWindow>();
-    private final List<long[]> windows = new ArrayList<AggregateWindow>();      // {kind, measure, a, b} in registration order
+    private final List<NativeFunctions.Binding> bindings = new ArrayList<NativeFunctions.Binding>();
+    private final List<long[]> windows = new ArrayList<long[]>();      // {kind, measure, a, b} in registration order
     private long maxLateness = 1000;                              // S/WindowManager.java:24
     private boolean latenessSet = false;
     private final boolean keyed;
@@ -257,7 +257,7 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
 
     private void bindEngine() {
         if (engine != null) return;
-        List<Integer> kinds = new ArrayList<AggregateWindow>();
+        List<Integer> kinds = new ArrayList<Integer>();
         StringBuilder sig = new StringBuilder().append(valueType).append('|').append(latenessSet ? maxLateness : "d");
         for (long[] w : windows) sig.append("|w").append(w[0]).append(',').append(w[1]).append(',').append(w[2])
                 .append(',').append(w[3]);
