@@ -109,7 +109,7 @@ def test_keyed_engine_has_explicit_opt_in():
     assert "getClassContext()" in ke and "LAST_HIT" in ke
 
 
-GENERIC_DECL = re.compile(r"\b(?:List|Set|Map|Collection|Iterable)\s*<((?:[^<>]|<[^<>]*>)*)>\s+\w+\s*=\s*"
+GENERIC_DECL = re.compile(r"\b(?:List|Set|Map|Collection|Iterable|ThreadLocal)\s*<((?:[^<>]|<[^<>]*>)*)>\s+\w+\s*=\s*"
                           r"new\s+\w+\s*<((?:[^<>]|<[^<>]*>)*)>\s*\(")
 
 
