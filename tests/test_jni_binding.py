@@ -213,7 +213,7 @@ def test_jni_operator_matches_oracle(name):
         got, exp = op.processWatermark(wm), ora.processWatermark(wm)
         same_windows(got, exp)
         total += len(exp)
-    assert total > 50
+    assert total > 10  # (6 s of event time: ~20 sliding windows per config)
     op.close()
     mock().mock_reset()
 
