@@ -705,6 +705,51 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
                               "frac": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9 / HBM_PEAK_GBS}}
 
 
+def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12):
+    """Keyed sessions at scale: KeyedScottyWindowOperator with SessionWindow(gap 1 s) +
+    SlidingWindow(60 s, 1 s) per key, SUM_I32, `keys` uniform keys, 20 % out-of-order tuples late by U[1,500] ms,
+    watermark lag 500 ms, maxLateness 1000, a 2 s pause every 10 s of event time (every key's session closes, C3's
+    shape per key).  Session windows take the wavefront-per-key replay (exact_kernels.hip replay_kernel: one wavefront
+    restates one key's operator, simple tuples folded 64 at a time, session / edge events exactly).  The timed steps
+    cover one whole 10-step period (the pause step included); a second period with HIP events gives the device split."""
+    import torch
+    rate = max(1, batch // 1000)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    op = pkg.KeyedSlicingWindowOperator(device=dev.index)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.setMaxLateness(1000)
+    op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
+    op.addWindowAssigner(pkg.SessionWindow(pkg.WindowMeasure.Time, 1000))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    times, rows = [], 0
+    for s in range(warm + 2 * steps):
+        if s == warm + steps:
+            op.enableTiming(True)
+        t_begin = s * 1000 + 1000 + (s // 10) * 2000
+        k = torch.randint(0, keys, (batch,), device=dev, dtype=torch.int64, generator=g).to(torch.int32)
+        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        d = torch.randint(1, 501, (batch,), device=dev, generator=g)
+        ts = torch.where(late, base + t_begin - d, base + t_begin).contiguous()
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op.processElementsDevice(k.data_ptr(), ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(t_begin + (batch - 1) // rate - 500)
+        torch.cuda.synchronize(dev)
+        if warm <= s < warm + steps:
+            times.append(time.perf_counter() - t0)
+            rows += n
+    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
+                           "keyed replay: radix sort by key + replay_kernel (wavefront per key)")
+    return {"workload": "C4s: keyed SessionWindow(gap 1s) + SlidingWindow(60s,1s) SUM_I32, %d uniform keys, 20%% "
+                        "out-of-order (delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, maxLateness 1000, "
+                        "wavefront-per-key replay, results left in HBM" % keys,
+            "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
+            "ms_per_step": 1e3 * sum(times) / len(times), "ms_per_step_each": [round(1e3 * t, 3) for t in times],
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows, "roofline": roof}
+
+
 def extra_pcie(pkg, sizes, batch, steps):
     """PCIe-inclusive C2: the same operator fed from HOST memory through scotty_process_elements --
     (a) the op's pinned staging slots (scotty_host_buffers: DMA in place, double-buffered), (b) pageable numpy
@@ -764,7 +809,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
-    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c5,c5t,pcie; c3nb: C3 with the start band "
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c5,c5t,pcie; c3nb: C3 with the start band "
                     "off, A/B); default all but c3nb")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
@@ -889,7 +934,7 @@ def main():
                                        % world) if sharded else "single GPU"},
             "roofline": roof,
         }
-    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c5", "c5t", "pcie"}
+    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c4s", "c5", "c5t", "pcie"}
     extra = {}
     if not args.no_extra:
         del batches
@@ -911,6 +956,9 @@ def main():
             if "c4" in legs:
                 extra["c4"] = extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5)
                 log("bench: C4 done")
+            if "c4s" in legs:
+                extra["c4s"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20)
+                log("bench: C4s (keyed sessions) done")
             if "c5" in legs:
                 extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)
                 log("bench: C5 done")
