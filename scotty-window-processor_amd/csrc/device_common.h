@@ -76,6 +76,7 @@ struct IngestArgs {
   uint32_t* cix;
   int64_t* cix_meta;         // [base, shift, n, cells indexed, ts end of the indexed range]
   int64_t cix_margin;        // ms past the stream front (prev_max) the index covers
+  long long* stamps;         // nullable: per-workgroup clock stamps [blocks][4] (debugging aid, "ingest_stamps")
 };
 
 struct CommitArgs {

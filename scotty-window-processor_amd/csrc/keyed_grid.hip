@@ -302,50 +302,11 @@ __device__ __forceinline__ bool tile_records(const KgArgs& a, int64_t i0, int ti
   return bad;
 }
 
-// Variant 2's tile: the same records and buckets, with the tile's loads issued behind the workgroup's column of bucket
-// bases (so the wait for the bases does not wait for the tile: vmcnt counts in issue order) and the in-order check's
-// previous timestamp taken from the next lower lane (one uniform load per wave and round instead of a second load of
-// every timestamp).
-template <int VB, int IT, int ST, int NBS>
-__device__ __forceinline__ void tile_load_ov(const KgArgs& a, int64_t i0, int tid, uint32_t (&kk)[IT],
-                                             int64_t (&tt)[IT], int64_t (&tw)[IT], KRec<VB> (&rec)[IT]) {
-#pragma unroll
-  for (int j = 0; j < IT; j++) {
-    const int64_t i = i0 + j * ST + tid;
-    const int64_t ic = i < a.n ? i : a.n - 1;
-    kk[j] = __builtin_nontemporal_load(a.key + ic);
-    tt[j] = a.ts[ic];
-    const int64_t iw = i0 + j * ST + (tid & ~63) - 1;  // the tuple before the wave's first (same address in every lane)
-    tw[j] = a.ts[iw < 0 ? 0 : (iw < a.n ? iw : a.n - 1)];
-    rec[j] = KRec<VB>::make(0, 0, a.val, ic);
-  }
-}
-template <int VB, int IT, int ST, int NBS>
-__device__ __forceinline__ bool tile_rank_ov(const KgArgs& a, int64_t i0, int tid, int64_t f, int32_t* cnt,
-                                             const uint32_t (&kk)[IT], const int64_t (&tt)[IT],
-                                             const int64_t (&tw)[IT], KRec<VB> (&rec)[IT], int32_t (&bk)[IT],
-                                             int32_t (&rk)[IT]) {
-  const int lane = tid & 63;
-  bool bad = false;
-#pragma unroll
-  for (int j = 0; j < IT; j++) {
-    const int64_t i = i0 + j * ST + tid;
-    const bool in = i < a.n;
-    const int64_t up = (int64_t)__shfl_up((long long)tt[j], 1);
-    const int64_t tp = lane == 0 ? tw[j] : up;
-    bad |= in && i > 0 && tp > tt[j];
-    rec[j].set(kk[j], (uint32_t)(tt[j] - f));
-    bk[j] = in ? (int32_t)bucket_of(kk[j], a.kmask) : NBS;
-    rk[j] = atomicAdd(&cnt[bk[j]], 1);
-  }
-  return bad;
-}
-
 // Scatter into bucket runs, staged in LDS: a tile is counted per bucket, ranked, laid out bucket by bucket in LDS
 // and written as contiguous per-bucket runs (a wave writes a few runs, not 64 scattered records).  Order inside a
 // bucket is not kept: the per-cell partials commute (counts, wrapping integer sums, min/max; f64 sums
-// reassociate, within SUM_F64's stated tolerance).  OV: variant 2's load order (tile_load_ov).
-template <int VB, int T, int NBS, int ST, bool OV = false>
+// reassociate, within SUM_F64's stated tolerance).
+template <int VB, int T, int NBS, int ST>
 __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   constexpr int IT = T / ST;
   constexpr int PER = NBS / ST;
@@ -360,36 +321,12 @@ __global__ __launch_bounds__(ST) void kg_scatter_kernel(KgArgs a) {
   const int64_t i0 = tile * T;
   KRec<VB> rec[IT];
   int32_t bk[IT], rk[IT];
-  bool bad;
-  if constexpr (OV) {
-    constexpr int PB = (NBS + ST - 1) / ST;
-    int32_t bv[PB];
-#pragma unroll
-    for (int q = 0; q < PB; q++) {  // the bases first (unconditional loads, index clamped)
-      const int b = tid + q * ST;
-      bv[q] = a.hist[(int64_t)(b < a.nbk ? b : a.nbk - 1) * a.ntiles + tile];
-    }
-    uint32_t kk[IT];
-    int64_t tt[IT], tw[IT];
-    tile_load_ov<VB, IT, ST, NBS>(a, i0, tid, kk, tt, tw, rec);
-#pragma unroll
-    for (int q = 0; q < PB; q++) {
-      const int b = tid + q * ST;
-      if (b < a.nbk) {
-        cnt[b] = 0;
-        base[b] = bv[q];
-      }
-    }
-    __syncthreads();
-    bad = tile_rank_ov<VB, IT, ST, NBS>(a, i0, tid, f, cnt, kk, tt, tw, rec, bk, rk);
-  } else {
-    for (int b = tid; b < a.nbk; b += ST) {
-      cnt[b] = 0;
-      base[b] = a.hist[(int64_t)b * a.ntiles + tile];
-    }
-    __syncthreads();
-    bad = tile_records<VB, IT, ST, NBS>(a, i0, tid, f, cnt, rec, bk, rk);
+  for (int b = tid; b < a.nbk; b += ST) {
+    cnt[b] = 0;
+    base[b] = a.hist[(int64_t)b * a.ntiles + tile];
   }
+  __syncthreads();
+  const bool bad = tile_records<VB, IT, ST, NBS>(a, i0, tid, f, cnt, rec, bk, rk);
   if (__ballot(bad) && (tid & 63) == 0) atomicOr(&a.ctl->flag, KG_UNSORTED);
   __syncthreads();
   // tile-local exclusive scan of the bucket counts
@@ -910,8 +847,9 @@ hipError_t launch_kg_partition(const KgArgs& a, int vt, hipStream_t st) {
 
 // tuples per partition tile: the LDS stage holds one tile (int32 values with <= 2048 buckets: 8192 tuples; else 4096).
 // Variant 0 (A/B baseline, scotty_tune "keyed_grid_variant"): 512-thread scatter workgroups and 12-byte records only.
-// (Measured and removed in round 4: a persistent software-pipelined scatter and a 72-KB two-workgroups-per-CU scatter,
-// both equal or slower, profiles/r03/r03k_c4_variant_ab.log.)
+// (Measured and removed: a persistent software-pipelined scatter and a 72-KB two-workgroups-per-CU scatter, both equal
+// or slower, profiles/r03/r03k_c4_variant_ab.log; round 5: the tile's loads issued behind the bucket bases with the
+// previous timestamp from the next lower lane, 0.96 vs 1.01 ms data pass, profiles/r05/ab_c4_variants.json.)
 int kg_tile(int vt, int64_t nbk, int variant) {
   (void)variant;
   return vt == VT_I32 && nbk <= 2048 ? 8192 : 4096;
@@ -920,9 +858,7 @@ int kg_tile(int vt, int64_t nbk, int variant) {
 hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st) {
   const unsigned grid = (unsigned)(((a.ntiles + 7) / 8) * 8);
   if (vt == VT_I32) {
-    if (a.tile == 8192 && a.variant == 2)
-      hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 1024, true>), dim3(grid), dim3(1024), 0, st, a);
-    else if (a.tile == 8192 && a.variant == 1)
+    if (a.tile == 8192 && a.variant == 1)
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 1024>), dim3(grid), dim3(1024), 0, st, a);
     else if (a.tile == 8192)
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 512>), dim3(grid), dim3(512), 0, st, a);

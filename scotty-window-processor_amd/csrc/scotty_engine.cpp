@@ -120,6 +120,8 @@ struct scotty_op {
   long long* d_tilemax = nullptr;
   uint32_t* d_cix = nullptr;      // cell index (slicing_kernels.hip cix_build_kernel)
   int64_t* d_cixmeta = nullptr;
+  long long* d_stamps = nullptr;  // ingest phase stamps (scotty_tune "ingest_stamps", a debugging aid)
+  bool stamps_on = false;
   long long* d_pmax = nullptr;
   int32_t* d_rank = nullptr;
   int32_t* d_flag = nullptr;
@@ -543,6 +545,10 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   ia.cix = op->d_cix;
   ia.cix_meta = op->d_cixmeta;
   ia.cix_margin = std::max<int64_t>(4 * op->last_span, 4000);
+  if (op->stamps_on) {
+    if (!op->d_stamps) HIPCHK(dev_malloc(&op->d_stamps, 8192 * 4 * 8));
+    ia.stamps = op->d_stamps;
+  }
   if (!op->cix_ready) {
     rc = enqueue_cix(op);
     if (rc) return rc;
@@ -806,7 +812,7 @@ void scotty_destroy(scotty_op* op) {
   for (auto& e : op->ev_pool) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   delete op->x;
   delete op->c;
-  F(op->d_shrank); F(op->d_shflag); F(op->d_cix); F(op->d_cixmeta);
+  F(op->d_shrank); F(op->d_shflag); F(op->d_cix); F(op->d_cixmeta); F(op->d_stamps);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
 }
@@ -1476,8 +1482,13 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     op->ingest_blocks = value;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "ingest_mode") == 0) {  // int32 SUM / COUNT ingest loop (A/B only): 6 plain, 7 pipelined
-    if (value != -1 && value != 6 && value != 7) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "ingest_stamps") == 0) {  // per-workgroup phase clock stamps of the ingest (debugging aid)
+    op->stamps_on = value != 0;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "ingest_mode") == 0) {  // int32 ingest loop (A/B only): 6 plain, 7 pipelined, 22 / 23 the same
+                                                // with the DQ2 deferred queue (23 also for MIN / MAX)
+    if (value != -1 && value != 6 && value != 7 && value != 22 && value != 23) return SCOTTY_ERR_ARG;
     op->ingest_mode = (int)value;
     return SCOTTY_OK;
   }
@@ -1529,8 +1540,8 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->c) op->c->shard_async = op->shard_async;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only: 0 baseline, 1 default, 2 overlapped scatter loads)
-    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "keyed_grid_variant") == 0) {  // sort-free path kernel variant (A/B only: 0 baseline, 1 default)
+    if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;
     op->x_kg_variant = (int32_t)value;
     if (op->x) op->x->kg_variant = op->x_kg_variant;
     return SCOTTY_OK;
@@ -1580,6 +1591,15 @@ int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
   if (which == 10) return op->last_ingest_streaming;
   if (which == 11) return (int64_t)op->h_snap->slow_last;
   return -1;
+}
+
+// Internal (not in the header): the last grid ingest's phase stamps (s_memtime ticks), [workgroups][4]: start, LDS
+// window ready, every wave's range done, window flushed to the cells.  Returns the workgroups copied.
+int64_t scotty_debug_ingest_stamps(scotty_op* op, long long* out, int64_t max_blocks) {
+  if (!op || !op->d_stamps) return -1;
+  const int64_t nb = std::min<int64_t>(std::min<int64_t>(op->last_ingest_blocks, 8192), max_blocks);
+  if (hipMemcpy(out, op->d_stamps, nb * 4 * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return nb;
 }
 
 // Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds; keyed:

@@ -66,6 +66,18 @@ __device__ __forceinline__ uint32_t wsum32(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
   return v;
 }
+// inclusive wave scan of a u32 over DPP (row_shr 1 / 2 / 4 / 8 inside each row of 16, row_bcast 15 / 31 across rows;
+// lanes a shift leaves without a source add the identity 0): no LDS crossbar.  Every lane must be active.
+__device__ __forceinline__ uint32_t dpp_iscan_u32(uint32_t x) {
+  uint32_t v = x;
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
+  return v;
+}
 
 // Ordered int64 keys for Java Math.min/Math.max on double: NaN dominates, -0.0 < +0.0.
 __device__ __forceinline__ int64_t f64_key(double d) {
@@ -330,59 +342,23 @@ __host__ __device__ constexpr size_t ingest_lds_bytes() {
   return (b + 15) & ~(size_t)15;
 }
 
-// ================================================================ 1. ingest
-// MODE bit0: software-pipelined (next step's loads in flight while the current step is combined)
-// MODE bit1: non-temporal loads for the once-read tuple columns
-// MODE bit2: deferred slow path -- tuples outside the wave's current cell but inside the workgroup's LDS window
-//            (out-of-order tuples) are appended to a per-wave LDS queue (ballot + mbcnt, no dependent loads) and
-//            folded 64 at a time with every lane busy, instead of a per-lane loop of dependent lookups whose
-//            iterations run with a fraction of the lanes active
-// MODE bit3: per-tile minima as well (a.tilemin; the exact engine's quiet path: the lowest tuple of a batch is the
-//            new start of a session whose start the batch moves down, exact_quiet.h)
-template <int VT, int NEED, int MODE>
-__global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
-  using V = typename ValT<VT>::T;
-  constexpr bool DEFER = (MODE & 4) != 0;
-  constexpr bool TMIN = (MODE & 8) != 0;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int64_t* sc = (int64_t*)smem;  // block scalars [ING_SC]
-  LdsWin<VT> w;
-  unsigned char* p = smem + 8 * ING_SC;
-  w.tw = (int64_t*)p;
-  p += 8 * (WCAP + 2);
-  using MMT = typename LdsMM<VT>::T;
-  w.tmax = (uint32_t*)p;
-  p += 4 * WCAP;
-  w.mn = nullptr;
-  w.mx = nullptr;
-  if (NEED & NEED_MIN) {
-    w.mn = (MMT*)p;
-    p += sizeof(MMT) * WCAP;
-  }
-  if (NEED & NEED_MAX) {
-    w.mx = (MMT*)p;
-    p += sizeof(MMT) * WCAP;
-  }
-  w.sum = nullptr;
-  if (NEED & NEED_SUM) {
-    w.sum = (typename LdsSum<VT>::T*)p;
-    p += sizeof(typename LdsSum<VT>::T) * WCAP;
-  }
-  w.cnt = (uint32_t*)p;
-  p += 4 * WCAP;
-  uint16_t* lcix = (uint16_t*)p;  // [LCIX] cell index entries of the window, relative to wbase
-  p += 2 * LCIX;
+// Block-uniform scalars of an ingest workgroup's LDS cell window (ingest_window)
+struct WinScal {
+  int64_t head, tail, j0, kc, h_end, first_start, wbase, wn, lk0, lcn;
+  bool qok;
+  CellView cv;
+  CellIndex cx;
+};
 
+// The prologue every ingest kernel shares: the block's LDS window of cells.  Anchor = max ts over the block's first
+// and last 64 tuples (a single endpoint may be an out-of-order tuple; a window placed below the block's in-order front
+// sends most of its late tuples to global atomics); the window [wbase, wbase + wn) ends 16 cells past the anchor's
+// cell and is cut so every cell ends within 2^32 - 1 of its first start (32-bit tmax offsets); tw[0..wn] = the window's
+// cell starts; lcix[0..lcn) = the staged cell index of the window's recent part.  Returns false for an overflowed /
+// refused interval (no index was built this push: nothing may read cix_meta).  sc: LDS block scalars [ING_SC].
+__device__ __forceinline__ bool ingest_window(const IngestArgs& a, int64_t* sc, int64_t* tw, uint16_t* lcix,
+                                              int64_t b0, int64_t b1, bool defer, WinScal& ws) {
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  // per-wave deferred queue: time offsets from the window's first cell start + values
-  uint32_t* q_t = DEFER ? (uint32_t*)p + wid * DEFER_CAP : nullptr;
-  V* q_v = DEFER ? (V*)((uint32_t*)p + 4 * DEFER_CAP) + wid * DEFER_CAP : nullptr;
-  const int64_t per_block = a.per_wave * 4;
-  const int64_t b0 = (int64_t)blockIdx.x * per_block;
-  const int64_t b1 = min(a.n, b0 + per_block);
-
   // Window anchor: max ts over the block's first and last 64 tuples (a single endpoint may be an out-of-order
   // tuple; a window placed below the block's in-order front sends most of its late tuples to global atomics)
   if (tid < 64) {
@@ -397,7 +373,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   // the window search to an arbitrary cix entry.  Decide the early return before any index read.
   if (tid == 0) sc[0] = a.meta->overflow;
   __syncthreads();
-  if (sc[0] != 0) return;  // an earlier push of this interval overflowed: nothing is committed until replay
+  if (sc[0] != 0) return false;  // an earlier push of this interval overflowed: nothing is committed until replay
   if (tid == 0) {
     const DevMeta& m = *a.meta;
     int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
@@ -442,7 +418,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     sc[16] = c_full;
     sc[17] = span_end;
     // deferred queue: time offsets from the window's first start must fit 32 bits
-    sc[18] = (DEFER && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
+    sc[18] = (defer && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
     sc[19] = cv.s0;
   }
   __syncthreads();
@@ -455,13 +431,91 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
                      (int)uni64(sc[10])};
   const int64_t lk0 = uni64(sc[12]), lcn = uni64(sc[13]);
   const bool qok = uni64(sc[18]) != 0;
-  for (int64_t i = tid; i <= wn; i += 256) w.tw[i] = cv.start(wbase + i);
+  for (int64_t i = tid; i <= wn; i += 256) tw[i] = cv.start(wbase + i);
   for (int64_t i = tid; i < lcn; i += 256) {
     const int64_t kk = lk0 + i;
     int64_t v = (int64_t)cx.cix[kk];
     v = min(max(v - wbase, (int64_t)0), wn - 1);
     lcix[i] = (uint16_t)v;
   }
+  ws.head = head; ws.tail = tail; ws.j0 = j0; ws.kc = kc; ws.h_end = h_end; ws.first_start = first_start;
+  ws.wbase = wbase; ws.wn = wn; ws.lk0 = lk0; ws.lcn = lcn; ws.qok = qok;
+  ws.cv = cv;
+  ws.cx = cx;
+  return true;
+}
+
+// ================================================================ 1. ingest
+// MODE bit0: software-pipelined (next step's loads in flight while the current step is combined)
+// MODE bit1: non-temporal loads for the once-read tuple columns
+// MODE bit2: deferred slow path -- tuples outside the wave's current cell but inside the workgroup's LDS window
+//            (out-of-order tuples) are appended to a per-wave LDS queue (ballot + mbcnt, no dependent loads) and
+//            folded 64 at a time with every lane busy, instead of a per-lane loop of dependent lookups whose
+//            iterations run with a fraction of the lanes active
+// MODE bit3: per-tile minima as well (a.tilemin; the exact engine's quiet path: the lowest tuple of a batch is the
+//            new start of a session whose start the batch moves down, exact_quiet.h)
+// MODE bit4: the deferred queue (bit 2) with one DPP scan per step instead of a ballot per tuple slot, folded in full
+//            passes of 64 (the remainder stays queued) instead of draining every entry with part of the lanes idle
+template <int VT, int NEED, int MODE>
+__global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
+  using V = typename ValT<VT>::T;
+  constexpr bool DEFER = (MODE & 4) != 0;
+  constexpr bool TMIN = (MODE & 8) != 0;
+  constexpr bool DQ2 = DEFER && (MODE & 16) != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int64_t* sc = (int64_t*)smem;  // block scalars [ING_SC]
+  LdsWin<VT> w;
+  unsigned char* p = smem + 8 * ING_SC;
+  w.tw = (int64_t*)p;
+  p += 8 * (WCAP + 2);
+  using MMT = typename LdsMM<VT>::T;
+  w.tmax = (uint32_t*)p;
+  p += 4 * WCAP;
+  w.mn = nullptr;
+  w.mx = nullptr;
+  if (NEED & NEED_MIN) {
+    w.mn = (MMT*)p;
+    p += sizeof(MMT) * WCAP;
+  }
+  if (NEED & NEED_MAX) {
+    w.mx = (MMT*)p;
+    p += sizeof(MMT) * WCAP;
+  }
+  w.sum = nullptr;
+  if (NEED & NEED_SUM) {
+    w.sum = (typename LdsSum<VT>::T*)p;
+    p += sizeof(typename LdsSum<VT>::T) * WCAP;
+  }
+  w.cnt = (uint32_t*)p;
+  p += 4 * WCAP;
+  uint16_t* lcix = (uint16_t*)p;  // [LCIX] cell index entries of the window, relative to wbase
+  p += 2 * LCIX;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  // per-wave deferred queue: time offsets from the window's first cell start + values
+  uint32_t* q_t = DEFER ? (uint32_t*)p + wid * DEFER_CAP : nullptr;
+  V* q_v = DEFER ? (V*)((uint32_t*)p + 4 * DEFER_CAP) + wid * DEFER_CAP : nullptr;
+  const int64_t per_block = a.per_wave * 4;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = min(a.n, b0 + per_block);
+
+  // phase stamps (debugging aid): start, window ready, waves' ranges done, LDS window flushed
+  auto stamp = [&](int k) {
+    if (a.stamps && tid == 0) a.stamps[(int64_t)blockIdx.x * 4 + k] = (long long)__builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  WinScal ws;
+  if (!ingest_window(a, sc, w.tw, lcix, b0, b1, DEFER, ws)) return;
+  const int64_t head = ws.head, tail = ws.tail, j0 = ws.j0, kc = ws.kc;
+  const int64_t h_end = ws.h_end, first_start = ws.first_start;
+  const int64_t wbase = ws.wbase, wn = ws.wn;
+  const CellView cv = ws.cv;
+  const CellIndex cx = ws.cx;
+  const int64_t lk0 = ws.lk0, lcn = ws.lcn;
+  const bool qok = ws.qok;
+  (void)head; (void)tail; (void)j0; (void)kc;
   for (int64_t i = tid; i < wn; i += 256) {
     w.cnt[i] = 0;
     w.tmax[i] = 0;
@@ -470,6 +524,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     if (NEED & NEED_MAX) w.mx[i] = std::numeric_limits<MMT>::min();
   }
   __syncthreads();
+  stamp(1);
   const int64_t tw0 = uni64(w.tw[0]), twn = uni64(w.tw[wn]);
   w.tbase = tw0;
   // window cell of t (tw0 <= t < twn): staged cell index, else binary search over the window's starts
@@ -572,6 +627,22 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     }
     qn = 0;
   };
+  // DQ2: whole passes only (every lane busy); the < 64 entries left move to the queue's front
+  auto drain_full = [&]() {
+    const int full = qn & ~63;
+    for (int b = 0; b < full; b += 64) {
+      const int64_t t = tw0 + (int64_t)q_t[b + lane];
+      lds_one(wfind(t), t, q_v[b + lane]);
+    }
+    const int rem = qn - full;
+    if (lane < rem) {  // sources [full, qn) and destinations [0, rem) do not overlap (full >= 64 > rem)
+      const uint32_t qt = q_t[full + lane];
+      const V qv = q_v[full + lane];
+      q_t[lane] = qt;
+      q_v[lane] = qv;
+    }
+    qn = rem;
+  };
 
   constexpr bool PIPE = (MODE & 1) != 0;
   constexpr bool NTL = (MODE & 2) != 0;
@@ -641,7 +712,31 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       else sm |= 1u << j;
     }
     n_slow += __popc(sm);
-    if constexpr (DEFER) {
+    if constexpr (DQ2) {
+      // one scan places every lane's queued tuples: the queue holds < 64 entries here, so 256 more fit (DEFER_CAP)
+      if (qok && __ballot(sm != 0) != 0) {
+        const uint64_t qspan = (uint64_t)(twn - tw0);
+        uint32_t qm = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          qm |= (((sm >> j) & 1) && (uint64_t)(t[j] - tw0) < qspan) ? (1u << j) : 0u;
+        const uint32_t c = (uint32_t)__popc(qm);
+        const uint32_t inc = dpp_iscan_u32(c);
+        const int tot = (int)__builtin_amdgcn_readlane(inc, 63);
+        int pos = qn + (int)(inc - c);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          if ((qm >> j) & 1) {
+            q_t[pos] = (uint32_t)(t[j] - tw0);
+            q_v[pos] = v[j];
+            pos++;
+          }
+        }
+        qn += tot;
+        sm &= ~qm;
+        if (qn >= 64) drain_full();
+      }
+    } else if constexpr (DEFER) {
       // (wave-uniform test first: in an in-order stretch no lane has a slow tuple, and the four ballots below are skipped)
       if (qok && __ballot(sm != 0) != 0) {
         if (qn > DEFER_CAP - 256) drain();
@@ -755,6 +850,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     }
   }
   __syncthreads();
+  stamp(2);
   // the window's partials to the global cells; the lowest touched cell bounds the commit's fold
   int64_t bmin = INT64_MAX;
   for (int64_t i = tid; i < wn; i += 256) {
@@ -769,6 +865,10 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   }
   bmin = wmin64(bmin);
   if (lane == 0 && bmin != INT64_MAX) atomicMin((long long*)&a.meta->cmin, (long long)bmin);
+  if (a.stamps) {
+    __syncthreads();
+    stamp(3);
+  }
 }
 
 // ================================================================ 2. commit (single workgroup)
@@ -1462,6 +1562,21 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
     if (vt == VT_I32) return launch_ingest_vt<VT_I32, 8>(a, need, nblocks, st);
     if (vt == VT_I64) return launch_ingest_vt<VT_I64, 8>(a, need, nblocks, st);
     return launch_ingest_vt<VT_F64, 8>(a, need, nblocks, st);
+  }
+  if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 22 || mode == 23)) {  // DQ2 queue (A/B)
+    if (mode == 22) return nd ? launch_ingest_t<VT_I32, NEED_SUM, 22>(a, nblocks, st)
+                              : launch_ingest_t<VT_I32, 0, 22>(a, nblocks, st);
+    return nd ? launch_ingest_t<VT_I32, NEED_SUM, 23>(a, nblocks, st) : launch_ingest_t<VT_I32, 0, 23>(a, nblocks, st);
+  }
+  if (vt == VT_I32 && (nd & (NEED_MIN | NEED_MAX)) && mode == 23) {  // MIN / MAX with the DQ2 queue (A/B)
+    switch (nd) {
+      case 2: return launch_ingest_t<VT_I32, 2, 23>(a, nblocks, st);
+      case 3: return launch_ingest_t<VT_I32, 3, 23>(a, nblocks, st);
+      case 4: return launch_ingest_t<VT_I32, 4, 23>(a, nblocks, st);
+      case 5: return launch_ingest_t<VT_I32, 5, 23>(a, nblocks, st);
+      case 6: return launch_ingest_t<VT_I32, 6, 23>(a, nblocks, st);
+      default: return launch_ingest_t<VT_I32, 7, 23>(a, nblocks, st);
+    }
   }
   if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 6 || mode == 7 || mode == INGEST_STREAMING)) {
     if (mode == 6) return nd ? launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st)

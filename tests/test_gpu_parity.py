@@ -317,3 +317,25 @@ def test_f64_sum_at_bench_scale(pkg):
         assert rel <= 1e-6, (w.getStart(), w.getEnd(), s, float(exp_sum))
         checked += 1
     assert checked > 1000 and worst < 1e-6
+
+
+# ---------------------------------------------------------------- every ingest loop of the grid path
+@pytest.mark.parametrize("mode", [6, 7, 22, 23])
+@pytest.mark.parametrize("seed", range(4))
+def test_ingest_loops_match_oracle(mode, seed):
+    """The int32 ingest loops scotty_tune("ingest_mode") selects (6 plain, 7 software-pipelined, 22 / 23 the same with
+    the DQ2 deferred queue: one DPP scan per step, full-pass folds) on out-of-order streams dense enough that every
+    wave queues and folds many out-of-order tuples (the queue's remainder carried across steps, the end-of-range fold
+    of a partial pass), against the oracle.  SUM / COUNT and MIN / MAX configurations (mode 23 covers both)."""
+    rng = np.random.default_rng(7700 + seed)
+    aggs = [[SUM, COUNT], [SUM], [COUNT, MIN, MAX], [MIN, SUM]][seed]
+    if mode == 22 and (MIN in aggs or MAX in aggs):
+        pytest.skip("mode 22 is the SUM / COUNT loop only")
+    cfg = dict(windows=[Sliding(Time, _not_pow2(int(rng.integers(200, 3000))), _not_pow2(int(rng.integers(5, 90)))),
+                        Tumbling(Time, _not_pow2(int(rng.integers(30, 700))))], aggs=aggs, lateness=1000)
+    n = 1_500_000
+    ts, vals = product().workloads.stream(n, 400, t0=100, ooo_frac=[0.2, 0.5, 0.05, 0.3][seed], max_delay=400,
+                                          seed=seed, value_type="i32")
+    gpu, ora = build_ops(cfg, "i32", tune={"ingest_mode": mode})
+    sched = interval_schedule(ts, 4, lag=400, pushes_per_interval=2)
+    assert run_schedule(gpu, ora, ts, vals, sched) > 0

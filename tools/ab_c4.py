@@ -1,5 +1,5 @@
 """Interleaved same-box A/B of the keyed sort-free path's kernel variants on C4 (2^26 tuples, 2^20 keys, SUM_I32):
-`python tools/ab_c4.py 1 2` runs variant 1, variant 2, variant 1, variant 2, ... (3 rounds), one JSON line per run with
+`python tools/ab_c4.py 0 1` runs variant 0, variant 1, variant 0, variant 1, ... (3 rounds), one JSON line per run with
 the wall ms per step and the per-class device ms (HIP events).  GPU box tool."""
 import importlib
 import json
@@ -15,7 +15,7 @@ import bench  # noqa: E402
 
 pkg = importlib.import_module("scotty-window-processor_amd")
 dev = torch.device("cuda", 0)
-variants = [int(x) for x in sys.argv[1:]] or [1, 2]
+variants = [int(x) for x in sys.argv[1:]] or [0, 1]
 for rep in range(3):
     for v in variants:
         r = bench.extra_c4(pkg, dev, 1 << 26, 1 << 20, 5, tune={"keyed_grid_variant": v})
