@@ -25,7 +25,12 @@ enum : int { VT_I32 = 0, VT_I64 = 1, VT_F64 = 2 };
 // launch_ingest's mode for a stream whose last push was in order (DevMeta.slow_last): the software-pipelined loop on
 // fewer, longer waves (r04f A/B on C2: 279 -> 264 us per 2^27 tuples; an out-of-order stream wants the default)
 constexpr int INGEST_STREAMING = -2;
-constexpr int INGEST_STREAMING_WGS_PER_CU = 2;  // x 256 CUs (C2: 448-640 workgroups measured best, 1024 slowest)
+// workgroups of the streaming launch (C2, same-box sweeps: 416-480 -> 0.257-0.261 ms, 512 -> 0.267, 1024 -> 0.285;
+// profiles/r05/ab_c2_blocks.json)
+constexpr int INGEST_STREAMING_WGS = 448;
+// workgroups of the int32 COUNT / SUM launch for out-of-order streams (C2s with the DQ2 queue: 704-896 -> 0.305-0.309
+// ms, 1024 -> 0.342; profiles/r05/ab_c2s_dq2_blocks.json)
+constexpr int INGEST_OOO_I32_WGS = 768;
 enum : int { NEED_SUM = 1, NEED_MIN = 2, NEED_MAX = 4 };
 
 // Device-resident scalars.  The StreamSlicer state (maxEventTime, min_next_edge_ts) lives here so

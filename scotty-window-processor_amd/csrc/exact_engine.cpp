@@ -853,7 +853,8 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   if (rc) return rc;
   int64_t tile = TILE_MIN;
   while ((n + tile - 1) / tile > NT_MAX) tile <<= 1;
-  const int64_t target_blocks = 256 * ingest_wgs_per_cu(vt, cfg.need);  // one round of resident workgroups
+  const int64_t target_blocks = xq_ingest_blocks > 0 ? xq_ingest_blocks
+                                                     : 256 * ingest_wgs_per_cu(vt, cfg.need);  // one round of resident workgroups
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
   per_wave = std::max(((per_wave + tile - 1) / tile) * tile, tile);
   const int64_t nblocks = (n + per_wave * 4 - 1) / (per_wave * 4);
@@ -908,7 +909,7 @@ int XEngine::push_quiet(const int64_t* d_ts, const void* d_val, int64_t n, int32
   XCHK(launch_cix_build(ia, stream));
   if ((rc = tend(t0, 0))) return rc;
   if ((rc = tbegin(t1, SCOTTY_TIME_INGEST))) return rc;
-  XCHK(launch_ingest(ia, vt, cfg.need, nblocks, stream, -1));
+  XCHK(launch_ingest(ia, vt, cfg.need, nblocks, stream, xq_ingest_mode));
   if ((rc = tend(t1, n))) return rc;
   if ((rc = tbegin(t2, SCOTTY_TIME_PUSH_OTHER))) return rc;
   XCHK(launch_xq_commit(q, stream));

@@ -63,6 +63,10 @@ class XEngine {
   bool band_usable() const { return band_on && cfg.n_ctx == 1 && !cfg.lazy; }
   // first event-exact piece of a refused quiet batch, in tuples (scotty_tune "exact_prefix"; 0: max(n / 32, 2^20))
   int64_t xq_prefix = 0;
+  // the quiet pass's ingest launch (A/B, scotty_tune "quiet_ingest_mode" / "quiet_ingest_blocks"): mode 7 = the loop
+  // without the DQ2 deferred queue, -1 the default; blocks 0 = one round of resident workgroups
+  int32_t xq_ingest_mode = -1;
+  int64_t xq_ingest_blocks = 0;
   // batches whose own quiet verdict fails on their tuples (below the cell view / too late / past the grid horizon:
   // XQCtl.why bit 1; below the last session's start: bit 2) back the quiet path off: after two such batches in a row,
   // the next 1, 2, 4 .. 16 batches go straight to the event-exact path

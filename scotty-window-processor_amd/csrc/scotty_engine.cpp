@@ -175,6 +175,8 @@ struct scotty_op {
   bool x_kg_off = false;
   int64_t x_kg_chunk = -1;
   int64_t x_prefix = 0;      // exact engine: first event-exact prefix of a refused quiet batch (0: default)
+  int32_t x_qmode = -1;      // exact engine: quiet-pass ingest loop (A/B: -1 default, 23 DQ2 queue)
+  int64_t x_qblocks = 0;     // exact engine: quiet-pass ingest workgroups (A/B: 0 default)
   int32_t x_kg_variant = -1;
   int64_t shard_count_total = 0;
   int64_t count_shard_cap = 1 << 16;
@@ -565,8 +567,10 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   const DevMeta& hs = *op->h_snap;
   const bool streaming = op->ingest_mode < 0 && op->ingest_blocks <= 0 && op->vt == VT_I32 &&
                          !(op->need & (NEED_MIN | NEED_MAX)) && hs.n_last > 0 && hs.slow_last * 100 < hs.n_last;
+  const bool i32_sum = op->vt == VT_I32 && !(op->need & (NEED_MIN | NEED_MAX));
   const int64_t target_blocks = op->ingest_blocks > 0 ? op->ingest_blocks
-                                : streaming          ? 256 * INGEST_STREAMING_WGS_PER_CU
+                                : streaming          ? INGEST_STREAMING_WGS
+                                : i32_sum            ? INGEST_OOO_I32_WGS
                                                      : 256 * ingest_wgs_per_cu(op->vt, op->need);
   int64_t per_wave = (n + target_blocks * 4 - 1) / (target_blocks * 4);
   per_wave = ((per_wave + tile - 1) / tile) * tile;
@@ -955,6 +959,8 @@ static int decide_mode(scotty_op* op) {
   if (op->x_kg_chunk >= 0) op->x->kg_min_chunk = op->x_kg_chunk;
   if (op->x_kg_variant >= 0) op->x->kg_variant = op->x_kg_variant;
   op->x->xq_prefix = op->x_prefix;
+  op->x->xq_ingest_mode = op->x_qmode;
+  op->x->xq_ingest_blocks = op->x_qblocks;
   op->x->timing = op->timing;  // scotty_enable_timing before the first push (the natural order) reaches the engine
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
@@ -1486,8 +1492,8 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     op->stamps_on = value != 0;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "ingest_mode") == 0) {  // int32 ingest loop (A/B only): 6 plain, 7 pipelined, 22 / 23 the same
-                                                // with the DQ2 deferred queue (23 also for MIN / MAX)
+  if (std::strcmp(key, "ingest_mode") == 0) {  // ingest loop (A/B only, launch_ingest): 7 pipelined without the DQ2
+                                                // queue; int32 COUNT / SUM also 6 plain, 22 plain + DQ2, 23 the default
     if (value != -1 && value != 6 && value != 7 && value != 22 && value != 23) return SCOTTY_ERR_ARG;
     op->ingest_mode = (int)value;
     return SCOTTY_OK;
@@ -1516,6 +1522,18 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (value != 0 && (value < 4096 || value > ((int64_t)1 << 40))) return SCOTTY_ERR_ARG;
     op->x_prefix = value;
     if (op->x) op->x->xq_prefix = value;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "quiet_ingest_mode") == 0) {  // exact engine's quiet pass: -1 default loop, 7 without DQ2 (A/B)
+    if (value != -1 && value != 7) return SCOTTY_ERR_ARG;
+    op->x_qmode = (int32_t)value;
+    if (op->x) op->x->xq_ingest_mode = op->x_qmode;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "quiet_ingest_blocks") == 0) {  // exact engine's quiet pass: ingest workgroups (A/B, 0 default)
+    if (value < 0 || value > 65536) return SCOTTY_ERR_ARG;
+    op->x_qblocks = value;
+    if (op->x) op->x->xq_ingest_blocks = value;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "shard_count_cells") == 0) {  // cells per rank record of the count path's exchange

@@ -359,52 +359,76 @@ struct WinScal {
 __device__ __forceinline__ bool ingest_window(const IngestArgs& a, int64_t* sc, int64_t* tw, uint16_t* lcix,
                                               int64_t b0, int64_t b1, bool defer, WinScal& ws) {
   const int tid = threadIdx.x;
-  // Window anchor: max ts over the block's first and last 64 tuples (a single endpoint may be an out-of-order
-  // tuple; a window placed below the block's in-order front sends most of its late tuples to global atomics)
+  // (1) the anchor (wave 0) and the operator's scalars (wave 1) in one round of loads.  The chain of dependent loads
+  //     is what this prologue costs every workgroup at once before any tuple streams (~10 us when one thread walked
+  //     the window cut through global memory), so every step below that can run wide does
   if (tid < 64) {
     int64_t x = INT64_MIN;
     if (b0 + tid < b1) x = max(a.ts[b0 + tid], a.ts[b1 - 1 - tid]);
     x = wmax64(x);
     if (tid == 0) sc[15] = x;
+  } else if (tid == 64) {
+    const DevMeta& m = *a.meta;
+    // An overflowed / refused interval: the cell-index build wrote no index this push (cix_build_kernel returns at
+    // once), so nothing may look at cix_meta -- a previous push's index (or never-written memory) would send the
+    // window search to an arbitrary cix entry.  The early return is decided before any index read.
+    sc[0] = m.overflow;
+    sc[1] = m.head; sc[2] = m.tail; sc[3] = m.j0; sc[4] = m.gcount;
+    sc[19] = m.view_s0_on ? m.view_s0 : INT64_MIN;
   }
   __syncthreads();
-  // An overflowed / refused interval: the cell-index build wrote no index this push (cix_build_kernel returns at
-  // once), so nothing below may look at cix_meta -- a previous push's index (or never-written memory) would send
-  // the window search to an arbitrary cix entry.  Decide the early return before any index read.
-  if (tid == 0) sc[0] = a.meta->overflow;
-  __syncthreads();
   if (sc[0] != 0) return false;  // an earlier push of this interval overflowed: nothing is committed until replay
+  // (2) one thread: the anchor's cell (cell index: one or two loads) -> the window's first cell
   if (tid == 0) {
-    const DevMeta& m = *a.meta;
-    int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
+    const int64_t head = sc[1], tail = sc[2], j0 = sc[3], gcount = sc[4];
     int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
     if (kc < 0) kc = 0;
-    int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
-    CellView cv = make_view(a, m, head, tail, j0, kc, h_end);
-    int64_t ctot = cv.c_old + kc;
-    int64_t first_start = cv.start(0);
+    const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
+    const int64_t* t0p = a.s_tstart + head;
+    const int64_t s0 = tail > head ? (sc[19] != INT64_MIN ? sc[19] : t0p[0]) : 0;
+    const CellView cv{t0p, a.grid + j0, tail - head, kc, h_end, s0};
+    const int64_t ctot = cv.c_old + kc;
+    const int64_t first_start = cv.start(0);
     const int64_t cbase = a.cix_meta[0], cshift = a.cix_meta[1], cn = a.cix_meta[2];
     const int64_t c_full = a.cix_meta[3], span_end = a.cix_meta[4];
     const CellIndex cx0{a.cix, cbase, cn, ctot, c_full, span_end, (int)cshift};
-    int64_t x = sc[15];
+    const int64_t x = sc[15];
     int64_t chi;
     if (x < first_start) chi = 0;
     else if (x >= h_end) chi = ctot - 1;
     else chi = cx0.find(cv, x);
-    int64_t wbase = max((int64_t)0, chi + 16 - WCAP);
-    int64_t wn = min((int64_t)WCAP, ctot - wbase);
-    {  // every window cell ends within 2^32 - 1 of the window's first start (the LDS keeps 32-bit tmax offsets)
-      const int64_t tws = cv.start(wbase);
-      int64_t l_ = 0, h_ = wn;  // largest w <= wn with start(wbase + w) - tws <= 2^32 - 1 (starts increase)
-      while (l_ < h_) {
-        const int64_t mid = (l_ + h_ + 1) >> 1;
-        if ((uint64_t)(cv.start(wbase + mid) - tws) <= 0xFFFFFFFFull) l_ = mid; else h_ = mid - 1;
-      }
-      wn = l_;
+    const int64_t wbase = max((int64_t)0, chi + 16 - WCAP);
+    sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
+    sc[7] = wbase; sc[8] = min((int64_t)WCAP, ctot - wbase);
+    sc[9] = cbase; sc[10] = cshift; sc[11] = cn;
+    sc[14] = ctot;
+    sc[16] = c_full;
+    sc[17] = span_end;
+    sc[19] = s0;
+  }
+  __syncthreads();
+  // block-uniform scalars: readfirstlane keeps them in SGPRs (an LDS load alone yields VGPRs)
+  const int64_t head = uni64(sc[1]), tail = uni64(sc[2]), j0 = uni64(sc[3]), kc = uni64(sc[4]);
+  const int64_t h_end = uni64(sc[5]), first_start = uni64(sc[6]);
+  const int64_t wbase = uni64(sc[7]), wn0 = uni64(sc[8]);
+  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end, uni64(sc[19])};
+  const CellIndex cx{a.cix, uni64(sc[9]), uni64(sc[11]), uni64(sc[14]), uni64(sc[16]), uni64(sc[17]),
+                     (int)uni64(sc[10])};
+  // (3) every thread: the window's cell starts, one round of loads
+  for (int64_t i = tid; i <= wn0; i += 256) tw[i] = cv.start(wbase + i);
+  __syncthreads();
+  // (4) one thread, in LDS: the window cut so every cell of it ends within 2^32 - 1 of its first start (the LDS keeps
+  //     32-bit tmax offsets; starts increase), the staged part of the cell index
+  if (tid == 0) {
+    const int64_t tws = tw[0];
+    int64_t l_ = 0, h_ = wn0;  // largest w <= wn0 with tw[w] - tws <= 2^32 - 1
+    while (l_ < h_) {
+      const int64_t mid = (l_ + h_ + 1) >> 1;
+      if ((uint64_t)(tw[mid] - tws) <= 0xFFFFFFFFull) l_ = mid; else h_ = mid - 1;
     }
-    sc[1] = head; sc[2] = tail; sc[3] = j0; sc[4] = kc; sc[5] = h_end; sc[6] = first_start;
-    sc[7] = wbase; sc[8] = wn;
-    const int64_t twa = cv.start(wbase), twb = cv.start(wbase + wn);
+    const int64_t wn = l_;
+    const int64_t cbase = cx.base, cshift = cx.shift, cn = cx.n, span_end = cx.span_end;
+    const int64_t twa = tw[0], twb = tw[wn];
     // stage the cell index for the most recent part of the window (out-of-order tuples are mostly recent)
     int64_t k0 = (int64_t)((uint64_t)(twa - cbase) >> cshift);
     const int64_t kl = (int64_t)((uint64_t)(twb - 1 - cbase) >> cshift);
@@ -412,26 +436,17 @@ __device__ __forceinline__ bool ingest_window(const IngestArgs& a, int64_t* sc, 
     int64_t lcn = (twb != INT64_MAX && twb > twa) ? kl - k0 + 2 : 0;  // staged entries (0: LDS binary search)
     if (lcn > cn - k0) lcn = max((int64_t)0, cn - k0);                 // only entries of the built index
     if (twb > span_end && lcn > 0) lcn = max((int64_t)0, min(lcn, ((span_end - 1 - cbase) >> cshift) - k0));
-    sc[9] = cbase; sc[10] = cshift; sc[11] = cn; sc[12] = k0;
+    sc[8] = wn;
+    sc[12] = k0;
     sc[13] = lcn;
-    sc[14] = ctot;
-    sc[16] = c_full;
-    sc[17] = span_end;
     // deferred queue: time offsets from the window's first start must fit 32 bits
     sc[18] = (defer && twb != INT64_MAX && (uint64_t)(twb - twa) < 0xFFFFFFFFull) ? 1 : 0;
-    sc[19] = cv.s0;
   }
   __syncthreads();
-  // block-uniform scalars: readfirstlane keeps them in SGPRs (an LDS load alone yields VGPRs)
-  const int64_t head = uni64(sc[1]), tail = uni64(sc[2]), j0 = uni64(sc[3]), kc = uni64(sc[4]);
-  const int64_t h_end = uni64(sc[5]), first_start = uni64(sc[6]);
-  const int64_t wbase = uni64(sc[7]), wn = uni64(sc[8]);
-  const CellView cv{a.s_tstart + head, a.grid + j0, tail - head, kc, h_end, uni64(sc[19])};
-  const CellIndex cx{a.cix, uni64(sc[9]), uni64(sc[11]), uni64(sc[14]), uni64(sc[16]), uni64(sc[17]),
-                     (int)uni64(sc[10])};
+  const int64_t wn = uni64(sc[8]);
   const int64_t lk0 = uni64(sc[12]), lcn = uni64(sc[13]);
   const bool qok = uni64(sc[18]) != 0;
-  for (int64_t i = tid; i <= wn; i += 256) tw[i] = cv.start(wbase + i);
+  // (5) every thread: the staged cell index, one round of loads
   for (int64_t i = tid; i < lcn; i += 256) {
     const int64_t kk = lk0 + i;
     int64_t v = (int64_t)cx.cix[kk];
@@ -500,6 +515,48 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
   const int64_t per_block = a.per_wave * 4;
   const int64_t b0 = (int64_t)blockIdx.x * per_block;
   const int64_t b1 = min(a.n, b0 + per_block);
+  const int64_t w0 = b0 + (int64_t)wid * a.per_wave;
+  const int64_t w1 = min(b1, w0 + a.per_wave);
+  constexpr bool PIPE = (MODE & 1) != 0;
+  constexpr bool NTL = (MODE & 2) != 0;
+  const V* vp = (const V*)a.val;
+  typedef long long v2i64 __attribute__((ext_vector_type(2)));
+  typedef int v2i32 __attribute__((ext_vector_type(2)));
+  auto ld2 = [&](const void* p) -> v2i64 {
+    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(p));
+    else return *reinterpret_cast<const v2i64*>(p);
+  };
+  auto ld2i = [&](const void* p) -> v2i32 {
+    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const v2i32*>(p));
+    else return *reinterpret_cast<const v2i32*>(p);
+  };
+  struct Step {
+    v2i64 ta, tb;
+    typename std::conditional<VT == VT_I32, v2i32, v2i64>::type va, vb;
+  };
+  auto load_step = [&](int64_t s, Step& st) {
+    const int64_t i0 = s + 2 * lane, i1 = s + 128 + 2 * lane;
+    st.ta = ld2(a.ts + i0);
+    st.tb = ld2(a.ts + i1);
+    if constexpr (VT == VT_I32) {
+      st.va = ld2i(vp + i0);
+      st.vb = ld2i(vp + i1);
+    } else {
+      st.va = ld2(vp + i0);
+      st.vb = ld2(vp + i1);
+    }
+  };
+  const int64_t w1_full = w0 + ((w1 - w0) / 256) * 256;  // end of the full steps
+  // PIPE: the wave's first two steps are loaded before the prologue (they depend on nothing it computes), so the
+  // window setup overlaps the first HBM round trip instead of preceding it
+  Step pre0{}, pre1{};
+  if constexpr (PIPE) {
+    const int64_t nfull = (w1_full - w0) / 256;
+    if (nfull > 0) {
+      load_step(w0, pre0);
+      load_step(nfull > 1 ? w0 + 256 : w0, pre1);
+    }
+  }
 
   // phase stamps (debugging aid): start, window ready, waves' ranges done, LDS window flushed
   auto stamp = [&](int k) {
@@ -541,9 +598,6 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     }
     return l;
   };
-
-  const int64_t w0 = b0 + (int64_t)wid * a.per_wave;
-  const int64_t w1 = min(b1, w0 + a.per_wave);
 
   Acc<VT, NEED> acc;
   acc.reset();
@@ -644,35 +698,6 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     qn = rem;
   };
 
-  constexpr bool PIPE = (MODE & 1) != 0;
-  constexpr bool NTL = (MODE & 2) != 0;
-  const V* vp = (const V*)a.val;
-  typedef long long v2i64 __attribute__((ext_vector_type(2)));
-  typedef int v2i32 __attribute__((ext_vector_type(2)));
-  auto ld2 = [&](const void* p) -> v2i64 {
-    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(p));
-    else return *reinterpret_cast<const v2i64*>(p);
-  };
-  auto ld2i = [&](const void* p) -> v2i32 {
-    if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const v2i32*>(p));
-    else return *reinterpret_cast<const v2i32*>(p);
-  };
-  struct Step {
-    v2i64 ta, tb;
-    typename std::conditional<VT == VT_I32, v2i32, v2i64>::type va, vb;
-  };
-  auto load_step = [&](int64_t s, Step& st) {
-    const int64_t i0 = s + 2 * lane, i1 = s + 128 + 2 * lane;
-    st.ta = ld2(a.ts + i0);
-    st.tb = ld2(a.ts + i1);
-    if constexpr (VT == VT_I32) {
-      st.va = ld2i(vp + i0);
-      st.vb = ld2i(vp + i1);
-    } else {
-      st.va = ld2(vp + i0);
-      st.vb = ld2(vp + i1);
-    }
-  };
   auto unpack = [&](const Step& st, int64_t (&t)[4], V (&v)[4]) {
     t[0] = st.ta.x; t[1] = st.ta.y; t[2] = st.tb.x; t[3] = st.tb.y;
     if constexpr (VT == VT_F64) {
@@ -775,7 +800,6 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
       }
     }
   };
-  const int64_t w1_full = w0 + ((w1 - w0) / 256) * 256;  // end of the full steps
   if constexpr (PIPE) {
     // two full steps in flight ahead of the one being combined; loads are unconditional (a step index past the
     // wave's range is clamped to its last full step), so no load sits under a branch whose join would drain them
@@ -783,9 +807,7 @@ __global__ __launch_bounds__(256) void ingest_kernel(IngestArgs a) {
     const int64_t last = w0 + (nfull - 1) * 256;
     auto cl = [&](int64_t x) { return x < last ? x : last; };
     if (nfull > 0) {
-      Step b0, b1;
-      load_step(w0, b0);
-      load_step(cl(w0 + 256), b1);
+      Step b0 = pre0, b1 = pre1;  // (loaded before the prologue: w0 and cl(w0 + 256))
       const int64_t npair = nfull / 2;
       for (int64_t k = 0; k < npair; k++) {
         const int64_t s = w0 + k * 512;
@@ -1495,20 +1517,21 @@ static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStrea
 }
 
 // non-temporal loads + deferred out-of-order queue, no software pipelining (A/B: profiles/r01/ab_ingest_modes.json,
-// profiles/r02/)
+// profiles/r02/): int64 / double SUM / COUNT configurations (not measured with the loops below)
 constexpr int DEFAULT_MODE = 6;
 
-// MIN / MAX partials: software-pipelined as well (MM_MODE = 7; A/B r03m on C3: 0.258 -> 0.227 ms per 2^26 tuples).  Their
-// larger LDS window leaves 3 workgroups per CU instead of 4, and two steps in flight per wave make up the bytes in
-// flight; SUM / COUNT configurations measured equal with it (r02c) and keep the plain loop
-constexpr int MM_MODE = 7;
-// int32 COUNT / SUM: the software-pipelined loop as well (r04h, same box, C2s: 346 -> 332 us; C2 in order, see
-// INGEST_STREAMING); int64 / double values keep the plain loop (not measured with it)
-// TM: 8 (per-tile minima, a.tilemin) or 0
-template <int VT, int TM>
+// The software-pipelined loop with the DQ2 deferred queue (MODE 23 = 1 | 2 | 4 | 16) for int32 values and for every
+// MIN / MAX configuration.  Pipelining: MIN / MAX r03m on C3 0.258 -> 0.227 ms per 2^26 tuples, int32 SUM r04h on C2s
+// 346 -> 332 us.  DQ2 (one DPP scan per step places the step's out-of-order tuples, folds in full passes of 64): C2s
+// 0.337 -> 0.309 ms at 768 workgroups (profiles/r05/ab_c2s_dq2_blocks.json), C3's quiet ingest 0.204 -> 0.190 ms
+// (profiles/r05/ab_c3_dq2.json); the loop without it stays for A/B (scotty_tune "ingest_mode" 7)
+constexpr int MM_MODE = 23;
+// TM: 8 (per-tile minima, a.tilemin) or 0; DQ: 16 (the DQ2 queue) or 0
+template <int VT, int TM, int DQ = 16>
 static hipError_t launch_ingest_vt(const IngestArgs& a, int need, int64_t nblocks, hipStream_t st) {
-  constexpr int SUM_MODE = (VT == VT_I32 ? MM_MODE : DEFAULT_MODE) | TM;
-  constexpr int MMM = MM_MODE | TM;
+  constexpr int PM = (MM_MODE & ~16) | DQ;
+  constexpr int SUM_MODE = (VT == VT_I32 ? PM : DEFAULT_MODE) | TM;
+  constexpr int MMM = PM | TM;
   switch (need) {
     case 0: return launch_ingest_t<VT, 0, SUM_MODE>(a, nblocks, st);
     case 1: return launch_ingest_t<VT, 1, SUM_MODE>(a, nblocks, st);
@@ -1553,37 +1576,33 @@ hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// mode: -1 the default; INGEST_STREAMING (an in-order stream); 6 / 7 the int32 COUNT / SUM loop (A/B, scotty_tune
-// "ingest_mode": plain / software-pipelined)
-// a.tilemin non-null: the default loop with per-tile minima (mode ignored)
+// mode: -1 the default (MM_MODE / DEFAULT_MODE); INGEST_STREAMING (an in-order stream: the default loop on fewer
+// workgroups); for A/B (scotty_tune "ingest_mode" / the exact engine's "quiet_ingest_mode"): 7 the pipelined loop
+// without the DQ2 queue, and for int32 COUNT / SUM 6 plain, 22 plain with DQ2, 23 the default.
+// a.tilemin non-null (the exact engine's quiet pass): the default loops with per-tile minima (7: without DQ2)
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode) {
   const int nd = need & (NEED_SUM | NEED_MIN | NEED_MAX);
   if (a.tilemin) {
+    if (mode == 7) {
+      if (vt == VT_I32) return launch_ingest_vt<VT_I32, 8, 0>(a, need, nblocks, st);
+      if (vt == VT_I64) return launch_ingest_vt<VT_I64, 8, 0>(a, need, nblocks, st);
+      return launch_ingest_vt<VT_F64, 8, 0>(a, need, nblocks, st);
+    }
     if (vt == VT_I32) return launch_ingest_vt<VT_I32, 8>(a, need, nblocks, st);
     if (vt == VT_I64) return launch_ingest_vt<VT_I64, 8>(a, need, nblocks, st);
     return launch_ingest_vt<VT_F64, 8>(a, need, nblocks, st);
   }
-  if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 22 || mode == 23)) {  // DQ2 queue (A/B)
+  if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 6 || mode == 22)) {
     if (mode == 22) return nd ? launch_ingest_t<VT_I32, NEED_SUM, 22>(a, nblocks, st)
                               : launch_ingest_t<VT_I32, 0, 22>(a, nblocks, st);
-    return nd ? launch_ingest_t<VT_I32, NEED_SUM, 23>(a, nblocks, st) : launch_ingest_t<VT_I32, 0, 23>(a, nblocks, st);
+    return nd ? launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st) : launch_ingest_t<VT_I32, 0, 6>(a, nblocks, st);
   }
-  if (vt == VT_I32 && (nd & (NEED_MIN | NEED_MAX)) && mode == 23) {  // MIN / MAX with the DQ2 queue (A/B)
-    switch (nd) {
-      case 2: return launch_ingest_t<VT_I32, 2, 23>(a, nblocks, st);
-      case 3: return launch_ingest_t<VT_I32, 3, 23>(a, nblocks, st);
-      case 4: return launch_ingest_t<VT_I32, 4, 23>(a, nblocks, st);
-      case 5: return launch_ingest_t<VT_I32, 5, 23>(a, nblocks, st);
-      case 6: return launch_ingest_t<VT_I32, 6, 23>(a, nblocks, st);
-      default: return launch_ingest_t<VT_I32, 7, 23>(a, nblocks, st);
-    }
+  if (mode == 7) {
+    if (vt == VT_I32) return launch_ingest_vt<VT_I32, 0, 0>(a, need, nblocks, st);
+    if (vt == VT_I64) return launch_ingest_vt<VT_I64, 0, 0>(a, need, nblocks, st);
+    return launch_ingest_vt<VT_F64, 0, 0>(a, need, nblocks, st);
   }
-  if (vt == VT_I32 && (nd == 0 || nd == NEED_SUM) && (mode == 6 || mode == 7 || mode == INGEST_STREAMING)) {
-    if (mode == 6) return nd ? launch_ingest_t<VT_I32, NEED_SUM, 6>(a, nblocks, st)
-                             : launch_ingest_t<VT_I32, 0, 6>(a, nblocks, st);
-    // in order (INGEST_STREAMING) or 7: the software-pipelined loop, two steps of loads in flight
-    return nd ? launch_ingest_t<VT_I32, NEED_SUM, 7>(a, nblocks, st) : launch_ingest_t<VT_I32, 0, 7>(a, nblocks, st);
-  }
+  // -1, 23, INGEST_STREAMING: the default loops
   if (vt == VT_I32) return launch_ingest_vt<VT_I32, 0>(a, need, nblocks, st);
   if (vt == VT_I64) return launch_ingest_vt<VT_I64, 0>(a, need, nblocks, st);
   return launch_ingest_vt<VT_F64, 0>(a, need, nblocks, st);
