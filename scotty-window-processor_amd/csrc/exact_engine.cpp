@@ -23,6 +23,7 @@ hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group);
 hipError_t launch_wm_blocks(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st);
+hipError_t launch_lane_session(const XBatchArgs& a, int vt, hipStream_t st);
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st);
 hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
@@ -1360,7 +1361,9 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
     a.sl = sl;
     a.ss = ss;
     if (!lane_mode()) prefix_stale = true;  // the wavefront replay does not track the lane path's slice prefixes
-    XCHK(lane_mode() ? launch_lane_replay(a, cfg, stream) : launch_replay(a, vt, stream));
+    XCHK(lane_mode()           ? launch_lane_replay(a, cfg, stream)
+         : lane_session_mode() ? launch_lane_session(a, vt, stream)
+                               : launch_replay(a, vt, stream));
     XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
     if (h_misc[0] == 0 && h_misc[1] == 0 && h_misc[2] == 0) return SCOTTY_OK;

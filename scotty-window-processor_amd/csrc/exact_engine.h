@@ -111,6 +111,15 @@ class XEngine {
   bool lane_mode() const {  // keyed_lane.hip: context-free time windows on Eager slices only
     return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && !records && cfg.n_cf > 0;
   }
+  bool lane_session_off = false;  // keyed: sessions through the wavefront replay instead (A/B, "keyed_lane_session" 0)
+  // keyed_lane_session.hip: time-measured session windows (beside context-free time windows) on Eager slices
+  bool lane_session_mode() const {
+    if (!keyed || lane_session_off || cfg.n_ctx == 0 || cfg.has_count || cfg.lazy || records || !cfg.has_time)
+      return false;
+    for (int k = 0; k < cfg.n_ctx; k++)
+      if (cfg.ctx_measure[k] != 0) return false;
+    return true;
+  }
   // non-keyed: the single-wavefront replay (LazySlice record sets live only there)
   bool use_serial() const { return serial || records; }
   bool records = false;   // LazySlice record sets kept (XCfg.records)

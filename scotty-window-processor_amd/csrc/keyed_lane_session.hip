@@ -1,0 +1,519 @@
+// keyed_lane_session.hip -- one LANE per key for keyed operators with session windows (KeyedScottyWindowOperator over
+// SessionWindow, flink-connector/.../KeyedScottyWindowOperator.java:56-86, C/windowType/SessionWindow.java:40-116),
+// beside any context-free time windows, on Eager slices.
+//
+// The wavefront replay (exact_kernels.hip replay_kernel) gives each key a whole wavefront: right for a few keys with
+// long micro-batches, but at 10^5-10^6 keys a key brings ~64 tuples per batch and its wavefront spends most of its life
+// waiting on that key's cold slice and session lines, one dependent access after another (C4s: 24 ms per 2^26-tuple
+// batch at 1 M keys, three wavefronts per SIMD).  Here a lane walks its key's tuples in arrival order with the
+// reference's per-tuple state machine as scalar code -- StreamSlicer.determineSlices (S/StreamSlicer.java:36-130),
+// SliceManager.processElement / checkSliceEdges / splitSlice (S/SliceManager.java:27-192), SessionContext.updateContext
+// (SessionWindow.java:40-98) -- so the 64 keys of a wavefront wait on memory together.  The state layout (XState, slice
+// SoA, session columns) is the wavefront replay's, restated operation for operation from exact_op.h's Op with
+// sequential loops where Op uses the wavefront's lanes; configurations move freely between the two kernels (scotty_tune
+// "keyed_lane_session" 0 runs the wavefront replay instead, the A/B and the parity test's reference).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "exact_common.h"
+#include "exact_op.h"
+
+namespace scotty {
+namespace ls {
+using namespace x;
+
+template <int VT>
+struct LaneS {
+  const XCfg* c;
+  XSlices sl;     // the store's columns (uniform); this key's slice i is element b + i
+  int64_t b;
+  int64_t sb;     // this key's session base: context k, session i at sb + k * sesscap + i
+  XState s;
+  int32_t exc;
+
+  __device__ int64_t& TS(int i) const { return sl.ts[b + i]; }
+  __device__ int64_t& TE(int i) const { return sl.te[b + i]; }
+  __device__ int64_t& TL(int i) const { return sl.tl[b + i]; }
+  __device__ int64_t& TF(int i) const { return sl.tf[b + i]; }
+  __device__ int64_t& CS(int i) const { return sl.cs[b + i]; }
+  __device__ int64_t& CL(int i) const { return sl.cl[b + i]; }
+  __device__ int32_t& TY(int i) const { return sl.ty[b + i]; }
+  __device__ unsigned long long& CNT(int i) const { return sl.cnt[b + i]; }
+  __device__ unsigned long long& P(int k, int i) const { return sl.p[k][b + i]; }
+  __device__ int64_t* SSp(const XSess& x, int k) const { return x.start + sb + (int64_t)k * c->sesscap; }
+
+  // ---------------------------------------------------------------- slice list primitives (exact_op.h Op)
+  __device__ void copy_slice(int dst, int src) {
+    TS(dst) = TS(src); TE(dst) = TE(src); TL(dst) = TL(src); TF(dst) = TF(src);
+    CS(dst) = CS(src); CL(dst) = CL(src); TY(dst) = TY(src);
+    CNT(dst) = CNT(src); P(0, dst) = P(0, src); P(1, dst) = P(1, src); P(2, dst) = P(2, src);
+  }
+  __device__ void move_range(int dst, int src, int n) {
+    if (n <= 0 || dst == src) return;
+    if (dst < src) {
+      for (int i = 0; i < n; i++) copy_slice(dst + i, src + i);
+    } else {
+      for (int i = n - 1; i >= 0; i--) copy_slice(dst + i, src + i);
+    }
+  }
+  __device__ bool ensure_room() {
+    if (s.tail < c->sc) return true;
+    if (s.head == 0) {
+      exc = XERR_SLICE_CAP;
+      return false;
+    }
+    move_range(0, s.head, s.tail - s.head);
+    s.tail -= s.head;
+    s.head = 0;
+    return true;
+  }
+  __device__ void init_slice(int i, int64_t start, int64_t end, int64_t c_s, int64_t c_l, int32_t type) {
+    TS(i) = start; TE(i) = end; TL(i) = start; TF(i) = JMAX; CS(i) = c_s; CL(i) = c_l; TY(i) = type;
+    CNT(i) = 0; P(0, i) = 0; P(1, i) = (unsigned long long)ID_MIN; P(2, i) = (unsigned long long)ID_MAX;
+  }
+  __device__ void note_order(int i) {
+    if (i > s.head && TS(i - 1) > TS(i)) s.unsorted |= 1;
+    if (i + 1 < s.tail && TS(i) > TS(i + 1)) s.unsorted |= 1;
+  }
+  __device__ int insert_at(int i) {
+    const int rel = i - s.head;
+    if (!ensure_room()) return -1;
+    i = s.head + rel;
+    move_range(i + 1, i, s.tail - i);
+    s.tail++;
+    return i;
+  }
+  __device__ void remove_at(int i) {
+    move_range(i, i + 1, s.tail - i - 1);
+    s.tail--;
+  }
+  __device__ bool valid(int i) {
+    if (i < s.head || i >= s.tail) {
+      exc = XERR_INDEX;
+      return false;
+    }
+    return true;
+  }
+  // LazyAggregateStore.findSliceIndexByTimestamp (:29-37): last slice with tStart <= t, -1 if none.  A sorted list is
+  // searched by galloping down from the tail (an out-of-order tuple mostly lands in one of the last slices: one or
+  // two loads instead of a bisection's chain); an unsorted one backwards, as the reference's loop runs
+  __device__ int find_ts(int64_t t) const {
+    if (s.tail <= s.head) return -1;
+    if (!(s.unsorted & 1)) {
+      int hi = s.tail - 1;
+      if (TS(hi) <= t) return hi;
+      int step = 1, lo;
+      for (;;) {  // TS(hi) > t
+        const int nx = hi - step;
+        if (nx <= s.head) {
+          if (TS(s.head) > t) return -1;
+          lo = s.head;
+          break;
+        }
+        if (TS(nx) <= t) {
+          lo = nx;
+          break;
+        }
+        hi = nx;
+        step <<= 1;
+      }
+      while (hi - lo > 1) {  // TS(lo) <= t < TS(hi)
+        const int m = (lo + hi) >> 1;
+        if (TS(m) <= t) lo = m; else hi = m;
+      }
+      return lo;
+    }
+    for (int i = s.tail - 1; i >= s.head; i--)
+      if (TS(i) <= t) return i;
+    return -1;
+  }
+  // LazyAggregateStore.findSliceByEnd (:127-135)
+  __device__ int find_end(int64_t e) const {
+    for (int i = s.tail - 1; i >= s.head; i--)
+      if (TE(i) == e) return i;
+    return -1;
+  }
+  // AbstractSlice.addElement + AggregateState.addElement (one tuple, exact)
+  __device__ void add_element(int i, int64_t t, int64_t vbits) {
+    TL(i) = max(TL(i), t);
+    TF(i) = min(TF(i), t);
+    CL(i) = jadd(CL(i), 1);
+    CNT(i) = CNT(i) + 1;
+    const Lift l = lift(VT, vbits);
+    if (c->need & NEED_SUM) {
+      if (VT == VT_F64)
+        P(0, i) = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)P(0, i)) +
+                                                           __longlong_as_double((long long)l.sum));
+      else
+        P(0, i) = P(0, i) + l.sum;
+    }
+    if (c->need & NEED_MIN) P(1, i) = (unsigned long long)min((int64_t)P(1, i), l.mn);
+    if (c->need & NEED_MAX) P(2, i) = (unsigned long long)max((int64_t)P(2, i), l.mx);
+  }
+  // SliceManager.appendSlice (S/SliceManager.java:27-38)
+  __device__ void append_slice(int64_t start, int32_t type) {
+    if (s.tail > s.head) {
+      const int k = s.tail - 1;
+      TE(k) = start;
+      TY(k) = type;
+    }
+    if (!ensure_room()) return;
+    const int i = s.tail;
+    init_slice(i, start, JMAX, s.currentCount, s.currentCount, 1);
+    s.tail++;
+    if (i > s.head && TS(i - 1) > start) s.unsorted |= 1;
+  }
+  // SliceManager.splitSlice (S/SliceManager.java:168-192); Eager slices move no tuples
+  __device__ void split_slice(int idx, int64_t timestamp) {
+    if (!valid(idx)) return;
+    int a = idx;
+    int bpos;
+    if (timestamp < TE(a)) {
+      bpos = a + 1;
+    } else if (idx + 1 < s.tail) {
+      a = idx + 1;
+      bpos = idx + 2;
+    } else {
+      return;
+    }
+    const int64_t a_end = TE(a), a_cs = CS(a), a_cl = CL(a);
+    const int32_t a_ty = TY(a);
+    const int rel_a = a - s.head;
+    bpos = insert_at(bpos);
+    if (bpos < 0) return;
+    a = s.head + rel_a;
+    init_slice(bpos, timestamp, a_end, a_cs, a_cl, ty_kind(a_ty));
+    TE(a) = timestamp;
+    TY(a) = 1;
+    note_order(bpos);
+  }
+  // AbstractSlice.merge + LazyAggregateStore.mergeSlice (:119-124)
+  __device__ void merge_slice(int idx) {
+    if (!valid(idx) || !valid(idx + 1)) return;
+    const int q = idx + 1;
+    TL(idx) = max(TL(idx), TL(q));
+    TF(idx) = min(TF(idx), TF(q));
+    TE(idx) = max(TE(idx), TE(q));
+    CNT(idx) = CNT(idx) + CNT(q);
+    if (VT == VT_F64)
+      P(0, idx) = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)P(0, idx)) +
+                                                           __longlong_as_double((long long)P(0, q)));
+    else
+      P(0, idx) = P(0, idx) + P(0, q);
+    P(1, idx) = (unsigned long long)min((int64_t)P(1, idx), (int64_t)P(1, q));
+    P(2, idx) = (unsigned long long)max((int64_t)P(2, idx), (int64_t)P(2, q));
+    remove_at(q);
+  }
+  // SliceManager.checkSliceEdges (S/SliceManager.java:89-166), modifications in insertion order
+  __device__ void check_slice_edges(const Mod* mods, int nm) {
+    for (int k = 0; k < nm && !exc; k++) {
+      const Mod m = mods[k];
+      if (m.kind == 0) {  // ShiftModification
+        const int si = find_end(m.pre);
+        if (si == -1) continue;
+        const int32_t st = TY(si);
+        if (ty_movable(st)) {
+          if (!valid(si + 1)) return;
+          TE(si) = m.post;
+          TS(si + 1) = m.post;
+          s.unsorted |= 2;
+          note_order(si + 1);
+        } else {
+          if (!ty_fixed(st)) TY(si) = ty_flex(st - 1);
+          split_slice(si, m.post);
+        }
+      } else if (m.kind == 1) {  // DeleteModification
+        const int si = find_end(m.pre);
+        if (si >= 0) {
+          const int32_t st = TY(si);
+          if (ty_movable(st)) {
+            if (!valid(si + 1)) return;
+            merge_slice(si);
+          } else if (!ty_fixed(st)) {
+            TY(si) = ty_flex(st - 1);
+          }
+        }
+      } else {  // AddModification
+        const int si = find_ts(m.post);
+        if (!valid(si)) return;
+        if (TS(si) != m.post && TE(si) != m.post) split_slice(si, m.post);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- SessionContext (SessionWindow.java:40-116)
+  __device__ void add_window(const XSess& x, int k, int i, int64_t start, int64_t end, Mod* mods, int& nm) {
+    const int n = s.ns(k);  // WindowContext :19-25
+    if (i < 0 || i > n) {
+      exc = XERR_INDEX;
+      return;
+    }
+    if (n >= c->sesscap) {
+      exc = XERR_SESS_CAP;
+      return;
+    }
+    int64_t* st = SSp(x, k);
+    int64_t* en = x.end + (st - x.start);
+    for (int q = n; q > i; q--) {
+      st[q] = st[q - 1];
+      en[q] = en[q - 1];
+    }
+    st[i] = start;
+    en[i] = end;
+    s.set_ns(k, n + 1);
+    if (mods && nm + 2 <= XMAXMODS) {
+      mods[nm++] = Mod{2, 0, start};
+      mods[nm++] = Mod{2, 0, end};
+    }
+  }
+  __device__ void remove_window(const XSess& x, int k, int i, Mod* mods, int& nm) {  // :48-52
+    const int n = s.ns(k);
+    if (i < 0 || i >= n) {
+      exc = XERR_INDEX;
+      return;
+    }
+    int64_t* st = SSp(x, k);
+    int64_t* en = x.end + (st - x.start);
+    if (mods && nm + 2 <= XMAXMODS) {
+      mods[nm++] = Mod{1, st[i], 0};
+      mods[nm++] = Mod{1, en[i], 0};
+    }
+    for (int q = i; q < n - 1; q++) {
+      st[q] = st[q + 1];
+      en[q] = en[q + 1];
+    }
+    s.set_ns(k, n - 1);
+  }
+  __device__ void merge_with_pre(const XSess& x, int k, int idx, Mod* mods, int& nm) {  // :39-46
+    if (idx < 0 || idx >= s.ns(k) || idx - 1 < 0) {
+      exc = XERR_INDEX;
+      return;
+    }
+    int64_t* en = x.end + (SSp(x, k) - x.start);
+    en[idx - 1] = en[idx];  // shiftEnd records no modification
+    remove_window(x, k, idx, mods, nm);
+  }
+  __device__ int get_session(const XSess& x, int k, int64_t pos) const {  // :89-101
+    const int64_t gap = c->gap[k];
+    const int n = s.ns(k);
+    const int64_t* st = SSp(x, k);
+    const int64_t* en = x.end + (st - x.start);
+    int i = 0;
+    for (; i < n; i++) {
+      const int64_t a = st[i], e = en[i];
+      if (jsub(a, gap) <= pos && jadd(e, gap) >= pos) return i;
+      if (jsub(a, gap) > pos) return i - 1;
+    }
+    return i - 1;
+  }
+  __device__ void session_update(const XSess& x, int k, int64_t pos, Mod* mods, int& nm) {  // :42-87
+    const int64_t gap = c->gap[k];
+    const int n = s.ns(k);
+    if (n == 0) {  // hasActiveWindows() returns isEmpty() (WindowContext.java:15-17)
+      add_window(x, k, 0, pos, pos, mods, nm);
+      return;
+    }
+    int64_t* st = SSp(x, k);
+    int64_t* en = x.end + (st - x.start);
+    // a position at or past the last session's end: getSession returns the last session (every earlier one ends more
+    // than a gap before the last one starts), so only the shiftEnd / new-session branches can apply
+    const int64_t le = en[n - 1];
+    int si;
+    if (pos >= le && pos >= st[n - 1]) {
+      si = n - 1;
+    } else {
+      si = get_session(x, k, pos);
+      if (si == -1) {
+        add_window(x, k, 0, pos, pos, mods, nm);
+        return;
+      }
+    }
+    const int64_t a = st[si], e = en[si];
+    if (jsub(a, gap) > pos) {
+      add_window(x, k, si, pos, pos, mods, nm);
+    } else if (a > pos && jsub(a, gap) < pos) {
+      if (mods && nm < XMAXMODS) mods[nm++] = Mod{0, a, pos};  // shiftStart
+      st[si] = pos;
+      if (si > 0) {
+        if (jadd(en[si - 1], gap) >= st[si]) merge_with_pre(x, k, si, mods, nm);
+      }
+    } else if (e < pos && jadd(e, gap) >= pos) {
+      en[si] = pos;  // shiftEnd
+      if (si < s.ns(k) - 1) {
+        if (jadd(en[si], gap) >= st[si + 1]) merge_with_pre(x, k, si + 1, mods, nm);
+      }
+    } else if (jadd(e, gap) < pos) {
+      add_window(x, k, si + 1, pos, pos, mods, nm);
+    }
+  }
+
+  // ---------------------------------------------------------------- StreamSlicer (S/StreamSlicer.java:36-130)
+  __device__ int64_t next_fixed_edge(int64_t te_) const {  // calculateNextFixedEdge (:103-116)
+    const int64_t cur = s.nextEdgeTs == JMIN ? JMAX : s.nextEdgeTs;
+    const int64_t t_c = max(jsub(te_, c->max_lateness), cur);
+    int64_t e = JMAX;
+    for (int w = 0; w < c->n_cf; w++) {
+      if (c->cf_measure[w] != 0) continue;
+      const int kd = c->cf_kind[w];
+      const int64_t wa = c->cf_a[w], wb = c->cf_b[w];
+      int64_t r;
+      if (kd == 0) r = jsub(jadd(t_c, wa), jmod(t_c, wa));
+      else if (kd == 1) r = jsub(jadd(t_c, wb), jmod(t_c, wb));
+      else if (t_c == JMAX || t_c < wa) r = wa;
+      else if (t_c >= wa && t_c < jadd(wa, wb)) r = jadd(wa, wb);
+      else r = JMAX;
+      e = min(e, r);
+    }
+    return e;
+  }
+  __device__ int flex_count(int64_t te_) const {  // calculateNextFlexEdge (:118-130)
+    const int64_t t_c = max(s.maxEventTime, s.nextEdgeTs);
+    int flex = 0;
+    for (int k = 0; k < c->n_ctx; k++)
+      if (te_ >= jadd(t_c, c->gap[k])) flex++;
+    return flex;
+  }
+  __device__ void determine_slices(int64_t te_) {  // :36-86 (time measure only: no count windows here)
+    if (te_ >= s.maxEventTime) {
+      if (c->has_fixed && s.nextEdgeTs == JMIN) s.nextEdgeTs = next_fixed_edge(te_);
+      const int flex = flex_count(te_);
+      while (c->has_fixed && te_ > s.nextEdgeTs) {
+        if (s.nextEdgeTs >= 0) append_slice(s.nextEdgeTs, XTYPE_FIXED);
+        if (exc) return;
+        s.nextEdgeTs = next_fixed_edge(te_);
+        if (s.nextEdgeTs == JMIN) {
+          exc = XERR_HANG;
+          return;
+        }
+      }
+      if (s.nextEdgeTs == te_) {
+        append_slice(te_, XTYPE_FIXED);
+        if (exc) return;
+        s.nextEdgeTs = next_fixed_edge(te_);
+      } else if (flex > 0) {
+        append_slice(te_, ty_flex(flex));
+        if (exc) return;
+      }
+    }
+    s.currentCount = jadd(s.currentCount, 1);  // WindowManager.incrementCount (:196-198)
+    s.maxEventTime = max(te_, s.maxEventTime);
+  }
+  // SliceManager.processElement (S/SliceManager.java:47-87)
+  __device__ void manager_process(const XSess& x, int64_t t, int64_t vbits) {
+    if (s.tail <= s.head) append_slice(0, 1);
+    if (exc) return;
+    s.started = 1;
+    const int cur = s.tail - 1;
+    if (t >= TL(cur)) {
+      add_element(cur, t, vbits);
+      for (int k = 0; k < c->n_ctx && !exc; k++) {
+        int nd = 0;
+        session_update(x, k, t, nullptr, nd);  // modifications are dropped (:59-62)
+      }
+      return;
+    }
+    for (int k = 0; k < c->n_ctx && !exc; k++) {
+      Mod mods[XMAXMODS];
+      int nm = 0;
+      session_update(x, k, t, mods, nm);
+      if (exc) return;
+      check_slice_edges(mods, nm);
+    }
+    if (exc) return;
+    const int idx = find_ts(t);
+    if (!valid(idx)) return;
+    add_element(idx, t, vbits);
+  }
+};
+
+template <int VT>
+__global__ __launch_bounds__(256) void lane_session_kernel(XBatchArgs a) {
+  const XCfg* cfg = a.cfg;
+  const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (op >= a.n_ops) return;
+  const int64_t b0 = a.seg_begin[op], b1 = a.seg_end[op];
+  if (b1 <= b0) return;
+  XState* sp = a.st + op;
+  if (sp->err) return;
+  if (a.retry && !sp->pending) return;
+  const unsigned char* rec = (const unsigned char*)a.ts;
+  auto load = [&](int64_t i, int64_t& t, int64_t& vb) {
+    const unsigned char* r = rec + i * a.rec_stride;
+    t = *(const int64_t*)r;
+    if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
+    else vb = *(const int64_t*)(r + 8);
+  };
+  LaneS<VT> L;
+  L.c = cfg;
+  L.sl = a.sl;
+  L.b = op * (int64_t)cfg->sc;
+  L.sb = op * cfg->ctx_alloc * (int64_t)cfg->sesscap;
+  L.s = *sp;
+  L.exc = 0;
+  // capacity pre-check (the wavefront replay's bound): a key that might overflow its slice or session capacity is
+  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry)
+  {
+    int64_t tmin = JMAX, tmax = JMIN;
+    for (int64_t i = b0; i < b1; i++) {
+      int64_t t, v_;
+      load(i, t, v_);
+      tmin = min(tmin, t);
+      tmax = max(tmax, t);
+    }
+    const int64_t seglen = b1 - b0;
+    int64_t from = L.s.started ? max(L.s.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
+    if (from > tmax) from = tmax;
+    const double span = (double)tmax - (double)from;
+    double bound = 0.0;
+    for (int w = 0; w < cfg->n_cf; w++) {
+      const int k = cfg->cf_kind[w];
+      const double step = k == 0 ? (double)cfg->cf_a[w] : (double)cfg->cf_b[w];
+      if (k == 2) bound += 2.0;
+      else bound += span / step + 2.0;
+    }
+    bound += 3.0 * (double)seglen;  // session edits: a flexible edge, a split and a shift per tuple at most
+    const double need_s = (double)(L.s.tail - L.s.head) + bound + 2.0;
+    int need_x = 0;
+    for (int k = 0; k < cfg->n_ctx; k++) need_x = max(need_x, L.s.ns(k));
+    const int64_t need_ss = (int64_t)need_x + seglen + 1;
+    if (need_s > (double)cfg->sc || need_ss > cfg->sesscap) {
+      atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
+      atomicMax(&a.need[1], (unsigned long long)need_ss);
+      sp->pending = 1;
+      return;
+    }
+  }
+  L.s.pending = 0;
+  // replay, the next record's load issued before the current one is processed
+  int64_t t_nx, v_nx;
+  load(b0, t_nx, v_nx);
+  for (int64_t j = b0; j < b1 && !L.s.err; j++) {
+    const int64_t t = t_nx, vb = v_nx;
+    if (j + 1 < b1) load(j + 1, t_nx, v_nx);
+    L.exc = 0;
+    L.determine_slices(t);
+    if (!L.exc) L.manager_process(a.ss, t, vb);
+    if (xerr_tuple_failed(L.exc)) {
+      L.s.dropped++;
+      L.exc = 0;
+    } else if (L.exc) {
+      L.s.err = L.exc;
+    }
+  }
+  *sp = L.s;
+}
+
+}  // namespace ls
+
+// Eligible: keyed, one or more time-measured session windows beside context-free time windows, Eager slices (no count
+// windows, no LazySlice record sets) -- exact_engine.cpp lane_session_mode()
+hipError_t launch_lane_session(const XBatchArgs& a, int vt, hipStream_t st) {
+  if (a.n_ops <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
+  if (vt == VT_I32) hipLaunchKernelGGL(ls::lane_session_kernel<VT_I32>, grid, block, 0, st, a);
+  else if (vt == VT_I64) hipLaunchKernelGGL(ls::lane_session_kernel<VT_I64>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(ls::lane_session_kernel<VT_F64>, grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace scotty
