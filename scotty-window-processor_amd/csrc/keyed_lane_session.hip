@@ -426,8 +426,24 @@ struct LaneS {
   }
 };
 
+// One tuple through the general restatement (everything the fast path below does not take: flexible edges, session
+// edits that move, split or merge slices, new sessions before the last, several session contexts, capacity edges).
+// Out of line: its state lives in the caller's LaneS, in scratch memory, which only these rare tuples pay for.
 template <int VT>
-__global__ __launch_bounds__(256) void lane_session_kernel(XBatchArgs a) {
+__device__ __noinline__ void general_tuple(LaneS<VT>& L, const XSess x, int64_t t, int64_t vb) {
+  L.exc = 0;
+  L.determine_slices(t);
+  if (!L.exc) L.manager_process(x, t, vb);
+  if (xerr_tuple_failed(L.exc)) {
+    L.s.dropped++;
+    L.exc = 0;
+  } else if (L.exc) {
+    L.s.err = L.exc;
+  }
+}
+
+template <int VT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void lane_session_kernel(XBatchArgs a) {
   const XCfg* cfg = a.cfg;
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (op >= a.n_ops) return;
@@ -443,25 +459,30 @@ __global__ __launch_bounds__(256) void lane_session_kernel(XBatchArgs a) {
     if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
     else vb = *(const int64_t*)(r + 8);
   };
-  LaneS<VT> L;
-  L.c = cfg;
-  L.sl = a.sl;
-  L.b = op * (int64_t)cfg->sc;
-  L.sb = op * cfg->ctx_alloc * (int64_t)cfg->sesscap;
-  L.s = *sp;
-  L.exc = 0;
+  XState s0 = *sp;
   // capacity pre-check (the wavefront replay's bound): a key that might overflow its slice or session capacity is
-  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry)
+  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry).  Four records per
+  // round, so four scattered loads are in flight at once
   {
     int64_t tmin = JMAX, tmax = JMIN;
-    for (int64_t i = b0; i < b1; i++) {
+    int64_t i = b0;
+    for (; i + 4 <= b1; i += 4) {
+      int64_t t0, t1, t2, t3, v_;
+      load(i, t0, v_);
+      load(i + 1, t1, v_);
+      load(i + 2, t2, v_);
+      load(i + 3, t3, v_);
+      tmin = min(tmin, min(min(t0, t1), min(t2, t3)));
+      tmax = max(tmax, max(max(t0, t1), max(t2, t3)));
+    }
+    for (; i < b1; i++) {
       int64_t t, v_;
       load(i, t, v_);
       tmin = min(tmin, t);
       tmax = max(tmax, t);
     }
     const int64_t seglen = b1 - b0;
-    int64_t from = L.s.started ? max(L.s.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
+    int64_t from = s0.started ? max(s0.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
     if (from > tmax) from = tmax;
     const double span = (double)tmax - (double)from;
     double bound = 0.0;
@@ -472,9 +493,9 @@ __global__ __launch_bounds__(256) void lane_session_kernel(XBatchArgs a) {
       else bound += span / step + 2.0;
     }
     bound += 3.0 * (double)seglen;  // session edits: a flexible edge, a split and a shift per tuple at most
-    const double need_s = (double)(L.s.tail - L.s.head) + bound + 2.0;
+    const double need_s = (double)(s0.tail - s0.head) + bound + 2.0;
     int need_x = 0;
-    for (int k = 0; k < cfg->n_ctx; k++) need_x = max(need_x, L.s.ns(k));
+    for (int k = 0; k < cfg->n_ctx; k++) need_x = max(need_x, s0.ns(k));
     const int64_t need_ss = (int64_t)need_x + seglen + 1;
     if (need_s > (double)cfg->sc || need_ss > cfg->sesscap) {
       atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
@@ -483,24 +504,259 @@ __global__ __launch_bounds__(256) void lane_session_kernel(XBatchArgs a) {
       return;
     }
   }
-  L.s.pending = 0;
-  // replay, the next record's load issued before the current one is processed
+  s0.pending = 0;
+
+  // ---- fast path state, in registers: the StreamSlicer / store scalars, the one session context's last session, and
+  //      the current (last) slice's fields.  It takes the steady-state tuples of one session context: in-order tuples
+  //      that cross fixed edges, extend the last session or open a new one behind it without a flexible edge, and
+  //      out-of-order tuples inside the last session -- the same transitions the general code makes for them.
+  // the store's columns as plain uniform pointers (a reference into the kernel argument would keep the argument block
+  // in scratch memory and reload a pointer from it on every access)
+  int64_t* const Q_ts = a.sl.ts;
+  int64_t* const Q_te = a.sl.te;
+  int64_t* const Q_tl = a.sl.tl;
+  int64_t* const Q_tf = a.sl.tf;
+  int64_t* const Q_cs = a.sl.cs;
+  int64_t* const Q_cl = a.sl.cl;
+  int32_t* const Q_ty = a.sl.ty;
+  unsigned long long* const Q_cnt = a.sl.cnt;
+  unsigned long long* const Q_p0 = a.sl.p[0];
+  unsigned long long* const Q_p1 = a.sl.p[1];
+  unsigned long long* const Q_p2 = a.sl.p[2];
+  const int64_t bb = op * (int64_t)cfg->sc;
+  const int64_t sbase = op * cfg->ctx_alloc * (int64_t)cfg->sesscap;
+  int64_t* const sst = a.ss.start + sbase;  // context 0
+  int64_t* const sen = a.ss.end + sbase;
+  const bool one_ctx = cfg->n_ctx == 1;
+  const int64_t gap = cfg->gap[0];
+  const int32_t sc = cfg->sc;
+  int64_t mx = s0.maxEventTime, ne = s0.nextEdgeTs, cc = s0.currentCount;
+  int32_t head = s0.head, tail = s0.tail, uns = s0.unsorted, started = s0.started, ns = s0.nsess[0];
+  uint64_t dropped = s0.dropped;
+  int32_t err = s0.err;
+  int64_t st_l = JMIN, en_l = JMIN;
+  int32_t ci = -1;
+  int64_t c_tl = 0, c_tf = 0, c_cl = 0, c_p1 = 0, c_p2 = 0;
+  uint64_t c_cnt = 0, c_p0 = 0;
+  auto load_fast = [&]() {  // session tail and current slice from memory
+    if (one_ctx && ns > 0) {
+      st_l = sst[ns - 1];
+      en_l = sen[ns - 1];
+    }
+    ci = tail > head ? tail - 1 : -1;
+    if (ci >= 0) {
+      const int64_t j = bb + ci;
+      c_tl = Q_tl[j]; c_tf = Q_tf[j]; c_cl = Q_cl[j]; c_cnt = Q_cnt[j];
+      c_p0 = Q_p0[j]; c_p1 = (int64_t)Q_p1[j]; c_p2 = (int64_t)Q_p2[j];
+    }
+  };
+  auto flush_cur = [&]() {
+    if (ci < 0) return;
+    const int64_t j = bb + ci;
+    Q_tl[j] = c_tl; Q_tf[j] = c_tf; Q_cl[j] = c_cl; Q_cnt[j] = c_cnt;
+    Q_p0[j] = c_p0; Q_p1[j] = (unsigned long long)c_p1; Q_p2[j] = (unsigned long long)c_p2;
+  };
+  auto add_cur = [&](int64_t t, int64_t vb) {
+    c_tl = max(c_tl, t);
+    c_tf = min(c_tf, t);
+    c_cl = jadd(c_cl, 1);
+    c_cnt++;
+    const Lift l = lift(VT, vb);
+    if (cfg->need & NEED_SUM) {
+      if (VT == VT_F64)
+        c_p0 = (uint64_t)__double_as_longlong(__longlong_as_double((long long)c_p0) + __longlong_as_double((long long)l.sum));
+      else
+        c_p0 += l.sum;
+    }
+    if (cfg->need & NEED_MIN) c_p1 = min(c_p1, l.mn);
+    if (cfg->need & NEED_MAX) c_p2 = max(c_p2, l.mx);
+  };
+  auto add_mem = [&](int i, int64_t t, int64_t vb) {  // an older slice, in memory
+    const int64_t j = bb + i;
+    Q_tl[j] = max(Q_tl[j], t);
+    Q_tf[j] = min(Q_tf[j], t);
+    Q_cl[j] = jadd(Q_cl[j], 1);
+    Q_cnt[j] = Q_cnt[j] + 1;
+    const Lift l = lift(VT, vb);
+    if (cfg->need & NEED_SUM) {
+      if (VT == VT_F64)
+        Q_p0[j] = (unsigned long long)__double_as_longlong(__longlong_as_double((long long)Q_p0[j]) +
+                                                             __longlong_as_double((long long)l.sum));
+      else
+        Q_p0[j] = Q_p0[j] + l.sum;
+    }
+    if (cfg->need & NEED_MIN) Q_p1[j] = (unsigned long long)min((int64_t)Q_p1[j], l.mn);
+    if (cfg->need & NEED_MAX) Q_p2[j] = (unsigned long long)max((int64_t)Q_p2[j], l.mx);
+  };
+  // calculateNextFixedEdge (S/StreamSlicer.java:103-116) from the pending edge cur
+  auto next_edge = [&](int64_t te_, int64_t cur) {
+    const int64_t cur_ = cur == JMIN ? JMAX : cur, lt_ = jsub(te_, cfg->max_lateness);
+    const int64_t t_c = lt_ > cur_ ? lt_ : cur_;
+    int64_t e = JMAX;
+    for (int w = 0; w < cfg->n_cf; w++) {
+      if (cfg->cf_measure[w] != 0) continue;
+      const int kd = cfg->cf_kind[w];
+      const int64_t wa = cfg->cf_a[w], wb = cfg->cf_b[w];
+      int64_t r;
+      if (kd == 0) r = jsub(jadd(t_c, wa), jmod(t_c, wa));
+      else if (kd == 1) r = jsub(jadd(t_c, wb), jmod(t_c, wb));
+      else if (t_c == JMAX || t_c < wa) r = wa;
+      else if (t_c >= wa && t_c < jadd(wa, wb)) r = jadd(wa, wb);
+      else r = JMAX;
+      e = min(e, r);
+    }
+    return e;
+  };
+  // SliceManager.appendSlice (S/SliceManager.java:27-38) of a fixed edge, the current slice in registers
+  auto append_fixed = [&](int64_t start) {
+    if (ci >= 0) {
+      flush_cur();
+      Q_te[bb + ci] = start;
+      Q_ty[bb + ci] = XTYPE_FIXED;
+    }
+    const int64_t j = bb + tail;
+    Q_ts[j] = start; Q_te[j] = JMAX; Q_cs[j] = cc; Q_ty[j] = 1;
+    if (tail > head && Q_ts[j - 1] > start) uns |= 1;
+    ci = tail;
+    tail++;
+    c_tl = start; c_tf = JMAX; c_cl = cc; c_cnt = 0; c_p0 = 0; c_p1 = ID_MIN; c_p2 = ID_MAX;
+  };
+  // last slice with tStart <= t on a sorted list, galloping down from the tail (out-of-order tuples land near it)
+  auto find_sorted = [&](int64_t t) -> int {
+    int hi = tail - 1;
+    if (Q_ts[bb + hi] <= t) return hi;
+    int step = 1, lo;
+    for (;;) {
+      const int nx = hi - step;
+      if (nx <= head) {
+        if (Q_ts[bb + head] > t) return -1;
+        lo = head;
+        break;
+      }
+      if (Q_ts[bb + nx] <= t) {
+        lo = nx;
+        break;
+      }
+      hi = nx;
+      step <<= 1;
+    }
+    while (hi - lo > 1) {
+      const int m = (lo + hi) >> 1;
+      if (Q_ts[bb + m] <= t) lo = m; else hi = m;
+    }
+    return lo;
+  };
+  const XSess xs{a.ss.start, a.ss.end};  // (by value: no reference may point into the argument block)
+  LaneS<VT> L;  // the general path's state (scratch; only rare tuples touch it)
+  L.c = cfg;
+  L.sl = a.sl;
+  L.b = bb;
+  L.sb = sbase;
+  load_fast();
   int64_t t_nx, v_nx;
   load(b0, t_nx, v_nx);
-  for (int64_t j = b0; j < b1 && !L.s.err; j++) {
+  for (int64_t j = b0; j < b1 && !err; j++) {
     const int64_t t = t_nx, vb = v_nx;
     if (j + 1 < b1) load(j + 1, t_nx, v_nx);
-    L.exc = 0;
-    L.determine_slices(t);
-    if (!L.exc) L.manager_process(a.ss, t, vb);
-    if (xerr_tuple_failed(L.exc)) {
-      L.s.dropped++;
-      L.exc = 0;
-    } else if (L.exc) {
-      L.s.err = L.exc;
+    bool fast = one_ctx && ns > 0 && ci >= 0 && started;
+    int n_app = 0;
+    if (fast) {
+      if (t >= mx) {  // in-order: no flexible edge, a first pending edge, room for the fixed edges it crosses
+        const int64_t t_c = max(mx, ne);
+        if (ne == JMIN || (cfg->has_fixed == 0 && ne != JMIN) || t >= jadd(t_c, gap)) {
+          fast = false;
+        } else if (t >= ne) {
+          int64_t e = ne;
+          while (t > e && n_app <= 8) {
+            if (e >= 0) n_app++;
+            const int64_t nx = next_edge(t, e);
+            if (nx == JMIN || nx <= e) {  // the reference's hang / overflow: the general path reports it
+              n_app = 99;
+              break;
+            }
+            e = nx;
+          }
+          if (e == t) n_app++;
+          if (n_app > 8 || tail + n_app > sc) fast = false;
+        }
+        // the session: extended, unchanged, or a new one behind the last (t >= maxEventTime >= its end)
+        if (fast && jadd(en_l, gap) < t && ns >= cfg->sesscap) fast = false;
+      } else {  // out-of-order: inside the last session (updateContext changes nothing, no modification)
+        if (!(t >= st_l && t <= en_l)) fast = false;
+      }
     }
+    if (fast) {
+      if (t >= mx) {
+        // StreamSlicer.determineSlices, in-order branch (:51-86), without a flexible edge
+        if (n_app > 0) {
+          while (t > ne) {
+            if (ne >= 0) append_fixed(ne);
+            ne = next_edge(t, ne);
+          }
+          if (ne == t) {
+            append_fixed(t);
+            ne = next_edge(t, ne);
+          }
+        }
+        cc = jadd(cc, 1);
+        mx = t;
+        // SliceManager.processElement in-order branch (:56-63): the current slice, then updateContext whose
+        // modifications are dropped -- shiftEnd of the last session, or a new session at the end
+        add_cur(t, vb);
+        if (t != en_l) {
+          if (t <= jadd(en_l, gap)) {
+            en_l = t;
+            sen[ns - 1] = t;
+          } else {
+            sst[ns] = t;
+            sen[ns] = t;
+            ns++;
+            st_l = t;
+            en_l = t;
+          }
+        }
+      } else {
+        cc = jadd(cc, 1);  // determineSlices: out of order, WindowManager.incrementCount only
+        if (t >= c_tl) {
+          add_cur(t, vb);  // the in-order branch of processElement (t >= the current slice's tLast)
+        } else {
+          const int idx = (uns & 1) ? -2 : find_sorted(t);
+          if (idx == -2) {
+            // an unsorted list: the reference's backward scan (LazyAggregateStore.findSliceIndexByTimestamp)
+            int k = tail - 1;
+            while (k >= head && Q_ts[bb + k] > t) k--;
+            if (k < head) dropped++;  // IndexOutOfBoundsException: the tuple is lost
+            else if (k == ci) add_cur(t, vb);
+            else add_mem(k, t, vb);
+          } else if (idx < 0) {
+            dropped++;
+          } else if (idx == ci) {
+            add_cur(t, vb);
+          } else {
+            add_mem(idx, t, vb);
+          }
+        }
+      }
+      continue;
+    }
+    // ---- the general path for this tuple
+    flush_cur();
+    L.s = s0;
+    L.s.maxEventTime = mx; L.s.nextEdgeTs = ne; L.s.currentCount = cc;
+    L.s.head = head; L.s.tail = tail; L.s.unsorted = uns; L.s.started = started; L.s.nsess[0] = ns;
+    L.s.dropped = dropped; L.s.err = err;
+    general_tuple<VT>(L, xs, t, vb);
+    s0 = L.s;
+    mx = s0.maxEventTime; ne = s0.nextEdgeTs; cc = s0.currentCount;
+    head = s0.head; tail = s0.tail; uns = s0.unsorted; started = s0.started; ns = s0.nsess[0];
+    dropped = s0.dropped; err = s0.err;
+    load_fast();
   }
-  *sp = L.s;
+  flush_cur();
+  s0.maxEventTime = mx; s0.nextEdgeTs = ne; s0.currentCount = cc;
+  s0.head = head; s0.tail = tail; s0.unsorted = uns; s0.started = started; s0.nsess[0] = ns;
+  s0.dropped = dropped; s0.err = err;
+  *sp = s0;
 }
 
 }  // namespace ls
