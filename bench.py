@@ -705,18 +705,22 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
                               "frac": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9 / HBM_PEAK_GBS}}
 
 
-def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12):
+def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
     """Keyed sessions at scale: KeyedScottyWindowOperator with SessionWindow(gap 1 s) +
     SlidingWindow(60 s, 1 s) per key, SUM_I32, `keys` uniform keys, 20 % out-of-order tuples late by U[1,500] ms,
     watermark lag 500 ms, maxLateness 1000, a 2 s pause every 10 s of event time (every key's session closes, C3's
-    shape per key).  Session windows take the wavefront-per-key replay (exact_kernels.hip replay_kernel: one wavefront
-    restates one key's operator, simple tuples folded 64 at a time, session / edge events exactly).  The timed steps
-    cover one whole 10-step period (the pause step included); a second period with HIP events gives the device split."""
+    shape per key).  Session windows take the lane-per-key session replay (keyed_lane_session.hip: one lane restates one
+    key's StreamSlicer / SliceManager / SessionContext, steady-state tuples in registers).  The timed steps cover one
+    whole 10-step period (the pause step included); a second period with HIP events gives the device split.
+    `tune`: scotty_tune knobs (the "c4s2" leg: {"keyed_lane_session": 2}, the kernel's 3-waves build, A/B;
+    profiles/r05/ab_c4s_occupancy.json: 2 waves 8.04 ms/step, 3 waves 8.93)."""
     import torch
     rate = max(1, batch // 1000)
     g = torch.Generator(device=dev)
     g.manual_seed(77)
     op = pkg.KeyedSlicingWindowOperator(device=dev.index)
+    for k_, v_ in (tune or {}).items():
+        op.tune(k_, v_)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.setMaxLateness(1000)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
@@ -741,10 +745,10 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12):
             times.append(time.perf_counter() - t0)
             rows += n
     roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
-                           "keyed replay: radix sort by key + replay_kernel (wavefront per key)")
+                           "keyed replay: radix sort by key + lane_session_kernel (lane per key)")
     return {"workload": "C4s: keyed SessionWindow(gap 1s) + SlidingWindow(60s,1s) SUM_I32, %d uniform keys, 20%% "
                         "out-of-order (delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, maxLateness 1000, "
-                        "wavefront-per-key replay, results left in HBM" % keys,
+                        "lane-per-key session replay, results left in HBM" % keys, "tune": tune or {},
             "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
             "ms_per_step": 1e3 * sum(times) / len(times), "ms_per_step_each": [round(1e3 * t, 3) for t in times],
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows, "roofline": roof}
@@ -810,7 +814,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
     ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c5,c5t,pcie; c3nb: C3 with the start band "
-                    "off, A/B); default all but c3nb")
+                    "off, A/B; c4s2: C4s on the lane-session kernel's 3-waves build, A/B); default all but c3nb, c4s2")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
@@ -958,6 +962,8 @@ def main():
                 log("bench: C4 done")
             if "c4s" in legs:
                 extra["c4s"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20)
+            if "c4s2" in args.only.split(","):  # A/B only: the lane-session kernel's 3-waves-per-SIMD build
+                extra["c4s2"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 2})
                 log("bench: C4s (keyed sessions) done")
             if "c5" in legs:
                 extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)

@@ -23,7 +23,7 @@ hipError_t launch_wm_emit(const XWmArgs& a, hipStream_t st);
 hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group);
 hipError_t launch_wm_blocks(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st);
-hipError_t launch_lane_session(const XBatchArgs& a, int vt, hipStream_t st);
+hipError_t launch_lane_session(const XBatchArgs& a, int vt, int occ, hipStream_t st);
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st);
 hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
@@ -1362,7 +1362,7 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
     a.ss = ss;
     if (!lane_mode()) prefix_stale = true;  // the wavefront replay does not track the lane path's slice prefixes
     XCHK(lane_mode()           ? launch_lane_replay(a, cfg, stream)
-         : lane_session_mode() ? launch_lane_session(a, vt, stream)
+         : lane_session_mode() ? launch_lane_session(a, vt, lane_session_occ, stream)
                                : launch_replay(a, vt, stream));
     XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
@@ -1530,7 +1530,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   int rct = tbegin(tw1, SCOTTY_TIME_WATERMARK);
   if (rct) return rct;
   XCHK(hipMemsetAsync(d_misc, 0, 3 * 8, stream));
-  XCHK(lane_mode() ? launch_lane_wm_count(a, stream) : launch_wm_count(a, stream));
+  XCHK(lane_wm_mode() ? launch_lane_wm_count(a, stream) : launch_wm_count(a, stream));
   XCHK(launch_scan_i64(d_wcount, d_woff, n_ops, d_scan64, stream));
   XCHK(launch_copy_to_host(d_misc, h_misc_dev, 3 * 8, stream));
   XCHK(launch_copy_to_host(d_woff + n_ops - 1, h_misc_dev + 3, 8, stream));
@@ -1558,7 +1558,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.n_rows = rows;
   TEv tw2;
   if ((rct = tbegin(tw2, SCOTTY_TIME_WATERMARK))) return rct;
-  if (lane_mode()) {
+  if (lane_wm_mode()) {
     XCHK(launch_lane_wm_emit(a, prefix_agg, stream));
     if (prefix_agg) prefix_stale = false;
   } else {

@@ -111,6 +111,7 @@ class XEngine {
   bool lane_mode() const {  // keyed_lane.hip: context-free time windows on Eager slices only
     return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && !records && cfg.n_cf > 0;
   }
+  int lane_session_occ = 2;       // lane-session kernel build: 2 or 3 waves per SIMD (A/B, "keyed_lane_session" 2)
   bool lane_session_off = false;  // keyed: sessions through the wavefront replay instead (A/B, "keyed_lane_session" 0)
   // keyed_lane_session.hip: time-measured session windows (beside context-free time windows) on Eager slices
   bool lane_session_mode() const {
@@ -120,6 +121,9 @@ class XEngine {
       if (cfg.ctx_measure[k] != 0) return false;
     return true;
   }
+  // keyed_lane.hip's lane-per-key watermark (count / emit / scan range / GC): context-free windows, and sessions on
+  // the lane-session path
+  bool lane_wm_mode() const { return lane_mode() || lane_session_mode(); }
   // non-keyed: the single-wavefront replay (LazySlice record sets live only there)
   bool use_serial() const { return serial || records; }
   bool records = false;   // LazySlice record sets kept (XCfg.records)

@@ -331,6 +331,48 @@ __device__ int64_t lane_triggers(const XCfg* c, int64_t last, int64_t wm, int64_
   return k;
 }
 
+// SessionContext.triggerWindows of each session context (C/windowType/SessionWindow.java:107-116, after the
+// context-free windows, S/WindowManager.java:104-118): the sessions with end + gap < wm, oldest first, as windows
+// [start, end + gap); EMIT also drops them from the context (the remaining ones move to the front).  Returns -1 for
+// an empty context (getWindow(0) throws IndexOutOfBoundsException).
+template <bool EMIT>
+__device__ int64_t lane_session_triggers(const XCfg* c, const XSess& x, int64_t op, XState& s, int64_t wm,
+                                         int64_t* w_start, int64_t* w_end, int32_t* w_meas, int32_t* w_op, int64_t off,
+                                         int64_t& minTs, int64_t& maxTs) {
+  int64_t k = 0;
+  for (int ctx = 0; ctx < c->n_ctx; ctx++) {
+    const int64_t gap = c->gap[ctx];
+    const int ns = s.ns(ctx);
+    if (ns == 0) return -1;
+    const int64_t sb = (op * c->ctx_alloc + ctx) * (int64_t)c->sesscap;
+    int64_t* const st = x.start + sb;
+    int64_t* const en = x.end + sb;
+    int i = 0;
+    for (; i < ns; i++) {
+      const int64_t e = jadd(en[i], gap);
+      if (!(e < wm)) break;
+      const int64_t b = st[i];
+      if (EMIT) {
+        w_start[off + k] = b;
+        w_end[off + k] = e;
+        w_meas[off + k] = 0;  // time-measured contexts only on this path
+        w_op[off + k] = (int32_t)op;
+      }
+      minTs = min(minTs, b);
+      maxTs = max(maxTs, e);
+      k++;
+    }
+    if (EMIT && i > 0) {
+      for (int j = i; j < ns; j++) {
+        st[j - i] = st[j];
+        en[j - i] = en[j];
+      }
+      s.set_ns(ctx, ns - i);
+    }
+  }
+  return k;
+}
+
 template <class V>
 __global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -345,6 +387,13 @@ __global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
     if (last < oldest) last = oldest;
     int64_t mn = JMAX, mx = 0;
     k = lane_triggers<false>(a.cfg, last, a.wm, nullptr, nullptr, nullptr, nullptr, 0, 0, mn, mx);
+    if (a.cfg->n_ctx > 0) {
+      XState s2 = s;
+      const int64_t ks = lane_session_triggers<false>(a.cfg, a.ss, op, s2, a.wm, nullptr, nullptr, nullptr, nullptr, 0,
+                                                      mn, mx);
+      if (ks < 0) atomicOr(a.err_flag, 1);
+      else k += ks;
+    }
   }
   a.wcount[op] = k;
 }
@@ -463,6 +512,8 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
   int64_t minTs = JMAX, maxTs = 0;
   k = lane_triggers<true>(c, s.lastWatermark, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, off, (int32_t)op, minTs,
                           maxTs);
+  if (!AGG && c->n_ctx > 0)  // (the count pass has thrown for an empty context)
+    k += lane_session_triggers<true>(c, a.ss, op, s, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, off + k, minTs, maxTs);
   const int h = s.head, t = s.tail;
   // find_ts / find_count: last slice with key <= x (LazyAggregateStore.findSliceIndexBy*, :29-50), -1 if none
   auto last_ts_le_up = [&](int64_t x) { return first_true_up(h, t, [&](int i) { return ts[i] > x; }) - 1; };
@@ -593,7 +644,14 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
   }
   s.lastWatermark = a.wm;
   s.lastCount = s.currentCount;
-  const int64_t gt = jsub(jsub(a.wm, c->max_lateness), c->max_fixed);  // clearAfterWatermark (:82-95)
+  // clearAfterWatermark (:82-95): below the oldest session start of any context as well
+  const int64_t cw = jsub(a.wm, c->max_lateness);
+  int64_t first = cw;
+  for (int ctx = 0; !AGG && ctx < c->n_ctx; ctx++) {
+    const int64_t* st = a.ss.start + (op * c->ctx_alloc + ctx) * (int64_t)c->sesscap;
+    for (int i = 0; i < s.ns(ctx); i++) first = min(first, st[i]);
+  }
+  const int64_t gt = min(jsub(cw, c->max_fixed), first);
   const int idx = fix(last_ts_le_up(gt));
   if (idx > s.head) s.head = idx;
   a.st[op] = s;

@@ -442,8 +442,8 @@ __device__ __noinline__ void general_tuple(LaneS<VT>& L, const XSess x, int64_t 
   }
 }
 
-template <int VT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void lane_session_kernel(XBatchArgs a) {
+template <int VT, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void lane_session_kernel(XBatchArgs a) {
   const XCfg* cfg = a.cfg;
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (op >= a.n_ops) return;
@@ -461,19 +461,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
   };
   XState s0 = *sp;
   // capacity pre-check (the wavefront replay's bound): a key that might overflow its slice or session capacity is
-  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry).  Four records per
-  // round, so four scattered loads are in flight at once
+  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry).  Eight records per
+  // round, so eight scattered loads are in flight at once
   {
     int64_t tmin = JMAX, tmax = JMIN;
     int64_t i = b0;
-    for (; i + 4 <= b1; i += 4) {
-      int64_t t0, t1, t2, t3, v_;
-      load(i, t0, v_);
-      load(i + 1, t1, v_);
-      load(i + 2, t2, v_);
-      load(i + 3, t3, v_);
-      tmin = min(tmin, min(min(t0, t1), min(t2, t3)));
-      tmax = max(tmax, max(max(t0, t1), max(t2, t3)));
+    for (; i + 8 <= b1; i += 8) {
+      int64_t tt[8], v_;
+#pragma unroll
+      for (int u = 0; u < 8; u++) load(i + u, tt[u], v_);
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        tmin = min(tmin, tt[u]);
+        tmax = max(tmax, tt[u]);
+      }
     }
     for (; i < b1; i++) {
       int64_t t, v_;
@@ -535,42 +536,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
   uint64_t dropped = s0.dropped;
   int32_t err = s0.err;
   int64_t st_l = JMIN, en_l = JMIN;
-  int32_t ci = -1;
-  int64_t c_tl = 0, c_tf = 0, c_cl = 0, c_p1 = 0, c_p2 = 0;
+  // the current (last) slice ci and the one before it pv (the late tuples' usual target), in registers; c_ts / p_ts
+  // their tStart.  en_l is written back to the session list at flush_cur
+  int32_t ci = -1, pv = -1;
+  int64_t c_ts = 0, c_tl = 0, c_tf = 0, c_cl = 0, c_p1 = 0, c_p2 = 0;
   uint64_t c_cnt = 0, c_p0 = 0;
-  auto load_fast = [&]() {  // session tail and current slice from memory
+  int64_t p_ts = 0, p_tl = 0, p_tf = 0, p_cl = 0, p_p1 = 0, p_p2 = 0;
+  uint64_t p_cnt = 0, p_p0 = 0;
+  auto load_fast = [&]() {  // session tail and the last two slices from memory
     if (one_ctx && ns > 0) {
       st_l = sst[ns - 1];
       en_l = sen[ns - 1];
     }
     ci = tail > head ? tail - 1 : -1;
+    pv = tail - 1 > head ? tail - 2 : -1;
     if (ci >= 0) {
       const int64_t j = bb + ci;
-      c_tl = Q_tl[j]; c_tf = Q_tf[j]; c_cl = Q_cl[j]; c_cnt = Q_cnt[j];
+      c_ts = Q_ts[j]; c_tl = Q_tl[j]; c_tf = Q_tf[j]; c_cl = Q_cl[j]; c_cnt = Q_cnt[j];
       c_p0 = Q_p0[j]; c_p1 = (int64_t)Q_p1[j]; c_p2 = (int64_t)Q_p2[j];
     }
+    if (pv >= 0) {
+      const int64_t j = bb + pv;
+      p_ts = Q_ts[j]; p_tl = Q_tl[j]; p_tf = Q_tf[j]; p_cl = Q_cl[j]; p_cnt = Q_cnt[j];
+      p_p0 = Q_p0[j]; p_p1 = (int64_t)Q_p1[j]; p_p2 = (int64_t)Q_p2[j];
+    }
+  };
+  auto flush_prev = [&]() {
+    if (pv < 0) return;
+    const int64_t j = bb + pv;
+    Q_tl[j] = p_tl; Q_tf[j] = p_tf; Q_cl[j] = p_cl; Q_cnt[j] = p_cnt;
+    Q_p0[j] = p_p0; Q_p1[j] = (unsigned long long)p_p1; Q_p2[j] = (unsigned long long)p_p2;
   };
   auto flush_cur = [&]() {
+    if (one_ctx && ns > 0) sen[ns - 1] = en_l;
+    flush_prev();
     if (ci < 0) return;
     const int64_t j = bb + ci;
     Q_tl[j] = c_tl; Q_tf[j] = c_tf; Q_cl[j] = c_cl; Q_cnt[j] = c_cnt;
     Q_p0[j] = c_p0; Q_p1[j] = (unsigned long long)c_p1; Q_p2[j] = (unsigned long long)c_p2;
   };
-  auto add_cur = [&](int64_t t, int64_t vb) {
-    c_tl = max(c_tl, t);
-    c_tf = min(c_tf, t);
-    c_cl = jadd(c_cl, 1);
-    c_cnt++;
+  auto fold = [&](int64_t& tl, int64_t& tf, int64_t& cl, uint64_t& cnt, uint64_t& p0, int64_t& p1, int64_t& p2,
+                  int64_t t, int64_t vb) {
+    tl = max(tl, t);
+    tf = min(tf, t);
+    cl = jadd(cl, 1);
+    cnt++;
     const Lift l = lift(VT, vb);
     if (cfg->need & NEED_SUM) {
       if (VT == VT_F64)
-        c_p0 = (uint64_t)__double_as_longlong(__longlong_as_double((long long)c_p0) + __longlong_as_double((long long)l.sum));
+        p0 = (uint64_t)__double_as_longlong(__longlong_as_double((long long)p0) + __longlong_as_double((long long)l.sum));
       else
-        c_p0 += l.sum;
+        p0 += l.sum;
     }
-    if (cfg->need & NEED_MIN) c_p1 = min(c_p1, l.mn);
-    if (cfg->need & NEED_MAX) c_p2 = max(c_p2, l.mx);
+    if (cfg->need & NEED_MIN) p1 = min(p1, l.mn);
+    if (cfg->need & NEED_MAX) p2 = max(p2, l.mx);
   };
+  auto add_cur = [&](int64_t t, int64_t vb) { fold(c_tl, c_tf, c_cl, c_cnt, c_p0, c_p1, c_p2, t, vb); };
+  auto add_prev = [&](int64_t t, int64_t vb) { fold(p_tl, p_tf, p_cl, p_cnt, p_p0, p_p1, p_p2, t, vb); };
   auto add_mem = [&](int i, int64_t t, int64_t vb) {  // an older slice, in memory
     const int64_t j = bb + i;
     Q_tl[j] = max(Q_tl[j], t);
@@ -608,23 +630,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     return e;
   };
   // SliceManager.appendSlice (S/SliceManager.java:27-38) of a fixed edge, the current slice in registers
+  // (the current slice's fields move to the previous-slice registers, the old previous slice goes to memory)
   auto append_fixed = [&](int64_t start) {
     if (ci >= 0) {
-      flush_cur();
+      flush_prev();
       Q_te[bb + ci] = start;
       Q_ty[bb + ci] = XTYPE_FIXED;
+      pv = ci; p_ts = c_ts; p_tl = c_tl; p_tf = c_tf; p_cl = c_cl; p_cnt = c_cnt;
+      p_p0 = c_p0; p_p1 = c_p1; p_p2 = c_p2;
+      if (c_ts > start) uns |= 1;
     }
     const int64_t j = bb + tail;
     Q_ts[j] = start; Q_te[j] = JMAX; Q_cs[j] = cc; Q_ty[j] = 1;
-    if (tail > head && Q_ts[j - 1] > start) uns |= 1;
     ci = tail;
     tail++;
-    c_tl = start; c_tf = JMAX; c_cl = cc; c_cnt = 0; c_p0 = 0; c_p1 = ID_MIN; c_p2 = ID_MAX;
+    c_ts = start; c_tl = start; c_tf = JMAX; c_cl = cc; c_cnt = 0; c_p0 = 0; c_p1 = ID_MIN; c_p2 = ID_MAX;
   };
   // last slice with tStart <= t on a sorted list, galloping down from the tail (out-of-order tuples land near it)
   auto find_sorted = [&](int64_t t) -> int {
     int hi = tail - 1;
-    if (Q_ts[bb + hi] <= t) return hi;
+    if (c_ts <= t) return hi;
+    if (pv >= 0 && p_ts <= t) return pv;
+    if (pv >= 0) hi = pv;
     int step = 1, lo;
     for (;;) {
       const int nx = hi - step;
@@ -706,8 +733,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
         if (t != en_l) {
           if (t <= jadd(en_l, gap)) {
             en_l = t;
-            sen[ns - 1] = t;
           } else {
+            sen[ns - 1] = en_l;
             sst[ns] = t;
             sen[ns] = t;
             ns++;
@@ -727,11 +754,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             while (k >= head && Q_ts[bb + k] > t) k--;
             if (k < head) dropped++;  // IndexOutOfBoundsException: the tuple is lost
             else if (k == ci) add_cur(t, vb);
+            else if (k == pv) add_prev(t, vb);
             else add_mem(k, t, vb);
           } else if (idx < 0) {
             dropped++;
           } else if (idx == ci) {
             add_cur(t, vb);
+          } else if (idx == pv) {
+            add_prev(t, vb);
           } else {
             add_mem(idx, t, vb);
           }
@@ -763,12 +793,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
 
 // Eligible: keyed, one or more time-measured session windows beside context-free time windows, Eager slices (no count
 // windows, no LazySlice record sets) -- exact_engine.cpp lane_session_mode()
-hipError_t launch_lane_session(const XBatchArgs& a, int vt, hipStream_t st) {
+hipError_t launch_lane_session(const XBatchArgs& a, int vt, int occ, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
-  if (vt == VT_I32) hipLaunchKernelGGL(ls::lane_session_kernel<VT_I32>, grid, block, 0, st, a);
-  else if (vt == VT_I64) hipLaunchKernelGGL(ls::lane_session_kernel<VT_I64>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(ls::lane_session_kernel<VT_F64>, grid, block, 0, st, a);
+  if (occ == 2) {
+    if (vt == VT_I32) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 2>), grid, block, 0, st, a);
+    else if (vt == VT_I64) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I64, 2>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((ls::lane_session_kernel<VT_F64, 2>), grid, block, 0, st, a);
+  } else {
+    if (vt == VT_I32) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 3>), grid, block, 0, st, a);
+    else if (vt == VT_I64) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I64, 3>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((ls::lane_session_kernel<VT_F64, 3>), grid, block, 0, st, a);
+  }
   return hipGetLastError();
 }
 

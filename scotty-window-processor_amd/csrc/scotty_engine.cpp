@@ -177,6 +177,7 @@ struct scotty_op {
   int64_t x_prefix = 0;      // exact engine: first event-exact prefix of a refused quiet batch (0: default)
   int32_t x_qmode = -1;      // exact engine: quiet-pass ingest loop (A/B: -1 default, 7 without the DQ2 queue)
   bool x_ls_off = false;     // exact engine: keyed sessions through the wavefront replay (A/B)
+  int32_t x_ls_occ = 2;      // lane-session kernel's waves per SIMD (2 default: no spills; 3: A/B)
   int64_t x_qblocks = 0;     // exact engine: quiet-pass ingest workgroups (A/B: 0 default)
   int32_t x_kg_variant = -1;
   int64_t shard_count_total = 0;
@@ -963,6 +964,7 @@ static int decide_mode(scotty_op* op) {
   op->x->xq_ingest_mode = op->x_qmode;
   op->x->xq_ingest_blocks = op->x_qblocks;
   op->x->lane_session_off = op->x_ls_off;
+  op->x->lane_session_occ = op->x_ls_occ;
   op->x->timing = op->timing;  // scotty_enable_timing before the first push (the natural order) reaches the engine
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
@@ -1526,10 +1528,14 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->x) op->x->xq_prefix = value;
     return SCOTTY_OK;
   }
-  if (std::strcmp(key, "keyed_lane_session") == 0) {  // 0: keyed sessions through the wavefront replay (A/B)
-    if (op->mode != 0) return SCOTTY_ERR_ARG;
+  if (std::strcmp(key, "keyed_lane_session") == 0) {  // 0: keyed sessions through the wavefront replay (A/B),
+    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;  // 1 lane kernel, 2 its 3-waves build
     op->x_ls_off = value == 0;
-    if (op->x) op->x->lane_session_off = op->x_ls_off;
+    op->x_ls_occ = value == 2 ? 3 : 2;
+    if (op->x) {
+      op->x->lane_session_off = op->x_ls_off;
+      op->x->lane_session_occ = op->x_ls_occ;
+    }
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "quiet_ingest_mode") == 0) {  // exact engine's quiet pass: -1 default loop, 7 without DQ2 (A/B)

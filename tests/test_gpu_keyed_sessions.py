@@ -113,7 +113,7 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
 
     def make(lane):
         op = pkg.KeyedSlicingWindowOperator(device=0, value_type=vtc)
-        op.tune("keyed_lane_session", 1 if lane else 0)
+        op.tune("keyed_lane_session", (1 + seed % 2) if lane else 0)  # odd seeds: the kernel's 3-waves build
         for x in aggs:
             op.addWindowFunction(x)
         op.setMaxLateness(lateness)
