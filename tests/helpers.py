@@ -159,6 +159,29 @@ class KeyedOracle:
         return {k: op.processWatermark(wm) for k, op in self.ops.items()}
 
 
+def same_keyed_arrays(got, exp, f64_cols=()):
+    """Two keyed processWatermarkArrays results: the same rows key by key (keys as a set, each key's rows in order,
+    as same_keyed_windows), compared column-wise in numpy; f64 columns in f64_cols within 1e-6 relative."""
+    import numpy as np
+    n = len(exp["start"])
+    assert len(got["start"]) == n
+    if n == 0:
+        return 0
+    og, oe = np.argsort(got["key"], kind="stable"), np.argsort(exp["key"], kind="stable")
+    for c in ("key", "start", "end", "measure", "has_value"):
+        assert np.array_equal(got[c][og], exp[c][oe]), c
+    hv = exp["has_value"][oe]
+    for i, (a, b) in enumerate(zip(got["values"], exp["values"])):
+        a, b = a[og][hv], b[oe][hv]
+        if i in f64_cols:
+            nan = np.isnan(b)
+            assert np.array_equal(np.isnan(a), nan), i
+            assert np.all(np.abs(a[~nan] - b[~nan]) <= 1e-6 * np.maximum(1.0, np.abs(b[~nan]))), i
+        else:
+            assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), i
+    return n
+
+
 def same_keyed_windows(rows, expected, f64_cols=()):
     """rows: [(key, AggregateWindow)] of the product; expected: {key: [AggregateWindow]} of the oracle.
     Keys compare as a set (Java HashMap order is not a contract); windows of one key position by position."""

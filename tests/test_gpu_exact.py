@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import junit_cases
-from helpers import product, build_ops, run_schedule, interval_schedule, KeyedOracle, same_keyed_windows
+from helpers import product, build_ops, run_schedule, interval_schedule, KeyedOracle, same_keyed_windows, same_keyed_arrays
 from specs import Tumbling, Sliding, Session, FixedBand, Time, Count, SUM, COUNT, MIN, MAX, SUM_I64, \
     MIN_I64, MAX_I64, SUM_F64, MIN_F64, MAX_F64, INVERTIBLE
 
@@ -453,11 +453,8 @@ def test_keyed_lane_path_equals_wavefront_replay(pkg, seed):
                 for op in ops:
                     op.processElements(keys[step[1]:step[2]], ts[step[1]:step[2]], vals[step[1]:step[2]])
         else:
-            a, b = ops[0].processWatermark(step[1]), ops[1].processWatermark(step[1])
-            exp = {}
-            for k, w in b:
-                exp.setdefault(k, []).append(w)
-            total += same_keyed_windows(a, exp, f64_cols=f64_cols)
+            a, b = ops[0].processWatermarkArrays(step[1]), ops[1].processWatermarkArrays(step[1])
+            total += same_keyed_arrays(a, b, f64_cols=f64_cols)
             assert ops[0].droppedCount() == ops[1].droppedCount()
     assert total > 0
 

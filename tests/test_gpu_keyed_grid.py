@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from helpers import product, interval_schedule, KeyedOracle, same_keyed_windows
+from helpers import product, interval_schedule, KeyedOracle, same_keyed_windows, same_keyed_arrays
 from specs import Tumbling, Sliding, FixedBand, Time, SUM, COUNT, MIN, MAX, SUM_I64, MIN_I64, MAX_I64, \
     SUM_F64, MIN_F64, MAX_F64
 
@@ -80,10 +80,8 @@ def _run_pair(pkg, vt, wins, aggs, lateness, keys, ts, vals, sched, f64_cols):
             deferred += path == 2
             assert rp._debug_stat(2) == 0
         else:
-            exp = {}
-            for k, w in rp.processWatermark(step[1]):
-                exp.setdefault(k, []).append(w)
-            total += same_keyed_windows(kg.processWatermark(step[1]), exp, f64_cols=f64_cols)
+            exp = rp.processWatermarkArrays(step[1])
+            total += same_keyed_arrays(kg.processWatermarkArrays(step[1]), exp, f64_cols=f64_cols)
             assert kg.droppedCount() == rp.droppedCount()
     assert kg.keyCount() == rp.keyCount()
     return total, used, deferred

@@ -123,7 +123,7 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
     lane, wave = make(True), make(False)
     f64_cols = [i for i, x in enumerate(aggs) if x == SUM_F64]
     total = errors = 0
-    from helpers import interval_schedule
+    from helpers import interval_schedule, same_keyed_arrays
     for step in interval_schedule(ts, int(rng.integers(3, 12)), lag=int(rng.integers(0, 2 * max(gaps))),
                                   pushes_per_interval=int(rng.integers(1, 3))):
         if step[0] == "push":
@@ -132,22 +132,19 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
                 lane.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
                 wave.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
         else:
-            exp = {}
             try:
-                rows = wave.processWatermark(step[1])
+                exp = wave.processWatermarkArrays(step[1])
             except pkg.ScottyError as e:
                 # SessionWindow.triggerWindows reads getWindow(0) of a key whose sessions all closed at an earlier
                 # watermark (SessionWindow.java:107-116): the reference throws out of the connector's key loop.  Both
                 # kernels leave the same state behind, so the lane path must throw the same way
                 assert e.code == -5
                 with pytest.raises(pkg.ScottyError) as ei:
-                    lane.processWatermark(step[1])
+                    lane.processWatermarkArrays(step[1])
                 assert ei.value.code == -5
                 errors += 1
                 continue
-            for k, w in rows:
-                exp.setdefault(k, []).append(w)
-            total += same_keyed_windows(lane.processWatermark(step[1]), exp, f64_cols=f64_cols)
+            total += same_keyed_arrays(lane.processWatermarkArrays(step[1]), exp, f64_cols=f64_cols)
             assert lane.droppedCount() == wave.droppedCount()
     assert lane.keyCount() == wave.keyCount()
     assert total > 0 or errors > 0
