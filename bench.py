@@ -289,6 +289,49 @@ def cpu_c4(keys, batch, threads):
                       % (steps, batch, keys, threads, affinity, quota, threads)}
 
 
+def cpu_c4s(keys, batch, threads):
+    """C4s on the CPU: KeyedScottyWindowOperator with SessionWindow(1 s) + SlidingWindow(60 s, 1 s) per key on T
+    threads (key % T partitions), the GPU leg's stream (20 % of tuples late by U[1,500] ms, 2 s pause every 10 s,
+    watermark lag 500 ms), one watermark per step; two untimed steps, then timed steps until the budget."""
+    from oracle.oracle import KeyedOracleThreads, JavaError
+    op = KeyedOracleThreads(threads)
+    op.addWindowFunction(0)
+    op.setMaxLateness(1000)
+    op.addWindowAssigner(1, 0, 60_000, 1_000)
+    op.addWindowAssigner(2, 0, 1000, 0)
+    rng = np.random.default_rng(77)
+    rate = max(1, batch // 1000)
+    base = np.arange(batch, dtype=np.int64) // rate
+    done, t_proc, steps = 0, 0.0, 0
+    for s in range(1000):
+        t_begin = s * 1000 + 1000 + (s // 10) * 2000
+        k = rng.integers(0, keys, size=batch).astype(np.uint32)
+        late = rng.random(batch) < 0.2
+        ts = np.where(late, base + t_begin - rng.integers(1, 501, size=batch), base + t_begin)
+        v = rng.integers(-2**31, 2**31, size=batch, dtype=np.int64)
+        p = op.partition(k, ts, v)
+        t0 = time.perf_counter()
+        try:  # the first steps' too-late tuples throw per tuple in the reference (recorded, the batch continues)
+            op.process(p, t_begin + (batch - 1) // rate - 500)
+        except JavaError:
+            pass
+        dt = time.perf_counter() - t0
+        if s >= 2:
+            t_proc += dt
+            done += batch
+            steps += 1
+            if t_proc > CPU_BUDGET_S:
+                break
+    eff, affinity, quota = host_cores()
+    return {"value": done / t_proc, "unit": "tuples/s", "cores": threads, "kind": "port",
+            "affinity_threads": affinity, "cgroup_cpu_quota": quota,
+            "sample": "%d steps of %d tuples (%d uniform keys, the C4s stream: steps 2.. of one run from event time "
+                      "0, a 2 s pause every 10 steps) after 2 untimed steps; oracle/ KeyedScottyWindowOperator "
+                      "restatement on %d threads = the effective host cores of this process, min(sched_getaffinity "
+                      "%d, cgroup quota %s); key %% %d partitions" % (steps, batch, keys, threads, affinity, quota,
+                                                                      threads)}
+
+
 # ----------------------------------------------------------------------------------------------- GPU legs
 def extra_c1(pkg, dev, batch, steps):
     """BASELINE configs[0] (C1), the reference benchmark's own workload at GPU batch size: SlidingWindow(Time,
@@ -749,6 +792,8 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
     return {"workload": "C4s: keyed SessionWindow(gap 1s) + SlidingWindow(60s,1s) SUM_I32, %d uniform keys, 20%% "
                         "out-of-order (delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, maxLateness 1000, "
                         "lane-per-key session replay, results left in HBM" % keys, "tune": tune or {},
+            "lane_counters": ([op._debug_stat(103 + i) for i in range(4)]
+                              if (tune or {}).get("lane_session_counters") else None),
             "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
             "ms_per_step": 1e3 * sum(times) / len(times), "ms_per_step_each": [round(1e3 * t, 3) for t in times],
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows, "roofline": roof}
@@ -990,7 +1035,8 @@ def main():
             log("bench: host cores: %d effective (%d affinity threads, cgroup quota %s)" % (threads, affinity, quota))
             cb = {"c1": lambda: cpu_c1((1 << 26) // 1000),
                   "c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
-                  "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000),
+                  "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c4s": lambda: cpu_c4s(1 << 20, C4_BATCH, threads),
+                  "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000),
                   "c5t": lambda: cpu_c5t(1 << 20)}
             for name, fn in cb.items():
                 if name in extra:

@@ -23,6 +23,23 @@
 
 namespace scotty {
 
+// Key table entries (keyed_kernels.hip, keyed_grid.hip): key << 32 | 1 << 31 | slot; 0 = empty.  The occupied bit
+// keeps every uint32 key representable (a (key + 1) << 32 tag wrapped key 0xFFFFFFFF to the empty tag); slot field
+// 0x7FFFFFFF = inserted in this batch, slot not yet assigned (the entry's low word is then 0xFFFFFFFF).
+constexpr uint32_t KTAB_PENDING = 0xFFFFFFFFu;  // low word of a pending entry / a tuple's unassigned slot
+__host__ __device__ inline unsigned long long ktab_tag(uint32_t key) {
+  return ((unsigned long long)key << 32) | 0x80000000ull;
+}
+__host__ __device__ inline bool ktab_is(unsigned long long e, uint32_t key) {
+  return (e & 0xFFFFFFFF80000000ull) == ktab_tag(key);
+}
+__host__ __device__ inline uint32_t ktab_key(unsigned long long e) { return (uint32_t)(e >> 32); }
+// slot of an entry (KTAB_PENDING for a pending one)
+__host__ __device__ inline uint32_t ktab_slot(unsigned long long e) {
+  const uint32_t w = (uint32_t)e;
+  return w == KTAB_PENDING ? KTAB_PENDING : (w & 0x7FFFFFFFu);
+}
+
 constexpr int XMAXCTX = 4;        // session windows per operator
 constexpr int XMAXMODS = 8;       // WindowModifications produced by one updateContext call (<= 4 in practice)
 constexpr int SCOTTY_MAX_AGGS_ = 8;  // == SCOTTY_MAX_AGGS
@@ -115,13 +132,14 @@ struct XSlices {
   // below XState.pvalid -- a window's COUNT / SUM is then two reads instead of a scan of its slices
   unsigned long long *pc, *ps;
   // lane path for COUNT / integer SUM functions: the store kept key-interleaved instead (XKView, the columns above
-  // unused): word (op, slice position i, field f) at kw[((i * XK_NF + f) << kc_sh) + op], so the lanes of a
+  // unused): word (op, slice position i, field f) at kw[((i * kw_nf + f) << kc_sh) + op], so the lanes of a
   // wavefront -- consecutive keys -- touching the same field of the same slice position read or write one
   // contiguous 512-B run instead of 64 scattered lines.  Keys advance in lockstep in a steady stream (one slice per
   // grid interval each, compacted at the same batch), so their positions coincide.  sc and the key capacity are
   // powers of two (sc_sh, kc_sh their logs).
   unsigned long long* kw;
   int32_t sc_sh, kc_sh;
+  int32_t kw_nf;  // fields per position: XK_NF with MIN / MAX functions (their block summaries), else XK_NF_SUM
 };
 
 // Fields of the key-interleaved store (XSlices.kw), one 8-byte word each (ty in the low half of its word).
@@ -130,9 +148,11 @@ struct XSlices {
 // XState.pvalid, like PC / PS), SN / SX from this position to the block's end (kept for complete blocks only: the
 // emit kernel recomputes them for every complete block that holds a position at or above pvalid) -- a window of
 // positions [lo, hi) then reads SN[lo], QN at the end of each whole block and QN[hi - 1], not each of its slices.
+// Operators without MIN / MAX keep only the first XK_NF_SUM fields per position (the summaries are last).
 enum : int {
-  XK_TS, XK_TE, XK_TL, XK_TF, XK_CS, XK_CL, XK_CNT, XK_P0, XK_P1, XK_P2, XK_PC, XK_PS,
-  XK_QN, XK_SN, XK_QX, XK_SX, XK_TY, XK_NF
+  XK_TS, XK_TE, XK_TL, XK_TF, XK_CS, XK_CL, XK_CNT, XK_P0, XK_P1, XK_P2, XK_PC, XK_PS, XK_TY,
+  XK_NF_SUM,
+  XK_QN = XK_NF_SUM, XK_SN, XK_QX, XK_SX, XK_NF
 };
 constexpr int XK_MB = 16;  // slice positions per MIN / MAX summary block
 
@@ -142,11 +162,11 @@ struct XKCol0 {
   unsigned long long* w;
   int64_t off;
   int32_t sc_sh, kc_sh;
-  int32_t f;
+  int32_t f, nf;
   __host__ __device__ unsigned long long* addr(int64_t j) const {
     j += off;
     const int64_t op = j >> sc_sh, i = j & ((((int64_t)1) << sc_sh) - 1);
-    return w + (((i * XK_NF + f) << kc_sh) + op);
+    return w + (((i * nf + f) << kc_sh) + op);
   }
 };
 template <typename T>
@@ -176,7 +196,7 @@ struct XKView {
   XKCol<int32_t> ty;
   __host__ __device__ XKView() {}
   __host__ __device__ explicit XKView(const XSlices& s) {
-    XKCol0 b{s.kw, 0, s.sc_sh, s.kc_sh, 0};
+    XKCol0 b{s.kw, 0, s.sc_sh, s.kc_sh, 0, s.kw_nf};
     auto col = [&](auto& c, int f) {
       static_cast<XKCol0&>(c) = b;
       c.f = f;
@@ -214,6 +234,11 @@ struct XBatchArgs {
   int32_t rec_stride;       // keyed: tuples are AoS records (ts at +0, value at +8, op at +rec_stride-4)
   int32_t retry;            // process only ops marked pending by an earlier launch
   unsigned long long* need; // [3] capacity pre-check: max slices / sessions / records an op may need (atomicMax)
+  // nullable: the batch's largest timestamp, biased (ts ^ 1 << 63, an unsigned order) -- seg_kernel's by-product; the
+  // lane-session kernel bounds a started key's capacity need with it before it reads the key's tuples
+  const unsigned long long* ts_max_b;
+  unsigned long long* dbg;  // nullable: lane-session path counters (general / fast in-order / fast late in registers /
+                            // fast late in memory tuples), debugging aid
 };
 
 // Block summaries of one operator's slices for the watermark (exact_kernels.hip, wm_blocks_kernel): block b covers

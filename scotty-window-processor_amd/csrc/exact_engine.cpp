@@ -40,7 +40,8 @@ hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
                                void** result, hipStream_t st);
-hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end, hipStream_t st);
+hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end,
+                      unsigned long long* tmax_b, hipStream_t st);
 int64_t sort_tile();
 hipError_t launch_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t st);
 hipError_t launch_kg_build(const uint32_t* slot_key, int64_t n_ops, unsigned long long* tab, uint64_t mask,
@@ -117,6 +118,7 @@ void XEngine::release() {
   for (int k = 0; k < NPART; k++) dfree(sl.p[k]);
   dfree(sl.rlo); dfree(sl.rhi); dfree(sl.nn); dfree(sl.rts); dfree(sl.rv);
   dfree(ss.start); dfree(ss.end);
+  dfree(d_lsdbg);
   dfree(d_need); dfree(d_table); dfree(d_newpos); dfree(d_newcnt); dfree(d_full); dfree(d_slot_key);
   dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32); dfree(d_seg_b); dfree(d_seg_e);
   dfree(d_wcount); dfree(d_woff); dfree(d_scan64); dfree(d_misc);
@@ -311,12 +313,16 @@ int XEngine::grow_ops(int64_t need) {
     *p = np;
     return hipSuccess;
   };
-  if (ops_cap == 0)  // the store's layout is fixed with the first allocation
+  if (ops_cap == 0) {  // the store's layout is fixed with the first allocation
     aos = keyed && lane_mode() && vt != VT_F64;
+    // MIN / MAX block summaries only if used (the functions are fixed before the first push: scotty_add_aggregation
+    // refuses a function added after elements were processed)
+    sl.kw_nf = (cfg.need & (NEED_MIN | NEED_MAX)) ? XK_NF : XK_NF_SUM;
+  }
   XCHK(grow(&d_st, 1));
   if (aos) {  // key-interleaved store: rows (position, field) of cap words, re-strided from the old key capacity
     unsigned long long* nw = nullptr;
-    const int64_t rows = (int64_t)sc * XK_NF;
+    const int64_t rows = (int64_t)sc * sl.kw_nf;
     XCHK(dalloc(&nw, (size_t)(rows * cap)));
     XCHK(hipMemsetAsync(nw, 0, (size_t)(rows * cap) * 8, stream));
     if (sl.kw && n_ops > 0)
@@ -400,9 +406,9 @@ int XEngine::grow_caps(int64_t need_sc, int64_t need_sess, int32_t need_ctx, int
   };
   if (nsc != sc && sl.kw) {  // key-interleaved: positions are the outer index, the old store is a prefix
     unsigned long long* nw = nullptr;
-    XCHK(dalloc(&nw, (size_t)(nsc * XK_NF * rows)));
-    XCHK(hipMemsetAsync(nw, 0, (size_t)(nsc * XK_NF * rows) * 8, stream));
-    XCHK(hipMemcpyAsync(nw, sl.kw, (size_t)(sc * XK_NF * rows) * 8, hipMemcpyDeviceToDevice, stream));
+    XCHK(dalloc(&nw, (size_t)(nsc * sl.kw_nf * rows)));
+    XCHK(hipMemsetAsync(nw, 0, (size_t)(nsc * sl.kw_nf * rows) * 8, stream));
+    XCHK(hipMemcpyAsync(nw, sl.kw, (size_t)(sc * sl.kw_nf * rows) * 8, hipMemcpyDeviceToDevice, stream));
     XCHK(hipStreamSynchronize(stream));
     dfree(sl.kw);
     sl.kw = nw;
@@ -1295,7 +1301,10 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   if (n <= 0) return SCOTTY_OK;
   int rc = ensure_batch(n);
   if (rc) return rc;
-  rc = ensure_table(n_ops + std::min<int64_t>(n, 1 << 24));
+  // table sized for the known keys plus at most max(known, 2^20) new ones (<= 50 % load): sizing it for every tuple
+  // of the batch being a new key (up to 2^24) made a 512-MB table at 1 M keys, every probe a random HBM line;
+  // a batch with more new keys fills it and re-runs on a doubled table (below)
+  rc = ensure_table(n_ops + std::min<int64_t>(n, std::max<int64_t>(n_ops, 1 << 20)));
   if (rc) return rc;
   // 1. new keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator())).
   //    A table that fills up mid-pass is grown (the pass's unassigned insertions dropped) and the pass re-run.
@@ -1345,7 +1354,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   }
   XCHK(hipMemsetAsync(d_seg_b, 0, n_ops * 8, stream));
   XCHK(hipMemsetAsync(d_seg_e, 0, n_ops * 8, stream));
-  XCHK(launch_seg(rec, sorted, n, d_seg_b, d_seg_e, stream));
+  XCHK(hipMemsetAsync(d_need + 3, 0, 8, stream));  // the batch's largest timestamp (biased), written by seg_kernel
+  XCHK(launch_seg(rec, sorted, n, d_seg_b, d_seg_e, d_need + 3, stream));
   // 3. per-key replay; ops whose capacities might overflow are deferred, the tables grown, and relaunched
   XBatchArgs a = batch_args();
   a.ts = (const int64_t*)sorted;
@@ -1355,8 +1365,16 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   a.seg_end = d_seg_e;
   a.rec_stride = rec;
   a.need = d_need;
+  a.ts_max_b = d_need + 3;
+  if (lsdbg_on) {
+    if (!d_lsdbg) {
+      XCHK(dalloc(&d_lsdbg, 4));
+      XCHK(hipMemsetAsync(d_lsdbg, 0, 32, stream));
+    }
+    a.dbg = d_lsdbg;
+  }
   for (int attempt = 0; attempt < 6; attempt++) {
-    XCHK(hipMemsetAsync(d_need, 0, 32, stream));
+    XCHK(hipMemsetAsync(d_need, 0, 24, stream));
     a.retry = attempt > 0;
     a.sl = sl;
     a.ss = ss;
@@ -1708,7 +1726,7 @@ int XEngine::debug_dump(int64_t op, std::vector<int64_t>& out) {
   if (S > 0 && sl.kw) {  // key-interleaved store: the same columns, gathered (one word per position and field)
     const int64_t kc = (int64_t)1 << sl.kc_sh;
     auto kcol = [&](int f, bool ty32) -> int {
-      XCHK(hipMemcpy2D(tmp.data(), 8, sl.kw + ((s.head * (int64_t)XK_NF + f) << sl.kc_sh) + op, XK_NF * kc * 8, 8, S,
+      XCHK(hipMemcpy2D(tmp.data(), 8, sl.kw + ((s.head * (int64_t)sl.kw_nf + f) << sl.kc_sh) + op, sl.kw_nf * kc * 8, 8, S,
                        hipMemcpyDeviceToHost));
       for (int64_t i = 0; i < S; i++) out.push_back(ty32 ? (int64_t)(int32_t)tmp[i] : tmp[i]);
       return SCOTTY_OK;

@@ -111,6 +111,8 @@ class XEngine {
   bool lane_mode() const {  // keyed_lane.hip: context-free time windows on Eager slices only
     return keyed && !lane_off && cfg.n_ctx == 0 && !cfg.has_count && !cfg.lazy && !records && cfg.n_cf > 0;
   }
+  unsigned long long* d_lsdbg = nullptr;  // lane-session path counters (scotty_tune "lane_session_counters" 1)
+  bool lsdbg_on = false;
   int lane_session_occ = 2;       // lane-session kernel build: 2 or 3 waves per SIMD (A/B, "keyed_lane_session" 2)
   bool lane_session_off = false;  // keyed: sessions through the wavefront replay instead (A/B, "keyed_lane_session" 0)
   // keyed_lane_session.hip: time-measured session windows (beside context-free time windows) on Eager slices

@@ -109,7 +109,7 @@ __device__ __forceinline__ int64_t tile_of(int ntiles) {
 __global__ void kg_build_kernel(const uint32_t* slot_key, int64_t n_ops, unsigned long long* tab, uint64_t mask) {
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_ops; s += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t key = slot_key[s];
-    const unsigned long long e = (((unsigned long long)key + 1) << 32) | (unsigned long long)(uint32_t)s;
+    const unsigned long long e = ktab_tag(key) | (unsigned long long)(uint32_t)s;
     uint64_t h = (uint64_t)khash(key) & mask;
     while (atomicCAS(&tab[h], 0ull, e) != 0ull) h = (h + 1) & mask;
   }
@@ -394,10 +394,9 @@ struct KgLds {
 
 __device__ __forceinline__ int lds_probe(const unsigned long long* tab, uint32_t key, uint64_t kmask,
                                          uint64_t region) {
-  const unsigned long long tag = ((unsigned long long)key + 1) << 32;
   for (int p = (int)(((uint64_t)khash(key) & kmask) - region); p < KG_RP; p++) {
     const unsigned long long e = tab[p];
-    if ((e & 0xFFFFFFFF00000000ull) == tag) return p;
+    if (ktab_is(e, key)) return p;
     if (e == 0) return -1;
   }
   return -1;
@@ -527,12 +526,12 @@ __device__ __forceinline__ void kg_bucket_body(const KgArgs& a) {
   for (int p = tid; p < KG_RP; p += nt) {
     const unsigned long long e = L.tab[p];
     if (e == 0) continue;
-    if (bucket_of((uint32_t)((e >> 32) - 1), a.kmask) != bk) continue;  // a neighbour bucket's key
+    if (bucket_of(ktab_key(e), a.kmask) != bk) continue;  // a neighbour bucket's key
     uint32_t tot = 0;
 #pragma unroll
     for (int c = 0; c < CM; c++) tot += L.cnt[p * CM + c];
     if (tot == 0) continue;
-    KPart* kp = a.part + (int64_t)(uint32_t)e * CM;
+    KPart* kp = a.part + (int64_t)ktab_slot(e) * CM;
     for (int c = 0; c < nc; c++) {
       const int q = p * CM + c;
       KPart w;
@@ -744,14 +743,13 @@ __global__ __launch_bounds__(256) void kg_commit_kernel(KgArgs a, int64_t n_ops)
 __global__ void kg_mark_deferred_kernel(KgArgs a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t key = a.key[i];
-    const unsigned long long tag = ((unsigned long long)key + 1) << 32;
     const uint64_t h = (uint64_t)khash(key) & a.kmask;
     const uint64_t region = (h >> KG_RB) << KG_RB;
     bool m = true;
     for (int p = (int)(h - region); p < KG_RP; p++) {
       const unsigned long long e = a.ktab[(region + p) & a.kmask];
-      if ((e & 0xFFFFFFFF00000000ull) == tag) {
-        m = a.dflag[(uint32_t)e] != 0;
+      if (ktab_is(e, key)) {
+        m = a.dflag[ktab_slot(e)] != 0;
         break;
       }
       if (e == 0) break;

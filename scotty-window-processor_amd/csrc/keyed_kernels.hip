@@ -35,32 +35,39 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {  // murmur3 finaliser
 }
 
 // ---------------------------------------------------------------- hash table
-// entry: (key+1) << 32 | slot; 0 = empty; slot 0xFFFFFFFF = inserted in this batch, slot not yet assigned
+constexpr uint64_t KEY_PROBE_MAX = 2048;
+// entries: ktab_tag(key) | slot (exact_common.h); 0 = empty; low word KTAB_PENDING = inserted in this batch, slot not
+// yet assigned
 __global__ void key_insert_kernel(const uint32_t* keys, int64_t n, unsigned long long* table, uint64_t mask,
                                   uint32_t* new_pos, unsigned long long* new_count, int32_t* full, uint32_t* slot) {
   // also records each tuple's slot when its key already has one (0xFFFFFFFF: key new in this batch, fixed up by
   // slot_kernel<true> after key_assign) -- in the steady state of a keyed stream one probe pass does both
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t tag = ((uint64_t)keys[i] + 1) << 32;
-    uint64_t h = hash32(keys[i]) & mask;
-    uint32_t sl = 0xFFFFFFFFu;
+    const uint32_t key = keys[i];
+    uint64_t h = hash32(key) & mask;
+    uint32_t sl = KTAB_PENDING;
     for (uint64_t probe = 0; probe <= mask; probe++) {
       unsigned long long e = table[h];
-      if ((e & 0xFFFFFFFF00000000ull) == tag) {
-        sl = (uint32_t)e;
+      if (ktab_is(e, key)) {
+        sl = ktab_slot(e);
         break;
       }
       if (e == 0) {
-        const unsigned long long prev = atomicCAS(&table[h], 0ull, (unsigned long long)(tag | 0xFFFFFFFFull));
+        const unsigned long long prev = atomicCAS(&table[h], 0ull, ktab_tag(key) | KTAB_PENDING);
         if (prev == 0) {
           const unsigned long long p = atomicAdd(new_count, 1ull);
           new_pos[p] = (uint32_t)h;
           break;
         }
-        if ((prev & 0xFFFFFFFF00000000ull) == tag) break;
+        if (ktab_is(prev, key)) break;
       }
       h = (h + 1) & mask;
-      if (probe == mask) atomicOr(full, 1);
+      // a probe run this long means the table is (nearly) full for this batch's new keys: the host doubles it
+      // and re-runs the pass (bounded, so a batch of many new keys cannot scan a full table per tuple)
+      if (probe == mask || probe >= KEY_PROBE_MAX) {
+        atomicOr(full, 1);
+        break;
+      }
     }
     slot[i] = sl;
   }
@@ -71,8 +78,8 @@ __global__ void key_assign_kernel(unsigned long long* table, const uint32_t* new
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_new; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t h = new_pos[i];
     const unsigned long long e = table[h];
-    const uint32_t key = (uint32_t)((e >> 32) - 1);
-    table[h] = (e & 0xFFFFFFFF00000000ull) | (unsigned long long)(uint32_t)(base + i);
+    const uint32_t key = ktab_key(e);
+    table[h] = ktab_tag(key) | (unsigned long long)(uint32_t)(base + i);
     slot_key[base + i] = key;
   }
 }
@@ -85,8 +92,8 @@ __global__ void rehash_kernel(const unsigned long long* old_t, uint64_t old_n, u
        i += (int64_t)gridDim.x * blockDim.x) {
     const unsigned long long e = old_t[i];
     if (e == 0) continue;
-    if (drop_new && (uint32_t)e == 0xFFFFFFFFu) continue;
-    uint64_t h = hash32((uint32_t)((e >> 32) - 1)) & mask;
+    if (drop_new && (uint32_t)e == KTAB_PENDING) continue;
+    uint64_t h = hash32(ktab_key(e)) & mask;
     while (atomicCAS(&nt[h], 0ull, e) != 0ull) h = (h + 1) & mask;
   }
 }
@@ -95,16 +102,16 @@ template <bool FIXUP>
 __global__ void slot_kernel(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
                             uint32_t* slot) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (FIXUP && slot[i] != 0xFFFFFFFFu) continue;
-    const uint64_t tag = ((uint64_t)keys[i] + 1) << 32;
-    uint64_t h = hash32(keys[i]) & mask;
-    unsigned long long e;
+    if (FIXUP && slot[i] != KTAB_PENDING) continue;
+    const uint32_t key = keys[i];
+    uint64_t h = hash32(key) & mask;
+    unsigned long long e = 0;
     for (uint64_t probe = 0; probe <= mask; probe++) {
       e = table[h];
-      if ((e & 0xFFFFFFFF00000000ull) == tag) break;
+      if (ktab_is(e, key)) break;
       h = (h + 1) & mask;
     }
-    slot[i] = (uint32_t)e;
+    slot[i] = ktab_slot(e);
   }
 }
 
@@ -274,11 +281,24 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
 }
 
 template <int REC>
-__global__ void seg_kernel(const Rec<REC>* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end) {
+// also the batch's largest timestamp (biased to an unsigned order; one atomic per wavefront) when tmax_b is given
+__global__ void seg_kernel(const Rec<REC>* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end,
+                           unsigned long long* tmax_b) {
+  unsigned long long mx = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t s = recs[i].slot;
+    const unsigned long long b = (unsigned long long)recs[i].ts ^ 0x8000000000000000ull;
+    mx = b > mx ? b : mx;
     if (i == 0 || recs[i - 1].slot != s) seg_begin[s] = i;
     if (i == n - 1 || recs[i + 1].slot != s) seg_end[s] = i + 1;
+  }
+  if (tmax_b) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long u = __shfl_xor(mx, o);
+      mx = u > mx ? u : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(tmax_b, mx);
   }
 }
 
@@ -538,14 +558,15 @@ hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, cons
   return hipSuccess;
 }
 
-hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end, hipStream_t st) {
+hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end,
+                      unsigned long long* tmax_b, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (rec == 16)
     hipLaunchKernelGGL(k::seg_kernel<16>, dim3(grid_for(n)), dim3(256), 0, st, (const k::Rec<16>*)recs, n, seg_begin,
-                       seg_end);
+                       seg_end, tmax_b);
   else
     hipLaunchKernelGGL(k::seg_kernel<24>, dim3(grid_for(n)), dim3(256), 0, st, (const k::Rec<24>*)recs, n, seg_begin,
-                       seg_end);
+                       seg_end, tmax_b);
   return hipGetLastError();
 }
 

@@ -461,48 +461,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   };
   XState s0 = *sp;
   // capacity pre-check (the wavefront replay's bound): a key that might overflow its slice or session capacity is
-  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry).  Eight records per
-  // round, so eight scattered loads are in flight at once
+  // deferred untouched, the host grows the capacities and relaunches the deferred keys (retry).  The bound needs the
+  // span of event time the key's tuples can add slices over: for a started key that span lies within [maxEventTime,
+  // the batch's largest timestamp], so when that wider span already fits, the key's tuples are not read for it;
+  // otherwise they are, eight records per round (eight scattered loads in flight)
   {
-    int64_t tmin = JMAX, tmax = JMIN;
-    int64_t i = b0;
-    for (; i + 8 <= b1; i += 8) {
-      int64_t tt[8], v_;
-#pragma unroll
-      for (int u = 0; u < 8; u++) load(i + u, tt[u], v_);
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        tmin = min(tmin, tt[u]);
-        tmax = max(tmax, tt[u]);
-      }
-    }
-    for (; i < b1; i++) {
-      int64_t t, v_;
-      load(i, t, v_);
-      tmin = min(tmin, t);
-      tmax = max(tmax, t);
-    }
     const int64_t seglen = b1 - b0;
-    int64_t from = s0.started ? max(s0.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
-    if (from > tmax) from = tmax;
-    const double span = (double)tmax - (double)from;
-    double bound = 0.0;
-    for (int w = 0; w < cfg->n_cf; w++) {
-      const int k = cfg->cf_kind[w];
-      const double step = k == 0 ? (double)cfg->cf_a[w] : (double)cfg->cf_b[w];
-      if (k == 2) bound += 2.0;
-      else bound += span / step + 2.0;
-    }
-    bound += 3.0 * (double)seglen;  // session edits: a flexible edge, a split and a shift per tuple at most
-    const double need_s = (double)(s0.tail - s0.head) + bound + 2.0;
     int need_x = 0;
     for (int k = 0; k < cfg->n_ctx; k++) need_x = max(need_x, s0.ns(k));
     const int64_t need_ss = (int64_t)need_x + seglen + 1;
-    if (need_s > (double)cfg->sc || need_ss > cfg->sesscap) {
-      atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
-      atomicMax(&a.need[1], (unsigned long long)need_ss);
-      sp->pending = 1;
-      return;
+    auto need_slices = [&](double span) {
+      double bound = 0.0;
+      for (int w = 0; w < cfg->n_cf; w++) {
+        const int k = cfg->cf_kind[w];
+        const double step = k == 0 ? (double)cfg->cf_a[w] : (double)cfg->cf_b[w];
+        if (k == 2) bound += 2.0;
+        else bound += span / step + 2.0;
+      }
+      bound += 3.0 * (double)seglen;  // session edits: a flexible edge, a split and a shift per tuple at most
+      return (double)(s0.tail - s0.head) + bound + 2.0;
+    };
+    bool fits = false;
+    if (s0.started && a.ts_max_b) {
+      const int64_t tmax_b = (int64_t)(*a.ts_max_b ^ 0x8000000000000000ull);
+      const double span = tmax_b > s0.maxEventTime ? (double)tmax_b - (double)s0.maxEventTime : 0.0;
+      fits = need_slices(span) <= (double)cfg->sc && need_ss <= cfg->sesscap;
+    }
+    if (!fits) {
+      int64_t tmin = JMAX, tmax = JMIN;
+      int64_t i = b0;
+      for (; i + 8 <= b1; i += 8) {
+        int64_t tt[8], v_;
+#pragma unroll
+        for (int u = 0; u < 8; u++) load(i + u, tt[u], v_);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          tmin = min(tmin, tt[u]);
+          tmax = max(tmax, tt[u]);
+        }
+      }
+      for (; i < b1; i++) {
+        int64_t t, v_;
+        load(i, t, v_);
+        tmin = min(tmin, t);
+        tmax = max(tmax, t);
+      }
+      int64_t from = s0.started ? max(s0.maxEventTime, jsub(tmin, cfg->max_lateness)) : jsub(tmin, cfg->max_lateness);
+      if (from > tmax) from = tmax;
+      const double need_s = need_slices((double)tmax - (double)from);
+      if (need_s > (double)cfg->sc || need_ss > cfg->sesscap) {
+        atomicMax(&a.need[0], (unsigned long long)min(need_s, 1e15) + 2ull);
+        atomicMax(&a.need[1], (unsigned long long)need_ss);
+        sp->pending = 1;
+        return;
+      }
     }
   }
   s0.pending = 0;
@@ -680,11 +692,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   L.b = bb;
   L.sb = sbase;
   load_fast();
-  int64_t t_nx, v_nx;
-  load(b0, t_nx, v_nx);
-  for (int64_t j = b0; j < b1 && !err; j++) {
-    const int64_t t = t_nx, vb = v_nx;
-    if (j + 1 < b1) load(j + 1, t_nx, v_nx);
+  // the key's records go through a per-lane ring of 8 in LDS: the next 8 are loaded (one 128-B line of 16-B records)
+  // while the current 8 are processed, so the tuple loop does not wait on a load every iteration (the loads are
+  // unconditional, the index clamped, so no branch join waits for them)
+  __shared__ int64_t R_t[8][256], R_v[8][256];
+  const int tid = threadIdx.x;
+  int64_t pt[8], pw[8];
+  auto fetch8 = [&](int64_t c) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t i = min(c + u, b1 - 1);
+      if constexpr (VT == VT_I32) {
+        const uint4 w = *(const uint4*)(rec + i * 16);
+        pt[u] = (int64_t)(((uint64_t)w.y << 32) | w.x);
+        pw[u] = (int64_t)(int32_t)w.z;
+      } else {
+        load(i, pt[u], pw[u]);
+      }
+    }
+  };
+  auto stage8 = [&]() {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      R_t[u][tid] = pt[u];
+      R_v[u][tid] = pw[u];
+    }
+  };
+  uint32_t n_gen = 0, n_in = 0, n_late = 0, n_late_mem = 0;  // path counters (a.dbg)
+  fetch8(b0);
+  stage8();
+  for (int64_t c0 = b0; c0 < b1 && !err; c0 += 8) {
+  fetch8(c0 + 8);
+  const int m_ = (int)min((int64_t)8, b1 - c0);
+  for (int u_ = 0; u_ < m_ && !err; u_++) {
+    const int64_t t = R_t[u_][tid], vb = R_v[u_][tid];
     bool fast = one_ctx && ns > 0 && ci >= 0 && started;
     int n_app = 0;
     if (fast) {
@@ -727,6 +768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         }
         cc = jadd(cc, 1);
         mx = t;
+        n_in++;
         // SliceManager.processElement in-order branch (:56-63): the current slice, then updateContext whose
         // modifications are dropped -- shiftEnd of the last session, or a new session at the end
         add_cur(t, vb);
@@ -744,32 +786,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         }
       } else {
         cc = jadd(cc, 1);  // determineSlices: out of order, WindowManager.incrementCount only
-        if (t >= c_tl) {
-          add_cur(t, vb);  // the in-order branch of processElement (t >= the current slice's tLast)
+        n_late++;
+        // the in-order branch of processElement (t >= the current slice's tLast), else findSliceIndexByTimestamp:
+        // its first two probes from the tail are the current and the previous slice (registers), on a sorted list
+        // and on an unsorted one alike (the reference's loop runs backwards from the tail)
+        if (t >= c_tl || c_ts <= t) {
+          add_cur(t, vb);
+        } else if (pv >= 0 && p_ts <= t) {
+          add_prev(t, vb);
         } else {
-          const int idx = (uns & 1) ? -2 : find_sorted(t);
-          if (idx == -2) {
-            // an unsorted list: the reference's backward scan (LazyAggregateStore.findSliceIndexByTimestamp)
-            int k = tail - 1;
+          n_late_mem++;
+          int idx;
+          if (uns & 1) {  // an unsorted list: the rest of the reference's backward scan
+            int k = pv >= 0 ? pv - 1 : tail - 2;
             while (k >= head && Q_ts[bb + k] > t) k--;
-            if (k < head) dropped++;  // IndexOutOfBoundsException: the tuple is lost
-            else if (k == ci) add_cur(t, vb);
-            else if (k == pv) add_prev(t, vb);
-            else add_mem(k, t, vb);
-          } else if (idx < 0) {
-            dropped++;
-          } else if (idx == ci) {
-            add_cur(t, vb);
-          } else if (idx == pv) {
-            add_prev(t, vb);
+            idx = k >= head ? k : -1;
           } else {
-            add_mem(idx, t, vb);
+            idx = find_sorted(t);
           }
+          if (idx < 0) dropped++;  // IndexOutOfBoundsException: the tuple is lost
+          else add_mem(idx, t, vb);
         }
       }
       continue;
     }
     // ---- the general path for this tuple
+    n_gen++;
     flush_cur();
     L.s = s0;
     L.s.maxEventTime = mx; L.s.nextEdgeTs = ne; L.s.currentCount = cc;
@@ -782,11 +824,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     dropped = s0.dropped; err = s0.err;
     load_fast();
   }
+  stage8();
+  }
   flush_cur();
   s0.maxEventTime = mx; s0.nextEdgeTs = ne; s0.currentCount = cc;
   s0.head = head; s0.tail = tail; s0.unsorted = uns; s0.started = started; s0.nsess[0] = ns;
   s0.dropped = dropped; s0.err = err;
   *sp = s0;
+  if (a.dbg) {  // (lanes that returned early count nothing; the atomics below are per lane -- a debugging aid)
+    atomicAdd(&a.dbg[0], (unsigned long long)n_gen);
+    atomicAdd(&a.dbg[1], (unsigned long long)n_in);
+    atomicAdd(&a.dbg[2], (unsigned long long)n_late);
+    atomicAdd(&a.dbg[3], (unsigned long long)n_late_mem);
+  }
 }
 
 }  // namespace ls

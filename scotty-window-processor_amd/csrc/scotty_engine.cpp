@@ -178,6 +178,7 @@ struct scotty_op {
   int32_t x_qmode = -1;      // exact engine: quiet-pass ingest loop (A/B: -1 default, 7 without the DQ2 queue)
   bool x_ls_off = false;     // exact engine: keyed sessions through the wavefront replay (A/B)
   int32_t x_ls_occ = 2;      // lane-session kernel's waves per SIMD (2 default: no spills; 3: A/B)
+  bool x_lsdbg = false;      // lane-session path counters (debugging aid)
   int64_t x_qblocks = 0;     // exact engine: quiet-pass ingest workgroups (A/B: 0 default)
   int32_t x_kg_variant = -1;
   int64_t shard_count_total = 0;
@@ -965,6 +966,7 @@ static int decide_mode(scotty_op* op) {
   op->x->xq_ingest_blocks = op->x_qblocks;
   op->x->lane_session_off = op->x_ls_off;
   op->x->lane_session_occ = op->x_ls_occ;
+  op->x->lsdbg_on = op->x_lsdbg;
   op->x->timing = op->timing;  // scotty_enable_timing before the first push (the natural order) reaches the engine
   std::string e;
   int rc = op->x->init(op->device, op->stream, op->vt, op->keyed, e);
@@ -1538,6 +1540,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     }
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "lane_session_counters") == 0) {  // debugging aid: count the lane-session kernel's paths
+    if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;  // (debug stats 103-106)
+    op->x_lsdbg = value != 0;
+    if (op->x) op->x->lsdbg_on = op->x_lsdbg;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "quiet_ingest_mode") == 0) {  // exact engine's quiet pass: -1 default loop, 7 without DQ2 (A/B)
     if (value != -1 && value != 7) return SCOTTY_ERR_ARG;
     op->x_qmode = (int32_t)value;
@@ -1660,6 +1668,12 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
     case 100: return op->x->quiet_band_moves;   // committed quiet batches that moved a session start (start band)
     case 101: return op->x->quiet_jump_pieces;  // event-exact pieces cut right behind a located session-gap jump
     case 102: return op->x->quiet_band_noedge;  // of the band moves: sessions opened without a slice edge (start only)
+    case 103: case 104: case 105: case 106: {  // lane-session path counters (tune "lane_session_counters"): general,
+      unsigned long long v = 0;                // fast in-order, fast late (registers), fast late (memory) tuples
+      if (op->x->d_lsdbg && hipMemcpy(&v, op->x->d_lsdbg + (which - 103), 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+      return (int64_t)v;
+    }
     default:
       if (which >= 16 && which - 16 < (int)op->x->xq_trace.size()) return op->x->xq_trace[which - 16];
       return -1;

@@ -148,19 +148,23 @@ __device__ __forceinline__ int64_t wave_lower_bound(const int64_t* key, int64_t 
 
 // ================================================================ wm_prep (one workgroup of 1024 threads)
 __global__ __launch_bounds__(1024) void wm_prep_kernel(WmArgs a) {
-  __shared__ int64_t sc[8];
   __shared__ unsigned long long s_w[16];
+  __shared__ int64_t s_nh;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   DevMeta* meta = a.meta;
-  if (tid == 0) {
-    sc[0] = meta->overflow;
-    sc[1] = meta->head;
-    sc[2] = meta->tail;
-    sc[3] = meta->dirty_from;
+  // Every thread reads the operator's scalars itself (one line, uniform addresses) and issues its first trigger
+  // definition's loads at once, and the last wave runs the GC search while the others summarise the dirty blocks:
+  // this one-workgroup kernel is bound by its chain of dependent global accesses, not by its work
+  const int64_t ovf = meta->overflow, head = meta->head, tail = meta->tail, dirty_from = meta->dirty_from;
+  int kind0 = -1;
+  int64_t wa0 = 0, wb0 = 0;
+  if (tid < a.n_defs) {
+    kind0 = (int)a.wdef[3 * tid];
+    wa0 = a.wdef[3 * tid + 1];
+    wb0 = a.wdef[3 * tid + 2];
   }
-  __syncthreads();
   const WmLayout L(a.n_windows, a.n_aggs);
-  if (sc[0] != 0) {  // an earlier push of the interval overflowed: the host replays, nothing is assembled
+  if (ovf != 0) {  // an earlier push of the interval overflowed: the host replays, nothing is assembled
     if (tid == 0) {
       *(DevMeta*)a.out = *meta;
       *(int64_t*)(a.out + WM_HDR_N) = -1;
@@ -171,8 +175,19 @@ __global__ __launch_bounds__(1024) void wm_prep_kernel(WmArgs a) {
     }
     return;
   }
-  const int64_t head = sc[1], tail = sc[2];
-  const int64_t dirty = min(max(sc[3], (int64_t)0), tail);
+  // ---- 5 (early). GC (WindowManager.clearAfterWatermark): drop [head, idx) with idx the last slice whose
+  //      tStart <= remove_from; the window kernel still reads the pre-GC range [whead, tail)
+  if (wid == 15) {
+    int64_t nh = head;
+    if (tail > head) {  // idx = (count of tStart <= remove_from) - 1
+      const int64_t cnt_le = a.remove_from == INT64_MAX
+                                 ? tail
+                                 : wave_lower_bound(a.s_tstart, head, tail, a.remove_from + 1, lane);
+      nh = max(nh, cnt_le - 1);
+    }
+    if (lane == 0) s_nh = nh;
+  }
+  const int64_t dirty = min(max(dirty_from, (int64_t)0), tail);
   const bool need_min = (a.need & NEED_MIN) != 0, need_max = (a.need & NEED_MAX) != 0;
   const bool need_sum = (a.need & NEED_SUM) != 0;
   const bool f64 = a.vt == VT_F64;
@@ -259,9 +274,15 @@ __global__ __launch_bounds__(1024) void wm_prep_kernel(WmArgs a) {
     int kind = -1;
     int64_t wa = 0, wb = 0, cnt = 0;
     if (d < a.n_defs) {
-      kind = (int)a.wdef[3 * d];
-      wa = a.wdef[3 * d + 1];
-      wb = a.wdef[3 * d + 2];
+      if (base == 0) {
+        kind = kind0;
+        wa = wa0;
+        wb = wb0;
+      } else {
+        kind = (int)a.wdef[3 * d];
+        wa = a.wdef[3 * d + 1];
+        wb = a.wdef[3 * d + 2];
+      }
       cnt = trigger_def<false>(kind, wa, wb, a.last_wm, a.wm, nullptr, nullptr);
     }
     uint64_t tot;
@@ -274,17 +295,9 @@ __global__ __launch_bounds__(1024) void wm_prep_kernel(WmArgs a) {
   __threadfence_block();
   __syncthreads();
 
-  // ---- 5. GC (WindowManager.clearAfterWatermark): drop [head, idx) with idx the last slice whose
-  //      tStart <= remove_from; the window kernel still reads the pre-GC range [whead, tail)
-  if (wid == 0) {
-    int64_t nh = head;
-    if (tail > head) {  // idx = (count of tStart <= remove_from) - 1
-      const int64_t cnt_le = a.remove_from == INT64_MAX
-                                 ? tail
-                                 : wave_lower_bound(a.s_tstart, head, tail, a.remove_from + 1, lane);
-      nh = max(nh, cnt_le - 1);
-    }
-    if (lane != 0) return;
+  // ---- 6. the new head (the GC search above) and the watermark's header
+  if (tid == 0) {
+    const int64_t nh = s_nh;
     meta->whead = head;
     meta->head = nh;
     if (tail > nh) meta->oldest_start = a.s_tstart[nh];

@@ -519,6 +519,35 @@ def test_keyed_large_batch_count_property(pkg):
     assert sum(w.getAggValues()[1] for _, w in rows if w.hasValue()) == int(vals.astype(np.int64).sum())
 
 
+def test_keyed_table_growth_on_many_new_keys(pkg):
+    """One push bringing 3 M new keys (the key table is sized for the known keys + max(known, 2^20) new ones, so this
+    push overflows it: the insert pass stops, the table doubles and the pass re-runs), then a push of the same keys
+    again (lookups only on the grown table).  Every key: HashMap.put on first sight (KeyedScottyWindowOperator.java:
+    56-62), its tuples counted once per push; keys 0 and 0xFFFFFFFF among them."""
+    n = 3 << 20
+    rng = np.random.default_rng(31)
+    keys = ((np.arange(1, n + 1, dtype=np.uint64) * 2654435761) % (1 << 32)).astype(np.uint32)  # distinct
+    keys[0], keys[1] = 0xFFFFFFFF, 0  # the ends of the key range (0xFFFFFFFF once wrapped to the empty tag)
+    assert len(np.unique(keys)) == n
+    keys = rng.permutation(keys)
+    vals = rng.integers(-1000, 1000, size=n).astype(np.int32)
+    op = pkg.KeyedSlicingWindowOperator()
+    op.addWindowFunction(COUNT)
+    op.addWindowFunction(SUM)
+    op.addWindowAssigner(Tumbling(Time, 1001))
+    op.setMaxLateness(30_000)
+    for step in range(2):
+        ts = np.full(n, 10 + 1001 * step, dtype=np.int64)  # one tuple per key in tumbling window `step`
+        op.processElements(keys, ts, vals)
+        assert op.keyCount() == n
+        r = op.processWatermarkArrays(1001 * step + 1500)  # triggers exactly that window
+        assert len(r["start"]) == n and np.all(r["has_value"])
+        assert np.all(r["values"][0] == 1)
+        order = np.argsort(r["key"])
+        assert np.array_equal(r["key"][order], np.sort(keys))
+        assert np.array_equal(r["values"][1][order], vals[np.argsort(keys)].astype(np.int64))
+
+
 def test_keyed_hash_sharding_equals_single_operator(pkg):
     """SURVEY §8(e) keyed: ranks own disjoint key sets (the router's key groups) and need no collective.  G=3
     keyed operators fed by KeyedShardRouter's split of one stream (each shard in arrival order) leave exactly the
