@@ -40,8 +40,14 @@ hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
                                void** result, hipStream_t st);
-hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end,
-                      unsigned long long* tmax_b, hipStream_t st);
+hipError_t launch_key_max(const uint32_t* keys, int64_t n, unsigned int* kmax, hipStream_t st);
+int64_t seg_tiles(int64_t n);
+hipError_t launch_seg_count(int rec, const void* recs, int64_t n, int32_t* cnt, long long* tmax_tile,
+                            unsigned long long* tmax_b, hipStream_t st);
+hipError_t launch_seg_write(int rec, const void* recs, int64_t n, const int32_t* off, uint32_t* ukey, int64_t* ubeg,
+                            hipStream_t st);
+hipError_t launch_seg_fill(const int64_t* ubeg, const uint32_t* uslot, int64_t u_n, int64_t n, int64_t* seg_begin,
+                           int64_t* seg_end, hipStream_t st);
 int64_t sort_tile();
 hipError_t launch_scan_i32(const int32_t* in, int32_t* out, int64_t n, int32_t* tmp, hipStream_t st);
 hipError_t launch_kg_build(const uint32_t* slot_key, int64_t n_ops, unsigned long long* tab, uint64_t mask,
@@ -121,6 +127,7 @@ void XEngine::release() {
   dfree(d_lsdbg);
   dfree(d_need); dfree(d_table); dfree(d_newpos); dfree(d_newcnt); dfree(d_full); dfree(d_slot_key);
   dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32); dfree(d_seg_b); dfree(d_seg_e);
+  dfree(d_ukey); dfree(d_ubeg); dfree(d_segcnt); dfree(d_segoff); dfree(d_segscan); dfree(d_tmaxt); dfree(d_kmax);
   dfree(d_wcount); dfree(d_woff); dfree(d_scan64); dfree(d_misc);
   dfree(d_w_start); dfree(d_w_end); dfree(d_w_meas); dfree(d_w_op); dfree(d_w_key); dfree(d_has);
   for (int k = 0; k < SCOTTY_MAX_AGGS; k++) dfree(d_vals[k]);
@@ -472,8 +479,18 @@ int XEngine::ensure_batch(int64_t n) {
   XCHK(hipStreamSynchronize(stream));
   int64_t cap = std::max<int64_t>(n, 1 << 16);
   dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32);
+  dfree(d_ukey); dfree(d_ubeg); dfree(d_segcnt); dfree(d_segoff); dfree(d_segscan); dfree(d_tmaxt);
   const int rec = vt == VT_I32 ? 16 : 24;
   XCHK(dalloc(&d_slot, cap));
+  XCHK(dalloc(&d_ukey, cap));
+  XCHK(dalloc(&d_ubeg, cap));
+  {
+    const int64_t ns = seg_tiles(cap) + 1;
+    XCHK(dalloc(&d_segcnt, ns));
+    XCHK(dalloc(&d_segoff, ns));
+    XCHK(dalloc(&d_segscan, ns / 512 + 64));
+    XCHK(dalloc(&d_tmaxt, ns));
+  }
   XCHK(dalloc((unsigned char**)&d_recA, cap * rec));
   XCHK(dalloc((unsigned char**)&d_recB, cap * rec));
   const int64_t nb = (cap + sort_tile() - 1) / sort_tile();
@@ -1301,17 +1318,36 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   if (n <= 0) return SCOTTY_OK;
   int rc = ensure_batch(n);
   if (rc) return rc;
-  // table sized for the known keys plus at most max(known, 2^20) new ones (<= 50 % load): sizing it for every tuple
-  // of the batch being a new key (up to 2^24) made a 512-MB table at 1 M keys, every probe a random HBM line;
-  // a batch with more new keys fills it and re-runs on a doubled table (below)
-  rc = ensure_table(n_ops + std::min<int64_t>(n, std::max<int64_t>(n_ops, 1 << 20)));
+  if (!d_kmax) XCHK(dalloc(&d_kmax, 2));
+  // 1. stable sort of the batch by KEY (arrival order kept within each key, which the reference's out-of-order
+  //    handling depends on), over the bits the batch's largest key needs
+  XCHK(hipMemsetAsync(d_kmax, 0, 8, stream));
+  XCHK(launch_key_max(d_key, n, (unsigned int*)d_kmax, stream));
+  XCHK(hipMemcpyAsync(h_misc, d_kmax, 8, hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  const uint64_t kmax = (uint64_t)(uint32_t)h_misc[0];
+  const int rec = vt == VT_I32 ? 16 : 24;
+  void* sorted = nullptr;
+  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_key, n, bits_for((int64_t)kmax + 1), d_recA, d_recB, d_hist, d_scan32,
+                           &sorted, stream));
+  // 2. the batch's distinct keys in key order (segment u = [ubeg[u], ubeg[u + 1])) and its largest timestamp
+  const int64_t nbs = seg_tiles(n);
+  XCHK(launch_seg_count(rec, sorted, n, d_segcnt, (long long*)d_tmaxt, d_need + 3, stream));
+  XCHK(launch_scan_i32(d_segcnt, d_segoff, nbs, d_segscan, stream));
+  XCHK(launch_seg_write(rec, sorted, n, d_segoff, d_ukey, d_ubeg, stream));
+  XCHK(hipMemcpyAsync(h_misc, d_segoff + nbs - 1, 4, hipMemcpyDeviceToHost, stream));
+  XCHK(hipMemcpyAsync((unsigned char*)h_misc + 4, d_segcnt + nbs - 1, 4, hipMemcpyDeviceToHost, stream));
+  XCHK(hipStreamSynchronize(stream));
+  const int64_t u_n = (int64_t)((const int32_t*)h_misc)[0] + (int64_t)((const int32_t*)h_misc)[1];
+  // 3. distinct keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator()) for
+  //    a key's first tuple): one probe per key of the batch.  A table that fills up mid-pass is grown (the pass's
+  //    unassigned insertions dropped) and the pass re-run.
+  rc = ensure_table(n_ops + u_n);
   if (rc) return rc;
-  // 1. new keys -> slots (KeyedScottyWindowOperator.processElement: HashMap.put(key, initWindowOperator())).
-  //    A table that fills up mid-pass is grown (the pass's unassigned insertions dropped) and the pass re-run.
   for (int attempt = 0;; attempt++) {
     XCHK(hipMemsetAsync(d_newcnt, 0, 8, stream));
     XCHK(hipMemsetAsync(d_full, 0, 4, stream));
-    XCHK(launch_key_insert(d_key, n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, d_slot, stream));
+    XCHK(launch_key_insert(d_ukey, u_n, d_table, tcap - 1, d_newpos, d_newcnt, d_full, d_slot, stream));
     XCHK(hipMemcpyAsync(h_misc, d_newcnt, 8, hipMemcpyDeviceToHost, stream));
     XCHK(hipMemcpyAsync(h_misc + 1, d_full, 4, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
@@ -1337,13 +1373,9 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
       rc = ensure_table(n_ops);
       if (rc) return rc;
     }
+    XCHK(launch_slot(d_ukey, u_n, d_table, tcap - 1, d_slot, true, stream));  // the new keys' slots
   }
-  // 2. slots of the tuples whose key was new, stable sort by slot (arrival order kept within each key), segments
-  if (n_new > 0) XCHK(launch_slot(d_key, n, d_table, tcap - 1, d_slot, true, stream));
-  const int rec = vt == VT_I32 ? 16 : 24;
-  void* sorted = nullptr;
-  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_slot, n, bits_for(n_ops), d_recA, d_recB, d_hist, d_scan32, &sorted,
-                           stream));
+  // 4. every operator's segment of the sorted batch (empty for keys without tuples in it)
   if (seg_cap < n_ops) {
     XCHK(hipStreamSynchronize(stream));
     dfree(d_seg_b);
@@ -1354,9 +1386,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   }
   XCHK(hipMemsetAsync(d_seg_b, 0, n_ops * 8, stream));
   XCHK(hipMemsetAsync(d_seg_e, 0, n_ops * 8, stream));
-  XCHK(hipMemsetAsync(d_need + 3, 0, 8, stream));  // the batch's largest timestamp (biased), written by seg_kernel
-  XCHK(launch_seg(rec, sorted, n, d_seg_b, d_seg_e, d_need + 3, stream));
-  // 3. per-key replay; ops whose capacities might overflow are deferred, the tables grown, and relaunched
+  XCHK(launch_seg_fill(d_ubeg, d_slot, u_n, n, d_seg_b, d_seg_e, stream));
+  // 5. per-key replay; ops whose capacities might overflow are deferred, the tables grown, and relaunched
   XBatchArgs a = batch_args();
   a.ts = (const int64_t*)sorted;
   a.val = nullptr;

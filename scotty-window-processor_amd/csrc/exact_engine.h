@@ -202,7 +202,12 @@ class XEngine {
   std::vector<int64_t> h_kgpos;
   // batch scratch
   int64_t bcap = 0;
-  uint32_t* d_slot = nullptr;
+  uint32_t* d_slot = nullptr;         // replay path: the batch's distinct keys' slots
+  uint32_t* d_ukey = nullptr;         // replay path: the batch's distinct keys (sorted), segment starts, per-tile counts
+  int64_t* d_ubeg = nullptr;
+  int32_t *d_segcnt = nullptr, *d_segoff = nullptr, *d_segscan = nullptr;
+  int64_t* d_tmaxt = nullptr;
+  unsigned long long* d_kmax = nullptr;
   void *d_recA = nullptr, *d_recB = nullptr;
   int32_t *d_hist = nullptr, *d_scan32 = nullptr;
   int64_t seg_cap = 0;

@@ -3,14 +3,15 @@
 //
 // The reference keeps one SlicingWindowOperator per key in a HashMap and feeds each key's tuples in
 // arrival order (flink-connector/.../KeyedScottyWindowOperator.java:56-66).  Here:
-//   1. key_insert / key_assign: a device open-addressing hash table maps each key to a dense operator slot
-//      (new keys get the next free slots: the HashMap.put of initWindowOperator, :57-60);
-//   2. slot_kernel: slot of every tuple;
-//   3. an LDS-staged, stable LSD radix sort of the (ts, value, slot) records by slot, 8 bits per pass:
-//      radix_hist (per-tile digit counts) -> scan -> radix_scatter (tile ranked stably in LDS with
-//      wave ballots, written out as contiguous per-digit runs).  Stability keeps every key's tuples in
-//      arrival order, which the reference's out-of-order handling depends on;
-//   4. seg_kernel: [begin, end) of every operator's run.
+//   1. an LDS-staged, stable LSD radix sort of the (ts, value, key) records by key, 8 bits per pass over the
+//      bits the batch's largest key needs: radix_hist (per-tile digit counts) -> scan -> radix_scatter (tile
+//      ranked stably in LDS with wave ballots, written out as contiguous per-digit runs).  Stability keeps
+//      every key's tuples in arrival order, which the reference's out-of-order handling depends on;
+//   2. seg_count / seg_write: the batch's distinct keys and where each one's run starts;
+//   3. key_insert / key_assign: a device open-addressing hash table maps each distinct key to a dense operator
+//      slot (new keys get the next free slots: the HashMap.put of initWindowOperator, :57-60) -- one probe
+//      per key of the batch, not per tuple;
+//   4. seg_fill: [begin, end) of every operator's run.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -116,7 +117,8 @@ __global__ void slot_kernel(const uint32_t* keys, int64_t n, const unsigned long
 }
 
 // ---------------------------------------------------------------- records
-// REC = 16: {ts i64, val i32, slot u32};  REC = 24: {ts i64, val 64-bit, slot u32, pad}
+// REC = 16: {ts i64, val i32, slot u32};  REC = 24: {ts i64, val 64-bit, slot u32, pad}.  `slot` is the sort key:
+// the tuple's key on the replay path (push_keyed_replay)
 template <int REC>
 struct Rec;
 template <>
@@ -280,25 +282,140 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
   }
 }
 
-template <int REC>
-// also the batch's largest timestamp (biased to an unsigned order; one atomic per wavefront) when tmax_b is given
-__global__ void seg_kernel(const Rec<REC>* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end,
-                           unsigned long long* tmax_b) {
-  unsigned long long mx = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t s = recs[i].slot;
-    const unsigned long long b = (unsigned long long)recs[i].ts ^ 0x8000000000000000ull;
-    mx = b > mx ? b : mx;
-    if (i == 0 || recs[i - 1].slot != s) seg_begin[s] = i;
-    if (i == n - 1 || recs[i + 1].slot != s) seg_end[s] = i + 1;
-  }
-  if (tmax_b) {
+// ---------------------------------------------------------------- the batch's keys, after the sort by key
+// The replay path sorts the batch by KEY (stable: arrival order kept within a key) and maps each distinct key to its
+// operator slot once, instead of looking up every tuple's key before the sort (67 M random probes of the key table per
+// 2^26-tuple batch).  key_max_kernel: the largest key (the sort's bit count).  seg_count / seg_write: the positions
+// where the key changes, compacted in position order (per-tile counts, exclusive scan, write), so segment u spans
+// [ubeg[u], ubeg[u + 1]); seg_count also keeps each tile's largest timestamp (tmax_reduce: the batch's, biased).
+constexpr int SEG_ITEMS = 16;
+constexpr int SEG_THREADS = 256;
+constexpr int SEG_TILE = SEG_ITEMS * SEG_THREADS;
+
+__global__ __launch_bounds__(256) void key_max_kernel(const uint32_t* keys, int64_t n, unsigned int* kmax) {
+  __shared__ unsigned int s_m[4];
+  unsigned int m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, keys[i]);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long u = __shfl_xor(mx, o);
-      mx = u > mx ? u : mx;
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+    if (m) atomicMax(kmax, m);
+  }
+}
+
+// wave w of tile b: records [b * SEG_TILE + w * 64 * SEG_ITEMS, + 64 * SEG_ITEMS), read 64 consecutive records per
+// round (lane = record, coalesced); a segment starts where the key differs from the previous record's
+template <int REC>
+__device__ __forceinline__ void seg_wave_scan(const Rec<REC>* r, int64_t n, int64_t w0, int lane,
+                                              uint64_t (&starts)[SEG_ITEMS], uint32_t (&keys)[SEG_ITEMS],
+                                              long long& tmax) {
+  uint32_t prev_last = w0 > 0 && w0 - 1 < n ? r[w0 - 1].slot : 0;  // the record before the wave's range
+  tmax = INT64_MIN;
+#pragma unroll
+  for (int k = 0; k < SEG_ITEMS; k++) {
+    const int64_t i = w0 + (int64_t)k * 64 + lane;
+    uint32_t key = 0;
+    long long t = INT64_MIN;
+    if (i < n) {
+      key = r[i].slot;
+      t = r[i].ts;
     }
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(tmax_b, mx);
+    const uint32_t up = (uint32_t)__shfl_up((int)key, 1);
+    const uint32_t prev = lane == 0 ? prev_last : up;
+    starts[k] = __ballot(i < n && (i == 0 || key != prev));
+    keys[k] = key;
+    prev_last = (uint32_t)__shfl((int)key, 63);
+    tmax = max(tmax, t);
+  }
+}
+
+template <int REC>
+__global__ __launch_bounds__(SEG_THREADS) void seg_count_kernel(const Rec<REC>* r, int64_t n, int32_t* cnt,
+                                                                 long long* tmax_tile) {
+  __shared__ int s_c[SEG_THREADS / 64];
+  __shared__ long long s_t[SEG_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint64_t starts[SEG_ITEMS];
+  uint32_t keys[SEG_ITEMS];
+  long long tm;
+  seg_wave_scan<REC>(r, n, (int64_t)blockIdx.x * SEG_TILE + (int64_t)wid * 64 * SEG_ITEMS, lane, starts, keys, tm);
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < SEG_ITEMS; k++) c += __popcll(starts[k]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tm = max(tm, (long long)__shfl_xor(tm, o));
+  if (lane == 0) {
+    s_c[wid] = c;
+    s_t[wid] = tm;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int t = 0;
+    long long m = INT64_MIN;
+    for (int w = 0; w < SEG_THREADS / 64; w++) {
+      t += s_c[w];
+      m = max(m, s_t[w]);
+    }
+    cnt[blockIdx.x] = t;
+    tmax_tile[blockIdx.x] = m;
+  }
+}
+
+template <int REC>
+__global__ __launch_bounds__(SEG_THREADS) void seg_write_kernel(const Rec<REC>* r, int64_t n, const int32_t* off,
+                                                                 uint32_t* ukey, int64_t* ubeg) {
+  __shared__ int s_c[SEG_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t w0 = (int64_t)blockIdx.x * SEG_TILE + (int64_t)wid * 64 * SEG_ITEMS;
+  uint64_t starts[SEG_ITEMS];
+  uint32_t keys[SEG_ITEMS];
+  long long tm;
+  seg_wave_scan<REC>(r, n, w0, lane, starts, keys, tm);
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < SEG_ITEMS; k++) c += __popcll(starts[k]);
+  if (lane == 0) s_c[wid] = c;
+  __syncthreads();
+  int base = off[blockIdx.x];
+  for (int w = 0; w < wid; w++) base += s_c[w];
+  const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int k = 0; k < SEG_ITEMS; k++) {
+    if ((starts[k] >> lane) & 1) {
+      const int q = base + __popcll(starts[k] & lt);
+      ukey[q] = keys[k];
+      ubeg[q] = w0 + (int64_t)k * 64 + lane;
+    }
+    base += __popcll(starts[k]);
+  }
+}
+
+__global__ __launch_bounds__(1024) void tmax_reduce_kernel(const long long* tmax_tile, int64_t nb,
+                                                            unsigned long long* tmax_b) {
+  __shared__ long long s_t[16];
+  long long m = INT64_MIN;
+  for (int64_t b = threadIdx.x; b < nb; b += 1024) m = max(m, tmax_tile[b]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (long long)__shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) s_t[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; w++) m = max(m, s_t[w]);
+    *tmax_b = (unsigned long long)m ^ 0x8000000000000000ull;
+  }
+}
+
+// segment u of the sorted batch -> its operator's [begin, end)
+__global__ void seg_fill_kernel(const int64_t* ubeg, const uint32_t* uslot, int64_t u_n, int64_t n, int64_t* seg_begin,
+                                int64_t* seg_end) {
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < u_n; u += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t s = uslot[u];
+    seg_begin[s] = ubeg[u];
+    seg_end[s] = u + 1 < u_n ? ubeg[u + 1] : n;
   }
 }
 
@@ -558,15 +675,44 @@ hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, cons
   return hipSuccess;
 }
 
-hipError_t launch_seg(int rec, const void* recs, int64_t n, int64_t* seg_begin, int64_t* seg_end,
-                      unsigned long long* tmax_b, hipStream_t st) {
+hipError_t launch_key_max(const uint32_t* keys, int64_t n, unsigned int* kmax, hipStream_t st) {
   if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k::key_max_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0, st,
+                     keys, n, kmax);
+  return hipGetLastError();
+}
+int64_t seg_tiles(int64_t n) { return (n + k::SEG_TILE - 1) / k::SEG_TILE; }
+// segment starts of a batch sorted by key: cnt [seg_tiles(n)] (scanned in place), tmax_tile [seg_tiles(n)]
+hipError_t launch_seg_count(int rec, const void* recs, int64_t n, int32_t* cnt, long long* tmax_tile,
+                            unsigned long long* tmax_b, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nb = seg_tiles(n);
   if (rec == 16)
-    hipLaunchKernelGGL(k::seg_kernel<16>, dim3(grid_for(n)), dim3(256), 0, st, (const k::Rec<16>*)recs, n, seg_begin,
-                       seg_end, tmax_b);
+    hipLaunchKernelGGL(k::seg_count_kernel<16>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
+                       (const k::Rec<16>*)recs, n, cnt, tmax_tile);
   else
-    hipLaunchKernelGGL(k::seg_kernel<24>, dim3(grid_for(n)), dim3(256), 0, st, (const k::Rec<24>*)recs, n, seg_begin,
-                       seg_end, tmax_b);
+    hipLaunchKernelGGL(k::seg_count_kernel<24>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
+                       (const k::Rec<24>*)recs, n, cnt, tmax_tile);
+  hipLaunchKernelGGL(k::tmax_reduce_kernel, dim3(1), dim3(1024), 0, st, tmax_tile, nb, tmax_b);
+  return hipGetLastError();
+}
+hipError_t launch_seg_write(int rec, const void* recs, int64_t n, const int32_t* off, uint32_t* ukey, int64_t* ubeg,
+                            hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nb = seg_tiles(n);
+  if (rec == 16)
+    hipLaunchKernelGGL(k::seg_write_kernel<16>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
+                       (const k::Rec<16>*)recs, n, off, ukey, ubeg);
+  else
+    hipLaunchKernelGGL(k::seg_write_kernel<24>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
+                       (const k::Rec<24>*)recs, n, off, ukey, ubeg);
+  return hipGetLastError();
+}
+hipError_t launch_seg_fill(const int64_t* ubeg, const uint32_t* uslot, int64_t u_n, int64_t n, int64_t* seg_begin,
+                           int64_t* seg_end, hipStream_t st) {
+  if (u_n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k::seg_fill_kernel, dim3(grid_for(u_n)), dim3(256), 0, st, ubeg, uslot, u_n, n, seg_begin,
+                     seg_end);
   return hipGetLastError();
 }
 
