@@ -181,17 +181,18 @@ struct RV<24> {
 };
 
 // FIRST: input is SoA (ts, val, slot arrays); else AoS records
-template <int REC, bool FIRST>
+template <int REC, bool FIRST, int SI>
 __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>* in, const int64_t* ts,
                                                                    const void* val, const uint32_t* slot, int64_t n,
                                                                    int shift, int32_t* hist, int64_t nblocks) {
+  constexpr int TILE = SORT_THREADS * SI;
   __shared__ int32_t cnt[RADIX];
   const int tid = threadIdx.x;
   for (int d = tid; d < RADIX; d += SORT_THREADS) cnt[d] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
 #pragma unroll
-  for (int r = 0; r < SORT_ITEMS; r++) {
+  for (int r = 0; r < SI; r++) {
     const int64_t i = base + r * SORT_THREADS + tid;
     if (i < n) {
       const uint32_t s = FIRST ? slot[i] : in[i].slot;
@@ -202,30 +203,31 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>
   for (int d = tid; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = cnt[d];
 }
 
-// Stable scatter of one tile.  Each wavefront ranks its own contiguous 512-record sub-tile against
+// Stable scatter of one tile.  Each wavefront ranks its own contiguous SI * 64-record sub-tile against
 // wave-private digit counters in LDS (8 ballots per record, no block barrier between rounds); one barrier
 // then turns the per-wave counts into tile positions.  Arrival order inside the tile = (wave, round, lane).
-template <int REC, bool FIRST>
+template <int REC, bool FIRST, int SI>
 __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<REC>* in, const int64_t* ts,
                                                                       const void* val, const uint32_t* slot,
                                                                       int64_t n, int shift, const int32_t* offs,
                                                                       int64_t nblocks, Rec<REC>* out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  void* stage = smem;                                                      // [SORT_TILE] records
-  int32_t* wc = (int32_t*)(smem + sizeof(Rec<REC>) * SORT_TILE);          // [4][RADIX] per-wave counters
+  constexpr int TILE = SORT_THREADS * SI;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[REC * TILE + 4 * 6 * RADIX];
+  void* stage = smem;                                                      // [TILE] records
+  int32_t* wc = (int32_t*)(smem + sizeof(Rec<REC>) * TILE);               // [4][RADIX] per-wave counters
   int32_t* tot = wc + 4 * RADIX;                                           // [4] wave partial sums (scan)
   int32_t* tstart = tot + RADIX;                                           // [RADIX] tile digit starts
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t base = (int64_t)blockIdx.x * SORT_TILE;
-  constexpr int WAVE_ITEMS = SORT_ITEMS * 64;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  constexpr int WAVE_ITEMS = SI * 64;
   for (int d = tid; d < 4 * RADIX; d += SORT_THREADS) wc[d] = 0;
   __syncthreads();
-  RV<REC> item[SORT_ITEMS];
-  int32_t dig[SORT_ITEMS], rank[SORT_ITEMS];
+  RV<REC> item[SI];
+  int32_t dig[SI], rank[SI];
   int32_t* mine = wc + wid * RADIX;
   const unsigned long long lt = (1ull << lane) - 1;
 #pragma unroll
-  for (int r = 0; r < SORT_ITEMS; r++) {
+  for (int r = 0; r < SI; r++) {
     const int64_t i = base + wid * WAVE_ITEMS + r * 64 + lane;
     int d = -1;
     if (i < n) {
@@ -269,11 +271,11 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < SORT_ITEMS; r++)
+  for (int r = 0; r < SI; r++)
     if (dig[r] >= 0) item[r].store(stage, mine[dig[r]] + rank[r]);
   __syncthreads();
   // write out per-digit runs
-  const int64_t cnt_tile = min((int64_t)SORT_TILE, n - base);
+  const int64_t cnt_tile = min((int64_t)TILE, n - base);
   for (int i = tid; i < cnt_tile; i += SORT_THREADS) {
     const RV<REC> rr = RV<REC>::load(stage, i);
     const int d = (rr.slot() >> shift) & (RADIX - 1);
@@ -614,65 +616,49 @@ hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long
   return hipGetLastError();
 }
 
-int64_t sort_tile() { return k::SORT_TILE; }
+int64_t sort_tile() { return k::SORT_TILE; }  // the smallest tile (sizes the histogram buffers)
 
-// Stable sort of the batch by slot into records (AoS, rec bytes 16 or 24).  bufA/bufB: n records each;
-// hist/offs: RADIX * ceil(n / tile) int32; scan_tmp: int32 scratch.  Result lands in *result.
-hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
-                               int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
-                               void** result, hipStream_t st) {
-  const int64_t nb = (n + k::SORT_TILE - 1) / k::SORT_TILE;
-  int passes = (slot_bits + k::RB - 1) / k::RB;
-  if (passes < 1) passes = 1;
+template <int REC, int SI>
+static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t* slot, int64_t n, int passes,
+                              void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp, void** result, hipStream_t st) {
+  using R = k::Rec<REC>;
+  const int64_t nb = (n + k::SORT_THREADS * SI - 1) / (k::SORT_THREADS * SI);
   void* src = nullptr;
   void* dst = bufA;
   for (int p = 0; p < passes; p++) {
     const int shift = p * k::RB;
-    const size_t lds = (size_t)rec * k::SORT_TILE + 4 * (4 * k::RADIX + 2 * k::RADIX);
-    if (rec == 16) {
-      using R = k::Rec<16>;
-      if (p == 0) {
-        hipLaunchKernelGGL((k::radix_hist_kernel<16, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb);
-      } else {
-        hipLaunchKernelGGL((k::radix_hist_kernel<16, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                           (const R*)src, ts, val, slot, n, shift, hist, nb);
-      }
-      hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
-      if (e != hipSuccess) return e;
-      if (p == 0) {
-        hipLaunchKernelGGL((k::radix_scatter_kernel<16, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds, st,
-                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst);
-      } else {
-        hipLaunchKernelGGL((k::radix_scatter_kernel<16, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds,
-                           st, (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst);
-      }
-    } else {
-      using R = k::Rec<24>;
-      if (p == 0) {
-        hipLaunchKernelGGL((k::radix_hist_kernel<24, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb);
-      } else {
-        hipLaunchKernelGGL((k::radix_hist_kernel<24, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                           (const R*)src, ts, val, slot, n, shift, hist, nb);
-      }
-      hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
-      if (e != hipSuccess) return e;
-      if (p == 0) {
-        hipLaunchKernelGGL((k::radix_scatter_kernel<24, true>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds, st,
-                           (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst);
-      } else {
-        hipLaunchKernelGGL((k::radix_scatter_kernel<24, false>), dim3((unsigned)nb), dim3(k::SORT_THREADS), lds,
-                           st, (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst);
-      }
-    }
-    hipError_t e = hipGetLastError();
+    if (p == 0)
+      hipLaunchKernelGGL((k::radix_hist_kernel<REC, true, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb);
+    else
+      hipLaunchKernelGGL((k::radix_hist_kernel<REC, false, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                         (const R*)src, ts, val, slot, n, shift, hist, nb);
+    hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
     if (e != hipSuccess) return e;
+    if (p == 0)
+      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, true, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst);
+    else
+      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, false, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+                         (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst);
     src = dst;
-    dst = (dst == bufA) ? bufB : bufA;
+    dst = dst == bufA ? bufB : bufA;
   }
   *result = src;
-  return hipSuccess;
+  return hipGetLastError();
+}
+
+// Stable sort of the batch by slot into records (AoS, rec bytes 16 or 24).  bufA/bufB: n records each;
+// hist/offs: RADIX * ceil(n / sort_tile()) int32; scan_tmp: int32 scratch.  Result lands in *result.
+hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
+                               int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
+                               void** result, hipStream_t st) {
+  int passes = (slot_bits + k::RB - 1) / k::RB;
+  if (passes < 1) passes = 1;
+  // (4096-record tiles for 16-byte records, SI = 16: histogram 291 -> 240 us but scatter 593 -> 803 us per 2^26
+  // records -- the 70-KB stage halves the resident workgroups; profiles/r05/c4s_sort_by_key/)
+  if (rec == 16) return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st);
+  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st);
 }
 
 hipError_t launch_key_max(const uint32_t* keys, int64_t n, unsigned int* kmax, hipStream_t st) {
