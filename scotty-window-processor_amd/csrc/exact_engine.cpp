@@ -321,7 +321,7 @@ int XEngine::grow_ops(int64_t need) {
     return hipSuccess;
   };
   if (ops_cap == 0) {  // the store's layout is fixed with the first allocation
-    aos = keyed && lane_mode() && vt != VT_F64;
+    aos = keyed && (lane_mode() || lane_session_mode()) && vt != VT_F64;
     // MIN / MAX block summaries only if used (the functions are fixed before the first push: scotty_add_aggregation
     // refuses a function added after elements were processed)
     sl.kw_nf = (cfg.need & (NEED_MIN | NEED_MAX)) ? XK_NF : XK_NF_SUM;
@@ -1409,7 +1409,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
     a.retry = attempt > 0;
     a.sl = sl;
     a.ss = ss;
-    if (!lane_mode()) prefix_stale = true;  // the wavefront replay does not track the lane path's slice prefixes
+    // the wavefront replay does not track the lane paths' slice prefixes (XState.pvalid)
+    if (!lane_mode() && !lane_session_mode()) prefix_stale = true;
     XCHK(lane_mode()           ? launch_lane_replay(a, cfg, stream)
          : lane_session_mode() ? launch_lane_session(a, vt, lane_session_occ, stream)
                                : launch_replay(a, vt, stream));
@@ -1476,10 +1477,11 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   // the key-interleaved store's block summaries (XK_QN ...); f64 (and MIN / MAX outside that store) scan the slices
   // (wm_agg).  (MIN / MAX by a lane-per-key scan of each window's contained run in the key-major store measured
   // 2.46 ms per C4 watermark against 1.18 ms with wm_agg: the lanes walk 64 different lines per load.)
-  const bool prefix_agg = lane_mode() && !((cfg.need & NEED_SUM) && vt == VT_F64) &&
+  const bool prefix_agg = lane_wm_mode() && !((cfg.need & NEED_SUM) && vt == VT_F64) &&
                           (!(cfg.need & (NEED_MIN | NEED_MAX)) || sl.kw != nullptr);
   a.prefix_reset = prefix_stale ? 1 : 0;
-  const int64_t bound = prefix_agg ? lane_row_bound(wm) : -1;
+  // one-kernel watermark (rows from a host bound) for context-free windows only; sessions take the count pass
+  const int64_t bound = prefix_agg && lane_mode() ? lane_row_bound(wm) : -1;
   if (bound >= 0) {  // one kernel: count, reserve, emit, aggregate, GC -- rows sized from the bound
     int rc = ensure_rows(std::max<int64_t>(bound, 1));
     if (rc) return rc;

@@ -471,6 +471,17 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
         if (a.row_count) {
           int64_t mn = JMAX, mx = 0;
           k = lane_triggers<false>(c, s.lastWatermark, a.wm, nullptr, nullptr, nullptr, nullptr, 0, 0, mn, mx);
+          if (c->n_ctx > 0) {  // (the host takes this one-kernel mode for context-free windows only)
+            XState s2 = s;
+            const int64_t ks = lane_session_triggers<false>(c, a.ss, op, s2, a.wm, nullptr, nullptr, nullptr, nullptr,
+                                                            0, mn, mx);
+            if (ks < 0) {
+              atomicOr(a.err_flag, 1);
+              live = false;
+            } else {
+              k += ks;
+            }
+          }
         }
       }
     }
@@ -512,7 +523,7 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
   int64_t minTs = JMAX, maxTs = 0;
   k = lane_triggers<true>(c, s.lastWatermark, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, off, (int32_t)op, minTs,
                           maxTs);
-  if (!AGG && c->n_ctx > 0)  // (the count pass has thrown for an empty context)
+  if (c->n_ctx > 0)  // (the count pass has thrown for an empty context; no single-kernel row bound covers sessions)
     k += lane_session_triggers<true>(c, a.ss, op, s, a.wm, a.w_start, a.w_end, a.w_meas, a.w_op, off + k, minTs, maxTs);
   const int h = s.head, t = s.tail;
   // find_ts / find_count: last slice with key <= x (LazyAggregateStore.findSliceIndexBy*, :29-50), -1 if none
@@ -647,7 +658,7 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
   // clearAfterWatermark (:82-95): below the oldest session start of any context as well
   const int64_t cw = jsub(a.wm, c->max_lateness);
   int64_t first = cw;
-  for (int ctx = 0; !AGG && ctx < c->n_ctx; ctx++) {
+  for (int ctx = 0; ctx < c->n_ctx; ctx++) {
     const int64_t* st = a.ss.start + (op * c->ctx_alloc + ctx) * (int64_t)c->sesscap;
     for (int i = 0; i < s.ns(ctx); i++) first = min(first, st[i]);
   }

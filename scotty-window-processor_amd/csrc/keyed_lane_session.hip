@@ -22,24 +22,26 @@ namespace scotty {
 namespace ls {
 using namespace x;
 
-template <int VT>
+// V: the slice store's view -- XSlices (key-major columns) or XKView (key-interleaved words, COUNT / integer SUM /
+// MIN / MAX operators: the lanes of a wavefront touching one field of one slice position read one 512-B run)
+template <int VT, class V>
 struct LaneS {
   const XCfg* c;
-  XSlices sl;     // the store's columns (uniform); this key's slice i is element b + i
+  V q;            // the store's columns (uniform); this key's slice i is element b + i
   int64_t b;
   int64_t sb;     // this key's session base: context k, session i at sb + k * sesscap + i
   XState s;
   int32_t exc;
 
-  __device__ int64_t& TS(int i) const { return sl.ts[b + i]; }
-  __device__ int64_t& TE(int i) const { return sl.te[b + i]; }
-  __device__ int64_t& TL(int i) const { return sl.tl[b + i]; }
-  __device__ int64_t& TF(int i) const { return sl.tf[b + i]; }
-  __device__ int64_t& CS(int i) const { return sl.cs[b + i]; }
-  __device__ int64_t& CL(int i) const { return sl.cl[b + i]; }
-  __device__ int32_t& TY(int i) const { return sl.ty[b + i]; }
-  __device__ unsigned long long& CNT(int i) const { return sl.cnt[b + i]; }
-  __device__ unsigned long long& P(int k, int i) const { return sl.p[k][b + i]; }
+  __device__ int64_t& TS(int i) const { return q.ts[b + i]; }
+  __device__ int64_t& TE(int i) const { return q.te[b + i]; }
+  __device__ int64_t& TL(int i) const { return q.tl[b + i]; }
+  __device__ int64_t& TF(int i) const { return q.tf[b + i]; }
+  __device__ int64_t& CS(int i) const { return q.cs[b + i]; }
+  __device__ int64_t& CL(int i) const { return q.cl[b + i]; }
+  __device__ int32_t& TY(int i) const { return q.ty[b + i]; }
+  __device__ unsigned long long& CNT(int i) const { return q.cnt[b + i]; }
+  __device__ unsigned long long& P(int k, int i) const { return q.p[k][b + i]; }
   __device__ int64_t* SSp(const XSess& x, int k) const { return x.start + sb + (int64_t)k * c->sesscap; }
 
   // ---------------------------------------------------------------- slice list primitives (exact_op.h Op)
@@ -429,8 +431,8 @@ struct LaneS {
 // One tuple through the general restatement (everything the fast path below does not take: flexible edges, session
 // edits that move, split or merge slices, new sessions before the last, several session contexts, capacity edges).
 // Out of line: its state lives in the caller's LaneS, in scratch memory, which only these rare tuples pay for.
-template <int VT>
-__device__ __noinline__ void general_tuple(LaneS<VT>& L, const XSess x, int64_t t, int64_t vb) {
+template <int VT, class V>
+__device__ __noinline__ void general_tuple(LaneS<VT, V>& L, const XSess x, int64_t t, int64_t vb) {
   L.exc = 0;
   L.determine_slices(t);
   if (!L.exc) L.manager_process(x, t, vb);
@@ -442,7 +444,7 @@ __device__ __noinline__ void general_tuple(LaneS<VT>& L, const XSess x, int64_t 
   }
 }
 
-template <int VT, int OCC>
+template <int VT, int OCC, class V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void lane_session_kernel(XBatchArgs a) {
   const XCfg* cfg = a.cfg;
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -523,19 +525,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   //      the current (last) slice's fields.  It takes the steady-state tuples of one session context: in-order tuples
   //      that cross fixed edges, extend the last session or open a new one behind it without a flexible edge, and
   //      out-of-order tuples inside the last session -- the same transitions the general code makes for them.
-  // the store's columns as plain uniform pointers (a reference into the kernel argument would keep the argument block
-  // in scratch memory and reload a pointer from it on every access)
-  int64_t* const Q_ts = a.sl.ts;
-  int64_t* const Q_te = a.sl.te;
-  int64_t* const Q_tl = a.sl.tl;
-  int64_t* const Q_tf = a.sl.tf;
-  int64_t* const Q_cs = a.sl.cs;
-  int64_t* const Q_cl = a.sl.cl;
-  int32_t* const Q_ty = a.sl.ty;
-  unsigned long long* const Q_cnt = a.sl.cnt;
-  unsigned long long* const Q_p0 = a.sl.p[0];
-  unsigned long long* const Q_p1 = a.sl.p[1];
-  unsigned long long* const Q_p2 = a.sl.p[2];
+  // the store's columns as a local view (a reference into the kernel argument would keep the argument block in
+  // scratch memory and reload a pointer from it on every access)
+  const V q = xview<V>(a.sl);
+  const auto Q_ts = q.ts;
+  const auto Q_te = q.te;
+  const auto Q_tl = q.tl;
+  const auto Q_tf = q.tf;
+  const auto Q_cs = q.cs;
+  const auto Q_cl = q.cl;
+  const auto Q_ty = q.ty;
+  const auto Q_cnt = q.cnt;
+  const auto Q_p0 = q.p[0];
+  const auto Q_p1 = q.p[1];
+  const auto Q_p2 = q.p[2];
+  // lowest slice position whose partials this batch changes: the lane watermark's running prefixes and MIN / MAX
+  // block summaries (keyed_lane.hip, XState.pvalid) are valid below it only
+  int32_t minmod = INT32_MAX;
   const int64_t bb = op * (int64_t)cfg->sc;
   const int64_t sbase = op * cfg->ctx_alloc * (int64_t)cfg->sesscap;
   int64_t* const sst = a.ss.start + sbase;  // context 0
@@ -603,9 +609,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     if (cfg->need & NEED_MIN) p1 = min(p1, l.mn);
     if (cfg->need & NEED_MAX) p2 = max(p2, l.mx);
   };
-  auto add_cur = [&](int64_t t, int64_t vb) { fold(c_tl, c_tf, c_cl, c_cnt, c_p0, c_p1, c_p2, t, vb); };
-  auto add_prev = [&](int64_t t, int64_t vb) { fold(p_tl, p_tf, p_cl, p_cnt, p_p0, p_p1, p_p2, t, vb); };
+  auto add_cur = [&](int64_t t, int64_t vb) {
+    fold(c_tl, c_tf, c_cl, c_cnt, c_p0, c_p1, c_p2, t, vb);
+    minmod = min(minmod, ci);
+  };
+  auto add_prev = [&](int64_t t, int64_t vb) {
+    fold(p_tl, p_tf, p_cl, p_cnt, p_p0, p_p1, p_p2, t, vb);
+    minmod = min(minmod, pv);
+  };
   auto add_mem = [&](int i, int64_t t, int64_t vb) {  // an older slice, in memory
+    minmod = min(minmod, i);
     const int64_t j = bb + i;
     Q_tl[j] = max(Q_tl[j], t);
     Q_tf[j] = min(Q_tf[j], t);
@@ -654,6 +667,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     }
     const int64_t j = bb + tail;
     Q_ts[j] = start; Q_te[j] = JMAX; Q_cs[j] = cc; Q_ty[j] = 1;
+    minmod = min(minmod, tail);
     ci = tail;
     tail++;
     c_ts = start; c_tl = start; c_tf = JMAX; c_cl = cc; c_cnt = 0; c_p0 = 0; c_p1 = ID_MIN; c_p2 = ID_MAX;
@@ -686,9 +700,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     return lo;
   };
   const XSess xs{a.ss.start, a.ss.end};  // (by value: no reference may point into the argument block)
-  LaneS<VT> L;  // the general path's state (scratch; only rare tuples touch it)
+  LaneS<VT, V> L;  // the general path's state (scratch; only rare tuples touch it)
   L.c = cfg;
-  L.sl = a.sl;
+  L.q = q;
   L.b = bb;
   L.sb = sbase;
   load_fast();
@@ -817,7 +831,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     L.s.maxEventTime = mx; L.s.nextEdgeTs = ne; L.s.currentCount = cc;
     L.s.head = head; L.s.tail = tail; L.s.unsorted = uns; L.s.started = started; L.s.nsess[0] = ns;
     L.s.dropped = dropped; L.s.err = err;
-    general_tuple<VT>(L, xs, t, vb);
+    general_tuple<VT, V>(L, xs, t, vb);
+    minmod = 0;  // (session edits move, split and merge slices; a compaction moves them all)
     s0 = L.s;
     mx = s0.maxEventTime; ne = s0.nextEdgeTs; cc = s0.currentCount;
     head = s0.head; tail = s0.tail; uns = s0.unsorted; started = s0.started; ns = s0.nsess[0];
@@ -830,6 +845,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   s0.maxEventTime = mx; s0.nextEdgeTs = ne; s0.currentCount = cc;
   s0.head = head; s0.tail = tail; s0.unsorted = uns; s0.started = started; s0.nsess[0] = ns;
   s0.dropped = dropped; s0.err = err;
+  if (minmod < s0.pvalid) s0.pvalid = minmod;
   *sp = s0;
   if (a.dbg) {  // (lanes that returned early count nothing; the atomics below are per lane -- a debugging aid)
     atomicAdd(&a.dbg[0], (unsigned long long)n_gen);
@@ -846,15 +862,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
 hipError_t launch_lane_session(const XBatchArgs& a, int vt, int occ, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
-  if (occ == 2) {
-    if (vt == VT_I32) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 2>), grid, block, 0, st, a);
-    else if (vt == VT_I64) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I64, 2>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((ls::lane_session_kernel<VT_F64, 2>), grid, block, 0, st, a);
+#define SCOTTY_LS(VT_, OCC_, V_) hipLaunchKernelGGL((ls::lane_session_kernel<VT_, OCC_, V_>), grid, block, 0, st, a)
+  if (a.sl.kw) {  // key-interleaved store: integer values
+    if (occ == 2) {
+      if (vt == VT_I32) SCOTTY_LS(VT_I32, 2, XKView); else SCOTTY_LS(VT_I64, 2, XKView);
+    } else {
+      if (vt == VT_I32) SCOTTY_LS(VT_I32, 3, XKView); else SCOTTY_LS(VT_I64, 3, XKView);
+    }
+  } else if (occ == 2) {
+    if (vt == VT_I32) SCOTTY_LS(VT_I32, 2, XSlices);
+    else if (vt == VT_I64) SCOTTY_LS(VT_I64, 2, XSlices);
+    else SCOTTY_LS(VT_F64, 2, XSlices);
   } else {
-    if (vt == VT_I32) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 3>), grid, block, 0, st, a);
-    else if (vt == VT_I64) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I64, 3>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((ls::lane_session_kernel<VT_F64, 3>), grid, block, 0, st, a);
+    if (vt == VT_I32) SCOTTY_LS(VT_I32, 3, XSlices);
+    else if (vt == VT_I64) SCOTTY_LS(VT_I64, 3, XSlices);
+    else SCOTTY_LS(VT_F64, 3, XSlices);
   }
+#undef SCOTTY_LS
   return hipGetLastError();
 }
 

@@ -1532,6 +1532,9 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
   }
   if (std::strcmp(key, "keyed_lane_session") == 0) {  // 0: keyed sessions through the wavefront replay (A/B),
     if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;  // 1 lane kernel, 2 its 3-waves build
+    // (the store layout follows the kernel at the first push: the lane kernel's key-interleaved store cannot be
+    // handed to the wavefront replay later)
+    if (op->x && op->x->key_count() > 0 && (value == 0) != op->x_ls_off) return SCOTTY_ERR_STATE;
     op->x_ls_off = value == 0;
     op->x_ls_occ = value == 2 ? 3 : 2;
     if (op->x) {
