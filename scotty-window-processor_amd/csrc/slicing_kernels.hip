@@ -1044,7 +1044,8 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       const int64_t gk = gk_of(k);
       const int64_t ts_ = lower_bound_lds(s_p, nT, gk);
       const int64_t pprev = ts_ > 0 ? max(prev_max, (int64_t)s_p[ts_ - 1]) : prev_max;
-      const int64_t tm = a.tilemax[ts_];
+      // the first tile whose prefix max reaches gk: its own max is that prefix max (the prefix before it is < gk)
+      const int64_t tm = ts_ < nT ? (int64_t)s_p[ts_] : a.tilemax[ts_];
       int f;
       if (k == 0 || gk_of(k - 1) <= pprev || (int64_t)((uint64_t)tm - (uint64_t)gk) < L) f = 1;
       else f = 2;
