@@ -1183,8 +1183,8 @@ int XEngine::push_kg(const uint32_t* d_key, const int64_t* d_ts, const void* d_v
   a.cmax = cm;
   a.tile = tile;
   a.variant = kg_variant;
-  static const bool no_compact = getenv("SCOTTY_KG_NO_COMPACT") != nullptr;  // A/B of the 8-byte records
-  a.allow_compact = vt == VT_I32 && kg_variant >= 1 && tile == 8192 && !no_compact ? 1 : 0;  // default kernels only
+  // 8-byte records with the default kernels only (scotty_tune "keyed_grid_variant" 0: the 12-byte records, A/B)
+  a.allow_compact = vt == VT_I32 && kg_variant >= 1 && tile == 8192 ? 1 : 0;
   a.part = d_kgpart;
   a.dflag = d_kgdflag;
   a.hist = d_kghist;
