@@ -106,6 +106,7 @@ struct CommitArgs {
   int need;
   int vt;
   int64_t push_seq;
+  long long* stamps;         // nullable: phase clock stamps (scotty_tune "ingest_stamps"; a debugging aid)
 };
 
 // ---- watermark of the grid path (window_kernels.hip): window assembly over slice-block summaries.

@@ -634,6 +634,7 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
   scotty_op::TEv tc;
   rc = tbegin(op, tc, SCOTTY_TIME_PUSH_OTHER);
   if (rc) return rc;
+  if (op->stamps_on && op->d_stamps) ca.stamps = op->d_stamps + 8192 * 4 - 16;  // the commit's phase stamps
   HIPCHK(launch_commit(ca, op->stream));
   return tend(op, tc);
 }
@@ -1638,6 +1639,13 @@ int64_t scotty_debug_grid_stat(scotty_op* op, int which) {
 
 // Internal (not in the header): the last grid ingest's phase stamps (s_memtime ticks), [workgroups][4]: start, LDS
 // window ready, every wave's range done, window flushed to the cells.  Returns the workgroups copied.
+// The last commit's phase stamps (8: start, prefix maxima, candidates, edge decision, ambiguous scans, ranks and
+// appends, fold, before the meta write), in the same buffer's last 16 words.
+int64_t scotty_debug_commit_stamps(scotty_op* op, long long* out) {
+  if (!op || !op->d_stamps) return -1;
+  if (hipMemcpy(out, op->d_stamps + 8192 * 4 - 16, 8 * 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return 7;
+}
 int64_t scotty_debug_ingest_stamps(scotty_op* op, long long* out, int64_t max_blocks) {
   if (!op || !op->d_stamps) return -1;
   const int64_t nb = std::min<int64_t>(std::min<int64_t>(op->last_ingest_blocks, 8192), max_blocks);

@@ -937,6 +937,10 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
   __shared__ int64_t sc[16];
   __shared__ long long s_dirty;       // lowest slice whose partials change (watermark block summaries)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto stamp = [&](int k) {  // phase clock stamps (debugging aid)
+    if (a.stamps && tid == 0) a.stamps[k] = (long long)__builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   // Every thread reads the operator's scalars itself (one line, uniform addresses) and issues the tile-maxima and
   // grid-window loads at once: the chain of dependent global accesses is what bounds this one-workgroup kernel
   const DevMeta& m = *a.meta;
@@ -972,6 +976,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     if (t < nT) s_p[t] = max(carry, loc[j]);
   }
   __syncthreads();
+  stamp(1);
   const int64_t batch_max = max(prev_max, nT > 0 ? (int64_t)s_p[nT - 1] : INT64_MIN);
   const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
 
@@ -1019,6 +1024,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     }
   }
   __syncthreads();
+  stamp(2);
   const int64_t ncand = sc[8];
   int ovf = (int)sc[9];
   // flags and ranks of the candidates: LDS for the common case, the global scratch arrays beyond it
@@ -1057,6 +1063,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     }
   }
   __syncthreads();
+  stamp(3);
   const int namb = s_namb;
   if (!ovf && namb > 0) {
     const int64_t kn = namb <= AMB_CAP ? namb : ncand;  // list overflow: every candidate, flag checked
@@ -1097,6 +1104,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     __syncthreads();
   }
 
+  stamp(4);
   // ---- (d) rank = inclusive prefix count of emitted edges (ballot/popcount per wave)
   int64_t n_emit = 0;
   if (!ovf) {
@@ -1136,6 +1144,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     if (tail + n_emit > a.scap) ovf = 2;
   }
   __syncthreads();
+  stamp(5);
 
   if (!ovf) {
     // ---- (f) fold cells into slices (AbstractSlice.addElement + AggregateState.merge semantics); cells below
@@ -1180,6 +1189,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     }
   }
   __syncthreads();
+  stamp(6);
   if (tid == 0) {
     DevMeta& mw = *a.meta;
     mw.batch_max = batch_max;

@@ -1,7 +1,8 @@
 """Phase split of the grid ingest kernel from its per-workgroup clock stamps (scotty_tune "ingest_stamps"): C2 or C2s
 (--c2s) at the bench size, a few pushes, then for the last push the median over workgroups of (window ready - start),
 (ranges done - window ready), (window flushed - ranges done) and the spread of the workgroups' start and end
-stamps, in microseconds (s_memtime ticks / --ghz).  GPU box tool."""
+stamps, in microseconds (s_memtime ticks / --ghz); and the commit kernel's phase split (commit_*: the ticks between
+its stamps).  GPU box tool."""
 import argparse
 import ctypes
 import importlib
@@ -28,6 +29,8 @@ def main():
     L = pkg.lib()
     f = L.scotty_debug_ingest_stamps
     f.restype, f.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    fc = L.scotty_debug_commit_stamps
+    fc.restype, fc.argtypes = ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p]
     B = 1 << 27
     rate = B // 1000
     dev = torch.device("cuda", 0)
@@ -71,6 +74,9 @@ def main():
                "flush_us_max": us(np.max(st[:, 3] - st[:, 2])),
                "start_spread_us": us(st[:, 0].max() - t0), "end_spread_us": us(st[:, 3].max() - st[:, 3].min()),
                "span_us": us(st[:, 3].max() - t0)}
+        cb = np.zeros(8, dtype=np.int64)
+        if fc(op._h, cb.ctypes.data) == 7:
+            out["commit_ticks"] = [int(cb[i + 1] - cb[i]) for i in range(6)]
         print(json.dumps(out), flush=True)
 
 
