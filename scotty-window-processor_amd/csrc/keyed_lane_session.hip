@@ -741,6 +741,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   for (int u_ = 0; u_ < m_ && !err; u_++) {
     const int64_t t = R_t[u_][tid], vb = R_v[u_][tid];
     bool fast = one_ctx && ns > 0 && ci >= 0 && started;
+    bool shift = false;
     int n_app = 0;
     if (fast) {
       if (t >= mx) {  // in-order: no flexible edge, a first pending edge, room for the fixed edges it crosses
@@ -763,8 +764,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         }
         // the session: extended, unchanged, or a new one behind the last (t >= maxEventTime >= its end)
         if (fast && jadd(en_l, gap) < t && ns >= cfg->sesscap) fast = false;
-      } else {  // out-of-order: inside the last session (updateContext changes nothing, no modification)
-        if (!(t >= st_l && t <= en_l)) fast = false;
+      } else if (t >= st_l && t <= en_l) {
+        // out-of-order inside the last session: updateContext changes nothing, no modification
+      } else if (t < st_l && t < c_tl && c_ts == st_l && pv >= 0 && jsub(st_l, gap) < t) {
+        // out-of-order below the last session's start, within its gap: shiftStart (SessionWindow.java:56-66) when no
+        // earlier session reaches t (getSession returns the last one, no merge follows), and checkSliceEdges moves the
+        // movable edge between the previous slice and the current one -- which starts at the session start -- down to
+        // t (S/SliceManager.java:89-125)
+        shift = (ns < 2 || t > jadd(sen[ns - 2], gap)) && ty_movable(Q_ty[bb + pv]);
+        if (!shift) fast = false;
+      } else {
+        fast = false;
       }
     }
     if (fast) {
@@ -801,6 +811,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
       } else {
         cc = jadd(cc, 1);  // determineSlices: out of order, WindowManager.incrementCount only
         n_late++;
+        if (shift) {  // the session start and the edge below the current slice move down to t
+          Q_te[bb + pv] = t;
+          Q_ts[bb + ci] = t;
+          c_ts = t;
+          uns |= 2;
+          if (p_ts > t) uns |= 1;  // note_order of the moved slice
+          st_l = t;
+          sst[ns - 1] = t;
+        }
         // the in-order branch of processElement (t >= the current slice's tLast), else findSliceIndexByTimestamp:
         // its first two probes from the tail are the current and the previous slice (registers), on a sorted list
         // and on an unsorted one alike (the reference's loop runs backwards from the tail)
