@@ -654,13 +654,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     }
     return e;
   };
-  // SliceManager.appendSlice (S/SliceManager.java:27-38) of a fixed edge, the current slice in registers
-  // (the current slice's fields move to the previous-slice registers, the old previous slice goes to memory)
-  auto append_fixed = [&](int64_t start) {
+  // SliceManager.appendSlice (S/SliceManager.java:27-38) of an edge of type ety (fixed, or a flexible edge's counter),
+  // the current slice in registers (its fields move to the previous-slice registers, the old previous slice goes to
+  // memory)
+  auto append_edge = [&](int64_t start, int32_t ety) {
     if (ci >= 0) {
       flush_prev();
       Q_te[bb + ci] = start;
-      Q_ty[bb + ci] = XTYPE_FIXED;
+      Q_ty[bb + ci] = ety;
       pv = ci; p_ts = c_ts; p_tl = c_tl; p_tf = c_tf; p_cl = c_cl; p_cnt = c_cnt;
       p_p0 = c_p0; p_p1 = c_p1; p_p2 = c_p2;
       if (c_ts > start) uns |= 1;
@@ -741,25 +742,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   for (int u_ = 0; u_ < m_ && !err; u_++) {
     const int64_t t = R_t[u_][tid], vb = R_v[u_][tid];
     bool fast = one_ctx && ns > 0 && ci >= 0 && started;
-    bool shift = false;
+    bool shift = false, flexe = false;
     int n_app = 0;
     if (fast) {
-      if (t >= mx) {  // in-order: no flexible edge, a first pending edge, room for the fixed edges it crosses
+      if (t >= mx) {  // in-order: a first pending edge, room for the fixed edges it crosses and a flexible one
         const int64_t t_c = max(mx, ne);
-        if (ne == JMIN || (cfg->has_fixed == 0 && ne != JMIN) || t >= jadd(t_c, gap)) {
+        flexe = t >= jadd(t_c, gap);  // StreamSlicer.calculateNextFlexEdge (:118-130), one session context
+        if (ne == JMIN || cfg->has_fixed == 0) {
           fast = false;
-        } else if (t >= ne) {
+        } else {
           int64_t e = ne;
-          while (t > e && n_app <= 8) {
-            if (e >= 0) n_app++;
-            const int64_t nx = next_edge(t, e);
-            if (nx == JMIN || nx <= e) {  // the reference's hang / overflow: the general path reports it
-              n_app = 99;
-              break;
+          if (t >= ne) {
+            while (t > e && n_app <= 8) {
+              if (e >= 0) n_app++;
+              const int64_t nx = next_edge(t, e);
+              if (nx == JMIN || nx <= e) {  // the reference's hang / overflow: the general path reports it
+                n_app = 99;
+                break;
+              }
+              e = nx;
             }
-            e = nx;
           }
           if (e == t) n_app++;
+          else if (flexe) n_app++;
           if (n_app > 8 || tail + n_app > sc) fast = false;
         }
         // the session: extended, unchanged, or a new one behind the last (t >= maxEventTime >= its end)
@@ -782,12 +787,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         // StreamSlicer.determineSlices, in-order branch (:51-86), without a flexible edge
         if (n_app > 0) {
           while (t > ne) {
-            if (ne >= 0) append_fixed(ne);
+            if (ne >= 0) append_edge(ne, XTYPE_FIXED);
             ne = next_edge(t, ne);
           }
           if (ne == t) {
-            append_fixed(t);
+            append_edge(t, XTYPE_FIXED);
             ne = next_edge(t, ne);
+          } else if (flexe) {
+            append_edge(t, ty_flex(1));  // calculateNextFlexEdge: the session gap reached (one context)
           }
         }
         cc = jadd(cc, 1);
