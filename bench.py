@@ -788,7 +788,8 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
             times.append(time.perf_counter() - t0)
             rows += n
     roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
-                           "keyed replay: radix sort by key + lane_session_kernel (lane per key)")
+                           "lane_session_kernel (lane per key, the replay of the batch sorted by key; the sort, segment and "
+                           "key-table passes are push_other)")
     return {"workload": "C4s: keyed SessionWindow(gap 1s) + SlidingWindow(60s,1s) SUM_I32, %d uniform keys, 20%% "
                         "out-of-order (delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, maxLateness 1000, "
                         "lane-per-key session replay, results left in HBM" % keys, "tune": tune or {},

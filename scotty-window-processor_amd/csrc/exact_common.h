@@ -237,6 +237,9 @@ struct XBatchArgs {
   // nullable: the batch's largest timestamp, biased (ts ^ 1 << 63, an unsigned order) -- seg_kernel's by-product; the
   // lane-session kernel bounds a started key's capacity need with it before it reads the key's tuples
   const unsigned long long* ts_max_b;
+  // rec_stride 8 (lane-session replay of an int32 batch only): packed records {key << pk_bits | ts - pk_base, value}
+  int64_t pk_base;
+  int32_t pk_bits;
   unsigned long long* dbg;  // nullable: lane-session path counters (general / fast in-order / fast late in registers /
                             // fast late in memory tuples), debugging aid
 };

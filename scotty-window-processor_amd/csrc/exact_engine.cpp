@@ -39,13 +39,14 @@ hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long
                        uint32_t* slot, bool fixup, hipStream_t st);
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
-                               void** result, hipStream_t st);
-hipError_t launch_key_max(const uint32_t* keys, int64_t n, unsigned int* kmax, hipStream_t st);
+                               void** result, hipStream_t st, int64_t tbase, int tb);
+hipError_t launch_key_max(const uint32_t* keys, const int64_t* ts, int64_t n, unsigned long long* range,
+                          hipStream_t st);
 int64_t seg_tiles(int64_t n);
 hipError_t launch_seg_count(int rec, const void* recs, int64_t n, int32_t* cnt, long long* tmax_tile,
-                            unsigned long long* tmax_b, hipStream_t st);
+                            unsigned long long* tmax_b, hipStream_t st, int64_t tbase, int tb);
 hipError_t launch_seg_write(int rec, const void* recs, int64_t n, const int32_t* off, uint32_t* ukey, int64_t* ubeg,
-                            hipStream_t st);
+                            hipStream_t st, int64_t tbase, int tb);
 hipError_t launch_seg_fill(const int64_t* ubeg, const uint32_t* uslot, int64_t u_n, int64_t n, int64_t* seg_begin,
                            int64_t* seg_end, hipStream_t st);
 int64_t sort_tile();
@@ -1318,23 +1319,49 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   if (n <= 0) return SCOTTY_OK;
   int rc = ensure_batch(n);
   if (rc) return rc;
-  if (!d_kmax) XCHK(dalloc(&d_kmax, 2));
+  if (!d_kmax) XCHK(dalloc(&d_kmax, 4));
   // 1. stable sort of the batch by KEY (arrival order kept within each key, which the reference's out-of-order
   //    handling depends on), over the bits the batch's largest key needs
-  XCHK(hipMemsetAsync(d_kmax, 0, 8, stream));
-  XCHK(launch_key_max(d_key, n, (unsigned int*)d_kmax, stream));
-  XCHK(hipMemcpyAsync(h_misc, d_kmax, 8, hipMemcpyDeviceToHost, stream));
+  // device time: the sort, segment and key-table passes are PUSH_OTHER, the per-key replay kernel (the path's
+  // largest single kernel) is INGEST, timed per launch
+  TEv tk, ts0, tr;
+  if ((rc = tbegin(tk, SCOTTY_TIME_PUSH_OTHER))) return rc;
+  //    The lane-session replay of an int32 batch whose key bits and event-time span fit one 32-bit word sorts
+  //    packed 8-byte records (keyed_kernels.hip, Rec<8>): the key range pass then also takes the timestamp range
+  const bool pack_try = vt == VT_I32 && lane_session_mode() && !pack_off;
+  XCHK(hipMemsetAsync(d_kmax, 0, 24, stream));
+  XCHK(launch_key_max(d_key, pack_try ? d_ts : nullptr, n, d_kmax, stream));
+  if ((rc = tend(tk, 0))) return rc;
+  XCHK(hipMemcpyAsync(h_misc, d_kmax, 24, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
   const uint64_t kmax = (uint64_t)(uint32_t)h_misc[0];
-  const int rec = vt == VT_I32 ? 16 : 24;
+  const int kb = bits_for((int64_t)kmax + 1);
+  int rec = vt == VT_I32 ? 16 : 24;
+  int64_t tbase = 0;
+  int tb = 0;
+  if (pack_try) {
+    const int64_t tlo = (int64_t)(~(uint64_t)h_misc[1] ^ 0x8000000000000000ull);
+    const int64_t thi = (int64_t)((uint64_t)h_misc[2] ^ 0x8000000000000000ull);
+    const uint64_t span = (uint64_t)thi - (uint64_t)tlo;  // thi >= tlo (n > 0)
+    if (span < ((uint64_t)1 << 31)) {
+      tb = bits_for((int64_t)span + 1);
+      if (tb + kb <= 32) {
+        rec = 8;
+        tbase = tlo;
+      }
+    }
+  }
+  last_rec_bytes = rec;
   void* sorted = nullptr;
-  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_key, n, bits_for((int64_t)kmax + 1), d_recA, d_recB, d_hist, d_scan32,
-                           &sorted, stream));
+  if ((rc = tbegin(ts0, SCOTTY_TIME_PUSH_OTHER))) return rc;
+  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_key, n, kb, d_recA, d_recB, d_hist, d_scan32, &sorted, stream, tbase,
+                           tb));
   // 2. the batch's distinct keys in key order (segment u = [ubeg[u], ubeg[u + 1])) and its largest timestamp
   const int64_t nbs = seg_tiles(n);
-  XCHK(launch_seg_count(rec, sorted, n, d_segcnt, (long long*)d_tmaxt, d_need + 3, stream));
+  XCHK(launch_seg_count(rec, sorted, n, d_segcnt, (long long*)d_tmaxt, d_need + 3, stream, tbase, tb));
   XCHK(launch_scan_i32(d_segcnt, d_segoff, nbs, d_segscan, stream));
-  XCHK(launch_seg_write(rec, sorted, n, d_segoff, d_ukey, d_ubeg, stream));
+  XCHK(launch_seg_write(rec, sorted, n, d_segoff, d_ukey, d_ubeg, stream, tbase, tb));
+  if ((rc = tend(ts0, 0))) return rc;
   XCHK(hipMemcpyAsync(h_misc, d_segoff + nbs - 1, 4, hipMemcpyDeviceToHost, stream));
   XCHK(hipMemcpyAsync((unsigned char*)h_misc + 4, d_segcnt + nbs - 1, 4, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
@@ -1395,6 +1422,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   a.seg_begin = d_seg_b;
   a.seg_end = d_seg_e;
   a.rec_stride = rec;
+  a.pk_base = tbase;
+  a.pk_bits = tb;
   a.need = d_need;
   a.ts_max_b = d_need + 3;
   if (lsdbg_on) {
@@ -1411,9 +1440,11 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
     a.ss = ss;
     // the wavefront replay does not track the lane paths' slice prefixes (XState.pvalid)
     if (!lane_mode() && !lane_session_mode()) prefix_stale = true;
+    if ((rc = tbegin(tr, SCOTTY_TIME_INGEST))) return rc;
     XCHK(lane_mode()           ? launch_lane_replay(a, cfg, stream)
          : lane_session_mode() ? launch_lane_session(a, vt, lane_session_occ, stream)
                                : launch_replay(a, vt, stream));
+    if ((rc = tend(tr, n))) return rc;
     XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));
     XCHK(hipStreamSynchronize(stream));
     if (h_misc[0] == 0 && h_misc[1] == 0 && h_misc[2] == 0) return SCOTTY_OK;

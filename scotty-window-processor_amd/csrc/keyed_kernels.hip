@@ -118,9 +118,21 @@ __global__ void slot_kernel(const uint32_t* keys, int64_t n, const unsigned long
 
 // ---------------------------------------------------------------- records
 // REC = 16: {ts i64, val i32, slot u32};  REC = 24: {ts i64, val 64-bit, slot u32, pad}.  `slot` is the sort key:
-// the tuple's key on the replay path (push_keyed_replay)
+// the tuple's key on the replay path (push_keyed_replay).
+// REC = 8, packed: {w u32 = key << tb | (ts - tbase), val i32} -- an int32 batch whose key bits plus the bits of its
+// event-time span fit one word (C4s: 2^20 keys, ~1.5 s of milliseconds: 20 + 11 bits).  Half the bytes of every
+// sort pass, segment scan and replay read; the sort digits start at bit tb, so key order is word order.
+struct PackP {
+  int64_t tbase;  // the batch's smallest timestamp
+  int32_t tb;     // timestamp-offset bits (< 32); the key takes the bits above
+};
 template <int REC>
 struct Rec;
+template <>
+struct __attribute__((packed, aligned(8))) Rec<8> {
+  uint32_t slot;  // the packed word
+  int32_t v;
+};
 template <>
 struct __attribute__((packed, aligned(16))) Rec<16> {
   int64_t ts;
@@ -135,26 +147,38 @@ struct __attribute__((packed, aligned(8))) Rec<24> {
   uint32_t pad;
 };
 
+// a sorted record's key and timestamp
 template <int REC>
-__device__ __forceinline__ Rec<REC> make_rec(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i) {
-  Rec<REC> r;
-  r.ts = ts[i];
-  if constexpr (REC == 16) r.v = ((const int32_t*)val)[i];
-  else { r.v = ((const int64_t*)val)[i]; r.pad = 0; }
-  r.slot = slot[i];
-  return r;
+__device__ __forceinline__ uint32_t rec_key(const Rec<REC>& r, const PackP& pk) {
+  if constexpr (REC == 8) return r.slot >> pk.tb;
+  else return r.slot;
+}
+template <int REC>
+__device__ __forceinline__ int64_t rec_ts(const Rec<REC>& r, const PackP& pk) {
+  if constexpr (REC == 8) return pk.tbase + (int64_t)(r.slot & ((1u << pk.tb) - 1u));
+  else return r.ts;
 }
 
 // Register image of a record as plain 32-bit words (a packed struct copy would be lowered through scratch)
 template <int REC>
 struct RV;
 template <>
+struct RV<8> {
+  uint2 a;
+  __device__ uint32_t slot() const { return a.x; }
+  __device__ static RV load(const void* p, int64_t i) { return RV{((const uint2*)p)[i]}; }
+  __device__ void store(void* p, int64_t i) const { ((uint2*)p)[i] = a; }
+  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i, const PackP& pk) {
+    return RV{make_uint2((slot[i] << pk.tb) | (uint32_t)(ts[i] - pk.tbase), (uint32_t)((const int32_t*)val)[i])};
+  }
+};
+template <>
 struct RV<16> {
   uint4 a;
   __device__ uint32_t slot() const { return a.w; }
   __device__ static RV load(const void* p, int64_t i) { return RV{((const uint4*)p)[i]}; }
   __device__ void store(void* p, int64_t i) const { ((uint4*)p)[i] = a; }
-  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i) {
+  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i, const PackP&) {
     const uint64_t t = (uint64_t)ts[i];
     return RV{make_uint4((uint32_t)t, (uint32_t)(t >> 32), (uint32_t)((const int32_t*)val)[i], slot[i])};
   }
@@ -173,7 +197,7 @@ struct RV<24> {
     q[1] = b;
     q[2] = c;
   }
-  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i) {
+  __device__ static RV make(const int64_t* ts, const void* val, const uint32_t* slot, int64_t i, const PackP&) {
     const uint64_t t = (uint64_t)ts[i], v = (uint64_t)((const int64_t*)val)[i];
     return RV{make_uint2((uint32_t)t, (uint32_t)(t >> 32)), make_uint2((uint32_t)v, (uint32_t)(v >> 32)),
               make_uint2(slot[i], 0u)};
@@ -184,7 +208,8 @@ struct RV<24> {
 template <int REC, bool FIRST, int SI>
 __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>* in, const int64_t* ts,
                                                                    const void* val, const uint32_t* slot, int64_t n,
-                                                                   int shift, int32_t* hist, int64_t nblocks) {
+                                                                   int shift, int32_t* hist, int64_t nblocks,
+                                                                   PackP pk) {
   constexpr int TILE = SORT_THREADS * SI;
   __shared__ int32_t cnt[RADIX];
   const int tid = threadIdx.x;
@@ -195,7 +220,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>
   for (int r = 0; r < SI; r++) {
     const int64_t i = base + r * SORT_THREADS + tid;
     if (i < n) {
-      const uint32_t s = FIRST ? slot[i] : in[i].slot;
+      const uint32_t s = FIRST ? (REC == 8 ? slot[i] << pk.tb : slot[i]) : in[i].slot;
       atomicAdd(&cnt[(s >> shift) & (RADIX - 1)], 1);
     }
   }
@@ -210,7 +235,7 @@ template <int REC, bool FIRST, int SI>
 __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<REC>* in, const int64_t* ts,
                                                                       const void* val, const uint32_t* slot,
                                                                       int64_t n, int shift, const int32_t* offs,
-                                                                      int64_t nblocks, Rec<REC>* out) {
+                                                                      int64_t nblocks, Rec<REC>* out, PackP pk) {
   constexpr int TILE = SORT_THREADS * SI;
   __shared__ __attribute__((aligned(16))) unsigned char smem[REC * TILE + 4 * 6 * RADIX];
   void* stage = smem;                                                      // [TILE] records
@@ -231,7 +256,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
     const int64_t i = base + wid * WAVE_ITEMS + r * 64 + lane;
     int d = -1;
     if (i < n) {
-      item[r] = FIRST ? RV<REC>::make(ts, val, slot, i) : RV<REC>::load(in, i);
+      item[r] = FIRST ? RV<REC>::make(ts, val, slot, i, pk) : RV<REC>::load(in, i);
       d = (item[r].slot() >> shift) & (RADIX - 1);
     }
     dig[r] = d;
@@ -294,18 +319,56 @@ constexpr int SEG_ITEMS = 16;
 constexpr int SEG_THREADS = 256;
 constexpr int SEG_TILE = SEG_ITEMS * SEG_THREADS;
 
-__global__ __launch_bounds__(256) void key_max_kernel(const uint32_t* keys, int64_t n, unsigned int* kmax) {
+// range[0] (low word): the largest key; with ts: range[1] = ~ the smallest and range[2] the largest timestamp, biased
+// (ts ^ 1 << 63, an unsigned order; all three zeroed by the host) -- the packed records' fit test
+__global__ __launch_bounds__(256) void key_max_kernel(const uint32_t* keys, const int64_t* ts, int64_t n,
+                                                      unsigned long long* range) {
   __shared__ unsigned int s_m[4];
+  __shared__ unsigned long long s_lo[4], s_hi[4];
   unsigned int m = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+  unsigned long long lo = ~0ull, hi = 0;
+  auto take_ts = [&](long long t) {
+    const unsigned long long b = (unsigned long long)t ^ 0x8000000000000000ull;
+    lo = min(lo, b);
+    hi = max(hi, b);
+  };
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gstride = (int64_t)gridDim.x * blockDim.x;
+  // four tuples per load when the arrays are 16-byte aligned (the scalar loop takes the rest)
+  const int64_t n4 = (((uintptr_t)keys | (uintptr_t)ts) & 15) ? 0 : n / 4;
+  for (int64_t i = gid; i < n4; i += gstride) {
+    const uint4 k4 = ((const uint4*)keys)[i];
+    m = max(max(m, max(k4.x, k4.y)), max(k4.z, k4.w));
+    if (ts) {
+      const longlong2 a = ((const longlong2*)ts)[2 * i], b = ((const longlong2*)ts)[2 * i + 1];
+      take_ts(a.x);
+      take_ts(a.y);
+      take_ts(b.x);
+      take_ts(b.y);
+    }
+  }
+  for (int64_t i = n4 * 4 + gid; i < n; i += gstride) {
     m = max(m, keys[i]);
+    if (ts) take_ts(ts[i]);
+  }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned int)__shfl_xor((int)m, o));
-  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  for (int o = 32; o > 0; o >>= 1) {
+    m = max(m, (unsigned int)__shfl_xor((int)m, o));
+    lo = min(lo, (unsigned long long)__shfl_xor((long long)lo, o));
+    hi = max(hi, (unsigned long long)__shfl_xor((long long)hi, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_m[threadIdx.x >> 6] = m;
+    s_lo[threadIdx.x >> 6] = lo;
+    s_hi[threadIdx.x >> 6] = hi;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
-    if (m) atomicMax(kmax, m);
+    if (m) atomicMax((unsigned int*)range, m);
+    if (ts) {
+      atomicMax(range + 1, ~min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3])));
+      atomicMax(range + 2, max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3])));
+    }
   }
 }
 
@@ -314,8 +377,9 @@ __global__ __launch_bounds__(256) void key_max_kernel(const uint32_t* keys, int6
 template <int REC>
 __device__ __forceinline__ void seg_wave_scan(const Rec<REC>* r, int64_t n, int64_t w0, int lane,
                                               uint64_t (&starts)[SEG_ITEMS], uint32_t (&keys)[SEG_ITEMS],
-                                              long long& tmax) {
-  uint32_t prev_last = w0 > 0 && w0 - 1 < n ? r[w0 - 1].slot : 0;  // the record before the wave's range
+                                              long long& tmax, const PackP& pk) {
+  // the record before the wave's range
+  uint32_t prev_last = w0 > 0 && w0 - 1 < n ? rec_key<REC>(r[w0 - 1], pk) : 0;
   tmax = INT64_MIN;
 #pragma unroll
   for (int k = 0; k < SEG_ITEMS; k++) {
@@ -323,8 +387,9 @@ __device__ __forceinline__ void seg_wave_scan(const Rec<REC>* r, int64_t n, int6
     uint32_t key = 0;
     long long t = INT64_MIN;
     if (i < n) {
-      key = r[i].slot;
-      t = r[i].ts;
+      const Rec<REC> ri = r[i];
+      key = rec_key<REC>(ri, pk);
+      t = rec_ts<REC>(ri, pk);
     }
     const uint32_t up = (uint32_t)__shfl_up((int)key, 1);
     const uint32_t prev = lane == 0 ? prev_last : up;
@@ -337,14 +402,15 @@ __device__ __forceinline__ void seg_wave_scan(const Rec<REC>* r, int64_t n, int6
 
 template <int REC>
 __global__ __launch_bounds__(SEG_THREADS) void seg_count_kernel(const Rec<REC>* r, int64_t n, int32_t* cnt,
-                                                                 long long* tmax_tile) {
+                                                                 long long* tmax_tile, PackP pk) {
   __shared__ int s_c[SEG_THREADS / 64];
   __shared__ long long s_t[SEG_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint64_t starts[SEG_ITEMS];
   uint32_t keys[SEG_ITEMS];
   long long tm;
-  seg_wave_scan<REC>(r, n, (int64_t)blockIdx.x * SEG_TILE + (int64_t)wid * 64 * SEG_ITEMS, lane, starts, keys, tm);
+  seg_wave_scan<REC>(r, n, (int64_t)blockIdx.x * SEG_TILE + (int64_t)wid * 64 * SEG_ITEMS, lane, starts, keys, tm,
+                     pk);
   int c = 0;
 #pragma unroll
   for (int k = 0; k < SEG_ITEMS; k++) c += __popcll(starts[k]);
@@ -369,14 +435,14 @@ __global__ __launch_bounds__(SEG_THREADS) void seg_count_kernel(const Rec<REC>* 
 
 template <int REC>
 __global__ __launch_bounds__(SEG_THREADS) void seg_write_kernel(const Rec<REC>* r, int64_t n, const int32_t* off,
-                                                                 uint32_t* ukey, int64_t* ubeg) {
+                                                                 uint32_t* ukey, int64_t* ubeg, PackP pk) {
   __shared__ int s_c[SEG_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t w0 = (int64_t)blockIdx.x * SEG_TILE + (int64_t)wid * 64 * SEG_ITEMS;
   uint64_t starts[SEG_ITEMS];
   uint32_t keys[SEG_ITEMS];
   long long tm;
-  seg_wave_scan<REC>(r, n, w0, lane, starts, keys, tm);
+  seg_wave_scan<REC>(r, n, w0, lane, starts, keys, tm, pk);
   int c = 0;
 #pragma unroll
   for (int k = 0; k < SEG_ITEMS; k++) c += __popcll(starts[k]);
@@ -620,27 +686,28 @@ int64_t sort_tile() { return k::SORT_TILE; }  // the smallest tile (sizes the hi
 
 template <int REC, int SI>
 static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t* slot, int64_t n, int passes,
-                              void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp, void** result, hipStream_t st) {
+                              void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp, void** result, hipStream_t st,
+                              k::PackP pk) {
   using R = k::Rec<REC>;
   const int64_t nb = (n + k::SORT_THREADS * SI - 1) / (k::SORT_THREADS * SI);
   void* src = nullptr;
   void* dst = bufA;
   for (int p = 0; p < passes; p++) {
-    const int shift = p * k::RB;
+    const int shift = p * k::RB + (REC == 8 ? pk.tb : 0);
     if (p == 0)
       hipLaunchKernelGGL((k::radix_hist_kernel<REC, true, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb);
+                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb, pk);
     else
       hipLaunchKernelGGL((k::radix_hist_kernel<REC, false, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)src, ts, val, slot, n, shift, hist, nb);
+                         (const R*)src, ts, val, slot, n, shift, hist, nb, pk);
     hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
     if (e != hipSuccess) return e;
     if (p == 0)
       hipLaunchKernelGGL((k::radix_scatter_kernel<REC, true, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst);
+                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
     else
       hipLaunchKernelGGL((k::radix_scatter_kernel<REC, false, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst);
+                         (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
     src = dst;
     dst = dst == bufA ? bufB : bufA;
   }
@@ -648,50 +715,64 @@ static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t
   return hipGetLastError();
 }
 
-// Stable sort of the batch by slot into records (AoS, rec bytes 16 or 24).  bufA/bufB: n records each;
-// hist/offs: RADIX * ceil(n / sort_tile()) int32; scan_tmp: int32 scratch.  Result lands in *result.
+// Stable sort of the batch by slot into records (AoS, rec bytes 8 (packed: tbase / tb), 16 or 24).  bufA/bufB: n
+// records each; hist/offs: RADIX * ceil(n / sort_tile()) int32; scan_tmp: int32 scratch.  Result lands in *result.
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
-                               void** result, hipStream_t st) {
+                               void** result, hipStream_t st, int64_t tbase, int tb) {
+  const k::PackP pk{tbase, tb};
   int passes = (slot_bits + k::RB - 1) / k::RB;
   if (passes < 1) passes = 1;
   // (4096-record tiles for 16-byte records, SI = 16: histogram 291 -> 240 us but scatter 593 -> 803 us per 2^26
   // records -- the 70-KB stage halves the resident workgroups; profiles/r05/c4s_sort_by_key/)
-  if (rec == 16) return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st);
-  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st);
+  // packed 8-byte records: 2048-record tiles like the others (4096, SI = 16: histogram 350 -> 285 us but scatter
+  // 700 -> 893 us per two passes over 2^26 records, profiles/r05/c4s_packed/)
+  if (rec == 8) return sort_passes<8, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk);
+  if (rec == 16)
+    return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk);
+  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk);
 }
 
-hipError_t launch_key_max(const uint32_t* keys, int64_t n, unsigned int* kmax, hipStream_t st) {
+hipError_t launch_key_max(const uint32_t* keys, const int64_t* ts, int64_t n, unsigned long long* range,
+                          hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k::key_max_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0, st,
-                     keys, n, kmax);
+  hipLaunchKernelGGL(k::key_max_kernel, dim3((unsigned)std::min<int64_t>((n + 1023) / 1024, 4096)), dim3(256), 0, st,
+                     keys, ts, n, range);
   return hipGetLastError();
 }
 int64_t seg_tiles(int64_t n) { return (n + k::SEG_TILE - 1) / k::SEG_TILE; }
 // segment starts of a batch sorted by key: cnt [seg_tiles(n)] (scanned in place), tmax_tile [seg_tiles(n)]
 hipError_t launch_seg_count(int rec, const void* recs, int64_t n, int32_t* cnt, long long* tmax_tile,
-                            unsigned long long* tmax_b, hipStream_t st) {
+                            unsigned long long* tmax_b, hipStream_t st, int64_t tbase, int tb) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = seg_tiles(n);
-  if (rec == 16)
+  const k::PackP pk{tbase, tb};
+  if (rec == 8)
+    hipLaunchKernelGGL(k::seg_count_kernel<8>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
+                       (const k::Rec<8>*)recs, n, cnt, tmax_tile, pk);
+  else if (rec == 16)
     hipLaunchKernelGGL(k::seg_count_kernel<16>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
-                       (const k::Rec<16>*)recs, n, cnt, tmax_tile);
+                       (const k::Rec<16>*)recs, n, cnt, tmax_tile, pk);
   else
     hipLaunchKernelGGL(k::seg_count_kernel<24>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
-                       (const k::Rec<24>*)recs, n, cnt, tmax_tile);
+                       (const k::Rec<24>*)recs, n, cnt, tmax_tile, pk);
   hipLaunchKernelGGL(k::tmax_reduce_kernel, dim3(1), dim3(1024), 0, st, tmax_tile, nb, tmax_b);
   return hipGetLastError();
 }
 hipError_t launch_seg_write(int rec, const void* recs, int64_t n, const int32_t* off, uint32_t* ukey, int64_t* ubeg,
-                            hipStream_t st) {
+                            hipStream_t st, int64_t tbase, int tb) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = seg_tiles(n);
-  if (rec == 16)
+  const k::PackP pk{tbase, tb};
+  if (rec == 8)
+    hipLaunchKernelGGL(k::seg_write_kernel<8>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
+                       (const k::Rec<8>*)recs, n, off, ukey, ubeg, pk);
+  else if (rec == 16)
     hipLaunchKernelGGL(k::seg_write_kernel<16>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
-                       (const k::Rec<16>*)recs, n, off, ukey, ubeg);
+                       (const k::Rec<16>*)recs, n, off, ukey, ubeg, pk);
   else
     hipLaunchKernelGGL(k::seg_write_kernel<24>, dim3((unsigned)nb), dim3(k::SEG_THREADS), 0, st,
-                       (const k::Rec<24>*)recs, n, off, ukey, ubeg);
+                       (const k::Rec<24>*)recs, n, off, ukey, ubeg, pk);
   return hipGetLastError();
 }
 hipError_t launch_seg_fill(const int64_t* ubeg, const uint32_t* uslot, int64_t u_n, int64_t n, int64_t* seg_begin,

@@ -444,7 +444,9 @@ __device__ __noinline__ void general_tuple(LaneS<VT, V>& L, const XSess x, int64
   }
 }
 
-template <int VT, int OCC, class V>
+// PK: the batch comes as packed 8-byte records (a.rec_stride 8, int32 values; a compile-time choice, so the record
+// loads of the ring below keep one code path and no branch join waits on them)
+template <int VT, int OCC, class V, bool PK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void lane_session_kernel(XBatchArgs a) {
   const XCfg* cfg = a.cfg;
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -455,7 +457,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   if (sp->err) return;
   if (a.retry && !sp->pending) return;
   const unsigned char* rec = (const unsigned char*)a.ts;
+  // an int32 batch may come as packed 8-byte records {key << pk_bits | ts - pk_base, value} (keyed_kernels.hip Rec<8>)
+  constexpr bool packed = VT == VT_I32 && PK;
+  const uint32_t pk_mask = (1u << a.pk_bits) - 1u;
+  const int64_t pk_base = a.pk_base;
   auto load = [&](int64_t i, int64_t& t, int64_t& vb) {
+    if constexpr (packed) {
+      const uint2 w = *(const uint2*)(rec + i * 8);
+      t = pk_base + (int64_t)(w.x & pk_mask);
+      vb = (int64_t)(int32_t)w.y;
+      return;
+    }
     const unsigned char* r = rec + i * a.rec_stride;
     t = *(const int64_t*)r;
     if constexpr (VT == VT_I32) vb = (int64_t)*(const int32_t*)(r + 8);
@@ -707,9 +719,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   L.b = bb;
   L.sb = sbase;
   load_fast();
-  // the key's records go through a per-lane ring of 8 in LDS: the next 8 are loaded (one 128-B line of 16-B records)
-  // while the current 8 are processed, so the tuple loop does not wait on a load every iteration (the loads are
-  // unconditional, the index clamped, so no branch join waits for them)
+  // the key's records go through a per-lane ring of 8 in LDS: the next 8 are loaded (one 128-B line of 16-B records,
+  // half of one of packed 8-B records) while the current 8 are processed, so the tuple loop does not wait on a load
+  // every iteration (the loads are unconditional, the index clamped, so no branch join waits for them)
   __shared__ int64_t R_t[8][256], R_v[8][256];
   const int tid = threadIdx.x;
   int64_t pt[8], pw[8];
@@ -718,9 +730,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     for (int u = 0; u < 8; u++) {
       const int64_t i = min(c + u, b1 - 1);
       if constexpr (VT == VT_I32) {
-        const uint4 w = *(const uint4*)(rec + i * 16);
-        pt[u] = (int64_t)(((uint64_t)w.y << 32) | w.x);
-        pw[u] = (int64_t)(int32_t)w.z;
+        if constexpr (packed) {
+          const uint2 w = *(const uint2*)(rec + i * 8);
+          pt[u] = pk_base + (int64_t)(w.x & pk_mask);
+          pw[u] = (int64_t)(int32_t)w.y;
+        } else {
+          const uint4 w = *(const uint4*)(rec + i * 16);
+          pt[u] = (int64_t)(((uint64_t)w.y << 32) | w.x);
+          pw[u] = (int64_t)(int32_t)w.z;
+        }
       } else {
         load(i, pt[u], pw[u]);
       }
@@ -889,6 +907,12 @@ hipError_t launch_lane_session(const XBatchArgs& a, int vt, int occ, hipStream_t
   if (a.n_ops <= 0) return hipSuccess;
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
 #define SCOTTY_LS(VT_, OCC_, V_) hipLaunchKernelGGL((ls::lane_session_kernel<VT_, OCC_, V_>), grid, block, 0, st, a)
+  if (a.rec_stride == 8) {  // packed records: int32 values, key-interleaved store only (exact_engine.cpp)
+    if (vt != VT_I32 || !a.sl.kw) return hipErrorInvalidValue;
+    if (occ == 2) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 2, XKView, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 3, XKView, true>), grid, block, 0, st, a);
+    return hipGetLastError();
+  }
   if (a.sl.kw) {  // key-interleaved store: integer values
     if (occ == 2) {
       if (vt == VT_I32) SCOTTY_LS(VT_I32, 2, XKView); else SCOTTY_LS(VT_I64, 2, XKView);

@@ -26,6 +26,7 @@
 
 namespace scotty {
 hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks, hipStream_t st, int mode);
+void set_ingest_timing_events(hipEvent_t start, hipEvent_t stop);
 int ingest_wgs_per_cu(int vt, int need);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
@@ -178,6 +179,7 @@ struct scotty_op {
   int32_t x_qmode = -1;      // exact engine: quiet-pass ingest loop (A/B: -1 default, 7 without the DQ2 queue)
   bool x_ls_off = false;     // exact engine: keyed sessions through the wavefront replay (A/B)
   int32_t x_ls_occ = 2;      // lane-session kernel's waves per SIMD (2 default: no spills; 3: A/B)
+  bool x_pack_off = false;   // exact engine: keyed replay records always 16 bytes (A/B for the packed 8-byte ones)
   bool x_lsdbg = false;      // lane-session path counters (debugging aid)
   int64_t x_qblocks = 0;     // exact engine: quiet-pass ingest workgroups (A/B: 0 default)
   int32_t x_kg_variant = -1;
@@ -590,13 +592,12 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
       HIPCHK(hipEventCreate(&ev.first));
       HIPCHK(hipEventCreate(&ev.second));
     }
-    HIPCHK(hipEventRecord(ev.first, op->stream));
+    set_ingest_timing_events(ev.first, ev.second);
   }
   HIPCHK(launch_ingest(ia, op->vt, op->need, nblocks, op->stream, streaming ? INGEST_STREAMING : op->ingest_mode));
   op->last_ingest_blocks = nblocks;
   op->last_ingest_streaming = streaming ? 1 : 0;
   if (op->timing) {
-    HIPCHK(hipEventRecord(ev.second, op->stream));
     op->ev_pending.push_back(ev);
     op->t_tuples += n;
   }
@@ -967,6 +968,7 @@ static int decide_mode(scotty_op* op) {
   op->x->xq_ingest_blocks = op->x_qblocks;
   op->x->lane_session_off = op->x_ls_off;
   op->x->lane_session_occ = op->x_ls_occ;
+  op->x->pack_off = op->x_pack_off;
   op->x->lsdbg_on = op->x_lsdbg;
   op->x->timing = op->timing;  // scotty_enable_timing before the first push (the natural order) reaches the engine
   std::string e;
@@ -1544,6 +1546,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     }
     return SCOTTY_OK;
   }
+  if (std::strcmp(key, "keyed_pack_records") == 0) {  // 1 (default): the lane-session replay sorts packed 8-byte
+    if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;  // records when a batch fits; 0: 16-byte (A/B)
+    op->x_pack_off = value == 0;
+    if (op->x) op->x->pack_off = op->x_pack_off;
+    return SCOTTY_OK;
+  }
   if (std::strcmp(key, "lane_session_counters") == 0) {  // debugging aid: count the lane-session kernel's paths
     if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;  // (debug stats 103-106)
     op->x_lsdbg = value != 0;
@@ -1685,6 +1693,7 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
         return -1;
       return (int64_t)v;
     }
+    case 107: return op->x->last_rec_bytes;  // the last keyed replay's record bytes (8 packed, 16, 24)
     default:
       if (which >= 16 && which - 16 < (int)op->x->xq_trace.size()) return op->x->xq_trace[which - 16];
       return -1;

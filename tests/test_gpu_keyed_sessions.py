@@ -148,3 +148,66 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
             assert lane.droppedCount() == wave.droppedCount()
     assert lane.keyCount() == wave.keyCount()
     assert total > 0 or errors > 0
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_packed_replay_records_equal_16_byte_records(seed):
+    """An int32 keyed batch whose key bits plus the bits of its event-time span fit one 32-bit word is sorted and
+    replayed as packed 8-byte records {key << tb | ts - tbase, value} (keyed_kernels.hip Rec<8>); scotty_tune
+    "keyed_pack_records" 0 keeps the 16-byte records.  Dense key ranges of 3-20 bits, batches spanning a few ms to
+    minutes (some fit, some do not), timestamps offset up to 2^40: every watermark's rows and the dropped counts
+    match, and the packed layout is taken where it fits (debug stat 107: the last replay's record bytes)."""
+    pkg = product()
+    rng = np.random.default_rng(7300 + seed)
+    gap = int(rng.integers(20, 800))
+    wins = [Session(Time, gap)]
+    if seed % 2:
+        wins.append(Sliding(Time, 2000, 300 + seed))
+    aggs = [SUM, COUNT, MIN, MAX]
+    nkeys = [7, 300, 5000, 1 << 20][seed % 4]
+    n = int(rng.integers(100_000, 400_000))
+    rate = [0.5, 2, 10, 40][(seed // 2) % 4]
+    t0 = [0, 1 << 40][seed % 2] + int(rng.integers(0, 2000))
+    pauses = [(int(i), int(rng.integers(1, 4)) * gap) for i in range(int(rng.integers(5000, 40_000)), n, 50_000)]
+    ts, vals = pkg.workloads.stream(n, rate, t0=t0, ooo_frac=float(rng.choice([0.05, 0.2, 0.5])),
+                                    max_delay=int(rng.integers(1, 2 * gap + 2)), seed=seed, value_type="i32",
+                                    gaps=pauses)
+    keys = rng.integers(0, nkeys, size=n).astype(np.uint32)
+    lateness = int(rng.choice([50, 1000]))
+
+    def make(pack):
+        op = pkg.KeyedSlicingWindowOperator(device=0)
+        op.tune("keyed_pack_records", pack)
+        for x in aggs:
+            op.addWindowFunction(x)
+        op.setMaxLateness(lateness)
+        for w in wins:
+            op.addWindowAssigner(w)
+        return op
+    packed, plain = make(1), make(0)
+    from helpers import interval_schedule, same_keyed_arrays
+    total, errors, layouts = 0, 0, set()
+    for step in interval_schedule(ts, int(rng.integers(3, 12)), lag=int(rng.integers(0, 2 * gap)),
+                                  pushes_per_interval=int(rng.integers(1, 3))):
+        if step[0] == "push":
+            lo, hi = step[1], step[2]
+            if hi > lo:
+                packed.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                plain.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                layouts.add(packed._debug_stat(107))
+                assert plain._debug_stat(107) == 16
+        else:
+            try:
+                exp = plain.processWatermarkArrays(step[1])
+            except pkg.ScottyError as e:  # the reference's throw out of the key loop (see the test above): both alike
+                with pytest.raises(pkg.ScottyError) as ei:
+                    packed.processWatermarkArrays(step[1])
+                assert ei.value.code == e.code
+                errors += 1
+                continue
+            total += same_keyed_arrays(packed.processWatermarkArrays(step[1]), exp)
+            assert packed.droppedCount() == plain.droppedCount()
+    assert packed.keyCount() == plain.keyCount()
+    assert total > 0 or errors > 0
+    if nkeys <= 5000:
+        assert 8 in layouts
