@@ -39,9 +39,9 @@ hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long
                        uint32_t* slot, bool fixup, hipStream_t st);
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
-                               void** result, hipStream_t st, int64_t tbase, int tb);
-hipError_t launch_key_max(const uint32_t* keys, const int64_t* ts, int64_t n, unsigned long long* range,
-                          hipStream_t st);
+                               void** result, hipStream_t st, int64_t tbase, int tb, bool hist0);
+hipError_t launch_range_hist(const uint32_t* keys, const int64_t* ts, int64_t n, int32_t* hist,
+                             unsigned long long* part, unsigned long long* range, hipStream_t st);
 int64_t seg_tiles(int64_t n);
 hipError_t launch_seg_count(int rec, const void* recs, int64_t n, int32_t* cnt, long long* tmax_tile,
                             unsigned long long* tmax_b, hipStream_t st, int64_t tbase, int tb);
@@ -128,6 +128,7 @@ void XEngine::release() {
   dfree(d_lsdbg);
   dfree(d_need); dfree(d_table); dfree(d_newpos); dfree(d_newcnt); dfree(d_full); dfree(d_slot_key);
   dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32); dfree(d_seg_b); dfree(d_seg_e);
+  dfree(d_rpart);
   dfree(d_ukey); dfree(d_ubeg); dfree(d_segcnt); dfree(d_segoff); dfree(d_segscan); dfree(d_tmaxt); dfree(d_kmax);
   dfree(d_wcount); dfree(d_woff); dfree(d_scan64); dfree(d_misc);
   dfree(d_w_start); dfree(d_w_end); dfree(d_w_meas); dfree(d_w_op); dfree(d_w_key); dfree(d_has);
@@ -479,7 +480,7 @@ int XEngine::ensure_batch(int64_t n) {
   if (n <= bcap) return SCOTTY_OK;
   XCHK(hipStreamSynchronize(stream));
   int64_t cap = std::max<int64_t>(n, 1 << 16);
-  dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32);
+  dfree(d_slot); dfree(d_recA); dfree(d_recB); dfree(d_hist); dfree(d_scan32); dfree(d_rpart);
   dfree(d_ukey); dfree(d_ubeg); dfree(d_segcnt); dfree(d_segoff); dfree(d_segscan); dfree(d_tmaxt);
   const int rec = vt == VT_I32 ? 16 : 24;
   XCHK(dalloc(&d_slot, cap));
@@ -496,6 +497,7 @@ int XEngine::ensure_batch(int64_t n) {
   XCHK(dalloc((unsigned char**)&d_recB, cap * rec));
   const int64_t nb = (cap + sort_tile() - 1) / sort_tile();
   XCHK(dalloc(&d_hist, 256 * nb));
+  XCHK(dalloc(&d_rpart, 3 * nb));
   XCHK(dalloc(&d_scan32, 256 * nb / 512 + 64));
   XCHK(dalloc(&d_newpos, cap));
   bcap = cap;
@@ -1329,8 +1331,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   //    The lane-session replay of an int32 batch whose key bits and event-time span fit one 32-bit word sorts
   //    packed 8-byte records (keyed_kernels.hip, Rec<8>): the key range pass then also takes the timestamp range
   const bool pack_try = vt == VT_I32 && lane_session_mode() && !pack_off;
-  XCHK(hipMemsetAsync(d_kmax, 0, 24, stream));
-  XCHK(launch_key_max(d_key, pack_try ? d_ts : nullptr, n, d_kmax, stream));
+  // (one read of the keys, and of the timestamps when packing: also the sort's first digit histogram)
+  XCHK(launch_range_hist(d_key, pack_try ? d_ts : nullptr, n, d_hist, d_rpart, d_kmax, stream));
   if ((rc = tend(tk, 0))) return rc;
   XCHK(hipMemcpyAsync(h_misc, d_kmax, 24, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
@@ -1355,7 +1357,7 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   void* sorted = nullptr;
   if ((rc = tbegin(ts0, SCOTTY_TIME_PUSH_OTHER))) return rc;
   XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_key, n, kb, d_recA, d_recB, d_hist, d_scan32, &sorted, stream, tbase,
-                           tb));
+                           tb, true));
   // 2. the batch's distinct keys in key order (segment u = [ubeg[u], ubeg[u + 1])) and its largest timestamp
   const int64_t nbs = seg_tiles(n);
   XCHK(launch_seg_count(rec, sorted, n, d_segcnt, (long long*)d_tmaxt, d_need + 3, stream, tbase, tb));

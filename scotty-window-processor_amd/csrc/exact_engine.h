@@ -209,6 +209,7 @@ class XEngine {
   int64_t* d_ubeg = nullptr;
   int32_t *d_segcnt = nullptr, *d_segoff = nullptr, *d_segscan = nullptr;
   int64_t* d_tmaxt = nullptr;
+  unsigned long long* d_rpart = nullptr;  // range_hist_kernel's per-tile key / timestamp ranges (3 per sort tile)
   unsigned long long* d_kmax = nullptr;
   void *d_recA = nullptr, *d_recB = nullptr;
   int32_t *d_hist = nullptr, *d_scan32 = nullptr;

@@ -204,6 +204,18 @@ struct RV<24> {
   }
 };
 
+// A histogram workgroup counts HIST_TILES consecutive sort tiles, so each digit row of the [digit][tile] matrix is
+// written HIST_TILES counts at a time (a 32-byte run per digit, not one scattered dword per digit and tile: 256 partial
+// lines per tile were most of the histogram passes' HBM writes)
+constexpr int HIST_TILES = 8;
+__device__ __forceinline__ void hist_rows_out(const int32_t (&cnt)[HIST_TILES][RADIX], int32_t* hist, int64_t nblocks,
+                                              int64_t t0, int nt, int tid) {
+  for (int d = tid; d < RADIX; d += SORT_THREADS) {
+    int32_t* row = hist + (int64_t)d * nblocks + t0;
+    for (int j = 0; j < nt; j++) row[j] = cnt[j][d];
+  }
+}
+
 // FIRST: input is SoA (ts, val, slot arrays); else AoS records
 template <int REC, bool FIRST, int SI>
 __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>* in, const int64_t* ts,
@@ -211,21 +223,26 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_hist_kernel(const Rec<REC>
                                                                    int shift, int32_t* hist, int64_t nblocks,
                                                                    PackP pk) {
   constexpr int TILE = SORT_THREADS * SI;
-  __shared__ int32_t cnt[RADIX];
+  __shared__ int32_t cnt[HIST_TILES][RADIX];
   const int tid = threadIdx.x;
-  for (int d = tid; d < RADIX; d += SORT_THREADS) cnt[d] = 0;
+  for (int d = tid; d < HIST_TILES * RADIX; d += SORT_THREADS) (&cnt[0][0])[d] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t t0 = (int64_t)blockIdx.x * HIST_TILES;
+  const int nt = (int)min((int64_t)HIST_TILES, nblocks - t0);
+  for (int j = 0; j < nt; j++) {
+    const int64_t base = (t0 + j) * TILE;
+    uint32_t sv[SI];
 #pragma unroll
-  for (int r = 0; r < SI; r++) {
-    const int64_t i = base + r * SORT_THREADS + tid;
-    if (i < n) {
-      const uint32_t s = FIRST ? (REC == 8 ? slot[i] << pk.tb : slot[i]) : in[i].slot;
-      atomicAdd(&cnt[(s >> shift) & (RADIX - 1)], 1);
+    for (int r = 0; r < SI; r++) {  // every load issued before the first is used (indices clamped)
+      const int64_t i = min(base + r * SORT_THREADS + tid, n - 1);
+      sv[r] = FIRST ? (REC == 8 ? slot[i] << pk.tb : slot[i]) : in[i].slot;
     }
+#pragma unroll
+    for (int r = 0; r < SI; r++)
+      if (base + r * SORT_THREADS + tid < n) atomicAdd(&cnt[j][(sv[r] >> shift) & (RADIX - 1)], 1);
   }
   __syncthreads();
-  for (int d = tid; d < RADIX; d += SORT_THREADS) hist[(int64_t)d * nblocks + blockIdx.x] = cnt[d];
+  hist_rows_out(cnt, hist, nblocks, t0, nt, tid);
 }
 
 // Stable scatter of one tile.  Each wavefront ranks its own contiguous SI * 64-record sub-tile against
@@ -243,7 +260,13 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
   int32_t* tot = wc + 4 * RADIX;                                           // [4] wave partial sums (scan)
   int32_t* tstart = tot + RADIX;                                           // [RADIX] tile digit starts
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  // XCD-aware tile order: workgroups are dealt to the 8 XCDs round robin, so XCD x takes the consecutive tiles
+  // [x * per, (x + 1) * per) -- the runs adjacent tiles write for one digit are adjacent in memory and now meet in
+  // one L2, which merges their partial lines before they go to HBM
+  const int64_t per = (nblocks + 7) >> 3;
+  const int64_t tile = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (tile >= nblocks) return;
+  const int64_t base = tile * TILE;
   constexpr int WAVE_ITEMS = SI * 64;
   for (int d = tid; d < 4 * RADIX; d += SORT_THREADS) wc[d] = 0;
   __syncthreads();
@@ -304,7 +327,7 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
   for (int i = tid; i < cnt_tile; i += SORT_THREADS) {
     const RV<REC> rr = RV<REC>::load(stage, i);
     const int d = (rr.slot() >> shift) & (RADIX - 1);
-    const int64_t g = (int64_t)offs[(int64_t)d * nblocks + blockIdx.x] + (i - tstart[d]);
+    const int64_t g = (int64_t)offs[(int64_t)d * nblocks + tile] + (i - tstart[d]);
     rr.store(out, g);
   }
 }
@@ -312,63 +335,88 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
 // ---------------------------------------------------------------- the batch's keys, after the sort by key
 // The replay path sorts the batch by KEY (stable: arrival order kept within a key) and maps each distinct key to its
 // operator slot once, instead of looking up every tuple's key before the sort (67 M random probes of the key table per
-// 2^26-tuple batch).  key_max_kernel: the largest key (the sort's bit count).  seg_count / seg_write: the positions
+// 2^26-tuple batch).  range_hist_kernel: the largest key (the sort's bit count), the timestamp range (the packed
+// records' fit test) and the first digit's histogram.  seg_count / seg_write: the positions
 // where the key changes, compacted in position order (per-tile counts, exclusive scan, write), so segment u spans
 // [ubeg[u], ubeg[u + 1]); seg_count also keeps each tile's largest timestamp (tmax_reduce: the batch's, biased).
 constexpr int SEG_ITEMS = 16;
 constexpr int SEG_THREADS = 256;
 constexpr int SEG_TILE = SEG_ITEMS * SEG_THREADS;
 
-// range[0] (low word): the largest key; with ts: range[1] = ~ the smallest and range[2] the largest timestamp, biased
-// (ts ^ 1 << 63, an unsigned order; all three zeroed by the host) -- the packed records' fit test
-__global__ __launch_bounds__(256) void key_max_kernel(const uint32_t* keys, const int64_t* ts, int64_t n,
-                                                      unsigned long long* range) {
-  __shared__ unsigned int s_m[4];
-  __shared__ unsigned long long s_lo[4], s_hi[4];
-  unsigned int m = 0;
-  unsigned long long lo = ~0ull, hi = 0;
-  auto take_ts = [&](long long t) {
-    const unsigned long long b = (unsigned long long)t ^ 0x8000000000000000ull;
-    lo = min(lo, b);
-    hi = max(hi, b);
-  };
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gstride = (int64_t)gridDim.x * blockDim.x;
-  // four tuples per load when the arrays are 16-byte aligned (the scalar loop takes the rest)
-  const int64_t n4 = (((uintptr_t)keys | (uintptr_t)ts) & 15) ? 0 : n / 4;
-  for (int64_t i = gid; i < n4; i += gstride) {
-    const uint4 k4 = ((const uint4*)keys)[i];
-    m = max(max(m, max(k4.x, k4.y)), max(k4.z, k4.w));
-    if (ts) {
-      const longlong2 a = ((const longlong2*)ts)[2 * i], b = ((const longlong2*)ts)[2 * i + 1];
-      take_ts(a.x);
-      take_ts(a.y);
-      take_ts(b.x);
-      take_ts(b.y);
+// The key / timestamp range and the sort's first digit histogram in one read of the batch: block b = sort tiles
+// [HIST_TILES b, HIST_TILES (b + 1)) (radix_hist_kernel<.., FIRST>'s tiling; the first digit is key & 0xFF for every record layout, so it does not wait
+// for the layout choice the range decides).  part[3 b ..]: the block's largest key, ~ smallest and largest biased
+// timestamp (range_reduce_kernel folds them: no same-address atomics from thousands of blocks)
+template <int SI>
+__global__ __launch_bounds__(SORT_THREADS) void range_hist_kernel(const uint32_t* keys, const int64_t* ts, int64_t n,
+                                                                  int32_t* hist, int64_t nblocks,
+                                                                  unsigned long long* part) {
+  constexpr int TILE = SORT_THREADS * SI;
+  __shared__ int32_t cnt[HIST_TILES][RADIX];
+  __shared__ unsigned long long s_r[3][SORT_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int d = tid; d < HIST_TILES * RADIX; d += SORT_THREADS) (&cnt[0][0])[d] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * HIST_TILES;
+  const int nt = (int)min((int64_t)HIST_TILES, nblocks - t0);
+  unsigned long long m = 0, nlo = 0, hi = 0;
+  for (int j = 0; j < nt; j++) {
+    const int64_t base = (t0 + j) * TILE;
+    uint32_t k[SI];
+    int64_t t[SI];
+#pragma unroll
+    for (int r = 0; r < SI; r++) {  // every load issued before the first is used (indices clamped)
+      const int64_t i = min(base + r * SORT_THREADS + tid, n - 1);
+      k[r] = keys[i];
+      t[r] = ts ? ts[i] : 0;
     }
-  }
-  for (int64_t i = n4 * 4 + gid; i < n; i += gstride) {
-    m = max(m, keys[i]);
-    if (ts) take_ts(ts[i]);
+#pragma unroll
+    for (int r = 0; r < SI; r++) {
+      if (base + r * SORT_THREADS + tid < n) {
+        atomicAdd(&cnt[j][k[r] & (RADIX - 1)], 1);
+        m = max(m, (unsigned long long)k[r]);
+        const unsigned long long b = (unsigned long long)t[r] ^ 0x8000000000000000ull;
+        nlo = max(nlo, ~b);
+        hi = max(hi, b);
+      }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    m = max(m, (unsigned int)__shfl_xor((int)m, o));
-    lo = min(lo, (unsigned long long)__shfl_xor((long long)lo, o));
+    m = max(m, (unsigned long long)__shfl_xor((long long)m, o));
+    nlo = max(nlo, (unsigned long long)__shfl_xor((long long)nlo, o));
     hi = max(hi, (unsigned long long)__shfl_xor((long long)hi, o));
   }
-  if ((threadIdx.x & 63) == 0) {
-    s_m[threadIdx.x >> 6] = m;
-    s_lo[threadIdx.x >> 6] = lo;
-    s_hi[threadIdx.x >> 6] = hi;
+  if (lane == 0) {
+    s_r[0][wid] = m;
+    s_r[1][wid] = nlo;
+    s_r[2][wid] = hi;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    m = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
-    if (m) atomicMax((unsigned int*)range, m);
-    if (ts) {
-      atomicMax(range + 1, ~min(min(s_lo[0], s_lo[1]), min(s_lo[2], s_lo[3])));
-      atomicMax(range + 2, max(max(s_hi[0], s_hi[1]), max(s_hi[2], s_hi[3])));
-    }
+  hist_rows_out(cnt, hist, nblocks, t0, nt, tid);
+  if (tid < 3) {
+    unsigned long long v = 0;
+    for (int w = 0; w < SORT_THREADS / 64; w++) v = max(v, s_r[tid][w]);
+    part[3 * blockIdx.x + tid] = v;
+  }
+}
+
+__global__ __launch_bounds__(1024) void range_reduce_kernel(const unsigned long long* part, int64_t nb,
+                                                             unsigned long long* range) {
+  __shared__ unsigned long long s_r[3][16];
+  unsigned long long v[3] = {0, 0, 0};
+  for (int64_t b = threadIdx.x; b < nb; b += 1024)
+    for (int j = 0; j < 3; j++) v[j] = max(v[j], part[3 * b + j]);
+  for (int j = 0; j < 3; j++) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[j] = max(v[j], (unsigned long long)__shfl_xor((long long)v[j], o));
+    if ((threadIdx.x & 63) == 0) s_r[j][threadIdx.x >> 6] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long r = 0;
+    for (int w = 0; w < 16; w++) r = max(r, s_r[threadIdx.x][w]);
+    range[threadIdx.x] = r;
   }
 }
 
@@ -687,26 +735,30 @@ int64_t sort_tile() { return k::SORT_TILE; }  // the smallest tile (sizes the hi
 template <int REC, int SI>
 static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t* slot, int64_t n, int passes,
                               void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp, void** result, hipStream_t st,
-                              k::PackP pk) {
+                              k::PackP pk, bool hist0) {
   using R = k::Rec<REC>;
   const int64_t nb = (n + k::SORT_THREADS * SI - 1) / (k::SORT_THREADS * SI);
+  const unsigned hb = (unsigned)((nb + k::HIST_TILES - 1) / k::HIST_TILES);
+  const unsigned sb = (unsigned)(8 * ((nb + 7) / 8));  // scatter: XCD-aware tile order (radix_scatter_kernel)
   void* src = nullptr;
   void* dst = bufA;
   for (int p = 0; p < passes; p++) {
     const int shift = p * k::RB + (REC == 8 ? pk.tb : 0);
-    if (p == 0)
-      hipLaunchKernelGGL((k::radix_hist_kernel<REC, true, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+    if (p == 0 && hist0) {
+      // the first digit's histogram is range_hist_kernel's
+    } else if (p == 0)
+      hipLaunchKernelGGL((k::radix_hist_kernel<REC, true, SI>), dim3(hb), dim3(k::SORT_THREADS), 0, st,
                          (const R*)nullptr, ts, val, slot, n, shift, hist, nb, pk);
     else
-      hipLaunchKernelGGL((k::radix_hist_kernel<REC, false, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+      hipLaunchKernelGGL((k::radix_hist_kernel<REC, false, SI>), dim3(hb), dim3(k::SORT_THREADS), 0, st,
                          (const R*)src, ts, val, slot, n, shift, hist, nb, pk);
     hipError_t e = launch_scan_i32(hist, hist, (int64_t)k::RADIX * nb, scan_tmp, st);
     if (e != hipSuccess) return e;
     if (p == 0)
-      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, true, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, true, SI>), dim3(sb), dim3(k::SORT_THREADS), 0, st,
                          (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
     else
-      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, false, SI>), dim3((unsigned)nb), dim3(k::SORT_THREADS), 0, st,
+      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, false, SI>), dim3(sb), dim3(k::SORT_THREADS), 0, st,
                          (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
     src = dst;
     dst = dst == bufA ? bufB : bufA;
@@ -719,7 +771,7 @@ static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t
 // records each; hist/offs: RADIX * ceil(n / sort_tile()) int32; scan_tmp: int32 scratch.  Result lands in *result.
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
-                               void** result, hipStream_t st, int64_t tbase, int tb) {
+                               void** result, hipStream_t st, int64_t tbase, int tb, bool hist0) {
   const k::PackP pk{tbase, tb};
   int passes = (slot_bits + k::RB - 1) / k::RB;
   if (passes < 1) passes = 1;
@@ -727,17 +779,22 @@ hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, cons
   // records -- the 70-KB stage halves the resident workgroups; profiles/r05/c4s_sort_by_key/)
   // packed 8-byte records: 2048-record tiles like the others (4096, SI = 16: histogram 350 -> 285 us but scatter
   // 700 -> 893 us per two passes over 2^26 records, profiles/r05/c4s_packed/)
-  if (rec == 8) return sort_passes<8, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk);
+  if (rec == 8)
+    return sort_passes<8, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0);
   if (rec == 16)
-    return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk);
-  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk);
+    return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0);
+  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0);
 }
 
-hipError_t launch_key_max(const uint32_t* keys, const int64_t* ts, int64_t n, unsigned long long* range,
-                          hipStream_t st) {
+// range[0] the largest key, range[1] ~ the smallest and range[2] the largest timestamp biased (ts ^ 1 << 63; with ts
+// only), and the first sort digit's histogram; part: 3 * sort tiles
+hipError_t launch_range_hist(const uint32_t* keys, const int64_t* ts, int64_t n, int32_t* hist,
+                             unsigned long long* part, unsigned long long* range, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k::key_max_kernel, dim3((unsigned)std::min<int64_t>((n + 1023) / 1024, 4096)), dim3(256), 0, st,
-                     keys, ts, n, range);
+  const int64_t nb = (n + k::SORT_TILE - 1) / k::SORT_TILE, hb = (nb + k::HIST_TILES - 1) / k::HIST_TILES;
+  hipLaunchKernelGGL(k::range_hist_kernel<k::SORT_ITEMS>, dim3((unsigned)hb), dim3(k::SORT_THREADS), 0, st, keys, ts,
+                     n, hist, nb, part);
+  hipLaunchKernelGGL(k::range_reduce_kernel, dim3(1), dim3(1024), 0, st, part, hb, range);
   return hipGetLastError();
 }
 int64_t seg_tiles(int64_t n) { return (n + k::SEG_TILE - 1) / k::SEG_TILE; }
