@@ -373,13 +373,46 @@ __device__ int64_t lane_session_triggers(const XCfg* c, const XSess& x, int64_t 
   return k;
 }
 
+// The dropped-tuple total and the error bits of a workgroup's keys: one atomic each per workgroup (the compiler
+// combines a wavefront's same-address atomics into one, but one per wavefront still serialised 16 K atomics on one
+// word per watermark at 1 M keys -- ~90 atomics per us)
+template <int T>
+__device__ __forceinline__ void block_flush(unsigned long long dropped, int32_t err_bits, unsigned long long* d_total,
+                                            int32_t* d_err) {
+  __shared__ unsigned long long s_d[T / 64];
+  __shared__ int32_t s_e[T / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dropped += (unsigned long long)__shfl_xor((long long)dropped, o);
+    err_bits |= __shfl_xor(err_bits, o);
+  }
+  if (lane == 0) {
+    s_d[wid] = dropped;
+    s_e[wid] = err_bits;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long d = 0;
+    int32_t e = 0;
+    for (int w = 0; w < T / 64; w++) {
+      d += s_d[w];
+      e |= s_e[w];
+    }
+    if (d) atomicAdd(d_total, d);
+    if (e) atomicOr(d_err, e);
+  }
+}
+
+constexpr int COUNT_T = 1024;
 template <class V>
-__global__ __launch_bounds__(256) void lane_wm_count_kernel(XWmArgs a) {
+__global__ __launch_bounds__(COUNT_T) void lane_wm_count_kernel(XWmArgs a) {
   const int64_t op = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (op >= a.n_ops) return;
-  const XState s = a.st[op];
-  if (s.dropped) atomicAdd(a.dropped_total, (unsigned long long)s.dropped);
-  if (s.err) atomicOr(a.op_err, 1 << s.err);
+  const bool live = op < a.n_ops;
+  XState s{};
+  if (live) s = a.st[op];
+  block_flush<COUNT_T>(live ? s.dropped : 0, live && s.err ? 1 << s.err : 0, a.dropped_total, a.op_err);
+  if (!live) return;
   int64_t k = 0;
   if (!s.err && s.tail > s.head) {
     int64_t last = s.lastWatermark == -1 ? max((int64_t)0, jsub(a.wm, a.cfg->max_lateness)) : s.lastWatermark;
@@ -452,12 +485,10 @@ __global__ __launch_bounds__(EMIT_T) void lane_wm_emit_kernel(XWmArgs a) {
   XState s{};
   bool live = op < a.n_ops;
   int64_t k = 0;
+  if (live) s = a.st[op];
+  if (a.row_count)  // what the count pass accumulates (uniform: every thread of the workgroup takes this)
+    block_flush<EMIT_T>(live ? s.dropped : 0, live && s.err ? 1 << s.err : 0, a.dropped_total, a.op_err);
   if (live) {
-    s = a.st[op];
-    if (a.row_count) {  // what the count pass accumulates
-      if (s.dropped) atomicAdd(a.dropped_total, (unsigned long long)s.dropped);
-      if (s.err) atomicOr(a.op_err, 1 << s.err);
-    }
     if (s.err) {
       live = false;
     } else {
@@ -694,7 +725,7 @@ hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStre
 }
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
+  const dim3 grid((unsigned)((a.n_ops + ln::COUNT_T - 1) / ln::COUNT_T)), block(ln::COUNT_T);
   if (a.sl.kw) hipLaunchKernelGGL(ln::lane_wm_count_kernel<XKView>, grid, block, 0, st, a);
   else hipLaunchKernelGGL(ln::lane_wm_count_kernel<XSlices>, grid, block, 0, st, a);
   return hipGetLastError();
