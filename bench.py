@@ -793,7 +793,7 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
     return {"workload": "C4s: keyed SessionWindow(gap 1s) + SlidingWindow(60s,1s) SUM_I32, %d uniform keys, 20%% "
                         "out-of-order (delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, maxLateness 1000, "
                         "lane-per-key session replay, results left in HBM" % keys, "tune": tune or {},
-            "lane_counters": ([op._debug_stat(103 + i) for i in range(4)]
+            "lane_counters": ([op._debug_stat(103 + i) for i in range(4)] + [op._debug_stat(110 + i) for i in range(10)]
                               if (tune or {}).get("lane_session_counters") else None),
             "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
             "ms_per_step": 1e3 * sum(times) / len(times), "ms_per_step_each": [round(1e3 * t, 3) for t in times],

@@ -1430,8 +1430,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   a.ts_max_b = d_need + 3;
   if (lsdbg_on) {
     if (!d_lsdbg) {
-      XCHK(dalloc(&d_lsdbg, 4));
-      XCHK(hipMemsetAsync(d_lsdbg, 0, 32, stream));
+      XCHK(dalloc(&d_lsdbg, 16));
+      XCHK(hipMemsetAsync(d_lsdbg, 0, 16 * 8, stream));
     }
     a.dbg = d_lsdbg;
   }

@@ -761,13 +761,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     const int64_t t = R_t[u_][tid], vb = R_v[u_][tid];
     bool fast = one_ctx && ns > 0 && ci >= 0 && started;
     bool shift = false, flexe = false;
+    int edit = 0;  // 1: the movable edge below the previous slice moves; 2: the previous slice splits
     int n_app = 0;
+    int why = 0;  // debugging aid (a.dbg[4 + why]): why a tuple left the fast path
     if (fast) {
       if (t >= mx) {  // in-order: a first pending edge, room for the fixed edges it crosses and a flexible one
         const int64_t t_c = max(mx, ne);
         flexe = t >= jadd(t_c, gap);  // StreamSlicer.calculateNextFlexEdge (:118-130), one session context
         if (ne == JMIN || cfg->has_fixed == 0) {
           fast = false;
+          why = 1;
         } else {
           int64_t e = ne;
           if (t >= ne) {
@@ -783,10 +786,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
           }
           if (e == t) n_app++;
           else if (flexe) n_app++;
-          if (n_app > 8 || tail + n_app > sc) fast = false;
+          if (n_app > 8 || tail + n_app > sc) {
+            fast = false;
+            why = n_app > 8 ? 2 : 3;
+          }
         }
         // the session: extended, unchanged, or a new one behind the last (t >= maxEventTime >= its end)
-        if (fast && jadd(en_l, gap) < t && ns >= cfg->sesscap) fast = false;
+        if (fast && jadd(en_l, gap) < t && ns >= cfg->sesscap) {
+          fast = false;
+          why = 4;
+        }
       } else if (t >= st_l && t <= en_l) {
         // out-of-order inside the last session: updateContext changes nothing, no modification
       } else if (t < st_l && t < c_tl && c_ts == st_l && pv >= 0 && jsub(st_l, gap) < t) {
@@ -794,10 +803,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         // earlier session reaches t (getSession returns the last one, no merge follows), and checkSliceEdges moves the
         // movable edge between the previous slice and the current one -- which starts at the session start -- down to
         // t (S/SliceManager.java:89-125)
-        shift = (ns < 2 || t > jadd(sen[ns - 2], gap)) && ty_movable(Q_ty[bb + pv]);
-        if (!shift) fast = false;
+        const bool alone = ns < 2 || t > jadd(sen[ns - 2], gap);
+        const int32_t ty0 = Q_ty[bb + pv];
+        shift = alone && ty_movable(ty0);
+        if (!shift) {
+          // the edge below the current slice cannot move (a fixed grid edge, or a flexible edge of several contexts):
+          // checkSliceEdges splits the previous slice at t instead (S/SliceManager.java:140-150, splitSlice :168-192),
+          // room permitting without a compaction, the previous slice starting below t
+          if (alone && tail < sc && p_ts < t && Q_te[bb + pv] == st_l) {
+            edit = 2;
+          } else {
+            fast = false;
+            why = alone ? 5 : 6;
+          }
+        }
+      } else if (t < st_l && t < c_tl && c_ts != st_l && p_ts == st_l && pv - 1 >= head && jsub(st_l, gap) < t &&
+                 (ns < 2 || t > jadd(sen[ns - 2], gap)) && Q_te[bb + pv - 1] == st_l &&
+                 ty_movable(Q_ty[bb + pv - 1])) {
+        // the last session starts at the previous slice (after a split above): shiftStart, and checkSliceEdges moves
+        // the movable edge below the previous slice down to t
+        edit = 1;
       } else {
         fast = false;
+        why = t < st_l ? (c_ts != st_l ? 7 : 8) : 9;
       }
     }
     if (fast) {
@@ -844,6 +872,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
           if (p_ts > t) uns |= 1;  // note_order of the moved slice
           st_l = t;
           sst[ns - 1] = t;
+        } else if (edit == 1) {  // the session start and the edge below the previous slice move down to t
+          const int64_t pp_ts = Q_ts[bb + pv - 1];
+          Q_te[bb + pv - 1] = t;
+          Q_ts[bb + pv] = t;
+          p_ts = t;
+          uns |= 2;
+          if (pp_ts > t || t > c_ts) uns |= 1;  // note_order of the moved slice
+          st_l = t;
+          sst[ns - 1] = t;
+        } else if (edit == 2) {
+          // splitSlice(pv, t): the previous slice ends at t (a flexible edge), a new slice [t, session start) takes
+          // the old edge's kind, the current slice moves up one position (insert_at; tail < sc: no compaction)
+          const int32_t ty0 = Q_ty[bb + pv];
+          const int32_t ty1 = ty_fixed(ty0) ? ty0 : ty_flex(ty0 - 1);
+          const int64_t a_cs = Q_cs[bb + pv], a_cl = p_cl;
+          flush_prev();
+          Q_te[bb + pv] = t;
+          Q_ty[bb + pv] = 1;
+          const int nc = ci + 1;
+          Q_ts[bb + nc] = c_ts;
+          Q_te[bb + nc] = Q_te[bb + ci];
+          Q_cs[bb + nc] = Q_cs[bb + ci];
+          Q_ty[bb + nc] = Q_ty[bb + ci];
+          Q_ts[bb + ci] = t;
+          Q_te[bb + ci] = st_l;
+          Q_cs[bb + ci] = a_cs;
+          Q_ty[bb + ci] = ty_kind(ty1);
+          pv = ci;
+          p_ts = t; p_tl = t; p_tf = JMAX; p_cl = a_cl; p_cnt = 0; p_p0 = 0; p_p1 = ID_MIN; p_p2 = ID_MAX;
+          minmod = min(minmod, ci);
+          ci = nc;
+          tail++;
+          st_l = t;
+          sst[ns - 1] = t;
         }
         // the in-order branch of processElement (t >= the current slice's tLast), else findSliceIndexByTimestamp:
         // its first two probes from the tail are the current and the previous slice (registers), on a sorted list
@@ -870,6 +932,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     }
     // ---- the general path for this tuple
     n_gen++;
+    if (a.dbg) atomicAdd(&a.dbg[4 + why], 1ull);
     flush_cur();
     L.s = s0;
     L.s.maxEventTime = mx; L.s.nextEdgeTs = ne; L.s.currentCount = cc;

@@ -1693,7 +1693,14 @@ int64_t scotty_debug_stat(scotty_op* op, int which) {
         return -1;
       return (int64_t)v;
     }
-    case 107: return op->x->last_rec_bytes;  // the last keyed replay's record bytes (8 packed, 16, 24)
+    case 107: return op->x->last_rec_bytes;
+    case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119: {
+      // lane-session general-path tuples by the reason they left the fast path (keyed_lane_session.hip `why`)
+      unsigned long long v = 0;
+      if (op->x->d_lsdbg && hipMemcpy(&v, op->x->d_lsdbg + 4 + (which - 110), 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+      return (int64_t)v;
+    }  // the last keyed replay's record bytes (8 packed, 16, 24)
     default:
       if (which >= 16 && which - 16 < (int)op->x->xq_trace.size()) return op->x->xq_trace[which - 16];
       return -1;
