@@ -755,7 +755,7 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
     shape per key).  Session windows take the lane-per-key session replay (keyed_lane_session.hip: one lane restates one
     key's StreamSlicer / SliceManager / SessionContext, steady-state tuples in registers).  The timed steps cover one
     whole 10-step period (the pause step included); a second period with HIP events gives the device split.
-    `tune`: scotty_tune knobs (the "c4s2" leg: {"keyed_lane_session": 2}, the kernel's 3-waves build, A/B;
+    `tune`: scotty_tune knobs (the "c4s2" leg: {"keyed_lane_session": 1}, the kernel's 2-waves build, A/B;
     profiles/r05/ab_c4s_occupancy.json: 2 waves 8.04 ms/step, 3 waves 8.93)."""
     import torch
     rate = max(1, batch // 1000)
@@ -860,7 +860,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
     ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c5,c5t,pcie; c3nb: C3 with the start band "
-                    "off, A/B; c4s2: C4s on the lane-session kernel's 3-waves build, A/B); default all but c3nb, c4s2")
+                    "off, A/B; c4s2: C4s on the lane-session kernel's 2-waves build, A/B); default all but c3nb, c4s2")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     args = ap.parse_args()
@@ -1008,8 +1008,8 @@ def main():
                 log("bench: C4 done")
             if "c4s" in legs:
                 extra["c4s"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20)
-            if "c4s2" in args.only.split(","):  # A/B only: the lane-session kernel's 3-waves-per-SIMD build
-                extra["c4s2"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 2})
+            if "c4s2" in args.only.split(","):  # A/B only: the lane-session kernel's 2-waves-per-SIMD build
+                extra["c4s2"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 1})
                 log("bench: C4s (keyed sessions) done")
             if "c5" in legs:
                 extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)

@@ -115,7 +115,7 @@ class XEngine {
   bool lsdbg_on = false;
   bool pack_off = false;          // keyed replay: 16-byte records even when a batch fits 8 ("keyed_pack_records" 0)
   int64_t last_rec_bytes = 0;     // the last keyed replay's record size (debug stat 107)
-  int lane_session_occ = 2;       // lane-session kernel build: 2 or 3 waves per SIMD (A/B, "keyed_lane_session" 2)
+  int lane_session_occ = 3;       // lane-session kernel build: 3 (default) or 2 waves per SIMD ("keyed_lane_session" 1 / 2)
   bool lane_session_off = false;  // keyed: sessions through the wavefront replay instead (A/B, "keyed_lane_session" 0)
   // keyed_lane_session.hip: time-measured session windows (beside context-free time windows) on Eager slices
   bool lane_session_mode() const {
