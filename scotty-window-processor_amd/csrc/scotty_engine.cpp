@@ -31,6 +31,9 @@ int ingest_wgs_per_cu(int vt, int need);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_wm(const WmArgs& a, hipStream_t st);
+hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_wm(const WmArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_wm_publish(const void* d_src, void* h_dst_dev, int64_t bytes, hipStream_t st);
 hipError_t launch_fill_u64(unsigned long long* p, int64_t n, unsigned long long v, hipStream_t st);
 hipError_t launch_first_ge(const int64_t* ts, int64_t n, int64_t x, unsigned long long* out_idx, hipStream_t st);
@@ -244,6 +247,26 @@ int tbegin(scotty_op* op, scotty_op::TEv& e, int cls) {
   }
   HIPCHK(hipEventRecord(e.a, op->stream));
   return SCOTTY_OK;
+}
+// A timed launch group whose launch wrappers take the events and have the dispatches stamp them (hipExtLaunchKernel):
+// no marker packets between dependent kernels.  tlaunch acquires the pair (null when timing is off), tlaunched files
+// it for tresolve.
+int tlaunch(scotty_op* op, scotty_op::TEv& e, int cls) {
+  e.cls = cls;
+  e.a = e.b = nullptr;
+  if (!op->timing) return SCOTTY_OK;
+  if (!op->ev_pool.empty()) {
+    e.a = op->ev_pool.back().first;
+    e.b = op->ev_pool.back().second;
+    op->ev_pool.pop_back();
+  } else {
+    HIPCHK(hipEventCreate(&e.a));
+    HIPCHK(hipEventCreate(&e.b));
+  }
+  return SCOTTY_OK;
+}
+void tlaunched(scotty_op* op, scotty_op::TEv& e) {
+  if (op->timing && e.a) op->tev_pending.push_back(e);
 }
 int tend(scotty_op* op, scotty_op::TEv& e) {
   if (!op->timing || !e.a) return SCOTTY_OK;
@@ -524,10 +547,11 @@ int enqueue_cix(scotty_op* op) {
   ia.cix_meta = op->d_cixmeta;
   ia.cix_margin = std::max<int64_t>(4 * op->last_span, 4000);
   scotty_op::TEv tx;
-  int rc = tbegin(op, tx, SCOTTY_TIME_PUSH_OTHER);
+  int rc = tlaunch(op, tx, SCOTTY_TIME_PUSH_OTHER);
   if (rc) return rc;
-  HIPCHK(launch_cix_build(ia, op->stream));
-  return tend(op, tx);
+  HIPCHK(launch_cix_build(ia, op->stream, tx.a, tx.b));
+  tlaunched(op, tx);
+  return SCOTTY_OK;
 }
 
 // Ingest launch of one micro-batch (no host synchronisation); *tile_out = the arrival tile size used.
@@ -633,11 +657,12 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
   ca.vt = op->vt;
   ca.push_seq = seq;
   scotty_op::TEv tc;
-  rc = tbegin(op, tc, SCOTTY_TIME_PUSH_OTHER);
+  rc = tlaunch(op, tc, SCOTTY_TIME_PUSH_OTHER);
   if (rc) return rc;
   if (op->stamps_on && op->d_stamps) ca.stamps = op->d_stamps + 8192 * 4 - 16;  // the commit's phase stamps
-  HIPCHK(launch_commit(ca, op->stream));
-  return tend(op, tc);
+  HIPCHK(launch_commit(ca, op->stream, tc.a, tc.b));
+  tlaunched(op, tc);
+  return SCOTTY_OK;
 }
 
 // First tuple of the operator's life: StreamSlicer + SliceManager for tuple 0 (the store is empty).
@@ -1339,11 +1364,10 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     for (int attempt = 0; attempt < 2; attempt++) {
       // triggers + window assembly + GC (window_kernels.hip), then ONE transfer of the packed result
       scotty_op::TEv tw, tc;
-      rc = tbegin(op, tw, SCOTTY_TIME_WATERMARK);
+      rc = tlaunch(op, tw, SCOTTY_TIME_WATERMARK);
       if (rc) return rc;
-      HIPCHK(launch_wm(wa, op->stream));
-      rc = tend(op, tw);
-      if (rc) return rc;
+      HIPCHK(launch_wm(wa, op->stream, tw.a, tw.b));
+      tlaunched(op, tw);
       if (!op->h_out_dev) {  // no host-mapped result buffer: one DMA transfer (class RESULT_COPY)
         rc = tbegin(op, tc, SCOTTY_TIME_RESULT_COPY);
         if (rc) return rc;

@@ -1598,10 +1598,14 @@ int ingest_wgs_per_cu(int vt, int need) {
 }
 
 // mode < 0: default; mode 0..3 selects a variant for the (int32, SUM) configuration (A/B tuning)
-hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(cix_build_kernel, dim3(256), dim3(256), 0, st, a);
+// e0 / e1 (nullable): timing events the dispatch stamps with its own start / end (hipExtLaunchKernel), in place of
+// marker packets recorded around the launch (scotty_engine.cpp tlaunch)
+hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  if (e0 || e1) hipExtLaunchKernelGGL(cix_build_kernel, dim3(256), dim3(256), 0, st, e0, e1, 0, a);
+  else hipLaunchKernelGGL(cix_build_kernel, dim3(256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
+hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) { return launch_cix_build(a, st, nullptr, nullptr); }
 
 // mode: -1 the default (MM_MODE / DEFAULT_MODE); INGEST_STREAMING (an in-order stream: the default loop on fewer
 // workgroups); for A/B (scotty_tune "ingest_mode" / the exact engine's "quiet_ingest_mode"): 7 the pipelined loop
@@ -1635,10 +1639,12 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
   return launch_ingest_vt<VT_F64, 0>(a, need, nblocks, st);
 }
 
-hipError_t launch_commit(const CommitArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(1024), 0, st, a);
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  if (e0 || e1) hipExtLaunchKernelGGL(commit_kernel, dim3(1), dim3(1024), 0, st, e0, e1, 0, a);
+  else hipLaunchKernelGGL(commit_kernel, dim3(1), dim3(1024), 0, st, a);
   return hipGetLastError();
 }
+hipError_t launch_commit(const CommitArgs& a, hipStream_t st) { return launch_commit(a, st, nullptr, nullptr); }
 
 hipError_t launch_shard_export(const ShardArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(shard_export_kernel, dim3(1), dim3(1024), 0, st, a);

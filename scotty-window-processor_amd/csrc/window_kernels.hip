@@ -19,6 +19,7 @@
 //     S/aggregationstore/LazyAggregateStore.java:138-146).
 // Two launches per watermark: wm_prep_kernel (one workgroup: dirty block summaries, prefix, sparse table, triggers,
 // GC, metadata snapshot) and wm_windows_kernel (one wavefront per triggered window).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -452,12 +453,19 @@ hipError_t launch_wm_publish(const void* d_src, void* h_dst_dev, int64_t bytes, 
   return hipGetLastError();
 }
 
-hipError_t launch_wm(const WmArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(wk::wm_prep_kernel, dim3(1), dim3(1024), 0, st, a);
+// e0 / e1 (nullable): timing events stamped by the dispatches themselves (hipExtLaunchKernel): e0 with wm_prep's start,
+// e1 with the last launch's end
+hipError_t launch_wm(const WmArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  const bool more = a.n_windows > 0;
+  if (e0 || e1) hipExtLaunchKernelGGL(wk::wm_prep_kernel, dim3(1), dim3(1024), 0, st, e0, more ? nullptr : e1, 0, a);
+  else hipLaunchKernelGGL(wk::wm_prep_kernel, dim3(1), dim3(1024), 0, st, a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || a.n_windows <= 0) return e;
-  hipLaunchKernelGGL(wk::wm_windows_kernel, dim3((unsigned)((a.n_windows + 3) / 4)), dim3(256), 0, st, a);
+  if (e != hipSuccess || !more) return e;
+  const dim3 grid((unsigned)((a.n_windows + 3) / 4));
+  if (e1) hipExtLaunchKernelGGL(wk::wm_windows_kernel, grid, dim3(256), 0, st, nullptr, e1, 0, a);
+  else hipLaunchKernelGGL(wk::wm_windows_kernel, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
+hipError_t launch_wm(const WmArgs& a, hipStream_t st) { return launch_wm(a, st, nullptr, nullptr); }
 
 }  // namespace scotty
