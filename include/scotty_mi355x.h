@@ -224,8 +224,12 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
  * (exact engine, non-keyed: the first event-exact piece of a batch the one-pass quiet path refused, in tuples;
  * 0 = max(batch / 32, 2^20); later pieces grow 4x; the split is invisible in the results), "quiet_band" 1 (exact
  * engine, non-keyed, one session window: one-pass batches may move the last session's start down -- the stream
- * resuming after a silence then costs one pass instead of event-exact rounds; the results are the same; off by
- * default). */
+ * resuming after a silence then costs one pass instead of event-exact rounds; the results are the same; on by
+ * default, 0 for A/B), "keyed_lane_session" (keyed session windows: 0 the wavefront-per-key replay, 1 the lane-per-key
+ * kernel's 2-waves-per-SIMD build, 2 its 3-waves build, the default; A/B only, before the first push),
+ * "keyed_pack_records" 0 (keyed lane-session replay: 16-byte sort records even when a batch's key and event-time bits
+ * fit the packed 8-byte ones; A/B only), "lane_session_counters" 1 (debugging aid: count the lane-session kernel's
+ * paths). */
 int scotty_tune(scotty_op* op, const char* key, int64_t value);
 
 /* Wait for all work enqueued on the op's stream. */
