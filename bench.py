@@ -59,6 +59,45 @@ def device_roofline(op, steps, batch, bytes_per_tuple, kernel):
             "device_ms_per_step_by_class": {k: v[0] / max(1, steps) for k, v in t.items()}}
 
 
+KN_INGEST, KN_KG_HIST, KN_KG_SCATTER, KN_KG_BUCKET, KN_COUNT_INGEST = range(5)  # device_common.h KN_*
+
+
+def kernel_name(pkg, which):
+    """rocprofv3 name of this thread's last launch of a measured kernel class (scotty_debug_kernel_name)."""
+    f = pkg.lib().scotty_debug_kernel_name
+    f.restype, f.argtypes = ctypes.c_char_p, [ctypes.c_int]
+    return f(which).decode()
+
+
+def norm_kernel(name):
+    """A kernel name as rocprofv3 prints it, without namespaces, arguments or spaces (for matching)."""
+    name = name.split("(")[0].replace("void ", "")
+    for ns in ("scotty::", "kg::", "ck::", "k::", "ln::", "x::", "wk::"):
+        name = name.replace(ns, "")
+    return name.replace(" ", "")
+
+
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def pmc_traffic(leg, kernels, batch, algo_bytes):
+    """HBM traffic of a leg's measured kernel(s) per launch from profiles/traffic.json (tools/traffic.py: separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, per-pattern corrections calibrated by tools/pmc_calib.hip), used
+    only when the file measured exactly these kernels (rocprof names) at this batch size; else None with the reason."""
+    try:
+        tj = json.load(open(TRAFFIC_FILE))["legs"][leg]
+    except (OSError, KeyError, ValueError):
+        return {"traffic": None, "traffic_note": "no %s entry in profiles/traffic.json" % leg}
+    want = sorted(norm_kernel(k) for k in kernels)
+    have = sorted(norm_kernel(k) for k in tj.get("kernels", {}))
+    if tj.get("batch") != batch or want != have:
+        return {"traffic": None, "traffic_note": "profiles/traffic.json measured %s at batch %s, this run launched %s at "
+                                                 "batch %d" % (have, tj.get("batch"), want, batch)}
+    hbm = sum(v["hbm_bytes_per_launch"] for v in tj["kernels"].values())
+    return {"traffic": hbm, "traffic_kernels": sorted(tj["kernels"]), "traffic_over_algorithmic": hbm / algo_bytes,
+            "traffic_source": tj.get("source")}
+
+
 # ----------------------------------------------------------------------------------------------- CPU baselines
 def _cpu_nonkeyed(setup, gen_step, wm_of, steps_range, budget_s, chunk, warm=None, sample=""):
     """Oracle (C++ restatement of SlicingWindowOperator, 1 thread) on the same stream: an untimed sparse warm-up
@@ -333,7 +372,7 @@ def cpu_c4s(keys, batch, threads):
 
 
 # ----------------------------------------------------------------------------------------------- GPU legs
-def extra_c1(pkg, dev, batch, steps):
+def extra_c1(pkg, dev, batch, steps, warm=2):
     """BASELINE configs[0] (C1), the reference benchmark's own workload at GPU batch size: SlidingWindow(Time,
     60000, 1000), SUM_I32 of java.util.Random(43).nextInt() values (restated exactly, generated on the host before
     the timed region), in-order ts = i // rate, maxLateness 1 (Flink connector default), one key; grid path.  A sparse
@@ -353,31 +392,44 @@ def extra_c1(pkg, dev, batch, steps):
     op.processWatermarkRaw(59_999)
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     inputs = []
-    for s in range(2 * steps):
+    for s in range(warm + 2 * steps):
         inputs.append((base + 60_000 + s * 1000, torch.from_numpy(jr.next_ints(batch)).to(dev)))
     torch.cuda.synchronize(dev)
-    rows = 0
-    t0 = time.perf_counter()
-    for s in range(steps):
+
+    def step(s):
         ts, v = inputs[s]
         op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
-        n, _ = op.processWatermarkRaw(60_000 + s * 1000 + (batch - 1) // rate)
-        rows += n
+        return op.processWatermarkRaw(60_000 + s * 1000 + (batch - 1) // rate)[0]
+    # full-rate warm-up steps (untimed): the first full-size push sizes the operator's per-batch buffers (cells, tile
+    # maxima, the ingest arena) -- C2 has the same warm-up; round 5's C1 timed its first full-size step and showed a
+    # ~60 us/step wall-device gap from it
+    for s in range(warm):
+        step(s)
+    torch.cuda.synchronize(dev)
+    rows, each = 0, []
+    t0 = time.perf_counter()
+    for s in range(warm, warm + steps):
+        rows += step(s)
+        each.append(time.perf_counter())
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     op.enableTiming(True)
-    for s in range(steps, 2 * steps):
-        ts, v = inputs[s]
-        op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
-        op.processWatermarkRaw(60_000 + s * 1000 + (batch - 1) // rate)
+    for s in range(warm + steps, warm + 2 * steps):
+        step(s)
     torch.cuda.synchronize(dev)
+    roof = device_roofline(op, steps, batch, BYTES_PER_TUPLE, kernel_name(pkg, KN_INGEST))
+    roof.update(pmc_traffic("c1", [roof["kernel"]], batch, batch * BYTES_PER_TUPLE))
+    ms = 1e3 * elapsed / steps
     return {"workload": "C1: SlidingWindow(Time,60000,1000), SUM_I32 of Random(43).nextInt(), in-order, "
                         "maxLateness=1, one key (the reference benchmark's sliding workload)",
-            "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * elapsed / steps,
+            "tuples_per_step": batch, "steps": steps, "warmup_full_rate_steps": warm, "ms_per_step": ms,
+            "ms_per_step_each": [round(1e3 * (b - a), 4) for a, b in zip([t0] + each[:-1], each)],
+            "wall_minus_device_us_per_step": 1e3 * (ms - roof["device_ms_per_step"]),
+            "frac_step_wall": batch * BYTES_PER_TUPLE / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "value": batch * steps / elapsed, "unit": "tuples/s", "windows_emitted": rows,
             "published_reference_flink_scotty": {"value": C1_PUBLISHED, "unit": "events/s",
                                                  "source": "README.md:50-54"},
-            "roofline": device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")}
+            "roofline": roof}
 
 
 def extra_c3(pkg, dev, batch, steps=10, warm=61, tune=None):
@@ -423,7 +475,9 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61, tune=None):
             rows += n
             verdicts.append(op._debug_stat(8))
             rounds.append((op._debug_stat(0), op._debug_stat(1)))  # events, event-exact rounds of the batch
-    roof = device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_MIN|NEED_MAX> (quiet path)")
+    roof = device_roofline(op, steps, batch, BYTES_PER_TUPLE, kernel_name(pkg, KN_INGEST))
+    roof["kernel_role"] = "the grid ingest on the exact engine's quiet path"
+    roof.update(pmc_traffic("c3", [roof["kernel"]], batch, batch * BYTES_PER_TUPLE))
     return {"workload": "C3: SlidingWindow(60s,60ms) + SessionWindow(gap 1s), MIN_I32+MAX_I32, 20% out-of-order "
                         "(delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, non-keyed, exact engine",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * sum(times) / len(times),
@@ -498,11 +552,13 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
         % (f(op._h, 9), f(op._h, 10), f(op._h, 11)))
     log("c2s: cell index base %d shift %d buckets %d full %d span_end %d; slices %d, grid ahead %d, prev_max %d"
         % tuple(f(op._h, k) for k in range(1, 9)))
+    roof = device_roofline(op, steps, batch, BYTES_PER_TUPLE, kernel_name(pkg, KN_INGEST))
+    roof.update(pmc_traffic("c2s", [roof["kernel"]], batch, batch * BYTES_PER_TUPLE))
     return {"workload": "C2s: 1000 concurrent sliding windows, sizes randomTumbling(1000,1,20) Random(10), slide "
                         "size/20, SUM_I32+COUNT, 20% out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000",
             "tuples_per_step": batch, "steps": steps, "ms_per_step": 1e3 * elapsed / steps,
             "value": batch * steps / elapsed, "unit": "tuples/s", "windows_emitted": rows,
-            "roofline": device_roofline(op, steps, batch, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")}
+            "roofline": roof}
 
 
 def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20_000_000, rank=0, world=1,
@@ -529,7 +585,10 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
         op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, size))
     base = (torch.arange(batch, device=dev, dtype=torch.int64) + rank * batch) // rate
     times, rows = [], 0
-    for s in range(warm + steps):
+    roof_steps = steps if G == 1 else 0  # G == 1: as many instrumented steps after the timed ones (device roofline)
+    for s in range(warm + steps + roof_steps):
+        if s == warm + steps:
+            op.enableTiming(True)
         ts = base + s * 1000
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         torch.cuda.synchronize(dev)
@@ -543,16 +602,22 @@ def extra_c5(pkg, dev, batch, steps, warm=3, n_windows=1000, lo=1_000_000, hi=20
             op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
             n, _ = op.processWatermarkDevice(s * 1000 + (batch - 1) // rate)
         torch.cuda.synchronize(dev)
-        if s >= warm:
+        if warm <= s < warm + steps:
             times.append(time.perf_counter() - t0)
             rows += n
     elapsed = sum(times)
+    roof = None
+    if roof_steps:
+        roof = device_roofline(op, roof_steps, batch, BYTES_PER_TUPLE, kernel_name(pkg, KN_COUNT_INGEST))
+        roof["classes_note"] = ("push_other and watermark are marker-event intervals on the op's stream (any bubble a "
+                                "host read inside them leaves counts as device time: an upper bound)")
+        roof.update(pmc_traffic("c5", [roof["kernel"]], batch, batch * BYTES_PER_TUPLE))
     if dist is not None:
         t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    return {"workload": "C5: %d tumbling count windows, sizes randomCount(%d,%d,%d) Random(10), SUM_I32+COUNT, "
+    return {"roofline": roof, "workload": "C5: %d tumbling count windows, sizes randomCount(%d,%d,%d) Random(10), SUM_I32+COUNT, "
                         "in-order, maxLateness=1%s" % (n_windows, n_windows, lo, hi,
                                                        ", time-range sharded over %d GPUs (RCCL all-gather of count "
                                                        "cells)" % G if G > 1 else ""),
@@ -584,7 +649,10 @@ def extra_c5t(pkg, dev, batch, steps, warm=3, rank=0, world=1, dist=None):
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60000, 1000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) + rank * batch
     times, rows = [], 0
-    for s in range(warm + steps):
+    roof_steps = steps if G == 1 else 0  # G == 1: as many instrumented steps after the timed ones (device roofline)
+    for s in range(warm + steps + roof_steps):
+        if s == warm + steps:
+            op.enableTiming(True)
         ts = base + s * G * batch
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
         torch.cuda.synchronize(dev)
@@ -598,16 +666,22 @@ def extra_c5t(pkg, dev, batch, steps, warm=3, rank=0, world=1, dist=None):
             op.processElementsDevice(ts.data_ptr(), v.data_ptr(), batch)
         n, _ = op.processWatermarkDevice(wm)
         torch.cuda.synchronize(dev)
-        if s >= warm:
+        if warm <= s < warm + steps:
             times.append(time.perf_counter() - t0)
             rows += n
     elapsed = sum(times)
+    roof = None
+    if roof_steps:
+        roof = device_roofline(op, roof_steps, batch, BYTES_PER_TUPLE, kernel_name(pkg, KN_COUNT_INGEST))
+        roof["classes_note"] = ("push_other and watermark are marker-event intervals on the op's stream (the time-edge "
+                                "pass reads the batch's first / last ts on the host inside the push: upper bound)")
+        roof.update(pmc_traffic("c5t", [roof["kernel"]], batch, batch * BYTES_PER_TUPLE))
     if dist is not None:
         t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    return {"workload": "C5 (SURVEY): TumblingWindow(Count,1000) + SlidingWindow(Time,60000,1000), SUM_I32+COUNT, "
+    return {"roofline": roof, "workload": "C5 (SURVEY): TumblingWindow(Count,1000) + SlidingWindow(Time,60000,1000), SUM_I32+COUNT, "
                         "in-order unique ts (ts = arrival index), maxLateness=1, a watermark per %d-tuple micro-batch%s"
                         % (batch * G, ", arrival-range sharded over %d GPUs (RCCL all-gather of count cells)" % G
                            if G > 1 else ""),
@@ -675,7 +749,7 @@ def c4_routing(pkg, dev, batch, keys, steps, rank, world, dist, seed=4242):
             "received_tuples_rank0_per_step": got / steps, "backend": dist.get_backend()}
 
 
-def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None, aggs=None):
+def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None, tune=None, aggs=None, host_steps=0):
     """BASELINE configs[3] (C4): SlidingWindow(60 s, 1 s) SUM_I32 per key, uniform keys, maxLateness 1 (Flink
     connector default); 61 s of warm-up so every step emits each key's window.  world > 1: key-hash sharding
     with no collective -- rank r owns the keys KeyedShardRouter(world) assigns it (what an upstream keyBy delivers), `keys`
@@ -719,18 +793,29 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
             rows += n
         if dist is not None and s == warm + steps - 1:
             dist.barrier()
+    kn = [kernel_name(pkg, k) for k in (KN_KG_HIST, KN_KG_SCATTER, KN_KG_BUCKET)]
     roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
-                           "keyed data pass: kg_hist + scan + kg_scatter + kg_bucket (class ingest)")
-    roof["traffic"] = None  # HBM bytes of the data pass per step, from separate --pmc passes (tools/keyed_traffic.py)
-    tfile = os.path.join(ROOT, "profiles", "keyed_traffic.json")
-    if os.path.exists(tfile) and world == 1 and aggs is None:
-        try:
-            tj = json.load(open(tfile))
-            if tj.get("batch") == batch and tj.get("keys") == keys:
-                roof["traffic"] = tj.get("hbm_bytes_per_step")
-                roof["traffic_over_algorithmic"] = tj.get("traffic_over_algorithmic")
-        except Exception:
-            pass
+                           "keyed data pass (class ingest): %s + scans + %s + %s" % tuple(kn))
+    roof["kernels"] = kn
+    if world == 1 and aggs is None:  # HBM bytes of the data pass per step (tools/traffic.py; scans are not matched)
+        roof.update(pmc_traffic("c4", kn, batch, batch * KEYED_BYTES_PER_TUPLE))
+    host = None
+    if host_steps:  # the same steps with every window's row copied to host memory (scotty_process_watermark)
+        op.enableTiming(False)
+        ht = []
+        for s in range(warm + 2 * steps, warm + 2 * steps + host_steps):
+            k = own[torch.randint(0, len(own), (batch,), device=dev, dtype=torch.int64, generator=g)]
+            v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+            ts = base + s * 1000
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            op.processElementsDevice(k.data_ptr(), ts.data_ptr(), v.data_ptr(), batch)
+            n, _ = op.processWatermarkRaw(s * 1000 + (batch - 1) // rate)
+            ht.append(time.perf_counter() - t0)
+        host = {"what": "results to host memory (scotty_process_watermark: one packed D2H of the SoA rows), "
+                        "as KeyedScottyWindowOperator hands every window to out.collect", "steps": host_steps,
+                "windows_per_step": n, "ms_per_step": 1e3 * sum(ht) / len(ht),
+                "value": batch * world * len(ht) / sum(ht), "unit": "tuples/s"}
     elapsed = sum(times)
     if dist is not None:
         t = torch.tensor([elapsed], device=dev if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
@@ -743,7 +828,7 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
             "tuples_per_step": batch * world, "tuples_per_step_per_gpu": batch, "steps": steps,
             "keys_per_gpu": op.keyCount(), "ms_per_step": 1e3 * elapsed / len(times),
             "value": batch * world * len(times) / elapsed, "unit": "tuples/s", "scaling": "weak",
-            "windows_emitted_rank0": rows, "roofline": roof,
+            "windows_emitted_rank0": rows, "roofline": roof, "results_to_host": host,
             "roofline_wall": {"achieved": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9,
                               "frac": per_gpu * KEYED_BYTES_PER_TUPLE / 1e9 / HBM_PEAK_GBS}}
 
@@ -800,7 +885,148 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows, "roofline": roof}
 
 
+def _numa_of_addr(addr):
+    """NUMA node of the page at a host address (get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR), x86-64 syscall 239)."""
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        node = ctypes.c_int(-1)
+        rc = libc.syscall(239, ctypes.byref(node), None, ctypes.c_ulong(0), ctypes.c_void_p(addr), ctypes.c_ulong(3))
+        return node.value if rc == 0 else None
+    except Exception:
+        return None
+
+
+def _node_cpus(node):
+    try:
+        out = set()
+        for part in open("/sys/devices/system/node/node%d/cpulist" % node).read().strip().split(","):
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+        return out
+    except (OSError, ValueError):
+        return set()
+
+
+def gpu_numa_node(dev_index):
+    """NUMA node of the GPU's PCI function (sysfs), or None."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(dev_index)
+        path = "/sys/bus/pci/devices/%04x:%02x:%02x.0/numa_node" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        return int(open(path).read().strip())
+    except Exception:
+        return None
+
+
+def extra_c4c(pkg, dev, batch, keys, steps=10, warm=11):
+    """Keyed out-of-order count windows at scale: KeyedScottyWindowOperator with
+    TumblingWindow(Count, 1000) + SlidingWindow(Time, 10 s, 1 s) per key, SUM_I32, `keys` uniform keys, 20 % of tuples
+    late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000.  Count windows make every slice a LazySlice with its
+    TreeSet record set, and an out-of-order tuple runs SliceManager's count-shift loop (S/SliceManager.java:64-87) --
+    the per-key replay path (one wavefront per key, exact_kernels.hip replay_kernel).  11 s of warm-up fill the sliding
+    windows' retention; results stay in HBM; a second run of as many steps with HIP events gives the device split."""
+    import torch
+    rate = max(1, batch // 1000)
+    g = torch.Generator(device=dev)
+    g.manual_seed(78)
+    op = pkg.KeyedSlicingWindowOperator(device=dev.index)
+    op.addWindowFunction(pkg.AGG_SUM_I32)
+    op.setMaxLateness(1000)
+    op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, 1000))
+    op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 10_000, 1_000))
+    base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
+    times, rows, count_rows = [], 0, 0
+    for s in range(warm + 2 * steps):
+        if s == warm + steps:
+            op.enableTiming(True)
+        t_begin = s * 1000 + 1000
+        k = torch.randint(0, keys, (batch,), device=dev, dtype=torch.int64, generator=g).to(torch.int32)
+        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        d = torch.randint(1, 501, (batch,), device=dev, generator=g)
+        ts = torch.where(late, base + t_begin - d, base + t_begin).contiguous()
+        v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op.processElementsDevice(k.data_ptr(), ts.data_ptr(), v.data_ptr(), batch)
+        n, _ = op.processWatermarkDevice(t_begin + (batch - 1) // rate - 500)
+        torch.cuda.synchronize(dev)
+        if warm <= s < warm + steps:
+            times.append(time.perf_counter() - t0)
+            rows += n
+    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
+                           "keyed replay (class ingest: sort by key + wavefront-per-key replay of LazySlice record sets)")
+    roof["bound_note"] = ("latency-bound: one wavefront restates one key's operator tuple by tuple (record-set inserts, "
+                          "count shifts); the HBM fraction is reported for comparison only")
+    return {"workload": "C4c: keyed TumblingWindow(Count,1000) + SlidingWindow(10s,1s) SUM_I32, %d uniform keys, 20%% "
+                        "out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000, per-key replay with LazySlice "
+                        "record sets, results left in HBM" % keys,
+            "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
+            "ms_per_step": 1e3 * sum(times) / len(times), "ms_per_step_each": [round(1e3 * t, 3) for t in times],
+            "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows, "roofline": roof}
+
+
+def cpu_c4c(keys, batch, threads):
+    """C4c on the CPU: KeyedScottyWindowOperator with TumblingWindow(Count, 1000) + SlidingWindow(10 s, 1 s) per key on T
+    threads (key % T partitions), the GPU leg's stream shape, one watermark per step; two untimed steps, then timed
+    steps until the budget."""
+    from oracle.oracle import KeyedOracleThreads, JavaError
+    op = KeyedOracleThreads(threads)
+    op.addWindowFunction(0)
+    op.setMaxLateness(1000)
+    op.addWindowAssigner(0, 1, 1000, 0)
+    op.addWindowAssigner(1, 0, 10_000, 1_000)
+    rng = np.random.default_rng(78)
+    rate = max(1, batch // 1000)
+    base = np.arange(batch, dtype=np.int64) // rate
+    done, t_proc, steps = 0, 0.0, 0
+    for s in range(1000):
+        t_begin = s * 1000 + 1000
+        k = rng.integers(0, keys, size=batch).astype(np.uint32)
+        late = rng.random(batch) < 0.2
+        ts = np.where(late, base + t_begin - rng.integers(1, 501, size=batch), base + t_begin)
+        v = rng.integers(-2**31, 2**31, size=batch, dtype=np.int64)
+        p = op.partition(k, ts, v)
+        t0 = time.perf_counter()
+        try:
+            op.process(p, t_begin + (batch - 1) // rate - 500)
+        except JavaError:
+            pass
+        dt = time.perf_counter() - t0
+        if s >= 2:
+            t_proc += dt
+            done += batch
+            steps += 1
+            if t_proc > CPU_BUDGET_S:
+                break
+    eff, affinity, quota = host_cores()
+    return {"value": done / t_proc, "unit": "tuples/s", "cores": threads, "kind": "port",
+            "affinity_threads": affinity, "cgroup_cpu_quota": quota,
+            "sample": "%d steps of %d tuples (%d uniform keys, the C4c stream from event time 1 s) after 2 untimed "
+                      "steps; oracle/ KeyedScottyWindowOperator restatement on %d threads = the effective host cores "
+                      "of this process, min(sched_getaffinity %d, cgroup quota %s); key %% %d partitions"
+                      % (steps, batch, keys, threads, affinity, quota, threads)}
+
+
 def extra_pcie(pkg, sizes, batch, steps):
+    """Placement first (the pinned leg split 14.4 vs 17.8 ms across boxes): the GPU's NUMA node,
+    this process's CPUs on it, and -- when the process may run there -- the leg runs with its CPU affinity bound to that
+    node, so the pinned staging slots are allocated (first touched) there; the node of the slots' pages is recorded."""
+    node = gpu_numa_node(0)
+    before = os.sched_getaffinity(0)
+    local = (_node_cpus(node) & before) if node is not None and node >= 0 else set()
+    placement = {"gpu_numa_node": node, "affinity_cpus": len(before), "affinity_cpus_on_gpu_node": len(local),
+                 "bound_to_gpu_node": bool(local)}
+    if local:
+        os.sched_setaffinity(0, local)
+    try:
+        out = _extra_pcie(pkg, sizes, batch, steps, placement)
+    finally:
+        os.sched_setaffinity(0, before)
+    out["placement"] = placement
+    return out
+
+
+def _extra_pcie(pkg, sizes, batch, steps, placement):
     """PCIe-inclusive C2: the same operator fed from HOST memory through scotty_process_elements --
     (a) the op's pinned staging slots (scotty_host_buffers: DMA in place, double-buffered), (b) pageable numpy
     arrays (chunked through pinned staging).  Timed: push + watermark calls per step, each step ending with its
@@ -825,6 +1051,8 @@ def extra_pcie(pkg, sizes, batch, steps):
                 ts, vals = op.hostBuffers(batch)
                 np.add(base, s * 1000, out=ts)
                 vals[:] = vals0
+                if s < 2:  # the two staging slots' page placement
+                    placement["pinned_slot%d_numa_node" % s] = _numa_of_addr(ts.ctypes.data)
             else:
                 ts, vals = base + s * 1000, vals0
             t0 = time.perf_counter()
@@ -859,10 +1087,12 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 27, help="tuples per step (1 s of event time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
-    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c5,c5t,pcie; c3nb: C3 with the start band "
+    ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c4c,c5,c5t,pcie; c3nb: C3 with the start band "
                     "off, A/B; c4s2: C4s on the lane-session kernel's 2-waves build, A/B); default all but c3nb, c4s2")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
+    ap.add_argument("--skip-headline", action="store_true",
+                    help="profiling runs only (tools/gpu_traffic.sh): run just the --only legs, no C2 headline line")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -897,102 +1127,95 @@ def main():
     nroof = max(1, args.roof_steps)
     nsteps = args.steps + args.warmup + nroof
 
-    # ---- inputs resident in HBM before the timed region: this rank's arrival chunk of every global batch
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
-    batches = []
-    base = (torch.arange(B, device=dev, dtype=torch.int64) + rank * B) // rate
-    for s in range(nsteps):
-        ts = base + s * 1000
-        vals = torch.randint(-2**31, 2**31, (B,), device=dev, dtype=torch.int32, generator=gen)
-        batches.append((ts, vals, int(s * 1000 + (B * G - 1) // rate)))
-    torch.cuda.synchronize(dev)
+    res = {"metric": METRIC, "skipped_headline": True} if rank == 0 else None
+    batches = op = None
+    if not args.skip_headline:
+        # ---- inputs resident in HBM before the timed region: this rank's arrival chunk of every global batch
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1234 + rank)
+        batches = []
+        base = (torch.arange(B, device=dev, dtype=torch.int64) + rank * B) // rate
+        for s in range(nsteps):
+            ts = base + s * 1000
+            vals = torch.randint(-2**31, 2**31, (B,), device=dev, dtype=torch.int32, generator=gen)
+            batches.append((ts, vals, int(s * 1000 + (B * G - 1) // rate)))
+        torch.cuda.synchronize(dev)
 
-    op = pkg.ShardedSlicingWindowOperator(device=local) if sharded else pkg.SlicingWindowOperator(device=local)
-    op.addWindowFunction(pkg.AGG_SUM_I32)
-    op.addWindowFunction(pkg.AGG_COUNT)
-    op.setMaxLateness(1)
-    for s in sizes:
-        op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Time, s))
-    n_windows = 0
+        op = pkg.ShardedSlicingWindowOperator(device=local) if sharded else pkg.SlicingWindowOperator(device=local)
+        op.addWindowFunction(pkg.AGG_SUM_I32)
+        op.addWindowFunction(pkg.AGG_COUNT)
+        op.setMaxLateness(1)
+        for s in sizes:
+            op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Time, s))
+        n_windows = 0
 
-    def step(i):
-        ts, vals, wm = batches[i]
-        if sharded:
-            op.processChunk(ts.data_ptr(), vals.data_ptr(), B, 0)
-        else:
-            op.processElementsDevice(ts.data_ptr(), vals.data_ptr(), B)
-        nw, _ = op.processWatermarkRaw(wm)
-        return nw
+        def step(i):
+            ts, vals, wm = batches[i]
+            if sharded:
+                op.processChunk(ts.data_ptr(), vals.data_ptr(), B, 0)
+            else:
+                op.processElementsDevice(ts.data_ptr(), vals.data_ptr(), B)
+            nw, _ = op.processWatermarkRaw(wm)
+            return nw
 
-    for i in range(args.warmup):
-        step(i)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.warmup, args.warmup + args.steps):
-        n_windows += step(i)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    # roofline: the same step with HIP events around every launch group (after the wall-clock region, so the
-    # instrumentation does not count in `value`)
-    op.enableTiming(True)
-    for i in range(args.warmup + args.steps, nsteps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
-    assert op.processedCount() >= B * nsteps - 1, op.processedCount()
-    log("bench: C2 done, %.3f ms/step" % (elapsed * 1e3 / args.steps))
+        for i in range(args.warmup):
+            step(i)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.warmup, args.warmup + args.steps):
+            n_windows += step(i)
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        # roofline: the same step with HIP events around every launch group (after the wall-clock region, so the
+        # instrumentation does not count in `value`)
+        op.enableTiming(True)
+        for i in range(args.warmup + args.steps, nsteps):
+            step(i)
+        torch.cuda.synchronize(dev)
+        if dist:
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            dist.barrier()
+        assert op.processedCount() >= B * nsteps - 1, op.processedCount()
+        log("bench: C2 done, %.3f ms/step" % (elapsed * 1e3 / args.steps))
 
-    res = None
-    if rank == 0:
-        total = B * args.steps * world
-        roof = device_roofline(op, nroof, B, BYTES_PER_TUPLE, "ingest_kernel<VT_I32,NEED_SUM>")
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "ingest_traffic.json")
-        if os.path.exists(tfile):
-            try:
-                tj = json.load(open(tfile))
-                if tj.get("batch") == B:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        roof["traffic"] = traffic
-        res = {
-            "metric": METRIC,
-            "value": total / elapsed,
-            "unit": "tuples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int32 values / int64 timestamps",
-            "data": "synthetic (in-HBM, seeded): global stream ts = step*1000 + i//%d ms, int32 uniform values" % rate,
-            "config": {"workload": "C2: 1000 concurrent tumbling windows, sizes randomTumbling(1000,1,20) "
-                                   "java.util.Random(10), SUM_I32+COUNT, in-order, maxLateness=1",
-                       "tuples_per_step": B * world, "tuples_per_step_per_gpu": B, "event_ms_per_step": 1000,
-                       "windows_emitted": n_windows,
-                       "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch"
-                                       % world) if sharded else "single GPU"},
-            "roofline": roof,
-        }
-    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c4s", "c5", "c5t", "pcie"}
+        res = None
+        if rank == 0:
+            total = B * args.steps * world
+            roof = device_roofline(op, nroof, B, BYTES_PER_TUPLE, kernel_name(pkg, KN_INGEST))
+            roof.update(pmc_traffic("c2", [roof["kernel"]], B, B * BYTES_PER_TUPLE))
+            res = {
+                "metric": METRIC,
+                "value": total / elapsed,
+                "unit": "tuples/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": elapsed * 1e3 / args.steps,
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "int32 values / int64 timestamps",
+                "data": "synthetic (in-HBM, seeded): global stream ts = step*1000 + i//%d ms, int32 uniform values" % rate,
+                "config": {"workload": "C2: 1000 concurrent tumbling windows, sizes randomTumbling(1000,1,20) "
+                                       "java.util.Random(10), SUM_I32+COUNT, in-order, maxLateness=1",
+                           "tuples_per_step": B * world, "tuples_per_step_per_gpu": B, "event_ms_per_step": 1000,
+                           "windows_emitted": n_windows,
+                           "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch"
+                                           % world) if sharded else "single GPU"},
+                "roofline": roof,
+            }
+    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c4s", "c4c", "c5", "c5t", "pcie"}
     extra = {}
     if not args.no_extra:
-        del batches
-        del op
+        batches = op = None
         torch.cuda.empty_cache()
         if world == 1:
             if "c1" in legs:
-                extra["c1"] = extra_c1(pkg, dev, 1 << 26, 5)
+                extra["c1"] = extra_c1(pkg, dev, 1 << 26, 10)
                 log("bench: C1 done")
             if "c2s" in legs:
                 extra["c2s"] = extra_c2s(pkg, dev, 1 << 27, 5)
@@ -1004,10 +1227,13 @@ def main():
                 extra["c3nb"] = extra_c3(pkg, dev, 1 << 26, 10, tune={"quiet_band": 0})
                 log("bench: C3 (band off) done")
             if "c4" in legs:
-                extra["c4"] = extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5)
+                extra["c4"] = extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, host_steps=5)
                 log("bench: C4 done")
             if "c4s" in legs:
                 extra["c4s"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20)
+            if "c4c" in legs:
+                extra["c4c"] = extra_c4c(pkg, dev, C4_BATCH, 1 << 20)
+                log("bench: C4c (keyed out-of-order count windows) done")
             if "c4s2" in args.only.split(","):  # A/B only: the lane-session kernel's 2-waves-per-SIMD build
                 extra["c4s2"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 1})
                 log("bench: C4s (keyed sessions) done")
@@ -1037,6 +1263,7 @@ def main():
             cb = {"c1": lambda: cpu_c1((1 << 26) // 1000),
                   "c2s": lambda: cpu_c2s(pkg, (1 << 27) // 1000), "c3": lambda: cpu_c3((1 << 26) // 1000),
                   "c4": lambda: cpu_c4(1 << 20, C4_BATCH, threads), "c4s": lambda: cpu_c4s(1 << 20, C4_BATCH, threads),
+                  "c4c": lambda: cpu_c4c(1 << 20, C4_BATCH, threads),
                   "c5": lambda: cpu_c5(pkg, (1 << 27) // 1000),
                   "c5t": lambda: cpu_c5t(1 << 20)}
             for name, fn in cb.items():

@@ -1,5 +1,6 @@
 package de.tub.dima.scotty.slicing;
 
+import java.lang.ref.WeakReference;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayList;
@@ -65,6 +66,7 @@ final class KeyedEngine {
     };
 
     /** Whether an operator constructed now (not through perKey) is a per-key instance; see the class comment. */
+    @SuppressWarnings("unchecked")
     static boolean sharedForCaller() {
         if (SCOPE.get()[0] > 0) return true;
         String mode = System.getProperty("scotty.keyed.engine", "auto");
@@ -79,15 +81,19 @@ final class KeyedEngine {
         }
         // a keyed connector builds every key's operator from the same call site: the frame that matched last time on
         // this thread, at the same depth, answers at once (one array read instead of a walk per key at 1 M keys)
+        // The hit is kept with the caller set it matched (a changed scotty.keyed.callers invalidates it) and holds the
+        // class weakly (a pooled task thread must not pin a redeployed job's class loader).
         Object[] last = LAST_HIT.get();
-        if (last[0] != null) {
+        if (last[0] != null && last[2] == callers) {
+            Class<?> hit = ((WeakReference<Class<?>>) last[0]).get();
             int d = (Integer) last[1];
-            if (d < ctx.length && ctx[d] == last[0]) return true;
+            if (hit != null && d < ctx.length && ctx[d] == hit) return true;
         }
         for (int i = 0; i < ctx.length; i++) {
             if (callers.contains(ctx[i].getName())) {
-                last[0] = ctx[i];
+                last[0] = new WeakReference<Class<?>>(ctx[i]);
                 last[1] = i;
+                last[2] = callers;
                 return true;
             }
         }
@@ -112,11 +118,11 @@ final class KeyedEngine {
         return callers;
     }
 
-    /** {class, depth} of the stack frame that made the thread's last construction a per-key one. */
+    /** {weak class, depth, caller set} of the stack frame that made the thread's last construction a per-key one. */
     private static final ThreadLocal<Object[]> LAST_HIT = new ThreadLocal<Object[]>() {
         @Override
         protected Object[] initialValue() {
-            return new Object[2];
+            return new Object[3];
         }
     };
 

@@ -996,6 +996,7 @@ hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* 
 template <int VT, int NEED>
 static void launch_ingest_cn(const CPushArgs& a, hipStream_t st) {
   const int64_t waves = (a.nsteps + a.per_wave - 1) / a.per_wave;
+  note_kernel(KN_COUNT_INGEST, "count_ingest_kernel<%d, %d>", VT, NEED);
   hipLaunchKernelGGL((ck::count_ingest_kernel<VT, NEED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
 }
 template <int VT>

@@ -839,6 +839,7 @@ hipError_t launch_kg_build(const uint32_t* slot_key, int64_t n_ops, unsigned lon
 
 hipError_t launch_kg_partition(const KgArgs& a, int vt, hipStream_t st) {
   hipLaunchKernelGGL(kg::kg_prep_kernel, dim3(1), dim3(64), 0, st, a);
+  note_kernel(KN_KG_HIST, "kg_hist_kernel");
   hipLaunchKernelGGL(kg::kg_hist_kernel, dim3((unsigned)((a.ntiles + kg::HT - 1) / kg::HT)), dim3(kg::PT), 0, st, a);
   return hipGetLastError();
 }
@@ -856,13 +857,18 @@ int kg_tile(int vt, int64_t nbk, int variant) {
 hipError_t launch_kg_scatter(const KgArgs& a, int vt, hipStream_t st) {
   const unsigned grid = (unsigned)(((a.ntiles + 7) / 8) * 8);
   if (vt == VT_I32) {
-    if (a.tile == 8192 && a.variant == 1)
+    if (a.tile == 8192 && a.variant == 1) {
+      note_kernel(KN_KG_SCATTER, "kg_scatter_kernel<4, 8192, 2048, 1024>");
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 1024>), dim3(grid), dim3(1024), 0, st, a);
-    else if (a.tile == 8192)
+    } else if (a.tile == 8192) {
+      note_kernel(KN_KG_SCATTER, "kg_scatter_kernel<4, 8192, 2048, 512>");
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 8192, 2048, 512>), dim3(grid), dim3(512), 0, st, a);
-    else
+    } else {
+      note_kernel(KN_KG_SCATTER, "kg_scatter_kernel<4, 4096, 4096, 512>");
       hipLaunchKernelGGL((kg::kg_scatter_kernel<4, 4096, 4096, 512>), dim3(grid), dim3(512), 0, st, a);
+    }
   } else {
+    note_kernel(KN_KG_SCATTER, "kg_scatter_kernel<8, 4096, 4096, 512>");
     hipLaunchKernelGGL((kg::kg_scatter_kernel<8, 4096, 4096, 512>), dim3(grid), dim3(512), 0, st, a);
   }
   return hipGetLastError();
@@ -875,9 +881,11 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
   const bool B = (which & 1) != 0, C = (which & 2) != 0;
   if (a.sl.kw && mm) {  // key-interleaved store with MIN / MAX (integer values)
     if (vt == VT_I32) {
+      if (B) note_kernel(KN_KG_BUCKET, "kg_bucket_mm_kernel<0, true>");
       if (B) hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<VT_I32, true>), grid, block, 0, st, a);
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, true, XKView>), cgrid, cblock, 0, st, a, n_ops);
     } else {
+      if (B) note_kernel(KN_KG_BUCKET, "kg_bucket_mm_kernel<1, true>");
       if (B) hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<VT_I64, true>), grid, block, 0, st, a);
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I64, true, XKView>), cgrid, cblock, 0, st, a, n_ops);
     }
@@ -886,9 +894,11 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
   if (a.sl.kw) {  // key-interleaved store: COUNT / integer SUM
     if (vt == VT_I32) {
       // 8 records in flight per lane (A/B r03k: 2 -> 8 cut the data pass 1.14 -> 1.02 ms per 2^26 tuples)
+      if (B) note_kernel(KN_KG_BUCKET, "kg_bucket_kernel<0, false, 8>");
       if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I32, false, 8>), grid, block, 0, st, a);
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I32, false, XKView>), cgrid, cblock, 0, st, a, n_ops);
     } else {
+      if (B) note_kernel(KN_KG_BUCKET, "kg_bucket_kernel<1, false, 8>");
       if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<VT_I64, false, 8>), grid, block, 0, st, a);
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<VT_I64, false, XKView>), cgrid, cblock, 0, st, a, n_ops);
     }
@@ -897,9 +907,11 @@ hipError_t launch_kg_bucket(const KgArgs& a, int vt, bool mm, int64_t n_ops, hip
 #define SCOTTY_KG(V)                                                                                   \
   do {                                                                                                 \
     if (mm) {                                                                                          \
+      if (B) note_kernel(KN_KG_BUCKET, "kg_bucket_mm_kernel<%d, true>", V);                           \
       if (B) hipLaunchKernelGGL((kg::kg_bucket_mm_kernel<V, true>), grid, block, 0, st, a);           \
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<V, true, XSlices>), cgrid, cblock, 0, st, a, n_ops);  \
     } else {                                                                                           \
+      if (B) note_kernel(KN_KG_BUCKET, "kg_bucket_kernel<%d, false, 2>", V);                          \
       if (B) hipLaunchKernelGGL((kg::kg_bucket_kernel<V, false>), grid, block, 0, st, a);             \
       if (C) hipLaunchKernelGGL((kg::kg_commit_kernel<V, false, XSlices>), cgrid, cblock, 0, st, a, n_ops); \
     }                                                                                                  \

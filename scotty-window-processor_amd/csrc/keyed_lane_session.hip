@@ -768,7 +768,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
       if (t >= mx) {  // in-order: a first pending edge, room for the fixed edges it crosses and a flexible one
         const int64_t t_c = max(mx, ne);
         flexe = t >= jadd(t_c, gap);  // StreamSlicer.calculateNextFlexEdge (:118-130), one session context
-        if (ne == JMIN || cfg->has_fixed == 0) {
+        if (cfg->has_fixed == 0) {
+          // session windows only: no fixed edge is ever pending (min_next_edge_ts stays Long.MIN_VALUE, :52-54), so
+          // the only edge is the flexible one; te == Long.MIN_VALUE would meet the `min_next_edge_ts == te` branch
+          n_app = flexe ? 1 : 0;
+          if (t == JMIN) {
+            fast = false;
+            why = 1;
+          } else if (tail + n_app > sc) {
+            fast = false;
+            why = 3;
+          }
+        } else if (ne == JMIN) {
           fast = false;
           why = 1;
         } else {
@@ -830,8 +841,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     }
     if (fast) {
       if (t >= mx) {
-        // StreamSlicer.determineSlices, in-order branch (:51-86), without a flexible edge
-        if (n_app > 0) {
+        // StreamSlicer.determineSlices, in-order branch (:51-86). The pending edge advances whenever t passes it, also
+        // when every edge crossed is negative and none is appended (:65-69), so the next calculateNextFlexEdge sees it
+        if (cfg->has_fixed == 0) {
+          if (flexe) append_edge(t, ty_flex(1));  // calculateNextFlexEdge: the session gap reached (one context)
+        } else if (n_app > 0 || t > ne) {
           while (t > ne) {
             if (ne >= 0) append_edge(ne, XTYPE_FIXED);
             ne = next_edge(t, ne);

@@ -48,6 +48,11 @@ static std::atomic<int> g_alloc_poison{[] {
   return (e && *e) ? (int)(strtol(e, nullptr, 0) & 0xFF) : -1;
 }()};
 int alloc_poison() { return g_alloc_poison.load(std::memory_order_relaxed); }
+
+static thread_local char g_kernel_name[KN_N][96];
+void note_kernel(int which, const char* fmt, int a, int b, int c, int d) {
+  if (which >= 0 && which < KN_N) snprintf(g_kernel_name[which], sizeof(g_kernel_name[which]), fmt, a, b, c, d);
+}
 }  // namespace scotty
 
 using namespace scotty;
@@ -576,10 +581,6 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   ia.cix = op->d_cix;
   ia.cix_meta = op->d_cixmeta;
   ia.cix_margin = std::max<int64_t>(4 * op->last_span, 4000);
-  if (op->stamps_on) {
-    if (!op->d_stamps) HIPCHK(dev_malloc(&op->d_stamps, 8192 * 4 * 8));
-    ia.stamps = op->d_stamps;
-  }
   if (!op->cix_ready) {
     rc = enqueue_cix(op);
     if (rc) return rc;
@@ -607,6 +608,11 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
   ia.per_wave = per_wave;
   ia.tile = tile;
   const int64_t nblocks = (n + per_wave * 4 - 1) / (per_wave * 4);
+  // the stamps buffer holds 8192 x 4 words, the commit's 16 at its end: a launch of more workgroups records none
+  if (op->stamps_on && nblocks <= 8192 - 4) {
+    if (!op->d_stamps) HIPCHK(dev_malloc(&op->d_stamps, 8192 * 4 * 8));
+    ia.stamps = op->d_stamps;
+  }
   std::pair<hipEvent_t, hipEvent_t> ev{};
   if (op->timing) {
     if (!op->ev_pool.empty()) {
@@ -1025,8 +1031,16 @@ static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int6
         HIPCHK(hipEventCreate(&ev.second));
       }
     }
+    // device-time classes of the count path: the whole push on the op's stream (marker events: the interval holds
+    // any bubble a host read inside the push leaves, so push_other is an upper bound), less the ingest launch, whose
+    // dispatch stamps its own pair (ev) -> ingest
+    scotty_op::TEv tp;
+    rc = tbegin(op, tp, SCOTTY_TIME_PUSH_OTHER);
+    if (rc) return rc;
     rc = op->c->push(d_ts, d_val, n, ev.first, ev.second);
     if (rc) return fail(op, rc, op->c->err);
+    rc = tend(op, tp);
+    if (rc) return rc;
     if (op->timing) {
       op->ev_pending.push_back(ev);
       op->t_tuples += n;
@@ -1117,16 +1131,30 @@ int scotty_process_keyed_elements_device(scotty_op* op, const uint32_t* d_key, c
 static int exact_watermark(scotty_op* op, int64_t wm, scotty_windows* out, bool to_host) {
   XResult& r = op->xr;
   const uint64_t dropped_before = op->dropped;
+  scotty_op::TEv tw;
+  if (op->mode == 3) {
+    int rt = tbegin(op, tw, SCOTTY_TIME_WATERMARK);
+    if (rt) return rt;
+  }
   int rc = op->mode == 3 ? op->c->watermark(wm, r, to_host) : op->x->watermark(wm, r, to_host);
   if (rc) return fail(op, rc, op->mode == 3 ? op->c->err : op->x->err);
-  if (op->mode == 3) {  // ingest-kernel timing of the interval (scotty_enable_timing)
+  if (op->mode == 3) {  // device-time classes of the interval (scotty_enable_timing): ingest launches, the rest
+    rc = tend(op, tw);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(op->stream));
     for (auto& e : op->ev_pending) {
       float ms = 0.f;
-      if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) op->t_ms += ms;
+      if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+        op->t_ms += ms;
+        op->t_cls_ms[SCOTTY_TIME_INGEST] += ms;
+        op->t_cls_ms[SCOTTY_TIME_PUSH_OTHER] -= ms;  // inside a push interval
+      }
       op->t_launches++;
+      op->t_cls_n[SCOTTY_TIME_INGEST]++;
       op->ev_pool.push_back(e);
     }
     op->ev_pending.clear();
+    tresolve(op);
   }
   op->dropped = r.dropped;
   op->processed = op->x_pushed - r.dropped;
@@ -1688,6 +1716,12 @@ int64_t scotty_debug_ingest_stamps(scotty_op* op, long long* out, int64_t max_bl
 // Internal (not in the header): statistics of the last push of the exact engine (0 events, 1 rounds; keyed:
 // 2 path of the last push (0 replay, 1 sort-free, 2 sort-free + replay of deferred keys), 3 deferred tuples,
 // 4 keys committed on the sort-free path).
+// Internal (not in the header): the rocprofv3 name of the calling thread's last launch of kernel class `which`
+// (KN_* in device_common.h), "" if none -- the bench ties PMC traffic files to the kernel they measured.
+const char* scotty_debug_kernel_name(int which) {
+  return (which >= 0 && which < KN_N) ? g_kernel_name[which] : "";
+}
+
 int64_t scotty_debug_stat(scotty_op* op, int which) {
   if (!op) return -1;
   if (which == 5) return op->mode;  // 1 grid path, 2 exact engine, 3 count path

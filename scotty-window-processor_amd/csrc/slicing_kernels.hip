@@ -1533,6 +1533,7 @@ void set_ingest_timing_events(hipEvent_t start, hipEvent_t stop) {
 template <int VT, int NEED, int MODE>
 static hipError_t launch_ingest_t(const IngestArgs& a, int64_t nblocks, hipStream_t st) {
   constexpr size_t lds = ingest_lds_bytes<VT, NEED, MODE>();
+  note_kernel(KN_INGEST, "ingest_kernel<%d, %d, %d>", VT, NEED, MODE);
   if (g_ingest_ev[0]) {
     hipExtLaunchKernelGGL((ingest_kernel<VT, NEED, MODE>), dim3((unsigned)nblocks), dim3(256), lds, st,
                           g_ingest_ev[0], g_ingest_ev[1], 0, a);

@@ -224,20 +224,28 @@ def test_quiet_path_equals_event_exact_path_and_replay(pkg, seed):
         ops.append(op)
     f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
     sched = interval_schedule(ts, 12, lag=300, pushes_per_interval=3)
-    from helpers import same_windows
+    from helpers import same_windows, abs_twin
+    twin = abs_twin(cfg) if f64_cols else None  # sum |x| per window (helpers.F64_REL)
     quiet, event, why = 0, 0, []
     for step in sched:
         if step[0] == "push":
             for op in ops:
                 op.processElements(ts[step[1]:step[2]], vals[step[1]:step[2]])
+            if twin is not None and step[2] > step[1]:
+                twin.processElements(ts[step[1]:step[2]], np.zeros(step[2] - step[1], np.int64),
+                                     np.abs(vals[step[1]:step[2]]))
             v = ops[0]._debug_stat(8)
             quiet += v == 1
             event += v > 1
             why.append((v, ops[0]._debug_stat(11)))
         else:
             a, b, c = (op.processWatermark(step[1]) for op in ops)
-            same_windows(a, b, f64_cols=f64_cols)
-            same_windows(a, c, f64_cols=f64_cols)
+            sc = None
+            if twin is not None:
+                sc = [w.getAggValues() if w.hasValue() else [0.0] * len(cfg["aggs"])
+                      for w in twin.processWatermark(step[1])]
+            same_windows(a, b, f64_cols=f64_cols, scale=sc)
+            same_windows(a, c, f64_cols=f64_cols, scale=sc)
             assert ops[0].droppedCount() == ops[2].droppedCount()
     assert quiet > 0, ("no batch took the quiet path", cfg, why)
     assert event > 0, ("no batch needed the event-exact path", why)
@@ -355,21 +363,21 @@ def _keyed_run(pkg, cfg, keys, ts, vals, sched, vt="i32", f64_cols=()):
     for w in cfg["windows"]:
         gpu.addWindowAssigner(w)
     ora = KeyedOracle(cfg)
+    twin = KeyedOracle(cfg) if vt == "f64" and f64_cols else None  # sum |x| per window (helpers.F64_REL)
     total = 0
     for step in sched:
         if step[0] == "push":
             lo, hi = step[1], step[2]
             if hi > lo:
                 gpu.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
-                if vt == "f64":
-                    ora_vals = vals[lo:hi]
-                    ora.processElements(keys[lo:hi], ts[lo:hi], ora_vals)
-                else:
-                    ora.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                ora.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                if twin is not None:
+                    twin.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi], absolute=True)
         else:
             from oracle.oracle import JavaError
             try:
                 exp = ora.processWatermark(step[1])
+                scale = twin.processWatermark(step[1]) if twin is not None else None
             except JavaError:
                 # a key's SessionContext is empty: activeWindows.get(0) throws in the reference
                 # (SessionWindow.java:107), which ends a Flink job; the product reports the same exception
@@ -378,7 +386,7 @@ def _keyed_run(pkg, cfg, keys, ts, vals, sched, vt="i32", f64_cols=()):
                 assert ei.value.code == -5  # SCOTTY_ERR_INDEX
                 return total
             rows = gpu.processWatermark(step[1])
-            total += same_keyed_windows(rows, exp, f64_cols=f64_cols)
+            total += same_keyed_windows(rows, exp, f64_cols=f64_cols, scale=scale)
             assert gpu.droppedCount() == ora.failed
     assert gpu.keyCount() == len(ora.ops)
     return total
@@ -435,7 +443,8 @@ def test_keyed_lane_path_equals_wavefront_replay(pkg, seed):
     keys = rng.integers(0, nkeys, size=n).astype(np.uint32)
     lateness = int(rng.choice([1, 50, 500]))
     ops = []
-    for lane in (1, 0):
+    f64_cols = [i for i, a in enumerate(aggs) if a == SUM_F64]
+    for lane in (1, 0, 0)[:3 if f64_cols else 2]:  # f64: a third, |x|-fed replay operator gives sum |x| per row
         op = pkg.KeyedSlicingWindowOperator(device=0, value_type=vtc)
         op.tune("keyed_lane", lane)
         for a in aggs:
@@ -444,17 +453,18 @@ def test_keyed_lane_path_equals_wavefront_replay(pkg, seed):
         for w in wins:
             op.addWindowAssigner(w)
         ops.append(op)
-    f64_cols = [i for i, a in enumerate(aggs) if a == SUM_F64]
     sched = interval_schedule(ts, 12, lag=int(rng.integers(0, 300)), pushes_per_interval=2)
     total = 0
     for step in sched:
         if step[0] == "push":
             if step[2] > step[1]:
-                for op in ops:
-                    op.processElements(keys[step[1]:step[2]], ts[step[1]:step[2]], vals[step[1]:step[2]])
+                for j, op in enumerate(ops):
+                    v = vals[step[1]:step[2]]
+                    op.processElements(keys[step[1]:step[2]], ts[step[1]:step[2]], np.abs(v) if j == 2 else v)
         else:
             a, b = ops[0].processWatermarkArrays(step[1]), ops[1].processWatermarkArrays(step[1])
-            total += same_keyed_arrays(a, b, f64_cols=f64_cols)
+            sc = ops[2].processWatermarkArrays(step[1]) if len(ops) == 3 else None
+            total += same_keyed_arrays(a, b, f64_cols=f64_cols, scale=sc)
             assert ops[0].droppedCount() == ops[1].droppedCount()
     assert total > 0
 

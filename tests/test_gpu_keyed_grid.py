@@ -67,6 +67,7 @@ def _run_pair(pkg, vt, wins, aggs, lateness, keys, ts, vals, sched, f64_cols):
     """Feed both paths the same schedule; compare every watermark's rows.  Returns (rows, pushes taken by the
     sort-free path, pushes with deferred keys)."""
     kg, rp = _make(pkg, vt, wins, aggs, lateness, True), _make(pkg, vt, wins, aggs, lateness, False)
+    tw = _make(pkg, vt, wins, aggs, lateness, False) if f64_cols else None  # |x|-fed: sum |x| per row
     total, used, deferred = 0, 0, 0
     for step in sched:
         if step[0] == "push":
@@ -75,13 +76,16 @@ def _run_pair(pkg, vt, wins, aggs, lateness, keys, ts, vals, sched, f64_cols):
                 continue
             for op in (kg, rp):
                 op.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+            if tw is not None:
+                tw.processElements(keys[lo:hi], ts[lo:hi], np.abs(vals[lo:hi]))
             path = kg._debug_stat(2)
             used += path >= 1
             deferred += path == 2
             assert rp._debug_stat(2) == 0
         else:
             exp = rp.processWatermarkArrays(step[1])
-            total += same_keyed_arrays(kg.processWatermarkArrays(step[1]), exp, f64_cols=f64_cols)
+            sc = tw.processWatermarkArrays(step[1]) if tw is not None else None
+            total += same_keyed_arrays(kg.processWatermarkArrays(step[1]), exp, f64_cols=f64_cols, scale=sc)
             assert kg.droppedCount() == rp.droppedCount()
     assert kg.keyCount() == rp.keyCount()
     return total, used, deferred

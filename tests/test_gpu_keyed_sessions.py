@@ -77,13 +77,16 @@ def _nz(x):  # a power-of-two size / slide makes the reference loop forever
     return x + 1 if x & (x - 1) == 0 else x
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(16))
 def test_lane_session_kernel_equals_wavefront_replay(seed):
     """The lane-per-key session replay (keyed_lane_session.hip, the default for keyed session windows) against the
     wavefront replay (scotty_tune "keyed_lane_session" 0, exact_kernels.hip) on random keyed streams: one or two
     session windows (gaps 20-800 ms) beside 0-2 context-free windows, out-of-order shares 0-50 % with delays up to 2 gaps
     (shiftStart / split / merge / new-session-before edits), pauses that close sessions, i32 / i64 / f64 values.
-    Every watermark's rows (bounds, hasValue, values; f64 sums within 1e-6 relative) and the dropped counts match."""
+    Seeds 12-15 shift the stream below zero (negative event times: fixed edges crossed without an append still
+    advance the pending edge, S/StreamSlicer.java:65-69), seeds 12 and 14 register session windows only (no fixed
+    edge at all: the fast path's has_fixed == 0 case).
+    Every watermark's rows (bounds, hasValue, values; f64 sums within the f64 bound) and the dropped counts match."""
     from specs import Tumbling, SUM_I64, MIN_I64, MAX_I64, SUM_F64, MIN_F64, MAX_F64
     pkg = product()
     rng = np.random.default_rng(6100 + seed)
@@ -93,7 +96,7 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
     aggs = [x for x in aggs if rng.random() < 0.7] or [aggs[0]]
     gaps = [int(rng.integers(20, 800)) for _ in range(1 + (seed % 3 == 2))]
     wins = [Session(Time, g) for g in gaps]
-    for _ in range(int(rng.integers(0, 3))):
+    for _ in range(0 if seed in (12, 14) else int(rng.integers(1 if seed >= 12 else 0, 3))):
         if rng.random() < 0.5:
             wins.append(Tumbling(Time, _nz(int(rng.integers(50, 2000)))))
         else:
@@ -109,6 +112,8 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
                                     max_delay=int(rng.integers(1, 2 * max(gaps) + 2)), seed=seed, value_type=vt,
                                     gaps=pauses)
     keys = ((rng.integers(0, nkeys, size=n) * 2654435761) % (1 << 32)).astype(np.uint32)
+    if seed >= 12:  # the stream starts below zero and crosses it
+        ts = ts - int(rng.integers(2000, 30_000))
     vtc = {"i32": pkg.VALUE_I32, "i64": pkg.VALUE_I64, "f64": pkg.VALUE_F64}[vt]
 
     def make(lane):
@@ -122,6 +127,7 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
         return op
     lane, wave = make(True), make(False)
     f64_cols = [i for i, x in enumerate(aggs) if x == SUM_F64]
+    twin = make(False) if f64_cols else None  # |x|-fed replay: sum |x| per row (helpers.F64_REL)
     total = errors = 0
     from helpers import interval_schedule, same_keyed_arrays
     for step in interval_schedule(ts, int(rng.integers(3, 12)), lag=int(rng.integers(0, 2 * max(gaps))),
@@ -131,8 +137,16 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
             if hi > lo:
                 lane.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
                 wave.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                if twin is not None:
+                    twin.processElements(keys[lo:hi], ts[lo:hi], np.abs(vals[lo:hi]))
         else:
+            sc = None
             try:
+                if twin is not None:
+                    try:
+                        sc = twin.processWatermarkArrays(step[1])
+                    except pkg.ScottyError:
+                        pass  # the same throw as the wavefront replay's below (same timestamps)
                 exp = wave.processWatermarkArrays(step[1])
             except pkg.ScottyError as e:
                 # SessionWindow.triggerWindows reads getWindow(0) of a key whose sessions all closed at an earlier
@@ -144,7 +158,7 @@ def test_lane_session_kernel_equals_wavefront_replay(seed):
                 assert ei.value.code == -5
                 errors += 1
                 continue
-            total += same_keyed_arrays(lane.processWatermarkArrays(step[1]), exp, f64_cols=f64_cols)
+            total += same_keyed_arrays(lane.processWatermarkArrays(step[1]), exp, f64_cols=f64_cols, scale=sc)
             assert lane.droppedCount() == wave.droppedCount()
     assert lane.keyCount() == wave.keyCount()
     assert total > 0 or errors > 0
