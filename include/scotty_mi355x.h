@@ -57,6 +57,14 @@ extern "C" {
 #define SCOTTY_AGG_SUM_F64 7 /* within 1e-6 relative of the reference's arrival-order fold */
 #define SCOTTY_AGG_MIN_F64 8
 #define SCOTTY_AGG_MAX_F64 9
+/* The arrival index (0-based, counting every tuple pushed to the operator, WindowManager.currentCount order) of the
+ * window's FIRST partial: the first tuple added to the first non-empty slice the window contains.  It is what a
+ * combine that keeps partialAggregate1's fields returns (B/flinkBenchmark/aggregations/SumAggregation.java:16-18,
+ * D/flink-demo/.../SumWindowFunction.java:16-17) under AggregateValueState's lift-first / clone-first-then-fold order
+ * (S/state/AggregateValueState.java:23-31, 55-69): the host shim rebuilds those fields from the payload of that tuple
+ * (scotty_first_indices tells it which payloads to keep).  Grid path only (non-keyed, context-free time windows);
+ * other configurations return SCOTTY_ERR_UNSUPPORTED at the first push.  Value column: int64. */
+#define SCOTTY_AGG_FIRST 10
 /* OR-able flag: the function is an InvertibleAggregateFunction (C/windowFunction/InvertibleAggregateFunction.java):
  * a record leaving a LazySlice is removed by liftAndInvert instead of recomputing the slice from its record set
  * (S/state/AggregateValueState.java:33-41).  Sums and counts only. */
@@ -194,6 +202,10 @@ uint64_t scotty_dropped_count(scotty_op* op);
 uint64_t scotty_processed_count(scotty_op* op);
 /* Number of retained slices (LazyAggregateStore.size(), S/aggregationstore/LazyAggregateStore.java:54). */
 int64_t scotty_slice_count(scotty_op* op);
+/* SCOTTY_AGG_FIRST operators: the arrival indices a later window can still return -- the FIRST partial of every
+ * retained non-empty slice, ascending -- into out[0 .. cap).  Returns how many there are (may exceed cap), or a
+ * negative status.  The shim keeps the payloads of exactly these tuples after each watermark. */
+int64_t scotty_first_indices(scotty_op* op, int64_t* out, size_t cap);
 
 /* Optional HIP-event timing of the dominant (ingest) kernel on the op's stream.  When enabled, each
  * push records events around the ingest kernel; scotty_ingest_timing() returns the summed device
@@ -202,7 +214,8 @@ int scotty_enable_timing(scotty_op* op, int on);
 int scotty_ingest_timing(scotty_op* op, double* total_ms, uint64_t* launches, uint64_t* tuples);
 /* Device time per class since scotty_enable_timing, from HIP events around each launch group on the op's stream
  * (grid path: every launch and transfer of a micro-batch and a watermark is in exactly one class, so the sum over
- * the classes is the device time of the step; count path: ingest only).  Resolved at each watermark. */
+ * the classes is the device time of the step; count path: the ingest launch, and the rest of each push / watermark as
+ * marker-event intervals on the op's stream).  Resolved at each watermark. */
 #define SCOTTY_TIME_INGEST 0      /* the ingest kernel (the HBM-bound pass over the tuples) */
 #define SCOTTY_TIME_PUSH_OTHER 1  /* the other kernels of a micro-batch (cell index, edge commit) */
 #define SCOTTY_TIME_WATERMARK 2   /* triggers, window assembly, GC */

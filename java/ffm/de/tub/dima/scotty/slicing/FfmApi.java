@@ -45,6 +45,8 @@ final class FfmApi implements NativeApi {
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS, ADDRESS, JAVA_LONG));
     private static final MethodHandle PROCESS_WATERMARK = handle("scotty_process_watermark",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
+    private static final MethodHandle FIRST_INDICES = handle("scotty_first_indices",
+            FunctionDescriptor.of(JAVA_LONG, ADDRESS, ADDRESS, JAVA_LONG));
 
     // scotty_windows: size_t n_windows; int32 n_aggs (+4 pad); start, end, measure, has_value; values[8]; key
     private static final long RES_BYTES = 120, OFF_N = 0, OFF_NAGGS = 8, OFF_START = 16, OFF_END = 24,
@@ -158,6 +160,21 @@ final class FfmApi implements NativeApi {
         MemorySegment key = res.get(ADDRESS, OFF_KEY);
         out.key = key.address() == 0 || n == 0 ? null : key.reinterpret(4L * n).toArray(JAVA_INT);
         return rc;
+    }
+
+    @Override
+    public long[] firstIndices(long op) {
+        try {
+            long n = (long) FIRST_INDICES.invokeExact(ptr(op), MemorySegment.NULL, 0L);
+            if (n <= 0) return n < 0 ? null : new long[0];
+            try (Arena a = Arena.ofConfined()) {
+                MemorySegment buf = a.allocate(8L * n, 8);
+                long m = (long) FIRST_INDICES.invokeExact(ptr(op), buf, n);
+                return m == n ? buf.toArray(JAVA_LONG) : null;
+            }
+        } catch (Throwable t) {
+            throw new RuntimeException(t);
+        }
     }
 
     private static MemorySegment column(MemorySegment res, long off, int n) {

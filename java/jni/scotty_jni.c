@@ -11,6 +11,7 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "scotty_mi355x.h"
@@ -97,6 +98,21 @@ static int set_ints(JNIEnv* env, jobject out, jclass oc, const char* name, const
   (*env)->SetObjectField(env, out, (*env)->GetFieldID(env, oc, name, "[I"), a);
   (*env)->DeleteLocalRef(env, a);
   return 0;
+}
+
+/* scotty_first_indices -> long[] (null with the status in lastError0 on failure) */
+JNIEXPORT jlongArray JNICALL Java_de_tub_dima_scotty_slicing_JniApi_firstIndices0(JNIEnv* env, jclass cls, jlong op) {
+  (void)cls;
+  const int64_t n = scotty_first_indices(OP(op), NULL, 0);
+  if (n < 0) return NULL;
+  jlongArray a = (*env)->NewLongArray(env, (jsize)n);
+  if (!a || n == 0) return a;
+  int64_t* buf = (int64_t*)malloc((size_t)n * sizeof(int64_t));
+  if (!buf) return NULL;
+  const int64_t m = scotty_first_indices(OP(op), buf, (size_t)n);
+  if (m == n) (*env)->SetLongArrayRegion(env, a, 0, (jsize)n, (const jlong*)buf);
+  free(buf);
+  return m == n ? a : NULL;
 }
 
 /* scotty_process_watermark -> NativeApi.Windows {n, start, end, measure, has, values[n_aggs][n], key} */

@@ -33,6 +33,8 @@ final class JniApi implements NativeApi {
 
     private static native int processWatermark0(long op, long watermark, Windows out);
 
+    private static native long[] firstIndices0(long op);
+
     @Override
     public long create(int device, int valueType, int flags) {
         int[] rc = new int[1];
@@ -79,5 +81,10 @@ final class JniApi implements NativeApi {
     @Override
     public int processWatermark(long op, long watermark, Windows out) {
         return processWatermark0(op, watermark, out);
+    }
+
+    @Override
+    public long[] firstIndices(long op) {
+        return firstIndices0(op);
     }
 }

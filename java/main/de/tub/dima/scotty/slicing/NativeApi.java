@@ -45,6 +45,12 @@ interface NativeApi {
     /** scotty_process_watermark, the columns copied into {@code out}. */
     int processWatermark(long op, long watermark, Windows out);
 
+    /**
+     * scotty_first_indices: the arrival indices a later window can still return as its first partial's tuple
+     * (SCOTTY_AGG_FIRST operators), ascending; null on error (lastError has the message).
+     */
+    long[] firstIndices(long op);
+
     /** The binding of this JVM (see the class comment). */
     static NativeApi get() {
         return Holder.API;

@@ -28,11 +28,16 @@ import static de.tub.dima.scotty.slicing.NativeValues.*;
  * the identity, C/windowFunction/ReduceAggregateFunction.java:13-15): the demos' Flink functions aggregate
  * {@code Tuple2<Integer,Integer>} and keep {@code partialAggregate1.f0} (D/flink-demo/.../SumWindowFunction.java:
  * 8-19), Beam's keep {@code KV.getKey()}; the shim rebuilds those objects from the GPU's number and the f0 / key of
- * the operator's tuples.  That is exact when every tuple of one operator instance carries the same f0 / key -- the
- * keyed connectors' case (one operator per key, F/KeyedScottyWindowOperator.java:56-62) -- and the shim checks it
- * per tuple: if an instance sees two different f0 / keys it throws at the next processWatermark instead of
- * returning a value the reference would not.  The benchmark's {@code SumAggregation} (Tuple4 whose f2 / f3 are the
- * window's first tuple's timestamps) cannot be rebuilt from a number and is rejected.
+ * the operator's tuples.  These combines keep {@code partialAggregate1}'s other fields, so the reference's result
+ * carries the fields of the window's FIRST partial: the first tuple added to the first non-empty slice the window
+ * contains (AggregateValueState.merge clones the first non-empty partial and folds the rest into it,
+ * S/state/AggregateValueState.java:55-69).  A stand-alone operator registers the hidden SCOTTY_AGG_FIRST column,
+ * gets that tuple's arrival index per window and rebuilds the fields from the tuple itself (the benchmark's
+ * {@code SumAggregation} Tuple4 -- f0, f2, f3 of the first tuple, B/flinkBenchmark/aggregations/SumAggregation.java:
+ * 16-18 -- and the demos' Tuple2 / KV under GlobalScottyWindowOperator, whose f0 varies).  A per-key operator of the
+ * keyed engine has no FIRST column: there the rebuild uses the instance's one f0 / key -- exact for the keyed
+ * connectors (one operator per key, F/KeyedScottyWindowOperator.java:56-62) -- and throws at the next
+ * processWatermark if an instance sees two different ones; Tuple4 functions are refused there.
  */
 public final class NativeFunctions {
 
@@ -44,6 +49,8 @@ public final class NativeFunctions {
         NUMBER,     // Integer / Long / Double tuples, boxed result
         TUPLE2_F1,  // org.apache.flink.api.java.tuple.Tuple2: value f1, result new Tuple2(f0, value)
         KV_VALUE,   // org.apache.beam.sdk.values.KV: value getValue(), result KV.of(getKey(), value)
+        TUPLE4_F1,  // org.apache.flink.api.java.tuple.Tuple4: value f1, result new Tuple4(f0, value, f2, f3) of the
+                    // window's first partial's tuple (B/flinkBenchmark/aggregations/SumAggregation.java:16-18)
     }
 
     enum Op { SUM, COUNT, MIN, MAX }
@@ -91,14 +98,13 @@ public final class NativeFunctions {
         REGISTRY.put(d + "beam.windowFunctions.Min", new Spec(Op.MIN, Shape.KV_VALUE));
         REGISTRY.put(d + "beam.windowFunctions.Max", new Spec(Op.MAX, Shape.KV_VALUE));
         REGISTRY.put(d + "beam.windowFunctions.Count", new Spec(Op.COUNT, Shape.KV_VALUE));
+        // B/flinkBenchmark/aggregations/SumAggregation.java: Tuple4<String,Integer,Long,Long>, f1 summed, the first
+        // partial's f0 / f2 / f3 kept (a stand-alone operator's SCOTTY_AGG_FIRST column)
+        REGISTRY.put("de.tub.dima.scotty.flinkBenchmark.aggregations.SumAggregation", new Spec(Op.SUM, Shape.TUPLE4_F1));
     }
 
-    /** Functions known by name whose result cannot be rebuilt from the GPU's number: rejected with a reason. */
-    static final Map<String, String> REJECTED = Collections.singletonMap(
-            "de.tub.dima.scotty.flinkBenchmark.aggregations.SumAggregation",
-            "SumAggregation keeps the first partial's f0 / f2 / f3 (B/flinkBenchmark/aggregations/SumAggregation.java:"
-                    + "14-17): the window's first tuple, which the GPU does not track; implement NativeKind on a "
-                    + "function whose lower() is the sum only");
+    /** Functions known by name whose result cannot be rebuilt: rejected with a reason (none at present). */
+    static final Map<String, String> REJECTED = Collections.emptyMap();
 
     static int kindFor(Op op, int valueType) {
         switch (op) {
@@ -150,7 +156,7 @@ public final class NativeFunctions {
         private Object exemplar;
         private Object exemplarKey;
         private boolean keyVaries;
-        private MethodHandle valueOf, keyOf;
+        private MethodHandle valueOf, keyOf, f2Of, f3Of;
         private Constructor<?> tuple2;
         private Method kvOf;
 
@@ -159,6 +165,16 @@ public final class NativeFunctions {
             this.kind = kind;
             this.spec = spec;
             this.user = user;
+        }
+
+        /** The result keeps fields of the window's first partial's tuple (the SCOTTY_AGG_FIRST column rebuilds it). */
+        boolean keepsFirst() {
+            return user == null && spec.shape() != Shape.NUMBER;
+        }
+
+        /** Only the first partial's tuple can rebuild the result (no per-instance exemplar suffices). */
+        boolean needsFirst() {
+            return user == null && spec.shape() == Shape.TUPLE4_F1;
         }
 
         /** A copy for another operator instance (same function, its own exemplar). */
@@ -190,38 +206,54 @@ public final class NativeFunctions {
 
         private void accessors(Class<?> cls) throws ReflectiveOperationException {
             MethodHandles.Lookup l = MethodHandles.publicLookup();
-            if (spec.shape() == Shape.TUPLE2_F1) {
+            if (spec.shape() == Shape.TUPLE2_F1 || spec.shape() == Shape.TUPLE4_F1) {
                 valueOf = l.findGetter(cls, "f1", Object.class);
                 keyOf = l.findGetter(cls, "f0", Object.class);
+                if (spec.shape() == Shape.TUPLE4_F1) {
+                    f2Of = l.findGetter(cls, "f2", Object.class);
+                    f3Of = l.findGetter(cls, "f3", Object.class);
+                }
             } else {
                 valueOf = l.findVirtual(cls, "getValue", MethodType.methodType(Object.class));
                 keyOf = l.findVirtual(cls, "getKey", MethodType.methodType(Object.class));
             }
         }
 
-        /** The reference's lower() result for one window's lowered word. */
+        /**
+         * The reference's lower() result for one window's lowered word.  first: the window's first partial's tuple
+         * (SCOTTY_AGG_FIRST; null on a per-key operator, which uses its one f0 / key).
+         */
         @SuppressWarnings("unchecked")
-        Object rebuild(long bits) {
+        Object rebuild(long bits, Object first) {
             Object boxed = NativeValues.box(kind, bits);
             if (user != null) return user.scottyRebuild(boxed, exemplar);
             if (spec.shape() == Shape.NUMBER) return boxed;
-            if (keyVaries)
+            if (first == null && (keyVaries || spec.shape() == Shape.TUPLE4_F1))
                 throw new UnsupportedOperationException("the tuples of one operator carry different "
-                        + (spec.shape() == Shape.TUPLE2_F1 ? "f0" : "keys") + ": the reference's result keeps the "
-                        + "window's first partial's, which the GPU does not track (use the keyed connector, or a "
-                        + "NativeKind function)");
+                        + (spec.shape() == Shape.KV_VALUE ? "keys" : "fields") + ": the reference's result keeps the "
+                        + "window's first partial's, which this operator has no SCOTTY_AGG_FIRST column for (a per-key "
+                        + "operator of the keyed engine; use a stand-alone operator, or a NativeKind function)");
             try {
+                Object src = first != null ? first : exemplar;
+                if (valueOf == null) accessors(src.getClass());
+                Object key = first != null ? keyOf.invoke(first) : exemplarKey;
                 if (spec.shape() == Shape.TUPLE2_F1) {
-                    if (tuple2 == null) tuple2 = exemplar.getClass().getConstructor(Object.class, Object.class);
-                    return tuple2.newInstance(exemplarKey, boxed);
+                    if (tuple2 == null) tuple2 = src.getClass().getConstructor(Object.class, Object.class);
+                    return tuple2.newInstance(key, boxed);
+                }
+                if (spec.shape() == Shape.TUPLE4_F1) {
+                    if (tuple2 == null)
+                        tuple2 = src.getClass().getConstructor(Object.class, Object.class, Object.class, Object.class);
+                    return tuple2.newInstance(key, boxed, f2Of.invoke(first), f3Of.invoke(first));
                 }
                 if (kvOf == null) {
-                    Class<?> kv = Class.forName("org.apache.beam.sdk.values.KV", true,
-                            exemplar.getClass().getClassLoader());
+                    Class<?> kv = Class.forName("org.apache.beam.sdk.values.KV", true, src.getClass().getClassLoader());
                     kvOf = kv.getMethod("of", Object.class, Object.class);
                 }
-                return kvOf.invoke(null, exemplarKey, boxed);
-            } catch (ReflectiveOperationException e) {
+                return kvOf.invoke(null, key, boxed);
+            } catch (RuntimeException e) {
+                throw e;
+            } catch (Throwable e) {
                 throw new IllegalStateException("cannot rebuild " + spec.shape() + " result", e);
             }
         }

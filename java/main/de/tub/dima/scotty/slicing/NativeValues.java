@@ -14,6 +14,8 @@ public final class NativeValues {
 
     public static final int AGG_SUM_I32 = 0, AGG_COUNT = 1, AGG_MIN_I32 = 2, AGG_MAX_I32 = 3, AGG_SUM_I64 = 4,
             AGG_MIN_I64 = 5, AGG_MAX_I64 = 6, AGG_SUM_F64 = 7, AGG_MIN_F64 = 8, AGG_MAX_F64 = 9;
+    /** SCOTTY_AGG_FIRST: the arrival index of the window's first partial's tuple (registered by the shim itself). */
+    public static final int AGG_FIRST = 10;
     public static final int AGG_INVERTIBLE = 0x10000;
 
     private NativeValues() {

@@ -14,6 +14,7 @@ import de.tub.dima.scotty.state.StateFactory;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayList;
+import java.util.HashMap;
 import java.util.List;
 
 /**
@@ -62,6 +63,14 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
     // keyed mode: the shared engine and this instance's key
     private transient KeyedEngine engine;
     private int id = -1;
+    // stand-alone mode, functions whose result keeps the window's first partial's fields (NativeFunctions.Binding
+    // #keepsFirst): the hidden SCOTTY_AGG_FIRST column gives each window the arrival index of that tuple; the tuples
+    // since the last watermark and the first tuples of the retained slices (scotty_first_indices) are kept to rebuild
+    private final List<Integer> colOf = new ArrayList<Integer>();  // native result column of each binding
+    private int firstCol = -1;
+    private long arrivals = 0, recentBase = 0;
+    private transient ArrayList<Object> recent = new ArrayList<Object>();
+    private transient HashMap<Long, Object> retained = new HashMap<Long, Object>();
 
     /** S/SlicingWindowOperator.java:30-37: the state factory is not used (slices live in HBM). */
     public SlicingWindowOperator(StateFactory stateFactory) {
@@ -131,6 +140,8 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
             engine.add(id, ts, v);
             return;
         }
+        if (firstCol >= 0) recent.add(element);
+        arrivals++;
         if (buffered == tsBuf.capacity() / 8) allocate(2 * buffered);
         tsBuf.putLong((int) (8 * buffered), ts);
         if (valueType == NativeValues.VALUE_I32) valBuf.putInt((int) (4 * buffered), v.intValue());
@@ -146,7 +157,7 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
             bindEngine();
             List<KeyedEngine.Row> rows = engine.watermark(id, watermarkTs);
             List<AggregateWindow> out = new ArrayList<AggregateWindow>(rows.size());
-            for (KeyedEngine.Row r : rows) out.add(window(r.start, r.end, r.measure, r.has, r.words));
+            for (KeyedEngine.Row r : rows) out.add(window(r.start, r.end, r.measure, r.has, r.words, null));
             return out;
         }
         flush();
@@ -154,18 +165,40 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
         check(api.processWatermark(op, watermarkTs, w));
         List<AggregateWindow> out = new ArrayList<AggregateWindow>(w.n);
         for (int i = 0; i < w.n; i++) {
-            long[] words = new long[w.values.length];
-            for (int k = 0; k < words.length; k++) words[k] = w.values[k][i];
-            out.add(window(w.start[i], w.end[i], w.measure[i], w.has[i] != 0, words));
+            long[] words = new long[bindings.size()];
+            for (int k = 0; k < words.length; k++) words[k] = w.values[colOf.get(k)][i];
+            Object first = firstCol >= 0 && w.has[i] != 0 ? payload(w.values[firstCol][i]) : null;
+            out.add(window(w.start[i], w.end[i], w.measure[i], w.has[i] != 0, words, first));
         }
+        if (firstCol >= 0) retainFirsts();
         return out;
     }
 
-    private AggregateWindow window(long start, long end, int measure, boolean has, long[] words) {
+    private AggregateWindow window(long start, long end, int measure, boolean has, long[] words, Object first) {
         List<Object> agg = new ArrayList<Object>(words.length);
         if (has)
-            for (int k = 0; k < words.length; k++) agg.add(bindings.get(k).rebuild(words[k]));
+            for (int k = 0; k < words.length; k++) agg.add(bindings.get(k).rebuild(words[k], first));
         return new NativeAggregateWindow(measure == 0 ? WindowMeasure.Time : WindowMeasure.Count, start, end, has, agg);
+    }
+
+    /** The tuple with arrival index {@code index}: this interval's, or a retained slice's first tuple. */
+    private Object payload(long index) {
+        Object t = index >= recentBase ? recent.get((int) (index - recentBase)) : retained.get(index);
+        if (t == null)
+            throw new IllegalStateException("first partial's tuple " + index + " is neither in this interval nor a "
+                    + "retained slice's first tuple");
+        return t;
+    }
+
+    /** After a watermark: keep only the tuples a later window can still return as its first partial's. */
+    private void retainFirsts() {
+        long[] keep = api.firstIndices(op);
+        if (keep == null) throw new UnsupportedOperationException(api.lastError(op));
+        HashMap<Long, Object> next = new HashMap<Long, Object>(2 * keep.length + 1);
+        for (long x : keep) next.put(x, payload(x));
+        retained = next;
+        recent.clear();
+        recentBase = arrivals;
     }
 
     /** WindowManager.addWindowAssigner (S/WindowManager.java:121-147). */
@@ -202,13 +235,28 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
     @Override
     public <OutputType> void addAggregation(AggregateFunction<InputType, ?, OutputType> windowFunction) {
         NativeFunctions.Binding b = NativeFunctions.bind(windowFunction, valueType);
+        if (keyed && b.needsFirst())
+            throw new UnsupportedOperationException(windowFunction.getClass().getName() + " keeps the window's first "
+                    + "partial's fields, which the keyed engine does not track (SCOTTY_AGG_FIRST runs on stand-alone "
+                    + "operators)");
         bindings.add(b);
         if (keyed) {
+            colOf.add(bindings.size() - 1);
             configuredAfterUse();
             return;
         }
+        // SCOTTY_AGG_FIRST runs on the grid path: every window a context-free time window (the connectors register
+        // the windows before the function, F/GlobalScottyWindowOperator.java:40-47)
+        boolean grid = true;
+        for (long[] w : windows) grid &= w[0] != WIN_SESSION && w[1] == 0;
+        if (b.needsFirst() && !grid)
+            throw new UnsupportedOperationException(windowFunction.getClass().getName() + " keeps the window's first "
+                    + "partial's fields: SCOTTY_AGG_FIRST needs context-free time windows only (no session or count "
+                    + "windows)");
         flush();
-        check(api.addAggregation(op, b.kind));
+        colOf.add(check(api.addAggregation(op, b.kind)));
+        if (b.keepsFirst() && grid && firstCol < 0)
+            firstCol = check(api.addAggregation(op, NativeValues.AGG_FIRST));
     }
 
     /** S/SlicingWindowOperator.java:57-63. */
@@ -292,8 +340,8 @@ public class SlicingWindowOperator<InputType> implements WindowOperator<InputTyp
         valBuf = vals;
     }
 
-    private void check(int rc) {
-        if (rc >= 0) return;  // 1 = SCOTTY_WARN_LATE_DROPPED: tuples the reference drops too
+    private int check(int rc) {
+        if (rc >= 0) return rc;  // 1 = SCOTTY_WARN_LATE_DROPPED: tuples the reference drops too
         String msg = api.lastError(op);
         if (rc == ERR_INDEX) throw new IndexOutOfBoundsException(msg);  // the reference's exception type
         throw new UnsupportedOperationException(msg);

@@ -20,6 +20,7 @@ TIME, COUNT = 0, 1
 AGG_SUM_I32, AGG_COUNT, AGG_MIN_I32, AGG_MAX_I32 = 0, 1, 2, 3
 AGG_SUM_I64, AGG_MIN_I64, AGG_MAX_I64 = 4, 5, 6
 AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64 = 7, 8, 9
+AGG_FIRST = 10  # arrival index of the first partial's tuple (ORC_AGG_FIRST)
 AGG_SUB_I32 = 100
 AGG_INVERTIBLE = 0x10000
 STATE_MEMORY, STATE_MOCK = 0, 1

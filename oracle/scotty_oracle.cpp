@@ -66,6 +66,7 @@ inline double jmax_d(double a, double b) {
 struct Elem {
   i64 i = 0;
   double f = 0.0;
+  i64 seq = 0;  // arrival index (processElement calls before this one): the value ORC_AGG_FIRST lifts
 };
 // S/slice/StreamRecord.java:3-33 -- compareTo by ts only (:25-27)
 struct Record {
@@ -99,6 +100,7 @@ struct AggFn {
       case ORC_AGG_SUM_I32: case ORC_AGG_MIN_I32: case ORC_AGG_MAX_I32: case ORC_AGG_SUB_I32:
         p.i = (int32_t)e.i; break;
       case ORC_AGG_SUM_I64: case ORC_AGG_MIN_I64: case ORC_AGG_MAX_I64: p.i = e.i; break;
+      case ORC_AGG_FIRST: p.i = e.seq; break;
       default: p.f = e.f; break;
     }
     return p;
@@ -116,6 +118,9 @@ struct AggFn {
       case ORC_AGG_SUM_F64: r.f = a.f + b.f; break;
       case ORC_AGG_MIN_F64: r.f = jmin_d(a.f, b.f); break;
       case ORC_AGG_MAX_F64: r.f = jmax_d(a.f, b.f); break;
+      // a combine that keeps partialAggregate1's fields (B/flinkBenchmark/aggregations/SumAggregation.java:16-18,
+      // D/flink-demo/.../SumWindowFunction.java:16-17): the partial's identifying tuple stays the first one
+      case ORC_AGG_FIRST: r.i = a.i; break;
     }
     return r;
   }
@@ -790,9 +795,12 @@ struct Op {
   }
 
   // ---- SlicingWindowOperator.processElement (S/SlicingWindowOperator.java:41-44)
+  i64 arrivals = 0;  // processElement calls so far (the arrival index ORC_AGG_FIRST lifts)
   void processElement(const Elem& e, i64 ts) {
+    Elem x = e;
+    x.seq = arrivals++;
     determineSlices(ts);
-    managerProcessElement(e, ts);
+    managerProcessElement(x, ts);
   }
 
   // ---- LazyAggregateStore.aggregate (:83-111) + AggregateWindowState.containsSlice (:25-31)
@@ -915,7 +923,7 @@ int orc_add_window(orc_op* o, int kind, int measure, int64_t a, int64_t b) {
 int orc_add_aggregation(orc_op* o, int kind) {
   int base = kind & 0xFFFF;
   bool inv = (kind & ORC_AGG_INVERTIBLE) != 0;
-  bool ok = (base >= ORC_AGG_SUM_I32 && base <= ORC_AGG_MAX_F64) || base == ORC_AGG_SUB_I32;
+  bool ok = (base >= ORC_AGG_SUM_I32 && base <= ORC_AGG_MAX_F64) || base == ORC_AGG_SUB_I32 || base == ORC_AGG_FIRST;
   if (!ok || (inv && !(base == ORC_AGG_SUM_I32 || base == ORC_AGG_COUNT || base == ORC_AGG_SUM_I64 ||
                        base == ORC_AGG_SUM_F64))) {
     o->op.err = "unknown / non-invertible aggregation kind";

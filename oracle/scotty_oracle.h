@@ -40,6 +40,7 @@ extern "C" {
 #define ORC_AGG_SUM_F64 7
 #define ORC_AGG_MIN_F64 8
 #define ORC_AGG_MAX_F64 9
+#define ORC_AGG_FIRST 10   /* the arrival index of the first partial's tuple (include/scotty_mi355x.h SCOTTY_AGG_FIRST) */
 #define ORC_AGG_SUB_I32 100 /* (a,b)->a-b (TumblingWindowOperatorTest.java:212) */
 /* OR-able flag: function implements InvertibleAggregateFunction */
 #define ORC_AGG_INVERTIBLE 0x10000

@@ -32,6 +32,9 @@ VALUE_I32, VALUE_I64, VALUE_F64 = 0, 1, 2
 AGG_SUM_I32, AGG_COUNT, AGG_MIN_I32, AGG_MAX_I32 = 0, 1, 2, 3
 AGG_SUM_I64, AGG_MIN_I64, AGG_MAX_I64 = 4, 5, 6
 AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64 = 7, 8, 9
+# the arrival index of the window's first partial (include/scotty_mi355x.h SCOTTY_AGG_FIRST): what a combine keeping
+# partialAggregate1's fields returns (B/flinkBenchmark/aggregations/SumAggregation.java:16-18); grid path only
+AGG_FIRST = 10
 F64_AGGS = (AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64)
 AGG_INVERTIBLE = 0x10000  # OR-able: the function is an InvertibleAggregateFunction (include/scotty_mi355x.h)
 MAX_AGGS = 8
@@ -155,6 +158,7 @@ def lib():
             "scotty_dropped_count": (u64, [P]),
             "scotty_processed_count": (u64, [P]),
             "scotty_slice_count": (i64, [P]),
+            "scotty_first_indices": (i64, [P, P, ctypes.c_size_t]),
             "scotty_enable_timing": (ctypes.c_int, [P, ctypes.c_int]),
             "scotty_ingest_timing": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64),
                                                     ctypes.POINTER(u64)]),
@@ -416,6 +420,15 @@ class SlicingWindowOperator:
 
     def sliceCount(self):
         return self._l.scotty_slice_count(self._h)
+
+    def firstIndices(self):
+        """AGG_FIRST operators: the arrival indices a later window can still return (the FIRST partial of every
+        retained non-empty slice, ascending; scotty_first_indices) -- the payloads a shim must keep."""
+        self._flush()
+        n = self._check(self._l.scotty_first_indices(self._h, None, 0))
+        out = np.zeros(max(1, n), dtype=np.int64)
+        n = self._check(self._l.scotty_first_indices(self._h, out.ctypes.data, len(out)))
+        return out[:n]
 
     def enableTiming(self, on=True):
         self._check(self._l.scotty_enable_timing(self._h, 1 if on else 0))

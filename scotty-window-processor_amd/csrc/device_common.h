@@ -32,6 +32,7 @@ constexpr int INGEST_STREAMING_WGS = 448;
 // ms, 1024 -> 0.342; profiles/r05/ab_c2s_dq2_blocks.json)
 constexpr int INGEST_OOO_I32_WGS = 768;
 enum : int { NEED_SUM = 1, NEED_MIN = 2, NEED_MAX = 4 };
+constexpr int64_t FIRST_NONE = INT64_MAX;  // identity of a FIRST partial (no tuple yet)
 
 // The rocprofv3 name of the last launch of a measured kernel class on this thread ("ingest_kernel<0, 1, 23>", as the
 // profiler prints the template instance), so the bench can tie a PMC traffic file to the kernel it measured
@@ -88,6 +89,8 @@ struct IngestArgs {
   int64_t* cix_meta;         // [base, shift, n, cells indexed, ts end of the indexed range]
   int64_t cix_margin;        // ms past the stream front (prev_max) the index covers
   long long* stamps;         // nullable: per-workgroup clock stamps [blocks][4] (debugging aid, "ingest_stamps")
+  long long* c_first;        // SCOTTY_AGG_FIRST (first_kernel): per cell, the arrival index of its first tuple
+  int64_t seq_base;          //   arrival index of ts[0]
 };
 
 struct CommitArgs {
@@ -113,6 +116,8 @@ struct CommitArgs {
   int vt;
   int64_t push_seq;
   long long* stamps;         // nullable: phase clock stamps (scotty_tune "ingest_stamps"; a debugging aid)
+  long long* s_first;        // nullable (no SCOTTY_AGG_FIRST): per slice, the arrival index of its first tuple
+  long long* c_first;        //   per cell (first_kernel), folded by min and reset to FIRST_NONE
 };
 
 // ---- watermark of the grid path (window_kernels.hip): window assembly over slice-block summaries.
@@ -152,6 +157,7 @@ struct WmArgs {
   int32_t agg_kind[8];
   int need;
   int vt;
+  const long long* s_first;        // nullable: SCOTTY_AGG_FIRST per-slice partials
 };
 
 // byte offsets of the packed watermark output's columns for n windows and n_aggs aggregations

@@ -38,9 +38,10 @@ hipError_t launch_rehash(const unsigned long long* old_t, uint64_t old_n, unsign
 hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long* table, uint64_t mask,
                        uint32_t* slot, bool fixup, hipStream_t st);
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
-                               int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp,
-                               void** result, hipStream_t st, int64_t tbase, int tb, bool hist0);
-hipError_t launch_range_hist(const uint32_t* keys, const int64_t* ts, int64_t n, int32_t* hist,
+                               int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* hist10,
+                               int32_t* scan_tmp, void** result, hipStream_t st, int64_t tbase, int tb, bool hist0,
+                               int digit10);
+hipError_t launch_range_hist(const uint32_t* keys, const int64_t* ts, int64_t n, int32_t* hist, int32_t* hist10,
                              unsigned long long* part, unsigned long long* range, hipStream_t st);
 int64_t seg_tiles(int64_t n);
 hipError_t launch_seg_count(int rec, const void* recs, int64_t n, int32_t* cnt, long long* tmax_tile,
@@ -496,9 +497,9 @@ int XEngine::ensure_batch(int64_t n) {
   XCHK(dalloc((unsigned char**)&d_recA, cap * rec));
   XCHK(dalloc((unsigned char**)&d_recB, cap * rec));
   const int64_t nb = (cap + sort_tile() - 1) / sort_tile();
-  XCHK(dalloc(&d_hist, 256 * nb));
+  XCHK(dalloc(&d_hist, (256 + 1024) * nb));  // 8-bit digit histograms, then the 10-bit ones (launch_sort_by_slot)
   XCHK(dalloc(&d_rpart, 3 * nb));
-  XCHK(dalloc(&d_scan32, 256 * nb / 512 + 64));
+  XCHK(dalloc(&d_scan32, 1024 * nb / 512 + 64));
   XCHK(dalloc(&d_newpos, cap));
   bcap = cap;
   return SCOTTY_OK;
@@ -1332,7 +1333,9 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   //    packed 8-byte records (keyed_kernels.hip, Rec<8>): the key range pass then also takes the timestamp range
   const bool pack_try = vt == VT_I32 && lane_session_mode() && !pack_off;
   // (one read of the keys, and of the timestamps when packing: also the sort's first digit histogram)
-  XCHK(launch_range_hist(d_key, pack_try ? d_ts : nullptr, n, d_hist, d_rpart, d_kmax, stream));
+  const int64_t hist_nb = (bcap + sort_tile() - 1) / sort_tile();
+  int32_t* d_hist10 = d_hist + 256 * hist_nb;
+  XCHK(launch_range_hist(d_key, pack_try ? d_ts : nullptr, n, d_hist, d_hist10, d_rpart, d_kmax, stream));
   if ((rc = tend(tk, 0))) return rc;
   XCHK(hipMemcpyAsync(h_misc, d_kmax, 24, hipMemcpyDeviceToHost, stream));
   XCHK(hipStreamSynchronize(stream));
@@ -1356,8 +1359,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   last_rec_bytes = rec;
   void* sorted = nullptr;
   if ((rc = tbegin(ts0, SCOTTY_TIME_PUSH_OTHER))) return rc;
-  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_key, n, kb, d_recA, d_recB, d_hist, d_scan32, &sorted, stream, tbase,
-                           tb, true));
+  XCHK(launch_sort_by_slot(rec, d_ts, d_val, d_key, n, kb, d_recA, d_recB, d_hist, d_hist10, d_scan32, &sorted, stream,
+                           tbase, tb, true, sort_digit10));
   // 2. the batch's distinct keys in key order (segment u = [ubeg[u], ubeg[u + 1])) and its largest timestamp
   const int64_t nbs = seg_tiles(n);
   XCHK(launch_seg_count(rec, sorted, n, d_segcnt, (long long*)d_tmaxt, d_need + 3, stream, tbase, tb));

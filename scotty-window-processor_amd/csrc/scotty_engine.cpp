@@ -29,6 +29,7 @@ hipError_t launch_ingest(const IngestArgs& a, int vt, int need, int64_t nblocks,
 void set_ingest_timing_events(hipEvent_t start, hipEvent_t stop);
 int ingest_wgs_per_cu(int vt, int need);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st);
+hipError_t launch_first(const IngestArgs& a, hipStream_t st);
 hipError_t launch_commit(const CommitArgs& a, hipStream_t st);
 hipError_t launch_wm(const WmArgs& a, hipStream_t st);
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1);
@@ -158,12 +159,18 @@ struct scotty_op {
     const void* val;
     int64_t n;
     int64_t seq;
+    int64_t base = 0;  // arrival index of ts[0] (SCOTTY_AGG_FIRST)
   };
   std::vector<Push> pending;
   std::vector<void*> owned;  // (unused since the host ingest arena; kept empty)
   HostIngest* ingest = nullptr;  // host columns -> HBM (pinned slots, copy stream, arena reset per watermark)
   int64_t push_seq = 0;
   uint64_t dropped = 0, processed = 0;
+  // SCOTTY_AGG_FIRST (grid path): per-slice / per-cell arrival index of the first tuple (identity FIRST_NONE)
+  bool first = false;
+  int64_t arrivals = 0;  // tuples pushed so far (WindowManager.currentCount order, dropped ones included)
+  long long* d_sfirst = nullptr;
+  long long* d_cfirst = nullptr;
 
   int ingest_mode = -1;  // tuning knob (scotty_tune), -1 = default variant
   int64_t ingest_blocks = 0;  // tuning knob: target workgroups of the ingest launch (0: one round of resident ones)
@@ -188,6 +195,7 @@ struct scotty_op {
   bool x_ls_off = false;     // exact engine: keyed sessions through the wavefront replay (A/B)
   int32_t x_ls_occ = 3;      // lane-session kernel's waves per SIMD (3 default; 2: A/B, profiles/r05/c4s_pause_edits/)
   bool x_pack_off = false;   // exact engine: keyed replay records always 16 bytes (A/B for the packed 8-byte ones)
+  int x_digit10 = -1;        // exact engine: keyed replay sort digits ("keyed_sort_digit10": -1 auto, 0 8-bit, 1 10-bit)
   bool x_lsdbg = false;      // lane-session path counters (debugging aid)
   int64_t x_qblocks = 0;     // exact engine: quiet-pass ingest workgroups (A/B: 0 default)
   int32_t x_kg_variant = -1;
@@ -303,7 +311,7 @@ int agg_value_type(int kind) {
     case SCOTTY_AGG_SUM_I32: case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MAX_I32: return VT_I32;
     case SCOTTY_AGG_SUM_I64: case SCOTTY_AGG_MIN_I64: case SCOTTY_AGG_MAX_I64: return VT_I64;
     case SCOTTY_AGG_SUM_F64: case SCOTTY_AGG_MIN_F64: case SCOTTY_AGG_MAX_F64: return VT_F64;
-    case SCOTTY_AGG_COUNT: return -1;
+    case SCOTTY_AGG_COUNT: case SCOTTY_AGG_FIRST: return -1;
     default: return -2;
   }
 }
@@ -519,6 +527,10 @@ int compact_if_needed(scotty_op* op) {
     HIPCHK(hipMemcpyAsync(tmp, a + m.head, live * 8, hipMemcpyDeviceToDevice, op->stream));
     HIPCHK(hipMemcpyAsync(a, tmp, live * 8, hipMemcpyDeviceToDevice, op->stream));
   }
+  if (op->d_sfirst) {
+    HIPCHK(hipMemcpyAsync(tmp, op->d_sfirst + m.head, live * 8, hipMemcpyDeviceToDevice, op->stream));
+    HIPCHK(hipMemcpyAsync(op->d_sfirst, tmp, live * 8, hipMemcpyDeviceToDevice, op->stream));
+  }
   int64_t ht[2] = {0, live};
   HIPCHK(hipMemcpyAsync(&op->d_meta->head, ht, 16, hipMemcpyHostToDevice, op->stream));
   const int64_t zero = 0;  // block summaries follow slice indices: all of them are recomputed
@@ -636,10 +648,28 @@ int enqueue_ingest(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_
 }
 
 // Runs the ingest + commit launches of one micro-batch (no host synchronisation).
-int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t seq) {
+int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t n, int64_t seq, int64_t base) {
   int64_t tile = TILE_MIN;
   int rc = enqueue_ingest(op, d_ts, d_val, n, &tile);
   if (rc) return rc;
+  if (op->first) {  // SCOTTY_AGG_FIRST: the cells' first arrival indices (first_kernel), before the commit folds them
+    IngestArgs fa{};
+    fa.ts = d_ts;
+    fa.n = n;
+    fa.s_tstart = op->d_tstart;
+    fa.grid = op->d_grid;
+    fa.meta = op->d_meta;
+    fa.cix = op->d_cix;
+    fa.cix_meta = op->d_cixmeta;
+    fa.c_first = op->d_cfirst;
+    fa.seq_base = base;
+    scotty_op::TEv tf;
+    rc = tbegin(op, tf, SCOTTY_TIME_PUSH_OTHER);
+    if (rc) return rc;
+    HIPCHK(launch_first(fa, op->stream));
+    rc = tend(op, tf);
+    if (rc) return rc;
+  }
   CommitArgs ca{};
   ca.ts = d_ts;
   ca.n = n;
@@ -662,6 +692,8 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
   ca.need = op->need;
   ca.vt = op->vt;
   ca.push_seq = seq;
+  ca.s_first = op->d_sfirst;
+  ca.c_first = op->d_cfirst;
   scotty_op::TEv tc;
   rc = tlaunch(op, tc, SCOTTY_TIME_PUSH_OTHER);
   if (rc) return rc;
@@ -673,6 +705,11 @@ int enqueue_push(scotty_op* op, const int64_t* d_ts, const void* d_val, int64_t 
 
 // First tuple of the operator's life: StreamSlicer + SliceManager for tuple 0 (the store is empty).
 int start_stream(scotty_op* op, int64_t ts0) {
+  if (op->first && !op->d_sfirst) {  // SCOTTY_AGG_FIRST arrays (aggregations are fixed by the first push)
+    HIPCHK(dev_malloc(&op->d_sfirst, op->scap * 8));
+    HIPCHK(dev_malloc(&op->d_cfirst, op->ccap * 8));
+    HIPCHK(launch_fill_u64((unsigned long long*)op->d_cfirst, op->ccap, (unsigned long long)FIRST_NONE, op->stream));
+  }
   std::vector<int64_t> edges;
   int64_t n_pending = JMIN;
   if (op->has_fixed && !first_walk(op, ts0, edges, n_pending))
@@ -689,6 +726,7 @@ int start_stream(scotty_op* op, int64_t ts0) {
   HIPCHK(hipMemcpyAsync(op->d_spart[0], zeros.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
   HIPCHK(hipMemcpyAsync(op->d_spart[1], idmin.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
   HIPCHK(hipMemcpyAsync(op->d_spart[2], idmax.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
+  if (op->d_sfirst) HIPCHK(hipMemcpyAsync(op->d_sfirst, idmin.data(), s0 * 8, hipMemcpyHostToDevice, op->stream));
   DevMeta m{};
   m.head = 0;
   m.tail = s0;
@@ -746,7 +784,7 @@ int replay_after_overflow(scotty_op* op) {
     if (rc) return rc;
     for (auto& p : op->pending)
       if (p.seq >= failed) {
-        rc = enqueue_push(op, p.ts, p.val, p.n, p.seq);
+        rc = enqueue_push(op, p.ts, p.val, p.n, p.seq, p.base);
         if (rc) return rc;
       }
     rc = sync_snapshot(op);
@@ -836,7 +874,7 @@ void scotty_destroy(scotty_op* op) {
   (void)hipSetDevice(op->device);
   if (op->stream) (void)hipStreamSynchronize(op->stream);
   auto F = [](void* p) { if (p) (void)hipFree(p); };
-  F(op->d_meta); F(op->d_tstart); F(op->d_tlast); F(op->d_scnt); F(op->d_grid);
+  F(op->d_meta); F(op->d_tstart); F(op->d_tlast); F(op->d_scnt); F(op->d_grid); F(op->d_sfirst); F(op->d_cfirst);
   F(op->d_ccnt); F(op->d_ctmax); F(op->d_tilemax); F(op->d_pmax); F(op->d_rank); F(op->d_flag);
   F(op->d_scratch); F(op->d_bcnt); F(op->d_pcnt); F(op->d_psum); F(op->d_stmin); F(op->d_stmax); F(op->d_wdef);
   F(op->d_out);
@@ -936,6 +974,7 @@ int scotty_add_aggregation(scotty_op* op, int kind_flags) {
   op->aggs.push_back(kind);
   op->agg_inv.push_back(inv ? 1 : 0);
   op->need |= agg_need(kind);
+  if (kind == SCOTTY_AGG_FIRST) op->first = true;
   return (int)op->aggs.size() - 1;
 }
 
@@ -963,6 +1002,11 @@ static int decide_mode(scotty_op* op) {
   if (!exact) {
     op->mode = 1;
     return SCOTTY_OK;
+  }
+  if (op->first) {
+    op->failed = true;
+    return fail(op, SCOTTY_ERR_UNSUPPORTED, "SCOTTY_AGG_FIRST runs on the grid path only (non-keyed operators with "
+                                            "context-free time windows)");
   }
   // count path: context-free windows only, at least one of them on the count measure (time windows' edges come
   // from the in-order stream's timestamps, CEngine::time_edges)
@@ -1000,6 +1044,7 @@ static int decide_mode(scotty_op* op) {
   op->x->lane_session_off = op->x_ls_off;
   op->x->lane_session_occ = op->x_ls_occ;
   op->x->pack_off = op->x_pack_off;
+  op->x->sort_digit10 = op->x_digit10;
   op->x->lsdbg_on = op->x_lsdbg;
   op->x->timing = op->timing;  // scotty_enable_timing before the first push (the natural order) reaches the engine
   std::string e;
@@ -1062,8 +1107,10 @@ static int push_impl(scotty_op* op, const int64_t* d_ts, const void* d_val, int6
     if (rc) return rc;
   }
   const int64_t seq = op->push_seq++;
-  op->pending.push_back({d_ts, d_val, n, seq});
-  return enqueue_push(op, d_ts, d_val, n, seq);
+  const int64_t base = op->arrivals;
+  op->arrivals += n;
+  op->pending.push_back({d_ts, d_val, n, seq, base});
+  return enqueue_push(op, d_ts, d_val, n, seq, base);
 }
 
 static size_t value_bytes(const scotty_op* op) { return op->vt == VT_I32 ? 4 : 8; }
@@ -1247,6 +1294,7 @@ int scotty_shard_push(scotty_op* op, const int64_t* d_ts, const void* d_val, siz
     return fail(op, SCOTTY_ERR_ARG, "count windows: use scotty_shard_push_counted (the chunk's count offset)");
   if (op->mode != 1)
     return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs context-free time windows or count windows only");
+  if (op->first) return fail(op, SCOTTY_ERR_UNSUPPORTED, "SCOTTY_AGG_FIRST operators are not sharded");
   if (!op->has_fixed) return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharding needs at least one context-free window");
   if (!op->d_shrank) {
     HIPCHK(dev_malloc(&op->d_shrank, op->shard_kg * 4));
@@ -1388,6 +1436,7 @@ int scotty_process_watermark(scotty_op* op, int64_t wm, scotty_windows* out) {
     wa.n_aggs = (int32_t)op->aggs.size();
     for (size_t k = 0; k < op->aggs.size(); k++) wa.agg_kind[k] = op->aggs[k];
     wa.need = op->need;
+    wa.s_first = op->d_sfirst;
     wa.vt = op->vt;
     for (int attempt = 0; attempt < 2; attempt++) {
       // triggers + window assembly + GC (window_kernels.hip), then ONE transfer of the packed result
@@ -1499,6 +1548,25 @@ int64_t scotty_slice_count(scotty_op* op) {
   return op->h_snap->tail - op->h_snap->head;
 }
 
+int64_t scotty_first_indices(scotty_op* op, int64_t* out, size_t cap) {
+  if (!op || (cap && !out)) return SCOTTY_ERR_ARG;
+  if (!op->first) return fail(op, SCOTTY_ERR_ARG, "no SCOTTY_AGG_FIRST aggregation registered");
+  if (!op->started) return 0;
+  if (sync_snapshot(op)) return SCOTTY_ERR_HIP;
+  const DevMeta& m = *op->h_snap;
+  const int64_t live = m.tail - m.head;
+  if (live <= 0) return 0;
+  std::vector<int64_t> v((size_t)live);
+  HIPCHK(hipMemcpy(v.data(), op->d_sfirst + m.head, (size_t)live * 8, hipMemcpyDeviceToHost));
+  std::vector<int64_t> f;
+  for (int64_t x : v)
+    if (x != FIRST_NONE) f.push_back(x);
+  std::sort(f.begin(), f.end());
+  f.erase(std::unique(f.begin(), f.end()), f.end());
+  for (size_t i = 0; i < f.size() && i < cap; i++) out[i] = f[i];
+  return (int64_t)f.size();
+}
+
 int scotty_enable_timing(scotty_op* op, int on) {
   if (!op) return SCOTTY_ERR_ARG;
   op->timing = on != 0;
@@ -1596,6 +1664,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
       op->x->lane_session_off = op->x_ls_off;
       op->x->lane_session_occ = op->x_ls_occ;
     }
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "keyed_sort_digit10") == 0) {  // keyed replay sort: 10-bit digits for 17-20-bit keys (A/B)
+    if (value < -1 || value > 1) return fail(op, SCOTTY_ERR_ARG, "keyed_sort_digit10 is -1, 0 or 1");
+    op->x_digit10 = (int)value;
+    if (op->x) op->x->sort_digit10 = op->x_digit10;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_pack_records") == 0) {  // 1 (default): the lane-session replay sorts packed 8-byte

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <limits>
 #include <type_traits>
@@ -229,6 +230,48 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
       for (int64_t k = l_k0[i] + threadIdx.x; k < l_k1[i]; k += blockDim.x) a.cix[k] = cc;
     }
     if (__syncthreads_or(done)) break;
+  }
+}
+
+// SCOTTY_AGG_FIRST: per cell, the arrival index of the first tuple the cell receives.  A slice's FIRST partial is
+// the first tuple added to it -- AggregateValueState.addElement lifts the first element and then combines
+// (S/state/AggregateValueState.java:23-31) with a combine that keeps partialAggregate1's fields
+// (B/flinkBenchmark/aggregations/SumAggregation.java:16-18) -- and tuples reach a slice in arrival order, so it is the
+// minimum arrival index over the slice's tuples.  One extra 8-byte-per-tuple pass over the timestamps, launched
+// between the ingest and the commit of operators that register FIRST (the ingest kernel is not widened for it): each
+// wave streams a contiguous arrival range, finds each tuple's cell as the ingest does (cell index), and only the first
+// lane of a run of lanes in one cell -- the lowest index of the run -- offers it with an atomicMin after a plain read
+// shows it is lower (in-order streams: about one atomic per cell).  Late tuples (below the first cell) and tuples past
+// the grid horizon are the ingest's drop / replay cases and are skipped here likewise.
+__global__ __launch_bounds__(256) void first_kernel(IngestArgs a) {
+  const DevMeta& m = *a.meta;
+  if (m.overflow != 0) return;
+  const int64_t head = m.head, tail = m.tail, j0 = m.j0, gcount = m.gcount;
+  int64_t kc = gcount > 0 ? gcount - j0 - 1 : 0;
+  if (kc < 0) kc = 0;
+  const int64_t h_end = gcount > 0 ? a.grid[j0 + kc] : INT64_MAX;
+  const CellView cv = make_view(a, m, head, tail, j0, kc, h_end);
+  const int64_t ctot = cv.c_old + kc;
+  if (ctot <= 0) return;
+  const int64_t first_start = cv.start(0);
+  const CellIndex cx{a.cix, a.cix_meta[0], a.cix_meta[2], ctot, a.cix_meta[3], a.cix_meta[4], (int)a.cix_meta[1]};
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t per = (((a.n + nw - 1) / nw) + 63) & ~(int64_t)63;
+  const int64_t w0 = wave * per, w1 = min(a.n, w0 + per);
+  for (int64_t b = w0; b < w1; b += 64) {
+    const int64_t i = b + lane;
+    int64_t c = -1;
+    if (i < w1) {
+      const int64_t t = a.ts[i];
+      if (t >= first_start && (t < h_end || h_end == INT64_MAX)) c = cx.find(cv, t);
+    }
+    const int64_t cp = (int64_t)__shfl_up((long long)c, 1);
+    if (c >= 0 && (lane == 0 || cp != c)) {
+      const long long idx = (long long)(a.seq_base + i);
+      if (a.c_first[c] > idx) atomicMin(&a.c_first[c], idx);
+    }
   }
 }
 
@@ -1136,6 +1179,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
           a.s_part[0][sl] = 0;
           a.s_part[1][sl] = (unsigned long long)PART_ID_MIN;
           a.s_part[2][sl] = (unsigned long long)PART_ID_MAX;
+          if (a.s_first) a.s_first[sl] = FIRST_NONE;
         }
       }
       base_cnt += tot;
@@ -1171,6 +1215,10 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
       }
       if (a.need & NEED_MIN) atomicMin((long long*)&a.s_part[1][s], (long long)a.c_part[1][c]);
       if (a.need & NEED_MAX) atomicMax((long long*)&a.s_part[2][s], (long long)a.c_part[2][c]);
+      if (a.s_first) {  // FIRST: the slice's first tuple is the earliest of its cells' first tuples
+        atomicMin(&a.s_first[s], a.c_first[c]);
+        a.c_first[c] = FIRST_NONE;
+      }
       a.c_cnt[c] = 0;
       a.c_tmax[c] = INT64_MIN;
       a.c_part[0][c] = 0;
@@ -1182,6 +1230,7 @@ __global__ __launch_bounds__(1024) void commit_kernel(CommitArgs a) {
     const int64_t ncell = c_old + kc;
     for (int64_t c = tid; c < ncell; c += 1024) {
       if (a.c_cnt[c] == 0) continue;
+      if (a.c_first) a.c_first[c] = FIRST_NONE;
       a.c_cnt[c] = 0;
       a.c_tmax[c] = INT64_MIN;
       a.c_part[0][c] = 0;
@@ -1607,6 +1656,12 @@ hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st, hipEvent_t e0, 
   return hipGetLastError();
 }
 hipError_t launch_cix_build(const IngestArgs& a, hipStream_t st) { return launch_cix_build(a, st, nullptr, nullptr); }
+
+hipError_t launch_first(const IngestArgs& a, hipStream_t st) {
+  const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((a.n + 4095) / 4096, 4096));
+  hipLaunchKernelGGL(first_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
 // mode: -1 the default (MM_MODE / DEFAULT_MODE); INGEST_STREAMING (an in-order stream: the default loop on fewer
 // workgroups); for A/B (scotty_tune "ingest_mode" / the exact engine's "quiet_ingest_mode"): 7 the pipelined loop

@@ -317,8 +317,10 @@ __device__ __forceinline__ double key_to_f64(int64_t k) {  // inverse of the ord
 }
 
 // lowered value of one aggregation kind (AggregateValueState.getValue -> lower, S/state/AggregateValueState.java:75-79)
-__device__ __forceinline__ int64_t lower_value(int kind, uint64_t cnt, uint64_t sw, int64_t mn, int64_t mx) {
+__device__ __forceinline__ int64_t lower_value(int kind, uint64_t cnt, uint64_t sw, int64_t mn, int64_t mx,
+                                               int64_t first) {
   switch (kind) {
+    case SCOTTY_AGG_FIRST: return first;
     case SCOTTY_AGG_SUM_I32: return (int64_t)(int32_t)(uint32_t)sw;
     case SCOTTY_AGG_COUNT: return (int64_t)(int32_t)(uint32_t)cnt;
     case SCOTTY_AGG_MIN_I32: case SCOTTY_AGG_MIN_I64: return mn;
@@ -405,9 +407,34 @@ __global__ __launch_bounds__(256) void wm_windows_kernel(WmArgs a) {
   if (need_max) mx = wmax64(mx);
   if (f64 && need_sum) sw = (uint64_t)__double_as_longlong(sf);
   const bool has = cnt != 0;
+  // SCOTTY_AGG_FIRST: AggregateValueState.merge clones the first non-empty partial and folds the rest into it with a
+  // combine that keeps partialAggregate1 (S/state/AggregateValueState.java:55-69), so the window's value is the FIRST
+  // partial of the first non-empty slice in [sa, sb), slice order: 64 slices per probe, whole empty blocks skipped
+  // with their summaries (64 blocks per probe)
+  int64_t first = 0;
+  if (a.s_first && has) {
+    int64_t s0 = sa, found = -1;
+    while (s0 < sb && found < 0) {
+      if (s0 % SBLK == 0 && s0 + SBLK <= sb) {
+        const int64_t bl = sb / SBLK;  // blocks [s0 / SBLK, bl) lie wholly inside the range
+        const int64_t b = s0 / SBLK + lane;
+        const unsigned long long nb = __ballot(b < bl && a.b_cnt[b] != 0);
+        if (nb == 0) {
+          s0 = min(bl, s0 / SBLK + 64) * SBLK;
+          continue;
+        }
+        s0 = (s0 / SBLK + __ffsll((long long)nb) - 1) * SBLK;
+      }
+      const int64_t s1 = min(sb, (s0 / SBLK + 1) * SBLK);  // to the next block boundary
+      const unsigned long long ns = __ballot(s0 + lane < s1 && a.s_cnt[s0 + lane] != 0);
+      if (ns) found = s0 + __ffsll((long long)ns) - 1;
+      s0 = s1;
+    }
+    if (found >= 0) first = (int64_t)a.s_first[found];
+  }
   unsigned char* const o = a.hout ? a.hout : a.out;  // values and flags are read by the host only
   if (lane < a.n_aggs) {
-    const int64_t v = has ? lower_value(a.agg_kind[lane], cnt, sw, mn, mx) : 0;
+    const int64_t v = has ? lower_value(a.agg_kind[lane], cnt, sw, mn, mx, first) : 0;
     ((int64_t*)(o + L.vals))[(int64_t)lane * a.n_windows + wi] = v;
   }
   if (lane == 0) o[L.has + wi] = has ? 1 : 0;

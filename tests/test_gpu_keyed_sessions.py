@@ -225,3 +225,54 @@ def test_packed_replay_records_equal_16_byte_records(seed):
     assert total > 0 or errors > 0
     if nkeys <= 5000:
         assert 8 in layouts
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ten_bit_digit_sort_equals_eight_bit_sort(seed):
+    """The keyed replay's stable sort by key (keyed_kernels.hip): 17-20-bit keys take two 10-bit digit passes by default
+    (VERDICT r05 item 3), scotty_tune "keyed_sort_digit10" 0 keeps three 8-bit ones.  A stable sort has one result, so
+    every watermark's rows and the dropped counts must be identical; session and count windows (lane-session kernel,
+    wavefront replay), packed 8-byte and 16-byte records, key ranges from 2^16 + 1 to 2^20."""
+    from specs import Tumbling, Count
+    pkg = product()
+    rng = np.random.default_rng(8800 + seed)
+    nkeys = [(1 << 16) + 7, 1 << 18, 1 << 20, 700_001, 1 << 17, (1 << 20) - 3][seed]
+    wins = [Session(Time, int(rng.integers(50, 500))), Sliding(Time, 2000, 250)] if seed % 2 == 0 else \
+        [Tumbling(Count, int(rng.integers(3, 30))), Sliding(Time, 1500, 300)]
+    n = 600_000
+    ts, vals = pkg.workloads.stream(n, [20, 200][seed % 2], t0=int(rng.integers(0, 3000)), ooo_frac=0.2,
+                                    max_delay=400, seed=seed, value_type="i32")
+    keys = rng.integers(0, nkeys, size=n).astype(np.uint32)
+
+    def make(d10, pack):
+        op = pkg.KeyedSlicingWindowOperator(device=0)
+        op.tune("keyed_sort_digit10", d10)
+        op.tune("keyed_pack_records", pack)
+        for x in (SUM, COUNT, MIN, MAX):
+            op.addWindowFunction(x)
+        op.setMaxLateness(1000)
+        for w in wins:
+            op.addWindowAssigner(w)
+        return op
+    pack = seed % 3 != 2
+    a, b = make(1, pack), make(0, pack)
+    from helpers import interval_schedule, same_keyed_arrays
+    total = 0
+    for step in interval_schedule(ts, 6, lag=300, pushes_per_interval=2):
+        if step[0] == "push":
+            lo, hi = step[1], step[2]
+            if hi > lo:
+                a.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+                b.processElements(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        else:
+            try:
+                exp = b.processWatermarkArrays(step[1])
+            except pkg.ScottyError as e:
+                with pytest.raises(pkg.ScottyError) as ei:
+                    a.processWatermarkArrays(step[1])
+                assert ei.value.code == e.code
+                continue
+            total += same_keyed_arrays(a.processWatermarkArrays(step[1]), exp)
+            assert a.droppedCount() == b.droppedCount()
+    assert a.keyCount() == b.keyCount()
+    assert total > 0

@@ -37,6 +37,7 @@ NATIVES = {
     "processElements0": (i32, [i64, P, P, i64]),
     "processKeyedElements0": (i32, [i64, P, P, P, i64]),
     "processWatermark0": (i32, [i64, i64, P]),
+    "firstIndices0": (P, [i64]),
 }
 M_LONGS, M_INTS, M_BYTES, M_OBJS, M_STRING = 5, 6, 7, 8, 2
 
@@ -287,4 +288,92 @@ def test_jni_keyed_engine_matches_per_key_oracles():
         t += 1000
     assert total > nkeys
     jni("destroy0", eng.op)
+    mock().mock_reset()
+
+
+class JniFirstShim(JniOp):
+    """The stand-alone shim with a first-partial function (java/main/.../SlicingWindowOperator.java, NativeFunctions
+    TUPLE2_F1 / TUPLE4_F1): the hidden SCOTTY_AGG_FIRST column after the function's, the payloads of this interval's
+    tuples plus the retained slices' first tuples (firstIndices0 after every watermark), and each window's result
+    rebuilt from the payload of its first partial's tuple."""
+
+    def __init__(self, cfg, payload):
+        super().__init__(dict(cfg, aggs=list(cfg["aggs"]) + [10]))
+        self.payload = payload          # arrival index -> the tuple's other fields (the Java objects)
+        self.arrivals = self.base = 0
+        self.retained = {}
+
+    def processElements(self, ts, vals):
+        super().processElements(ts, vals)
+        self.arrivals += len(ts)
+
+    def fields(self, i):
+        if i >= self.base:
+            assert i < self.arrivals, (i, self.arrivals)
+            return self.payload(i)
+        assert i in self.retained, ("first tuple %d was pruned" % i)
+        return self.retained[i]
+
+    def processWatermark(self, wm):
+        rows = super().processWatermark(wm)
+        out = []
+        for w in rows:
+            if w.hasValue():
+                v = w.getAggValues()
+                out.append((w.getStart(), w.getEnd(), v[:-1], self.fields(v[-1])))
+            else:
+                out.append((w.getStart(), w.getEnd(), [], None))
+        L = mock()
+        arr = jni("firstIndices0", self.op)
+        assert arr, "firstIndices0 returned null"
+        keep = _array(L, arr, np.int64)
+        self.retained = {int(i): self.fields(int(i)) for i in keep}
+        self.base = self.arrivals
+        return out
+
+
+def _first_rows(ora_rows, payload):
+    return [(w.getStart(), w.getEnd(), w.getAggValues()[:-1] if w.hasValue() else [],
+             payload(w.getAggValues()[-1]) if w.hasValue() else None) for w in ora_rows]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["benchmark_tuple4_c1", "flink_demo_tuple2_varying_f0"])
+def test_jni_first_partial_rebuild_matches_oracle(case):
+    """the reference benchmark's SumAggregation (Tuple4 f0 / f2 / f3 of the first partial) on the C1
+    stream, and the Flink demo's SumWindowFunction (Tuple2 f0) under GlobalScottyWindowOperator with f0 varying from
+    tuple to tuple and 20 % late tuples: every window's rebuilt result equals the one the oracle's first-partial index
+    selects, and every needed payload was still held (retained firsts + this interval's tuples)."""
+    from oracle.oracle import OracleOperator, AGG_FIRST
+    rng = np.random.default_rng(606)
+    if case == "benchmark_tuple4_c1":
+        cfg = dict(windows=[Sliding(Time, 60_000, 1000)], aggs=[SUM], lateness=1)
+        rate, secs = 20, 75
+        ts = np.arange(secs * 1000 * rate, dtype=np.int64) // rate
+        vals = product().workloads.JavaRandomInts(43).next_ints(len(ts))
+        f2 = rng.integers(-2**63, 2**63 - 1, len(ts), dtype=np.int64)  # LoadGeneratorSource: nextLong, currentTimeMillis
+        payload = lambda i: ("key", int(f2[i]), int(ts[i]) + 1_700_000_000_000)  # noqa: E731
+        cuts = [(s * 1000 * rate, (s + 1) * 1000 * rate, s * 1000 + 999) for s in range(secs)]
+    else:
+        cfg = dict(windows=[Tumbling(Time, 700), Sliding(Time, 2000, 300)], aggs=[SUM], lateness=1000)
+        ts, vals = _stream(150_000, seed=9, ooo=0.2, delay=400, rate=20)
+        f0 = rng.integers(0, 1000, len(ts))
+        payload = lambda i: (int(f0[i]),)  # noqa: E731
+        cuts = [(lo, lo + 15_000, int(ts[:lo + 15_000].max()) - 400) for lo in range(0, len(ts), 15_000)]
+    shim = JniFirstShim(cfg, payload)
+    ora = OracleOperator()
+    for a in cfg["aggs"] + [AGG_FIRST]:
+        ora.addWindowFunction(a)
+    ora.setMaxLateness(cfg["lateness"])
+    for w in cfg["windows"]:
+        ora.addWindowAssigner(w)
+    total = 0
+    for lo, hi, wm in cuts:
+        shim.processElements(ts[lo:hi], vals[lo:hi])
+        ora.processElements(ts[lo:hi], vals[lo:hi])
+        got, exp = shim.processWatermark(wm), _first_rows(ora.processWatermark(wm), payload)
+        assert got == exp
+        total += sum(1 for r in exp if r[3] is not None)
+    assert total > 10
+    shim.close()
     mock().mock_reset()
