@@ -457,6 +457,8 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61, tune=None):
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     times, rows, verdicts, rounds = [], 0, [], []
     for s in range(warm + 2 * steps):
+        if s % 10 == 0:
+            log("c3: step %d" % s)
         if s == warm + steps:
             op.enableTiming(True)  # instrumented steps: after the wall-clock ones
         t_begin = s * 1000 + 1000 + (s // 10) * 2000
@@ -776,6 +778,8 @@ def extra_c4(pkg, dev, batch, keys, steps, lane=True, rank=0, world=1, dist=None
     own = torch.from_numpy(own.astype(np.int32)).to(dev)
     times, rows, elapsed = [], 0, 0.0
     for s in range(warm + 2 * steps):
+        if s % 10 == 0:
+            log("c4: step %d" % s)
         if s == warm + steps:
             op.enableTiming(True)  # instrumented steps (HIP events per launch class) after the wall-clock ones
         k = own[torch.randint(0, len(own), (batch,), device=dev, dtype=torch.int64, generator=g)]
@@ -856,6 +860,8 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     times, rows = [], 0
     for s in range(warm + 2 * steps):
+        if s % 5 == 0:
+            log("keyed leg: step %d" % s)
         if s == warm + steps:
             op.enableTiming(True)
         t_begin = s * 1000 + 1000 + (s // 10) * 2000
@@ -937,6 +943,8 @@ def extra_c4c(pkg, dev, batch, keys, steps=10, warm=11):
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     times, rows, count_rows = [], 0, 0
     for s in range(warm + 2 * steps):
+        if s % 5 == 0:
+            log("keyed leg: step %d" % s)
         if s == warm + steps:
             op.enableTiming(True)
         t_begin = s * 1000 + 1000

@@ -669,8 +669,7 @@ bool CEngine::trigger_segs(int64_t last_c, int64_t cur_c, int64_t last_t, int64_
 
 int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   r.n = 0;
-  r.start.clear(); r.end.clear(); r.meas.clear(); r.has.clear(); r.key.clear();
-  r.vals.assign(aggs.size(), {});
+  r.clear_cols(aggs.size());
   if (failed) return SCOTTY_ERR_STATE;
   // WindowManager.processWatermark (S/WindowManager.java:41-80)
   if (last_wm == -1) last_wm = std::max<int64_t>(0, jsub(wm, max_lateness));
@@ -827,12 +826,12 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
       CCHK(hipMemcpyAsync(r.end.data(), d_wend, nw * 8, hipMemcpyDeviceToHost, stream));
       CCHK(hipMemcpyAsync(r.meas.data(), d_meas, nw * 4, hipMemcpyDeviceToHost, stream));
     } else {
-      r.start = h_start;
-      r.end = h_end;
-      r.meas = h_meas;
+      r.start.assign(h_start.begin(), h_start.end());
+      r.end.assign(h_end.begin(), h_end.end());
+      r.meas.assign(h_meas.begin(), h_meas.end());
     }
     r.has.resize(nw);
-    r.vals.assign(aggs.size(), std::vector<int64_t>(nw));
+    for (size_t k = 0; k < aggs.size(); k++) r.vals[k].resize(nw);
     CCHK(hipMemcpyAsync(r.has.data(), d_has, nw, hipMemcpyDeviceToHost, stream));
     for (size_t k = 0; k < aggs.size(); k++)
       CCHK(hipMemcpyAsync(r.vals[k].data(), d_vals[k], nw * 8, hipMemcpyDeviceToHost, stream));

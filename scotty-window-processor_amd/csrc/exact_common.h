@@ -256,6 +256,7 @@ struct XBlocks {
 };
 
 struct XWmArgs {
+  unsigned long long* zero4;  // single mode: the 4 control words the emit kernel zeroes first (no host memset launch)
   const XCfg* cfg;
   XState* st;
   XSlices sl;

@@ -1485,8 +1485,7 @@ int XEngine::ensure_rows(int64_t rows) {
 int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   r.n = 0;
   r.dropped = 0;
-  r.start.clear(); r.end.clear(); r.meas.clear(); r.has.clear(); r.key.clear();
-  r.vals.assign(cfg.n_aggs, {});
+  r.clear_cols(cfg.n_aggs);
   if (n_ops == 0) return SCOTTY_OK;
   if (wcap < n_ops) {
     XCHK(hipStreamSynchronize(stream));
@@ -1581,7 +1580,7 @@ int XEngine::watermark(int64_t wm, XResult& r, bool to_host) {
     TEv tw;
     int rct = tbegin(tw, SCOTTY_TIME_WATERMARK);
     if (rct) return rct;
-    XCHK(hipMemsetAsync(d_misc, 0, 4 * 8, stream));
+    a.zero4 = (unsigned long long*)d_misc;  // zeroed by the emit kernel (n_ops == 1: one wave) instead of a memset
     XCHK(launch_wm_emit(a, stream));
     if (a.blk.cnt) XCHK(launch_wm_blocks(a, stream));
     XCHK(launch_wm_agg(a, stream, 64));
@@ -1735,7 +1734,8 @@ int XEngine::finish_rows(int64_t rows, XResult& r, bool to_host, bool check) {
   if (rct) return rct;
   if (to_host && rows > 0) {
     r.start.resize(rows); r.end.resize(rows); r.meas.resize(rows); r.has.resize(rows); r.key.resize(rows);
-    r.vals.assign(cfg.n_aggs, std::vector<int64_t>(rows));
+    if ((int)r.vals.size() < cfg.n_aggs) r.vals.resize(cfg.n_aggs);
+    for (int k = 0; k < cfg.n_aggs; k++) r.vals[k].resize(rows);
     XCHK(hipMemcpyAsync(r.start.data(), d_w_start, rows * 8, hipMemcpyDeviceToHost, stream));
     XCHK(hipMemcpyAsync(r.end.data(), d_w_end, rows * 8, hipMemcpyDeviceToHost, stream));
     XCHK(hipMemcpyAsync(r.meas.data(), d_w_meas, rows * 4, hipMemcpyDeviceToHost, stream));

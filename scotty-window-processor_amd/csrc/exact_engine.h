@@ -2,7 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/scotty_mi355x.h"
@@ -16,6 +18,33 @@ struct XWinDef {  // one Window of WindowOperator.addWindowAssigner, in registra
   int64_t a, b;
 };
 
+// Host result columns in pinned memory (the D2H copies run at DMA speed instead of being staged through pageable
+// bounce buffers) that keep their capacity across watermarks and grow without zero-filling: a keyed watermark returns
+// up to millions of rows (C4: 2^20 windows, ~33 MB per watermark).
+template <class T>
+struct PinnedAlloc {
+  using value_type = T;
+  PinnedAlloc() = default;
+  template <class U>
+  PinnedAlloc(const PinnedAlloc<U>&) {}
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+    return (T*)p;
+  }
+  void deallocate(T* p, size_t) { (void)hipHostFree(p); }
+  template <class U>
+  void construct(U* p) noexcept { ::new ((void*)p) U; }  // resize() leaves new elements uninitialised
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+  template <class U>
+  bool operator==(const PinnedAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+template <class T>
+using pinned_vec = std::vector<T, PinnedAlloc<T>>;
+
 struct XResult {
   int64_t n = 0;
   uint64_t dropped = 0;   // cumulative tuples dropped (reference: exception per tuple)
@@ -26,11 +55,17 @@ struct XResult {
   const uint8_t* d_has = nullptr;
   const int64_t* d_vals[SCOTTY_MAX_AGGS] = {};
   // host copies (when requested)
-  std::vector<int64_t> start, end;
-  std::vector<int32_t> meas;
-  std::vector<uint32_t> key;
-  std::vector<uint8_t> has;
-  std::vector<std::vector<int64_t>> vals;
+  pinned_vec<int64_t> start, end;
+  pinned_vec<int32_t> meas;
+  pinned_vec<uint32_t> key;
+  pinned_vec<uint8_t> has;
+  std::vector<pinned_vec<int64_t>> vals;
+  // empty columns that keep their capacity (clear() frees nothing)
+  void clear_cols(size_t n_aggs) {
+    start.clear(); end.clear(); meas.clear(); has.clear(); key.clear();
+    if (vals.size() < n_aggs) vals.resize(n_aggs);
+    for (auto& v : vals) v.clear();
+  }
 };
 
 class XEngine {

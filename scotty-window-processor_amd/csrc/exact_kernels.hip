@@ -413,6 +413,12 @@ __global__ __launch_bounds__(256) void wm_emit_kernel(XWmArgs a) {
   o.s = a.st[op];
   const XCfg* cfg = a.cfg;
   if (a.single && lane == 0) {  // the count pass's accounting (single mode has none)
+    if (a.zero4) {  // the control words (flags, dropped, op error, row count) start at 0: the one wave of op 0 writes them
+      a.zero4[0] = 0;
+      a.zero4[1] = 0;
+      a.zero4[2] = 0;
+      a.zero4[3] = 0;
+    }
     if (o.s.dropped) atomicAdd(a.dropped_total, (unsigned long long)o.s.dropped);
     if (o.s.err) atomicOr(a.op_err, 1 << o.s.err);
   }

@@ -13,13 +13,14 @@ not the scattered-run shape uses the coalesced-store factor.
 import collections
 import csv
 import glob
+import gzip
 import json
 import os
 import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "profiles", "traffic.json")
+OUT = os.environ.get("TRAFFIC_OUT", os.path.join(ROOT, "profiles", "traffic.json"))
 
 # kernel (normalised rocprof name prefix) -> (read calibration kernel, write calibration kernel)
 PATTERN = {
@@ -43,11 +44,12 @@ def per_kernel(d, counter):
     """{normalised kernel name: [kB per dispatch]} from a rocprofv3 counter-collection directory."""
     vals = collections.defaultdict(float)
     names = {}
-    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv*"), recursive=True)
     if not files:
         raise SystemExit("no counter_collection.csv under " + d)
     for f in files:
-        for r in csv.DictReader(open(f)):
+        fh = gzip.open(f, "rt") if f.endswith(".gz") else open(f)
+        for r in csv.DictReader(fh):
             if r["Counter_Name"] != counter:
                 continue
             key = (f, r["Dispatch_Id"])
@@ -113,8 +115,33 @@ def leg(name, batch, fdir, wdir, kernels):
     print(json.dumps(t["legs"][name], indent=1))
 
 
+def all_legs(root):
+    """Every leg profiled by tools/gpu_r06_prof.sh under root: the kernel names and batch from the bench line of the
+    leg's own FETCH_SIZE run (its roofline block), then leg()."""
+    calib(os.path.join(root, "calib_f"), os.path.join(root, "calib_w"))
+    for f in sorted(glob.glob(os.path.join(root, "pmc_*_FETCH_SIZE.json"))):
+        name = os.path.basename(f)[len("pmc_"):-len("_FETCH_SIZE.json")]
+        try:
+            d = json.loads(open(f).read().strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            print("%s: no bench line" % name)
+            continue
+        roof = d["roofline"] if name == "c2" else (d.get("extra", {}).get(name) or {}).get("roofline")
+        if not roof:
+            continue
+        kernels = roof.get("kernels") or [roof["kernel"]]
+        batch = int(roof["algorithmic_bytes_per_launch"]) // (16 if name.startswith("c4") else 12)
+        try:
+            leg(name, batch, os.path.join(root, "pmc_%s_FETCH_SIZE" % name), os.path.join(root, "pmc_%s_WRITE_SIZE" % name),
+                kernels)
+        except (SystemExit, KeyError) as e:
+            print("%s: %s" % (name, e))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "calib":
         calib(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "all":
+        all_legs(sys.argv[2])
     else:
         leg(sys.argv[2], int(sys.argv[3]), sys.argv[4], sys.argv[5], sys.argv[6:])
