@@ -44,6 +44,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+TUNE = {}  # --tune: scotty_tune knobs for the C2 / C1 / C2s / C3 operators (A/B runs)
+
+
+def apply_tune(op):
+    for k, v in TUNE.items():
+        op.tune(k, v)
+
+
 def device_roofline(op, steps, batch, bytes_per_tuple, kernel):
     """Roofline of the dominant kernel (ingest) and of the whole step (every timed launch/transfer class)."""
     t = op.deviceTiming()
@@ -59,7 +67,7 @@ def device_roofline(op, steps, batch, bytes_per_tuple, kernel):
             "device_ms_per_step_by_class": {k: v[0] / max(1, steps) for k, v in t.items()}}
 
 
-KN_INGEST, KN_KG_HIST, KN_KG_SCATTER, KN_KG_BUCKET, KN_COUNT_INGEST = range(5)  # device_common.h KN_*
+KN_INGEST, KN_KG_HIST, KN_KG_SCATTER, KN_KG_BUCKET, KN_COUNT_INGEST, KN_LANE_SESSION, KN_REPLAY = range(7)  # device_common.h
 
 
 def kernel_name(pkg, which):
@@ -72,7 +80,7 @@ def kernel_name(pkg, which):
 def norm_kernel(name):
     """A kernel name as rocprofv3 prints it, without namespaces, arguments or spaces (for matching)."""
     name = name.split("(")[0].replace("void ", "")
-    for ns in ("scotty::", "kg::", "ck::", "k::", "ln::", "x::", "wk::"):
+    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "ln::", "k::", "x::"):
         name = name.replace(ns, "")
     return name.replace(" ", "")
 
@@ -382,6 +390,7 @@ def extra_c1(pkg, dev, batch, steps, warm=2):
     rate = max(1, batch // 1000)
     jr = pkg.workloads.JavaRandomInts(43)
     op = pkg.SlicingWindowOperator(device=dev.index)
+    apply_tune(op)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.setMaxLateness(1)
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 60_000, 1_000))
@@ -449,6 +458,7 @@ def extra_c3(pkg, dev, batch, steps=10, warm=61, tune=None):
     op = pkg.SlicingWindowOperator(device=dev.index)
     for k, v in (tune or {}).items():
         op.tune(k, v)
+    apply_tune(op)
     op.addWindowFunction(pkg.AGG_MIN_I32)
     op.addWindowFunction(pkg.AGG_MAX_I32)
     op.setMaxLateness(1000)
@@ -507,6 +517,7 @@ def extra_c2s(pkg, dev, batch, steps, warm=21, tune=None, ooo=0.2):
     op = pkg.SlicingWindowOperator(device=dev.index)
     for k, v in (tune or {}).items():
         op.tune(k, v)
+    apply_tune(op)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.addWindowFunction(pkg.AGG_COUNT)
     op.setMaxLateness(1000)
@@ -844,7 +855,7 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
     shape per key).  Session windows take the lane-per-key session replay (keyed_lane_session.hip: one lane restates one
     key's StreamSlicer / SliceManager / SessionContext, steady-state tuples in registers).  The timed steps cover one
     whole 10-step period (the pause step included); a second period with HIP events gives the device split.
-    `tune`: scotty_tune knobs (the "c4s2" leg: {"keyed_lane_session": 1}, the kernel's 2-waves build, A/B;
+    `tune`: scotty_tune knobs (the "c4s3" leg: {"keyed_lane_session": 2}, the kernel's 3-waves build, A/B;
     profiles/r05/ab_c4s_occupancy.json: 2 waves 8.04 ms/step, 3 waves 8.93)."""
     import torch
     rate = max(1, batch // 1000)
@@ -878,9 +889,11 @@ def extra_c4s(pkg, dev, batch, keys, steps=10, warm=12, tune=None):
         if warm <= s < warm + steps:
             times.append(time.perf_counter() - t0)
             rows += n
-    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
-                           "lane_session_kernel (lane per key, the replay of the batch sorted by key; the sort, segment and "
-                           "key-table passes are push_other)")
+    kn = kernel_name(pkg, KN_LANE_SESSION)
+    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE, kn)
+    roof["kernel_note"] = ("lane per key, the replay of the batch sorted by key; the sort, segment and key-table passes "
+                           "are push_other")
+    roof.update(pmc_traffic("c4s", [kn], batch, batch * KEYED_BYTES_PER_TUPLE))
     return {"workload": "C4s: keyed SessionWindow(gap 1s) + SlidingWindow(60s,1s) SUM_I32, %d uniform keys, 20%% "
                         "out-of-order (delay U[1,500] ms), lag 500 ms, 2 s pause every 10 s, maxLateness 1000, "
                         "lane-per-key session replay, results left in HBM" % keys, "tune": tune or {},
@@ -924,21 +937,31 @@ def gpu_numa_node(dev_index):
         return None
 
 
-def extra_c4c(pkg, dev, batch, keys, steps=10, warm=11):
+C4C_COUNT = 500  # tuples per count window of the C4c leg (extra_c4c)
+
+
+def extra_c4c(pkg, dev, batch, keys, steps=10, warm=11, tune=None):
     """Keyed out-of-order count windows at scale: KeyedScottyWindowOperator with
     TumblingWindow(Count, 1000) + SlidingWindow(Time, 10 s, 1 s) per key, SUM_I32, `keys` uniform keys, 20 % of tuples
     late by U[1,500] ms, watermark lag 500 ms, maxLateness 1000.  Count windows make every slice a LazySlice with its
     TreeSet record set, and an out-of-order tuple runs SliceManager's count-shift loop (S/SliceManager.java:64-87) --
     the per-key replay path (one wavefront per key, exact_kernels.hip replay_kernel).  11 s of warm-up fill the sliding
-    windows' retention; results stay in HBM; a second run of as many steps with HIP events gives the device split."""
+    windows' retention; results stay in HBM; a second run of as many steps with HIP events gives the device split.
+    The shape is one the reference runs without throwing: the first step is in order (a late tuple below a key's first
+    slice throws IndexOutOfBounds in SliceManager.processElement), and a count window spans 500 tuples = ~7.8 s of a
+    key's 64 tuples per step, inside the 11 s the time window keeps (WindowManager.clearAfterWatermark removes slices
+    older than watermark - maxLateness - clearDelay, S/WindowManager.java:80-92; Count(1000) would span ~15.6 s and its
+    start slice is gone by the time it fires: LazyAggregateStore.aggregate's getSlice(-1), on the oracle and here)."""
     import torch
     rate = max(1, batch // 1000)
     g = torch.Generator(device=dev)
     g.manual_seed(78)
     op = pkg.KeyedSlicingWindowOperator(device=dev.index)
+    for k_, v_ in (tune or {}).items():
+        op.tune(k_, v_)
     op.addWindowFunction(pkg.AGG_SUM_I32)
     op.setMaxLateness(1000)
-    op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, 1000))
+    op.addWindowAssigner(pkg.TumblingWindow(pkg.WindowMeasure.Count, C4C_COUNT))
     op.addWindowAssigner(pkg.SlidingWindow(pkg.WindowMeasure.Time, 10_000, 1_000))
     base = torch.arange(batch, device=dev, dtype=torch.int64) // rate
     times, rows, count_rows = [], 0, 0
@@ -949,7 +972,7 @@ def extra_c4c(pkg, dev, batch, keys, steps=10, warm=11):
             op.enableTiming(True)
         t_begin = s * 1000 + 1000
         k = torch.randint(0, keys, (batch,), device=dev, dtype=torch.int64, generator=g).to(torch.int32)
-        late = torch.rand(batch, device=dev, generator=g) < 0.2
+        late = (torch.rand(batch, device=dev, generator=g) < 0.2) & (s > 0)
         d = torch.randint(1, 501, (batch,), device=dev, generator=g)
         ts = torch.where(late, base + t_begin - d, base + t_begin).contiguous()
         v = torch.randint(-2**31, 2**31, (batch,), device=dev, dtype=torch.int32, generator=g)
@@ -961,13 +984,16 @@ def extra_c4c(pkg, dev, batch, keys, steps=10, warm=11):
         if warm <= s < warm + steps:
             times.append(time.perf_counter() - t0)
             rows += n
-    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE,
-                           "keyed replay (class ingest: sort by key + wavefront-per-key replay of LazySlice record sets)")
+    kn = kernel_name(pkg, KN_REPLAY)
+    roof = device_roofline(op, steps, batch, KEYED_BYTES_PER_TUPLE, kn)
+    roof["kernel_note"] = ("wavefront-per-key replay of LazySlice record sets (class ingest); the sort by key, segment "
+                           "and key-table passes are push_other")
+    roof.update(pmc_traffic("c4c", [kn], batch, batch * KEYED_BYTES_PER_TUPLE))
     roof["bound_note"] = ("latency-bound: one wavefront restates one key's operator tuple by tuple (record-set inserts, "
                           "count shifts); the HBM fraction is reported for comparison only")
-    return {"workload": "C4c: keyed TumblingWindow(Count,1000) + SlidingWindow(10s,1s) SUM_I32, %d uniform keys, 20%% "
-                        "out-of-order (delay U[1,500] ms), lag 500 ms, maxLateness 1000, per-key replay with LazySlice "
-                        "record sets, results left in HBM" % keys,
+    return {"workload": "C4c: keyed TumblingWindow(Count,%d) + SlidingWindow(10s,1s) SUM_I32, %d uniform keys, 20%% "
+                        "out-of-order after the first step (delay U[1,500] ms), lag 500 ms, maxLateness 1000, per-key "
+                        "replay with LazySlice record sets, results left in HBM" % (C4C_COUNT, keys), "tune": tune or {},
             "tuples_per_step": batch, "steps": steps, "keys": op.keyCount(),
             "ms_per_step": 1e3 * sum(times) / len(times), "ms_per_step_each": [round(1e3 * t, 3) for t in times],
             "value": batch * len(times) / sum(times), "unit": "tuples/s", "windows_emitted": rows, "roofline": roof}
@@ -977,11 +1003,11 @@ def cpu_c4c(keys, batch, threads):
     """C4c on the CPU: KeyedScottyWindowOperator with TumblingWindow(Count, 1000) + SlidingWindow(10 s, 1 s) per key on T
     threads (key % T partitions), the GPU leg's stream shape, one watermark per step; two untimed steps, then timed
     steps until the budget."""
-    from oracle.oracle import KeyedOracleThreads, JavaError
+    from oracle.oracle import KeyedOracleThreads
     op = KeyedOracleThreads(threads)
     op.addWindowFunction(0)
     op.setMaxLateness(1000)
-    op.addWindowAssigner(0, 1, 1000, 0)
+    op.addWindowAssigner(0, 1, C4C_COUNT, 0)
     op.addWindowAssigner(1, 0, 10_000, 1_000)
     rng = np.random.default_rng(78)
     rate = max(1, batch // 1000)
@@ -990,15 +1016,12 @@ def cpu_c4c(keys, batch, threads):
     for s in range(1000):
         t_begin = s * 1000 + 1000
         k = rng.integers(0, keys, size=batch).astype(np.uint32)
-        late = rng.random(batch) < 0.2
+        late = (rng.random(batch) < 0.2) & (s > 0)
         ts = np.where(late, base + t_begin - rng.integers(1, 501, size=batch), base + t_begin)
         v = rng.integers(-2**31, 2**31, size=batch, dtype=np.int64)
         p = op.partition(k, ts, v)
         t0 = time.perf_counter()
-        try:
-            op.process(p, t_begin + (batch - 1) // rate - 500)
-        except JavaError:
-            pass
+        op.process(p, t_begin + (batch - 1) // rate - 500)  # the shape never throws (extra_c4c)
         dt = time.perf_counter() - t0
         if s >= 2:
             t_proc += dt
@@ -1096,12 +1119,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
     ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c4c,c5,c5t,pcie; c3nb: C3 with the start band "
-                    "off, A/B; c4s2: C4s on the lane-session kernel's 2-waves build, A/B); default all but c3nb, c4s2")
+                    "off, A/B; c4s3: C4s on the lane-session kernel's 3-waves build, A/B; c4s10: C4s with 10-bit sort digits, A/B); "
+                    "default all but c3nb, c4s3, c4s10")
+    ap.add_argument("--tune", default="", help="k=v[,k=v]: scotty_tune knobs for the C2, C1, C2s and C3 operators (A/B)")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
     ap.add_argument("--skip-headline", action="store_true",
                     help="profiling runs only (tools/gpu_traffic.sh): run just the --only legs, no C2 headline line")
     args = ap.parse_args()
+    for kv in (x for x in args.tune.split(",") if x):
+        k, v = kv.split("=")
+        TUNE[k] = int(v)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
@@ -1150,6 +1178,7 @@ def main():
         torch.cuda.synchronize(dev)
 
         op = pkg.ShardedSlicingWindowOperator(device=local) if sharded else pkg.SlicingWindowOperator(device=local)
+        apply_tune(op)
         op.addWindowFunction(pkg.AGG_SUM_I32)
         op.addWindowFunction(pkg.AGG_COUNT)
         op.setMaxLateness(1)
@@ -1213,7 +1242,8 @@ def main():
                            "tuples_per_step": B * world, "tuples_per_step_per_gpu": B, "event_ms_per_step": 1000,
                            "windows_emitted": n_windows,
                            "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch"
-                                           % world) if sharded else "single GPU"},
+                                           % world) if sharded else "single GPU",
+                           **({"tune": dict(TUNE)} if TUNE else {})},
                 "roofline": roof,
             }
     legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c4s", "c4c", "c5", "c5t", "pcie"}
@@ -1242,8 +1272,11 @@ def main():
             if "c4c" in legs:
                 extra["c4c"] = extra_c4c(pkg, dev, C4_BATCH, 1 << 20)
                 log("bench: C4c (keyed out-of-order count windows) done")
-            if "c4s2" in args.only.split(","):  # A/B only: the lane-session kernel's 2-waves-per-SIMD build
-                extra["c4s2"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 1})
+            if "c4s10" in args.only.split(","):  # A/B only: the replay sort's 10-bit digits (keyed_sort_digit10 1)
+                extra["c4s10"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_sort_digit10": 1})
+                log("bench: C4s (10-bit sort digits) done")
+            if "c4s3" in args.only.split(","):  # A/B only: the lane-session kernel's 3-waves-per-SIMD build
+                extra["c4s3"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 2})
                 log("bench: C4s (keyed sessions) done")
             if "c5" in legs:
                 extra["c5"] = extra_c5(pkg, dev, 1 << 27, 5)

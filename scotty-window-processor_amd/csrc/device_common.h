@@ -37,7 +37,10 @@ constexpr int64_t FIRST_NONE = INT64_MAX;  // identity of a FIRST partial (no tu
 // The rocprofv3 name of the last launch of a measured kernel class on this thread ("ingest_kernel<0, 1, 23>", as the
 // profiler prints the template instance), so the bench can tie a PMC traffic file to the kernel it measured
 // (scotty_debug_kernel_name).  Defined in scotty_engine.cpp.
-enum : int { KN_INGEST = 0, KN_KG_HIST = 1, KN_KG_SCATTER = 2, KN_KG_BUCKET = 3, KN_COUNT_INGEST = 4, KN_N = 5 };
+enum : int {
+  KN_INGEST = 0, KN_KG_HIST = 1, KN_KG_SCATTER = 2, KN_KG_BUCKET = 3, KN_COUNT_INGEST = 4, KN_LANE_SESSION = 5,
+  KN_REPLAY = 6, KN_N = 7
+};
 void note_kernel(int which, const char* fmt, int a = 0, int b = 0, int c = 0, int d = 0);
 
 // Device-resident scalars.  The StreamSlicer state (maxEventTime, min_next_edge_ts) lives here so

@@ -1334,7 +1334,8 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
   const bool pack_try = vt == VT_I32 && lane_session_mode() && !pack_off;
   // (one read of the keys, and of the timestamps when packing: also the sort's first digit histogram)
   const int64_t hist_nb = (bcap + sort_tile() - 1) / sort_tile();
-  int32_t* d_hist10 = d_hist + 256 * hist_nb;
+  // (the 10-bit first digit's histogram only for the 10-bit sort A/B: scotty_tune "keyed_sort_digit10" 1)
+  int32_t* d_hist10 = sort_digit10 == 1 ? d_hist + 256 * hist_nb : nullptr;
   XCHK(launch_range_hist(d_key, pack_try ? d_ts : nullptr, n, d_hist, d_hist10, d_rpart, d_kmax, stream));
   if ((rc = tend(tk, 0))) return rc;
   XCHK(hipMemcpyAsync(h_misc, d_kmax, 24, hipMemcpyDeviceToHost, stream));

@@ -149,9 +149,9 @@ class XEngine {
   unsigned long long* d_lsdbg = nullptr;  // lane-session path counters (scotty_tune "lane_session_counters" 1)
   bool lsdbg_on = false;
   bool pack_off = false;          // keyed replay: 16-byte records even when a batch fits 8 ("keyed_pack_records" 0)
-  int sort_digit10 = -1;          // keyed replay sort: 10-bit digits for 17-20-bit keys (-1), off (0), always (1)
+  int sort_digit10 = -1;          // keyed replay sort digits: 8-bit (-1 default, 0), 10-bit for 17-20-bit keys (1, A/B)
   int64_t last_rec_bytes = 0;     // the last keyed replay's record size (debug stat 107)
-  int lane_session_occ = 3;       // lane-session kernel build: 3 (default) or 2 waves per SIMD ("keyed_lane_session" 1 / 2)
+  int lane_session_occ = 2;       // lane-session kernel build: 2 (default) or 3 waves per SIMD ("keyed_lane_session" 1 / 2)
   bool lane_session_off = false;  // keyed: sessions through the wavefront replay instead (A/B, "keyed_lane_session" 0)
   // keyed_lane_session.hip: time-measured session windows (beside context-free time windows) on Eager slices
   bool lane_session_mode() const {

@@ -739,6 +739,7 @@ __global__ void xstate_init_kernel(XState* st, int64_t from, int64_t to, const u
 hipError_t launch_replay(const XBatchArgs& a, int vt, hipStream_t st) {
   if (a.n_ops <= 0) return hipSuccess;
   const int64_t blocks = std::min<int64_t>((a.n_ops + 3) / 4, 65536);
+  note_kernel(KN_REPLAY, "replay_kernel<%d>", vt);
   if (vt == VT_I32) hipLaunchKernelGGL(x::replay_kernel<VT_I32>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (vt == VT_I64) hipLaunchKernelGGL(x::replay_kernel<VT_I64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(x::replay_kernel<VT_F64>, dim3((unsigned)blocks), dim3(256), 0, st, a);

@@ -367,18 +367,19 @@ constexpr int SEG_TILE = SEG_ITEMS * SEG_THREADS;
 // [HIST_TILES b, HIST_TILES (b + 1)) (radix_hist_kernel<.., FIRST>'s tiling; the first digit is key & 0xFF for every record layout, so it does not wait
 // for the layout choice the range decides).  part[3 b ..]: the block's largest key, ~ smallest and largest biased
 // timestamp (range_reduce_kernel folds them: no same-address atomics from thousands of blocks)
-// hist10: the first 10-bit digit's histogram as well (key & 0x3FF: a 2-pass sort of 17-20-bit keys, sort_passes<.., 10>)
-template <int SI>
+// H10: the first 10-bit digit's histogram into hist10 as well (key & 0x3FF: the 2-pass sort, sort_passes<.., 10>)
+template <int SI, bool H10>
 __global__ __launch_bounds__(SORT_THREADS) void range_hist_kernel(const uint32_t* keys, const int64_t* ts, int64_t n,
                                                                   int32_t* hist, int32_t* hist10, int64_t nblocks,
                                                                   unsigned long long* part) {
   constexpr int TILE = SORT_THREADS * SI;
   __shared__ int32_t cnt[HIST_TILES][RADIX];
-  __shared__ int32_t cnt10[HIST_TILES][1024];
+  __shared__ int32_t cnt10[H10 ? HIST_TILES : 1][H10 ? 1024 : 1];
   __shared__ unsigned long long s_r[3][SORT_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int d = tid; d < HIST_TILES * RADIX; d += SORT_THREADS) (&cnt[0][0])[d] = 0;
-  for (int d = tid; d < HIST_TILES * 1024; d += SORT_THREADS) (&cnt10[0][0])[d] = 0;
+  if (H10)
+    for (int d = tid; d < HIST_TILES * 1024; d += SORT_THREADS) (&cnt10[0][0])[d] = 0;
   __syncthreads();
   const int64_t t0 = (int64_t)blockIdx.x * HIST_TILES;
   const int nt = (int)min((int64_t)HIST_TILES, nblocks - t0);
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(SORT_THREADS) void range_hist_kernel(const uint32_t
     for (int r = 0; r < SI; r++) {
       if (base + r * SORT_THREADS + tid < n) {
         atomicAdd(&cnt[j][k[r] & (RADIX - 1)], 1);
-        atomicAdd(&cnt10[j][k[r] & 1023], 1);
+        if (H10) atomicAdd(&cnt10[j][k[r] & 1023], 1);
         m = max(m, (unsigned long long)k[r]);
         const unsigned long long b = (unsigned long long)t[r] ^ 0x8000000000000000ull;
         nlo = max(nlo, ~b);
@@ -418,7 +419,7 @@ __global__ __launch_bounds__(SORT_THREADS) void range_hist_kernel(const uint32_t
   }
   __syncthreads();
   hist_rows_out(cnt, hist, nblocks, t0, nt, tid);
-  hist_rows_out<1024>(cnt10, hist10, nblocks, t0, nt, tid);
+  if constexpr (H10) hist_rows_out<1024>(cnt10, hist10, nblocks, t0, nt, tid);
   if (tid < 3) {
     unsigned long long v = 0;
     for (int w = 0; w < SORT_THREADS / 64; w++) v = max(v, s_r[tid][w]);
@@ -793,17 +794,18 @@ static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t
 }
 
 // Stable sort of the batch by slot into records (AoS, rec bytes 8 (packed: tbase / tb), 16 or 24).  bufA/bufB: n
-// records each; hist: RADIX * ceil(n / sort_tile()) int32, hist10: 1024 * ceil(n / sort_tile()) int32 (range_hist
-// writes both first-digit histograms); scan_tmp: int32 scratch.  Result lands in *result.  Digits: 8 bits, except for
-// 17-20-bit keys: two 10-bit passes instead of three 8-bit ones (one read + write of the batch, one histogram pass
-// fewer; the [digit][tile] matrix is 4x larger, so its scan costs more -- VERDICT r05 item 3).  digit10 < 0: choose
-// by key bits; 0 / 1: force 8-bit / 10-bit digits (scotty_tune "keyed_sort_digit10", A/B).
+// records each; hist: RADIX * ceil(n / sort_tile()) int32, hist10: 1024 * ceil(n / sort_tile()) int32 or null (range_hist
+// writes the first-digit histograms); scan_tmp: int32 scratch.  Result lands in *result.  Digits: 8 bits; with hist10
+// and digit10 != 0, 10 bits (two passes instead of three for 17-20-bit keys: one read + write of the batch and one
+// histogram pass fewer, but ranking 1024 digits per tile in LDS makes each scatter twice as slow -- C4s, 2^26 tuples,
+// 2^20 keys: 652 + 607 us scatters, 323 us range + first histograms, 205 us second histogram = 1.93 ms against
+// 1.53 ms for three 8-bit passes, profiles/r06/prof; kept as the scotty_tune "keyed_sort_digit10" 1 A/B).
 hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, const uint32_t* slot, int64_t n,
                                int slot_bits, void* bufA, void* bufB, int32_t* hist, int32_t* hist10,
                                int32_t* scan_tmp, void** result, hipStream_t st, int64_t tbase, int tb, bool hist0,
                                int digit10) {
   const k::PackP pk{tbase, tb};
-  const bool ten = hist10 && (digit10 < 0 ? (slot_bits > 16 && slot_bits <= 20) : digit10 == 1);
+  const bool ten = hist10 && digit10 != 0 && slot_bits > 16 && slot_bits <= 20;
   if (ten) {
     int passes = (slot_bits + 9) / 10;
     if (passes < 1) passes = 1;
@@ -835,8 +837,12 @@ hipError_t launch_range_hist(const uint32_t* keys, const int64_t* ts, int64_t n,
                              unsigned long long* part, unsigned long long* range, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = (n + k::SORT_TILE - 1) / k::SORT_TILE, hb = (nb + k::HIST_TILES - 1) / k::HIST_TILES;
-  hipLaunchKernelGGL(k::range_hist_kernel<k::SORT_ITEMS>, dim3((unsigned)hb), dim3(k::SORT_THREADS), 0, st, keys, ts,
-                     n, hist, hist10, nb, part);
+  if (hist10)
+    hipLaunchKernelGGL((k::range_hist_kernel<k::SORT_ITEMS, true>), dim3((unsigned)hb), dim3(k::SORT_THREADS), 0, st,
+                       keys, ts, n, hist, hist10, nb, part);
+  else
+    hipLaunchKernelGGL((k::range_hist_kernel<k::SORT_ITEMS, false>), dim3((unsigned)hb), dim3(k::SORT_THREADS), 0, st,
+                       keys, ts, n, hist, hist10, nb, part);
   hipLaunchKernelGGL(k::range_reduce_kernel, dim3(1), dim3(1024), 0, st, part, hb, range);
   return hipGetLastError();
 }

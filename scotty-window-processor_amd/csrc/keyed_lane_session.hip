@@ -984,6 +984,11 @@ hipError_t launch_lane_session(const XBatchArgs& a, int vt, int occ, hipStream_t
   if (a.n_ops <= 0) return hipSuccess;
   const dim3 grid((unsigned)((a.n_ops + 255) / 256)), block(256);
 #define SCOTTY_LS(VT_, OCC_, V_) hipLaunchKernelGGL((ls::lane_session_kernel<VT_, OCC_, V_>), grid, block, 0, st, a)
+  // the rocprofv3 name of the instance (scotty_debug_kernel_name): <VT, OCC, store view, packed records>
+  note_kernel(KN_LANE_SESSION, a.rec_stride == 8 ? "lane_session_kernel<%d, %d, XKView, true>"
+                               : a.sl.kw          ? "lane_session_kernel<%d, %d, XKView, false>"
+                                                  : "lane_session_kernel<%d, %d, XSlices, false>",
+              vt, occ == 2 ? 2 : 3);
   if (a.rec_stride == 8) {  // packed records: int32 values, key-interleaved store only (exact_engine.cpp)
     if (vt != VT_I32 || !a.sl.kw) return hipErrorInvalidValue;
     if (occ == 2) hipLaunchKernelGGL((ls::lane_session_kernel<VT_I32, 2, XKView, true>), grid, block, 0, st, a);

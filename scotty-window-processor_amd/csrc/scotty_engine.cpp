@@ -193,9 +193,9 @@ struct scotty_op {
   int64_t x_prefix = 0;      // exact engine: first event-exact prefix of a refused quiet batch (0: default)
   int32_t x_qmode = -1;      // exact engine: quiet-pass ingest loop (A/B: -1 default, 7 without the DQ2 queue)
   bool x_ls_off = false;     // exact engine: keyed sessions through the wavefront replay (A/B)
-  int32_t x_ls_occ = 3;      // lane-session kernel's waves per SIMD (3 default; 2: A/B, profiles/r05/c4s_pause_edits/)
+  int32_t x_ls_occ = 2;      // lane-session kernel's waves per SIMD (2 default, no VGPR spill; 3: A/B, profiles/r06/ab1/)
   bool x_pack_off = false;   // exact engine: keyed replay records always 16 bytes (A/B for the packed 8-byte ones)
-  int x_digit10 = -1;        // exact engine: keyed replay sort digits ("keyed_sort_digit10": -1 auto, 0 8-bit, 1 10-bit)
+  int x_digit10 = -1;        // exact engine: keyed replay sort digits ("keyed_sort_digit10": -1 default = 0 8-bit, 1 10-bit)
   bool x_lsdbg = false;      // lane-session path counters (debugging aid)
   int64_t x_qblocks = 0;     // exact engine: quiet-pass ingest workgroups (A/B: 0 default)
   int32_t x_kg_variant = -1;
@@ -1654,7 +1654,7 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_lane_session") == 0) {  // 0: keyed sessions through the wavefront replay (A/B),
-    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;  // 1 lane kernel 2-waves build, 2 3-waves (default)
+    if (op->mode != 0 || value < 0 || value > 2) return SCOTTY_ERR_ARG;  // 1 lane kernel 2-waves build (default), 2 3-waves
     // (the store layout follows the kernel at the first push: the lane kernel's key-interleaved store cannot be
     // handed to the wavefront replay later)
     if (op->x && op->x->key_count() > 0 && (value == 0) != op->x_ls_off) return SCOTTY_ERR_STATE;

@@ -229,8 +229,9 @@ def test_packed_replay_records_equal_16_byte_records(seed):
 
 @pytest.mark.parametrize("seed", range(6))
 def test_ten_bit_digit_sort_equals_eight_bit_sort(seed):
-    """The keyed replay's stable sort by key (keyed_kernels.hip): 17-20-bit keys take two 10-bit digit passes by default
-    (VERDICT r05 item 3), scotty_tune "keyed_sort_digit10" 0 keeps three 8-bit ones.  A stable sort has one result, so
+    """The keyed replay's stable sort by key (keyed_kernels.hip): scotty_tune "keyed_sort_digit10" 1 sorts 17-20-bit keys
+    in two 10-bit digit passes (measured slower, so the default keeps three 8-bit ones, 0).  A
+    stable sort has one result, so
     every watermark's rows and the dropped counts must be identical; session and count windows (lane-session kernel,
     wavefront replay), packed 8-byte and 16-byte records, key ranges from 2^16 + 1 to 2^20."""
     from specs import Tumbling, Count

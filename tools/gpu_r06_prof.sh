@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 measurement campaign: for every bench leg, one rocprofv3 --kernel-trace --stats run and
+# Round-6 measurement campaign: for every bench leg, one rocprofv3 --output-format csv --kernel-trace --stats run and
 # two --pmc passes (FETCH_SIZE, WRITE_SIZE; separate runs), plus the known-byte calibration kernels
 # (tools/pmc_calib.hip).  Every step has its own time limit and the chain stops at the first failure.
 # $1 = tag (output gpurun_out/r06/$1), $2 = legs (default: all), $3 = what (trace,pmc,calib; default all three)
@@ -23,22 +23,22 @@ args_of() {
   esac
 }
 if [[ $what == *calib* ]]; then
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $out/calib_f -o run -- ./tools/pmc_calib > $out/calib.json || exit 1
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $out/calib_w -o run -- ./tools/pmc_calib > /dev/null || exit 1
+  timeout -s KILL 120 rocprofv3 --output-format csv --pmc FETCH_SIZE -d $out/calib_f -o run -- ./tools/pmc_calib > $out/calib.json || exit 1
+  timeout -s KILL 120 rocprofv3 --output-format csv --pmc WRITE_SIZE -d $out/calib_w -o run -- ./tools/pmc_calib > /dev/null || exit 1
   shrink $out/calib_f; shrink $out/calib_w
   echo "calib done"
 fi
 for leg in $legs; do
   a=$(args_of $leg)
   if [[ $what == *trace* ]]; then
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/trace_$leg -o run -- python3 -u bench.py $a \
+    timeout -k 10 400 rocprofv3 --output-format csv --kernel-trace --stats -d $out/trace_$leg -o run -- python3 -u bench.py $a \
       > $out/trace_$leg.json 2> $out/trace_$leg.err || { echo "trace $leg failed"; exit 1; }
     shrink $out/trace_$leg
     echo "trace $leg done"
   fi
   if [[ $what == *pmc* ]]; then
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 500 rocprofv3 --pmc $c -d $out/pmc_${leg}_$c -o run -- python3 -u bench.py $a \
+      timeout -k 10 500 rocprofv3 --output-format csv --pmc $c -d $out/pmc_${leg}_$c -o run -- python3 -u bench.py $a \
         > $out/pmc_${leg}_$c.json 2> $out/pmc_${leg}_$c.err || { echo "pmc $leg $c failed"; exit 1; }
       shrink $out/pmc_${leg}_$c
     done

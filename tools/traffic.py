@@ -35,7 +35,7 @@ PATTERN = {
 
 def norm(name):
     name = name.split("(")[0].replace("void ", "")
-    for ns in ("scotty::", "kg::", "ck::", "k::", "ln::", "x::", "wk::"):
+    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "ln::", "k::", "x::"):
         name = name.replace(ns, "")
     return name.replace(" ", "")
 
@@ -101,7 +101,9 @@ def leg(name, batch, fdir, wdir, kernels):
         if kn not in f or kn not in w:
             raise SystemExit("kernel %s not in the traces (have: %s)" % (kn, sorted(f)))
         base = kn.split("<")[0]
-        rp, wp = PATTERN[base]
+        # kernels without a calibrated shape of their own take the streaming one (every calibrated read factor is
+        # 2.00 +- 0.01 and every write factor 1.00 on gfx950, profiles/traffic.json "calibration")
+        rp, wp = PATTERN.get(base, ("calib_read16", "calib_write16"))
         fk, wk = typical(f[kn]), typical(w[kn])
         rb, wb = fk * 1024 * cal[rp]["factor"], wk * 1024 * cal[wp]["factor"]
         out[k] = {"FETCH_SIZE_kB": fk, "WRITE_SIZE_kB": wk, "launches": len(f[kn]),
@@ -118,7 +120,8 @@ def leg(name, batch, fdir, wdir, kernels):
 def all_legs(root):
     """Every leg profiled by tools/gpu_r06_prof.sh under root: the kernel names and batch from the bench line of the
     leg's own FETCH_SIZE run (its roofline block), then leg()."""
-    calib(os.path.join(root, "calib_f"), os.path.join(root, "calib_w"))
+    if os.path.isdir(os.path.join(root, "calib_f")):  # else the calibration already in the output file
+        calib(os.path.join(root, "calib_f"), os.path.join(root, "calib_w"))
     for f in sorted(glob.glob(os.path.join(root, "pmc_*_FETCH_SIZE.json"))):
         name = os.path.basename(f)[len("pmc_"):-len("_FETCH_SIZE.json")]
         try:
