@@ -1119,8 +1119,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2s / C3 / C4 / C5 secondary measurements")
     ap.add_argument("--only", default="", help="comma list of extra legs to run (c1,c2s,c3,c4,c4s,c4c,c5,c5t,pcie; c3nb: C3 with the start band "
-                    "off, A/B; c4s3: C4s on the lane-session kernel's 3-waves build, A/B; c4s10: C4s with 10-bit sort digits, A/B); "
-                    "default all but c3nb, c4s3, c4s10")
+                    "off, A/B; c4s3: C4s on the lane-session kernel's 3-waves build, A/B; c4s10: C4s with 10-bit sort digits, A/B; c4cw: C4c on the "
+                    "wavefront replay, A/B); default all but c3nb, c4s3, c4s10, c4cw")
     ap.add_argument("--tune", default="", help="k=v[,k=v]: scotty_tune knobs for the C2, C1, C2s and C3 operators (A/B)")
     ap.add_argument("--shard", action="store_true", help="use the sharded (RCCL exchange) path even at N=1")
     ap.add_argument("--roof-steps", type=int, default=10, help="instrumented steps (HIP events) after the timed ones")
@@ -1272,6 +1272,9 @@ def main():
             if "c4c" in legs:
                 extra["c4c"] = extra_c4c(pkg, dev, C4_BATCH, 1 << 20)
                 log("bench: C4c (keyed out-of-order count windows) done")
+            if "c4cw" in args.only.split(","):  # A/B only: C4c through the wavefront replay (keyed_lane_count 0)
+                extra["c4cw"] = extra_c4c(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_count": 0})
+                log("bench: C4c (wavefront replay) done")
             if "c4s10" in args.only.split(","):  # A/B only: the replay sort's 10-bit digits (keyed_sort_digit10 1)
                 extra["c4s10"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_sort_digit10": 1})
                 log("bench: C4s (10-bit sort digits) done")

@@ -24,6 +24,7 @@ hipError_t launch_wm_agg(const XWmArgs& a, hipStream_t st, int group);
 hipError_t launch_wm_blocks(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_replay(const XBatchArgs& a, const XCfg& host_cfg, hipStream_t st);
 hipError_t launch_lane_session(const XBatchArgs& a, int vt, int occ, hipStream_t st);
+hipError_t launch_lane_count(const XBatchArgs& a, int vt, hipStream_t st);  // keyed_lane_count.hip
 hipError_t launch_lane_wm_count(const XWmArgs& a, hipStream_t st);
 hipError_t launch_lane_wm_emit(const XWmArgs& a, bool agg, hipStream_t st);
 hipError_t launch_xstate_init(XState* st_, int64_t from, int64_t to, const uint32_t* slot_key, hipStream_t st);
@@ -1449,6 +1450,7 @@ int XEngine::push_keyed_replay(const uint32_t* d_key, const int64_t* d_ts, const
     if ((rc = tbegin(tr, SCOTTY_TIME_INGEST))) return rc;
     XCHK(lane_mode()           ? launch_lane_replay(a, cfg, stream)
          : lane_session_mode() ? launch_lane_session(a, vt, lane_session_occ, stream)
+         : lane_count_mode()   ? launch_lane_count(a, vt, stream)
                                : launch_replay(a, vt, stream));
     if ((rc = tend(tr, n))) return rc;
     XCHK(hipMemcpyAsync(h_misc, d_need, 24, hipMemcpyDeviceToHost, stream));

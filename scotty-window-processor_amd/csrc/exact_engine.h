@@ -153,6 +153,9 @@ class XEngine {
   int64_t last_rec_bytes = 0;     // the last keyed replay's record size (debug stat 107)
   int lane_session_occ = 2;       // lane-session kernel build: 2 (default) or 3 waves per SIMD ("keyed_lane_session" 1 / 2)
   bool lane_session_off = false;  // keyed: sessions through the wavefront replay instead (A/B, "keyed_lane_session" 0)
+  bool lane_count_off = false;    // keyed: LazySlice record sets through the wavefront replay instead (A/B, "keyed_lane_count" 0)
+  // keyed_lane_count.hip: LazySlice record sets (count windows), no session windows -- one lane per key
+  bool lane_count_mode() const { return keyed && !lane_count_off && records && cfg.n_ctx == 0; }
   // keyed_lane_session.hip: time-measured session windows (beside context-free time windows) on Eager slices
   bool lane_session_mode() const {
     if (!keyed || lane_session_off || cfg.n_ctx == 0 || cfg.has_count || cfg.lazy || records || !cfg.has_time)

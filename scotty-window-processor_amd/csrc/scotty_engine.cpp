@@ -193,6 +193,7 @@ struct scotty_op {
   int64_t x_prefix = 0;      // exact engine: first event-exact prefix of a refused quiet batch (0: default)
   int32_t x_qmode = -1;      // exact engine: quiet-pass ingest loop (A/B: -1 default, 7 without the DQ2 queue)
   bool x_ls_off = false;     // exact engine: keyed sessions through the wavefront replay (A/B)
+  bool x_lc_off = false;     // exact engine: keyed LazySlice record sets through the wavefront replay (A/B)
   int32_t x_ls_occ = 2;      // lane-session kernel's waves per SIMD (2 default, no VGPR spill; 3: A/B, profiles/r06/ab1/)
   bool x_pack_off = false;   // exact engine: keyed replay records always 16 bytes (A/B for the packed 8-byte ones)
   int x_digit10 = -1;        // exact engine: keyed replay sort digits ("keyed_sort_digit10": -1 default = 0 8-bit, 1 10-bit)
@@ -1043,6 +1044,7 @@ static int decide_mode(scotty_op* op) {
   op->x->xq_ingest_blocks = op->x_qblocks;
   op->x->lane_session_off = op->x_ls_off;
   op->x->lane_session_occ = op->x_ls_occ;
+  op->x->lane_count_off = op->x_lc_off;
   op->x->pack_off = op->x_pack_off;
   op->x->sort_digit10 = op->x_digit10;
   op->x->lsdbg_on = op->x_lsdbg;
@@ -1651,6 +1653,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (value != 0 && (value < 4096 || value > ((int64_t)1 << 40))) return SCOTTY_ERR_ARG;
     op->x_prefix = value;
     if (op->x) op->x->xq_prefix = value;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "keyed_lane_count") == 0) {  // 0: keyed LazySlice record sets (count windows) through the
+    if (op->mode != 0 || value < 0 || value > 1) return SCOTTY_ERR_ARG;  // wavefront replay (A/B); 1 lane per key (default)
+    op->x_lc_off = value == 0;
+    if (op->x) op->x->lane_count_off = op->x_lc_off;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_lane_session") == 0) {  // 0: keyed sessions through the wavefront replay (A/B),
