@@ -194,16 +194,18 @@ __global__ __launch_bounds__(256) void cix_build_kernel(IngestArgs a) {
   // cells are sorted, so the block stops at its first cell starting at or beyond span_end.  A cell owning more
   // than CIX_RUN buckets (cells of seconds at one bucket per ms) is queued in LDS and written by the whole block,
   // not by its one thread bucket after bucket.  (CIX_RUN 16 queued every 60-ms cell of a 60 s window: 256 serial
-  // block rounds, 30 us; a thread's run of up to 128 stores issues without waiting.)
+  // block rounds, 30 us; a thread's run of up to 128 stores issues without waiting.)  Cells are dealt to the blocks
+  // round robin (cell cb + thread * blocks + block), so a few long cells -- C1's 61 one-second cells of 1000 buckets
+  // -- are written by as many blocks instead of all by the first one (20.7 us per push when block 0 held them all).
   constexpr int CIX_RUN = 128;
   __shared__ int64_t l_k0[256], l_k1[256];
   __shared__ uint32_t l_c[256];
   __shared__ int l_n;
   const uint64_t round = ((uint64_t)1 << shift) - 1;
-  for (int64_t cb = (int64_t)blockIdx.x * blockDim.x; cb < ctot; cb += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t cb = 0; cb < ctot; cb += (int64_t)gridDim.x * blockDim.x) {
     if (threadIdx.x == 0) l_n = 0;
     __syncthreads();
-    const int64_t c = cb + threadIdx.x;
+    const int64_t c = cb + (int64_t)threadIdx.x * gridDim.x + blockIdx.x;
     bool done = c >= ctot;
     if (!done) {
       const int64_t sc0 = cv.start(c);
