@@ -797,19 +797,12 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.pre_cnt = d_pre_cnt;
   a.pre_sum = d_pre_sum;
   a.has_value = d_has;
-  if (nw > 0) {  // LazyAggregateStore.aggregate runs only with windows (S/WindowManager.java:73-75)
-    CCHK(launch_count_wm_agg(a, (S_ub + 1023) / 1024 + 1, d_bsum, stream));
-    CCHK(launch_copy_to_host(d_meta, h_meta_dev, sizeof(CMeta), stream));
-    CCHK(hipStreamSynchronize(stream));
-    if (h_meta->range_err) {
-      err = "processWatermark threw IndexOutOfBoundsException (LazyAggregateStore.aggregate: a window starts before "
-            "the oldest retained slice, S/aggregationstore/LazyAggregateStore.java:83-90)";
-      return SCOTTY_ERR_INDEX;
-    }
-  }
-  last_wm = wm;
-  last_count = count;
-  CCHK(launch_count_gc(a, stream));  // clearAfterWatermark(wm - maxLateness) (S/WindowManager.java:82-95)
+  // LazyAggregateStore.aggregate runs only with windows (S/WindowManager.java:73-75), then clearAfterWatermark(wm -
+  // maxLateness) (:82-95) -- which the GC kernel skips when the aggregation's range check threw; the host learns
+  // that at the one synchronisation below, with the result copies
+  if (nw > 0) CCHK(launch_count_wm_agg(a, (S_ub + 1023) / 1024 + 1, d_bsum, stream));
+  CCHK(launch_count_gc(a, stream));
+  if (nw > 0) CCHK(launch_copy_to_host(d_meta, h_meta_dev, sizeof(CMeta), stream));
   r.n = nw;
   r.d_start = d_wstart;
   r.d_end = d_wend;
@@ -837,6 +830,14 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
       CCHK(hipMemcpyAsync(r.vals[k].data(), d_vals[k], nw * 8, hipMemcpyDeviceToHost, stream));
   }
   CCHK(hipStreamSynchronize(stream));
+  if (nw > 0 && h_meta->range_err) {
+    r.n = 0;
+    err = "processWatermark threw IndexOutOfBoundsException (LazyAggregateStore.aggregate: a window starts before "
+          "the oldest retained slice, S/aggregationstore/LazyAggregateStore.java:83-90)";
+    return SCOTTY_ERR_INDEX;
+  }
+  last_wm = wm;
+  last_count = count;
   return SCOTTY_OK;
 }
 

@@ -867,6 +867,9 @@ __global__ void count_rows_kernel(const CRowSeg* segs, const int64_t* seg_off, i
 __global__ void count_gc_kernel(CWmArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   CMeta& m = *a.meta;
+  // the aggregation threw (getSlice(-1)): the reference leaves processWatermark before clearAfterWatermark, so the
+  // store stays as it is (the host reports the exception after its one synchronisation)
+  if (a.nw > 0 && m.range_err) return;
   if (m.tail <= m.head) return;
   const int64_t idx = last_le(a.sl.ts, m.head, m.tail, a.gc_before);  // LazyAggregateStore.removeSlices
   if (idx > m.head) m.head = idx;

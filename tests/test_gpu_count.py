@@ -181,6 +181,38 @@ def test_survey_c5_reduced_matches_oracle(pkg):
     assert gpu._debug_stat(5) == 3
 
 
+def test_count_path_aggregate_range_exception_leaves_state(pkg):
+    """A count window longer than the time windows keep: clearAfterWatermark removes slices older than watermark -
+    maxLateness - the largest clearDelay (S/WindowManager.java:82-95), so a TumblingWindow(Count, 1000) spanning 16 s
+    of a one-tuple-per-16-ms stream, watermarks ~2 s apart, loses its start slice to a 10 s sliding window's retention
+    and LazyAggregateStore.aggregate throws getSlice(-1) (:83-90; the oracle throws at 23 of the 30 watermarks).  The count path's GC is skipped on the device when the
+    aggregation threw (one host synchronisation per watermark): every watermark throws or matches the oracle's, and
+    the state after a throw is the reference's."""
+    cfg = dict(windows=[Tumbling(Count, 1000), Sliding(Time, 10_000, 1000)], aggs=[SUM, COUNT], lateness=1000)
+    n = 4000
+    ts = 1000 + np.arange(n, dtype=np.int64) * 16
+    vals = np.random.default_rng(3).integers(-2**31, 2**31, size=n, dtype=np.int64).astype(np.int32)
+    gpu, ora = build_ops(cfg, tune={"count_path": 1})
+    throws = 0
+    for step in interval_schedule(ts, 30, lag=0, pushes_per_interval=1):
+        if step[0] == "push":
+            gpu.processElements(ts[step[1]:step[2]], vals[step[1]:step[2]])
+            ora.processElements(ts[step[1]:step[2]], vals[step[1]:step[2]])
+            continue
+        try:
+            got = gpu.processWatermark(step[1])
+        except pkg.ScottyError as e:
+            assert e.code == -5
+            from oracle.oracle import JavaError
+            with pytest.raises(JavaError):
+                ora.processWatermark(step[1])
+            throws += 1
+            continue
+        same_windows(got, ora.processWatermark(step[1]))
+    assert throws == 23
+    assert gpu._debug_stat(5) == 3
+
+
 @pytest.mark.parametrize("lateness", [1, 40, 100_000])
 def test_count_path_time_edges_small_pushes(pkg, lateness):
     """One-tuple and few-tuple pushes (the first tuple's edge walk alone, candidates at batch ends), a first
