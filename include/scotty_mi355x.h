@@ -239,7 +239,10 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
  * engine, non-keyed, one session window: one-pass batches may move the last session's start down -- the stream
  * resuming after a silence then costs one pass instead of event-exact rounds; the results are the same; on by
  * default, 0 for A/B), "keyed_lane_session" (keyed session windows: 0 the wavefront-per-key replay, 1 the lane-per-key
- * kernel's 2-waves-per-SIMD build, 2 its 3-waves build, the default; A/B only, before the first push),
+ * kernel's 2-waves-per-SIMD build, the default, 2 its 3-waves build; A/B only, before the first push),
+ * "keyed_lane_count" 0 (keyed operators with LazySlice record sets and no session window -- count windows -- through
+ * the wavefront-per-key replay instead of the lane-per-key kernel; A/B only), "keyed_sort_digit10" 1 (keyed replay:
+ * sort 17-20-bit keys in two 10-bit digit passes instead of three 8-bit ones; A/B only, slower),
  * "keyed_pack_records" 0 (keyed lane-session replay: 16-byte sort records even when a batch's key and event-time bits
  * fit the packed 8-byte ones; A/B only), "lane_session_counters" 1 (debugging aid: count the lane-session kernel's
  * paths). */
