@@ -80,7 +80,7 @@ def kernel_name(pkg, which):
 def norm_kernel(name):
     """A kernel name as rocprofv3 prints it, without namespaces, arguments or spaces (for matching)."""
     name = name.split("(")[0].replace("void ", "")
-    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "ln::", "k::", "x::"):
+    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "lc::", "ln::", "k::", "x::"):
         name = name.replace(ns, "")
     return name.replace(" ", "")
 

@@ -438,9 +438,75 @@ __global__ __launch_bounds__(256) void lane_count_kernel(XBatchArgs a) {
     }
   }
   if (o.s.rend + seglen + 64 > cfg->rcap) o.rec_compact();
+  // The current (last) slice in registers.  Most tuples are in order and open no slice: determineSlices only counts
+  // them (no count edge due, no time edge crossed, S/StreamSlicer.java:36-86) and processElement's in-order branch adds
+  // them to the last slice (S/SliceManager.java:56-63), whose record set they extend at its end (ts above its last
+  // record: TreeSet.add appends; an equal ts adds no record).  Those tuples touch only these registers and the two
+  // record words they append -- about 26 scattered lines per tuple otherwise (the slice's fields read and written, its
+  // record range), which bounded the kernel at 140 GB of line traffic per C4c batch (profiles/r06/prof).  Every other
+  // tuple flushes the registers and runs the restatement above, which then sees the store exactly as it would have.
+  int ci = -1;
+  bool dirty = false, c_lazy = false;
+  int64_t c_tl = 0, c_tf = 0, c_cl = 0, c_rhi = 0, c_last = JMIN;
+  uint64_t c_cnt = 0, c_p0 = 0;
+  int64_t c_p1 = 0, c_p2 = 0;
+  auto load_cur = [&]() {
+    ci = o.s.tail > o.s.head ? o.s.tail - 1 : -1;
+    dirty = false;
+    if (ci < 0) return;
+    c_tl = o.tl[ci]; c_tf = o.tf[ci]; c_cl = o.cl[ci]; c_cnt = o.cnt[ci];
+    c_p0 = o.p0[ci]; c_p1 = (int64_t)o.p1[ci]; c_p2 = (int64_t)o.p2[ci];
+    c_lazy = ty_lazy(o.ty[ci]);
+    c_rhi = o.rhi[ci];
+    c_last = c_rhi > o.rlo[ci] ? o.rts[c_rhi - 1] : JMIN;
+  };
+  auto flush_cur = [&]() {
+    if (ci < 0 || !dirty) return;
+    o.tl[ci] = c_tl; o.tf[ci] = c_tf; o.cl[ci] = c_cl; o.cnt[ci] = c_cnt;
+    o.p0[ci] = c_p0; o.p1[ci] = (unsigned long long)c_p1; o.p2[ci] = (unsigned long long)c_p2;
+    o.nn[ci] = 1;
+    o.rhi[ci] = c_rhi;
+    dirty = false;
+  };
+  load_cur();
   for (int64_t i = b0; i < b1 && !o.s.err; i++) {
     int64_t t, vb;
     load_rec<VT>(a, i, t, vb);
+    // the fast tuple: no count edge (nextEdgeCount pending and not reached), no time edge (t below the pending fixed
+    // edge, or out of order), in order in the last slice, and its record (if any) appended at the arena's end
+    bool fast = ci >= 0 && t >= c_tl && (!c_lazy || (c_last <= t && c_rhi == o.s.rend && o.s.rend < cfg->rcap));
+    if (fast && cfg->has_count) fast = o.s.nextEdgeCount != JMIN && o.s.currentCount != o.s.nextEdgeCount;
+    if (fast && cfg->has_time && t >= o.s.maxEventTime)
+      fast = cfg->has_fixed ? (o.s.nextEdgeTs != JMIN && t < o.s.nextEdgeTs) : t != o.s.nextEdgeTs;
+    if (fast) {
+      o.s.currentCount = jadd(o.s.currentCount, 1);
+      o.s.maxEventTime = max(t, o.s.maxEventTime);
+      o.s.started = 1;
+      c_tl = max(c_tl, t);
+      c_tf = min(c_tf, t);
+      c_cl = jadd(c_cl, 1);
+      c_cnt++;
+      const Lift l = lift(VT, vb);
+      if (cfg->need & NEED_SUM) {
+        if (VT == VT_F64)
+          c_p0 = (uint64_t)__double_as_longlong(__longlong_as_double((long long)c_p0) +
+                                                __longlong_as_double((long long)l.sum));
+        else
+          c_p0 += l.sum;
+      }
+      if (cfg->need & NEED_MIN) c_p1 = min(c_p1, l.mn);
+      if (cfg->need & NEED_MAX) c_p2 = max(c_p2, l.mx);
+      dirty = true;
+      if (c_lazy && c_last != t) {  // LazySlice.addElement: records.add, at the end of the set and of the arena
+        o.rts[o.s.rend] = t;
+        o.rv[o.s.rend] = vb;
+        o.s.rend++;
+        c_rhi++;
+        c_last = t;
+      }
+      continue;
+    }
+    flush_cur();
     o.exc = 0;
     o.determine_slices(t);
     if (!o.exc) o.manager_process(t, vb);
@@ -450,7 +516,9 @@ __global__ __launch_bounds__(256) void lane_count_kernel(XBatchArgs a) {
     } else if (o.exc) {
       o.s.err = o.exc;
     }
+    load_cur();
   }
+  flush_cur();
   a.st[op] = o.s;
 }
 

@@ -20,7 +20,7 @@ LEGS = ["c2", "c1", "c2s", "c3", "c4", "c4s", "c4c", "c5", "c5t"]
 
 def norm(name):
     name = name.split("(")[0].replace("void ", "")
-    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "ln::", "k::", "x::"):
+    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "lc::", "ln::", "k::", "x::"):
         name = name.replace(ns, "")
     return name.replace(" ", "")
 

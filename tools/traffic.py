@@ -35,7 +35,7 @@ PATTERN = {
 
 def norm(name):
     name = name.split("(")[0].replace("void ", "")
-    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "ln::", "k::", "x::"):
+    for ns in ("scotty::", "kg::", "ck::", "wk::", "xq::", "ls::", "lc::", "ln::", "k::", "x::"):
         name = name.replace(ns, "")
     return name.replace(" ", "")
 
