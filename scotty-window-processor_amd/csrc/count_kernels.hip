@@ -21,6 +21,7 @@
 //   count_wm_agg_kernel<G>   AggregateWindowState.containsSlice/addState (S/state/AggregateWindowState.java:25-53)
 //                            per window: prefix-sum difference for invertible integer aggregates, else a G-lane scan,
 //   count_gc_kernel          clearAfterWatermark / removeSlices (S/WindowManager.java:82-95).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -996,23 +997,27 @@ __global__ void count_shard_merge_kernel(CShardArgs a) {
 
 // ---------------------------------------------------------------- launch wrappers
 hipError_t launch_scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t st);
+// e0 / e1 (nullable): timing events the dispatch stamps with its own start / end (hipExtLaunchKernel), as the grid
+// path's ingest does -- marker events recorded around the launch also held the marker-to-dispatch gaps
 template <int VT, int NEED>
-static void launch_ingest_cn(const CPushArgs& a, hipStream_t st) {
+static void launch_ingest_cn(const CPushArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   const int64_t waves = (a.nsteps + a.per_wave - 1) / a.per_wave;
   note_kernel(KN_COUNT_INGEST, "count_ingest_kernel<%d, %d>", VT, NEED);
-  hipLaunchKernelGGL((ck::count_ingest_kernel<VT, NEED>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+  const dim3 g((unsigned)((waves + 3) / 4));
+  if (e0 || e1) hipExtLaunchKernelGGL((ck::count_ingest_kernel<VT, NEED>), g, dim3(256), 0, st, e0, e1, 0, a);
+  else hipLaunchKernelGGL((ck::count_ingest_kernel<VT, NEED>), g, dim3(256), 0, st, a);
 }
 template <int VT>
-static void launch_ingest_cv(const CPushArgs& a, hipStream_t st) {
+static void launch_ingest_cv(const CPushArgs& a, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   switch (a.need) {
-    case 0: launch_ingest_cn<VT, 0>(a, st); break;
-    case 1: launch_ingest_cn<VT, 1>(a, st); break;
-    case 2: launch_ingest_cn<VT, 2>(a, st); break;
-    case 3: launch_ingest_cn<VT, 3>(a, st); break;
-    case 4: launch_ingest_cn<VT, 4>(a, st); break;
-    case 5: launch_ingest_cn<VT, 5>(a, st); break;
-    case 6: launch_ingest_cn<VT, 6>(a, st); break;
-    default: launch_ingest_cn<VT, 7>(a, st); break;
+    case 0: launch_ingest_cn<VT, 0>(a, st, e0, e1); break;
+    case 1: launch_ingest_cn<VT, 1>(a, st, e0, e1); break;
+    case 2: launch_ingest_cn<VT, 2>(a, st, e0, e1); break;
+    case 3: launch_ingest_cn<VT, 3>(a, st, e0, e1); break;
+    case 4: launch_ingest_cn<VT, 4>(a, st, e0, e1); break;
+    case 5: launch_ingest_cn<VT, 5>(a, st, e0, e1); break;
+    case 6: launch_ingest_cn<VT, 6>(a, st, e0, e1); break;
+    default: launch_ingest_cn<VT, 7>(a, st, e0, e1); break;
   }
 }
 
@@ -1033,11 +1038,9 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
   hipLaunchKernelGGL(ck::count_cells_init_kernel, dim3((unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 4096)),
                      dim3(256), 0, st, a.cells, a.cell_cap);
   hipLaunchKernelGGL(ck::count_first_start_kernel, dim3(1), dim3(64), 0, st, a);
-  if (ingest_start) (void)hipEventRecord(ingest_start, st);
-  if (a.vt == VT_I32) launch_ingest_cv<VT_I32>(a, st);
-  else if (a.vt == VT_I64) launch_ingest_cv<VT_I64>(a, st);
-  else launch_ingest_cv<VT_F64>(a, st);
-  if (ingest_end) (void)hipEventRecord(ingest_end, st);
+  if (a.vt == VT_I32) launch_ingest_cv<VT_I32>(a, st, ingest_start, ingest_end);
+  else if (a.vt == VT_I64) launch_ingest_cv<VT_I64>(a, st, ingest_start, ingest_end);
+  else launch_ingest_cv<VT_F64>(a, st, ingest_start, ingest_end);
   // prefix max over the wave maxima
   const int64_t nb = (a.nwaves + 1023) / 1024;
   hipLaunchKernelGGL(ck::count_premax_block_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.stepmax, a.steppre,
