@@ -280,10 +280,11 @@ int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const Shar
     CCHK(dalloc(&d_te_pos, tecap));
     CCHK(dalloc(&d_te_g, tecap));
   }
-  if (nf > 0) {
-    std::vector<int64_t> zeros(nf, 0);
-    CCHK(hipMemcpyAsync(d_te_pos, zeros.data(), nf * 8, hipMemcpyHostToDevice, stream));
-    CCHK(hipMemcpyAsync(d_te_g, first.data(), nf * 8, hipMemcpyHostToDevice, stream));
+  if (nf > 0) {  // (member buffers: the copies may still read them after this call returns)
+    h_first_pos.assign(nf, 0);
+    h_first_g.assign(first.begin(), first.end());
+    CCHK(hipMemcpyAsync(d_te_pos, h_first_pos.data(), nf * 8, hipMemcpyHostToDevice, stream));
+    CCHK(hipMemcpyAsync(d_te_g, h_first_g.data(), nf * 8, hipMemcpyHostToDevice, stream));
   }
   int64_t nte = nf;
   if (nc > 0) {
@@ -542,11 +543,12 @@ int CEngine::shard_push(const int64_t* d_ts, const void* d_val, int64_t n, int64
     CCHK(launch_count_push(a, maxp, d_scan, d_premax, stream, nullptr, nullptr));
     CCHK(launch_count_export(a, d_rec, shard_cap, stream));
   } else {  // an empty chunk: no tuples, no edges, prefix max -inf
-    std::vector<int64_t> h(CSHARD_HDR, 0);
-    h[0] = JMIN;
-    h[4] = a.C;
+    CCHK(hipStreamSynchronize(stream));  // the previous header copy has read h_shard_hdr
+    h_shard_hdr.assign(CSHARD_HDR, 0);
+    h_shard_hdr[0] = JMIN;
+    h_shard_hdr[4] = a.C;
     CCHK(hipMemsetAsync(d_rec, 0, shard_words() * 8, stream));
-    CCHK(hipMemcpyAsync(d_rec, h.data(), CSHARD_HDR * 8, hipMemcpyHostToDevice, stream));
+    CCHK(hipMemcpyAsync(d_rec, h_shard_hdr.data(), CSHARD_HDR * 8, hipMemcpyHostToDevice, stream));
   }
   if (!shard_async) CCHK(hipStreamSynchronize(stream));  // the record is read by the collective on another stream
   return SCOTTY_OK;

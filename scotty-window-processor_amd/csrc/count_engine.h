@@ -125,6 +125,9 @@ class CEngine {
   int64_t* d_vals[SCOTTY_MAX_AGGS] = {};
   unsigned long long *d_pre_cnt = nullptr, *d_pre_sum = nullptr, *d_bsum = nullptr;
   std::vector<int64_t> h_start, h_end;
+  // host sources of asynchronous copies that outlive the call that queued them (the first walk's edges, an empty
+  // shard chunk's record header): rewritten only after the stream's next synchronisation
+  std::vector<int64_t> h_first_pos, h_first_g, h_shard_hdr;
 };
 
 }  // namespace scotty

@@ -782,7 +782,7 @@ int replay_after_overflow(scotty_op* op) {
       return fail(op, SCOTTY_ERR_UNSUPPORTED, "sharded batch exceeded the exchange capacity or the edge-grid horizon "
                                               "(scotty_tune \"shard_cells\" / \"shard_cands\")");
     const int64_t failed = m.failed_push;
-    int64_t zero = 0;
+    static const int64_t zero = 0;  // (static: the copy may read it after this scope ends)
     HIPCHK(hipMemcpyAsync(&op->d_meta->overflow, &zero, 8, hipMemcpyHostToDevice, op->stream));
     m.overflow = 0;
     int rc = maybe_extend_grid(op, true);
