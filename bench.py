@@ -1133,6 +1133,10 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
+    # stdout carries exactly one line, rank 0's JSON: anything else a library prints to file descriptor 1 (RCCL's
+    # version banner at communicator creation, on every rank) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1241,8 +1245,10 @@ def main():
                                        "java.util.Random(10), SUM_I32+COUNT, in-order, maxLateness=1",
                            "tuples_per_step": B * world, "tuples_per_step_per_gpu": B, "event_ms_per_step": 1000,
                            "windows_emitted": n_windows,
-                           "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch"
-                                           % world) if sharded else "single GPU",
+                           "parallelism": ("time-range shard x%d, RCCL all-gather of slice partials per micro-batch, "
+                                           "%s" % (world, "on the op's stream (no host sync)"
+                                                   if op.async_exchange else "host-synchronised"))
+                           if sharded else "single GPU",
                            **({"tune": dict(TUNE)} if TUNE else {})},
                 "roofline": roof,
             }
@@ -1314,7 +1320,7 @@ def main():
                 if name in extra:
                     extra[name]["cpu_baseline"] = fn()
                     log("bench: CPU %s done" % name)
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -189,10 +189,16 @@ int scotty_route_keyed(const uint32_t* key, const int64_t* ts, const void* val, 
  * is complete before the all-gather reads it); op_waits != 0: the op's stream waits for the work queued on `stream`
  * (the gathered records have landed before scotty_shard_commit reads them).  With scotty_tune("shard_async", 1) the
  * shard pushes then return without a host synchronisation.  `stream` is a hipStream_t (NULL: the default stream) of
- * the HIP runtime this library links: a caller with its own copy of the runtime (PyTorch wheels ship one) cannot
- * share streams or events with it, and host-synchronises both sides instead (the Python ShardedSlicingWindowOperator
- * does; shard_async stays off there). */
+ * the HIP runtime this library is bound to.  PyTorch wheels ship their own libamdhip64.so.7: imported first, it also
+ * serves this library (same soname, one runtime), and the Python ShardedSlicingWindowOperator orders torch's stream
+ * with this call; with two runtimes mapped (this library loaded before torch) it host-synchronises both sides. */
 int scotty_stream_order(scotty_op* op, void* stream, int op_waits);
+
+/* The op's own stream (a hipStream_t of the runtime this library is bound to), for a caller that queues its
+ * exchange on it directly (the Python ShardedSlicingWindowOperator runs the RCCL all-gather there, wrapped as a
+ * torch.cuda.ExternalStream: push, all-gather and commit then follow each other on one stream, no event, no host
+ * synchronisation). */
+void* scotty_op_stream(scotty_op* op);
 
 /* Number of keys (operators) of a keyed op. */
 int64_t scotty_key_count(scotty_op* op);

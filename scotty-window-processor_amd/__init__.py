@@ -124,7 +124,20 @@ def header_functions():
     """Function names declared by include/scotty_mi355x.h."""
     import re
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|uint64_t|int64_t|int32_t)\s+(scotty_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|void\*|const char\*|uint64_t|int64_t|int32_t)\s+(scotty_\w+)\(", txt, re.M)))
+
+
+def _single_hip_runtime():
+    """True when exactly one libamdhip64 is mapped into this process (after the library is loaded): the library
+    and torch then share one HIP runtime, and their streams and events can order each other."""
+    lib()
+    paths = set()
+    with open("/proc/self/maps") as f:
+        for line in f:
+            p = line.split()[-1]
+            if os.path.basename(p).startswith("libamdhip64.so"):
+                paths.add(os.path.realpath(p))
+    return len(paths) == 1
 
 
 def lib():
@@ -167,6 +180,7 @@ def lib():
             "scotty_sync": (ctypes.c_int, [P]),
             "scotty_key_shard": (ctypes.c_int32, [ctypes.c_uint32, ctypes.c_int, ctypes.c_int]),
             "scotty_stream_order": (ctypes.c_int, [P, P, ctypes.c_int]),
+            "scotty_op_stream": (P, [P]),
             "scotty_route_keyed": (ctypes.c_int, [P, P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                                   ctypes.c_int, ctypes.c_int, P, P, P, P]),
         }
@@ -377,6 +391,10 @@ class SlicingWindowOperator:
         True: the op's stream waits for the work queued on `stream`."""
         self._check(self._l.scotty_stream_order(self._h, stream, 1 if op_waits else 0))
 
+    def opStream(self):
+        """scotty_op_stream: the op's hipStream_t handle (an int)."""
+        return int(self._l.scotty_op_stream(self._h) or 0)
+
     def shardCommit(self, gathered_ptr, world):
         self._check(self._l.scotty_shard_commit(self._h, gathered_ptr, world))
 
@@ -560,10 +578,19 @@ class ShardedSlicingWindowOperator:
         self.world = dist.get_world_size(group)
         self.dev = torch.device("cuda", device)
         self.staged = dist.get_backend(group) != "nccl"
-        # No cross-stream event ordering: torch ships its own HIP runtime (torch/lib/libamdhip64.so) beside the one
-        # the library links (/opt/rocm), and an event or stream of one runtime means nothing to the other.  The
-        # push returns after its own stream has finished (shard_async off), and the commit waits for torch's
-        # stream to finish the collective.
+        # Stream ordering of the RCCL exchange.  With torch imported first, the library's libamdhip64.so.7 is bound
+        # to the runtime torch already loaded (same soname), so one HIP runtime serves both: the all-gather is then
+        # queued on the op's own stream (a torch.cuda.ExternalStream), between the push and the commit, with no
+        # host synchronisation per micro-batch.  When two runtimes are mapped (the library loaded before torch:
+        # INTEGRATION.md), a stream of one means nothing to the other, and the exchange falls back to host
+        # synchronisation on both sides.  SCOTTY_SHARD_SYNC=1 forces the fallback (A/B).
+        self.async_exchange = (not self.staged and _single_hip_runtime()
+                               and os.environ.get("SCOTTY_SHARD_SYNC", "0") == "0")
+        self._ext = None
+        if self.async_exchange:
+            self.op.tune("shard_async", 1)
+            # the all-gather runs on the op's own stream: push, collective and commit in stream order
+            self._ext = torch.cuda.ExternalStream(self.op.opStream(), device=self.dev)
         self._xb = None
         self._assigned = []
         self._measures = set()
@@ -630,6 +657,9 @@ class ShardedSlicingWindowOperator:
             self.dist.all_gather_into_tensor(self._hg, self._hx, group=self.group)
             gb.copy_(self._hg)
             self.torch.cuda.synchronize(self.dev)
+        elif self.async_exchange:
+            with self.torch.cuda.stream(self._ext):  # behind the push, ahead of the commit, on the op's stream
+                self.dist.all_gather_into_tensor(gb, xb, group=self.group)
         else:
             # the record is complete: the push synchronised the library's stream before returning
             self.dist.all_gather_into_tensor(gb, xb, group=self.group)

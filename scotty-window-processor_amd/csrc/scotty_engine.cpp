@@ -1881,4 +1881,6 @@ int scotty_stream_order(scotty_op* op, void* stream, int op_waits) {
   return SCOTTY_OK;
 }
 
+void* scotty_op_stream(scotty_op* op) { return op ? (void*)op->stream : nullptr; }
+
 }  // extern "C"

@@ -1,7 +1,8 @@
 """One rank of a sharded non-keyed run (launched by tests/test_gpu_shard.py through torch.distributed.run).
 Every rank feeds its arrival chunk of each global micro-batch and writes the windows of every watermark to
 <out>.rank<r> (every rank holds the same slice store, so every rank's rows are checked).  RCCL ("nccl"): no
-synchronisation by the test between chunks; the exchange buffer is poisoned on torch's stream before each chunk, so
+synchronisation by the test between chunks (and, unless SCOTTY_SHARD_SYNC=1, none by the operator: the exchange is
+ordered by events); the exchange buffer is poisoned on torch's stream before each chunk, so
 a commit that read it before the collective landed would fold garbage and fail the oracle comparison."""
 import json
 import os
@@ -46,6 +47,7 @@ def main():
             if backend == "nccl":
                 _, gb = op._bufs()
                 gb.fill_(-0x5A5A5A5A5A5A5A5A)  # poison: overwritten by the all-gather before the commit may read it
+                torch.cuda.synchronize(dev)  # (the fill runs on torch's stream, the exchange on the op's own)
             op.processChunk(t.data_ptr(), v.data_ptr(), b - a, int(ts[0]))
             if backend != "nccl":
                 torch.cuda.synchronize(dev)
@@ -59,6 +61,8 @@ def main():
                 continue
             res.append([list(w.key()[:4]) + [list(w.key()[4])] for w in ws] + [["dropped", op.droppedCount()]])
     json.dump(res, open("%s.rank%d" % (out, rank), "w"))
+    with open("%s.rank%d.mode" % (out, rank), "w") as f:
+        f.write("async" if op.async_exchange else "sync")
     dist.barrier()
     dist.destroy_process_group()
 

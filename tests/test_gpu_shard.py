@@ -17,10 +17,10 @@ from oracle.oracle import JavaError
 pytestmark = pytest.mark.gpu
 
 
-def _run_sharded(tmp_path, cid, nproc, backend):
+def _run_sharded(tmp_path, cid, nproc, backend, sync=False):
     out = str(tmp_path / "w.json")
-    port = str(29500 + cid + 8 * nproc + (os.getpid() % 400))
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    port = str(29500 + cid + 8 * nproc + (os.getpid() % 400) + (1000 if sync else 0))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", SCOTTY_SHARD_SYNC="1" if sync else "0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                         "--master-addr", "127.0.0.1", "--master-port", port,
                         os.path.join(ROOT, "tests", "shard_worker.py"), out, str(cid), backend],
@@ -28,13 +28,16 @@ def _run_sharded(tmp_path, cid, nproc, backend):
     return r, out
 
 
-@pytest.mark.parametrize("cid", [0, 4, 6])
-def test_rccl_exchange_single_rank_matches_oracle(tmp_path, cid):
-    """The RCCL ("nccl") exchange path -- device all-gather on torch's stream between the push (the library's
-    stream, synchronised) and the commit (after torch's stream is synchronised) -- on one rank of this one-GPU box:
-    time windows, count windows, count + time windows; the exchange buffer is poisoned before every chunk."""
-    r, out = _run_sharded(tmp_path, cid, 1, "nccl")
+@pytest.mark.parametrize("cid,sync", [(0, False), (1, False), (4, False), (6, False), (7, False), (0, True), (6, True)])
+def test_rccl_exchange_single_rank_matches_oracle(tmp_path, cid, sync):
+    """The RCCL ("nccl") exchange path on one rank of this one-GPU box: time windows (in order and out of order),
+    count windows, count + time windows; the exchange buffer is poisoned on torch's stream before every chunk.
+    Default: the all-gather queued on the op's own stream between the push and the commit (no host
+    synchronisation; the worker records that this mode ran); sync: SCOTTY_SHARD_SYNC=1, the push and torch's stream
+    synchronised by the host on both sides."""
+    r, out = _run_sharded(tmp_path, cid, 1, "nccl", sync)
     _check(r, out, cid, 1)
+    assert open(out + ".rank0.mode").read() == ("sync" if sync else "async")
 
 
 @pytest.mark.parametrize("cid", [0, 1, 2, 3, 4, 5, 6, 7])
