@@ -1258,6 +1258,11 @@ def main():
         batches = op = None
         torch.cuda.empty_cache()
         if world == 1:
+            if "pcie" in legs:
+                # first: run after the C4 leg in the same process, the host-fed steps take 18-19 ms instead of 14.4
+                # (plain pinned copies stay at 57 GB/s there; DESIGN.md §4, profiles/r06/ab/pcie_order/)
+                extra["pcie_inclusive"] = extra_pcie(pkg, sizes, 1 << 26, 5)
+                log("bench: PCIe-inclusive C2 done")
             if "c1" in legs:
                 extra["c1"] = extra_c1(pkg, dev, 1 << 26, 10)
                 log("bench: C1 done")
@@ -1293,9 +1298,6 @@ def main():
             if "c5t" in legs:
                 extra["c5t"] = extra_c5t(pkg, dev, 1 << 26, 5)
                 log("bench: C5t done")
-            if "pcie" in legs:
-                extra["pcie_inclusive"] = extra_pcie(pkg, sizes, 1 << 26, 5)
-                log("bench: PCIe-inclusive C2 done")
         else:  # every rank takes part: key-hash sharded C4, no collective on the data path
             extra = {"c4": extra_c4(pkg, dev, C4_BATCH, 1 << 20, 5, rank=rank, world=world, dist=dist),
                      "c5": extra_c5(pkg, dev, 1 << 27, 5, rank=rank, world=world, dist=dist),

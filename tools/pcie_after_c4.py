@@ -1,0 +1,46 @@
+"""Does a plain pinned host->HBM copy slow down after the C4 leg ran in the same process?  (The PCIe-inclusive leg
+measures 14.4 ms per step alone and 18-19 ms after C4: tools/gpu_r06_p17.sh / p18.)  Probe before, after C4, and
+after C4 with every C4 object released; one JSON line."""
+import gc
+import importlib
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import bench  # noqa: E402
+from pcie_probe import rate  # noqa: E402
+
+
+def probe(tag, out):
+    nb = 512 << 20
+    dev = torch.device("cuda", 0)
+    h = torch.empty(nb, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nb, dtype=torch.uint8, device=dev)
+    out[tag + "_h2d_pinned_GBs"] = rate(lambda: d.copy_(h, non_blocking=True), nb)
+    out[tag + "_d2d_GBs"] = rate(lambda: d[: nb // 2].copy_(d[nb // 2:]), nb // 2)
+    del h, d
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.init()
+    pkg = importlib.import_module("scotty-window-processor_amd")
+    out = {}
+    probe("before", out)
+    r = bench.extra_c4(pkg, dev, bench.C4_BATCH, 1 << 20, 5, host_steps=5)
+    out["c4_ms_per_step"] = r["ms_per_step"]
+    probe("after_c4", out)
+    del r
+    gc.collect()
+    torch.cuda.empty_cache()
+    probe("after_c4_released", out)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
