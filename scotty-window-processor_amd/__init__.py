@@ -660,6 +660,12 @@ class ShardedSlicingWindowOperator:
         elif self.async_exchange:
             with self.torch.cuda.stream(self._ext):  # behind the push, ahead of the commit, on the op's stream
                 self.dist.all_gather_into_tensor(gb, xb, group=self.group)
+            self.op.shardCommit(gb.data_ptr(), self.world)
+            # torch's stream waits for the chunk's push and commit (one event, no host wait): the caller's input
+            # tensors may be freed and their memory reused by torch as soon as processChunk returns, and torch's
+            # allocator only orders reuse on its own streams
+            self.op.streamOrder(self.torch.cuda.current_stream(self.dev).cuda_stream, False)
+            return
         else:
             # the record is complete: the push synchronised the library's stream before returning
             self.dist.all_gather_into_tensor(gb, xb, group=self.group)

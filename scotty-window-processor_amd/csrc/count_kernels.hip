@@ -55,6 +55,27 @@ __device__ __forceinline__ int64_t uni(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// First index in [l, h) where pred is false (pred true on a prefix of the range), h if there is none; searched by the
+// G lanes (lane = 0 .. G-1) of an aligned lane group together, G probes per round.  l, h group-uniform.
+template <int G, class P>
+__device__ __forceinline__ int64_t group_first_false(int64_t l, int64_t h, int lane, P pred) {
+  const int sh = (int)(threadIdx.x & 63) & ~(G - 1);
+  const unsigned long long gm = G == 64 ? ~0ull : ((1ull << G) - 1);
+  while (h - l > G) {
+    const int64_t stride = (h - l + G - 1) / G;
+    const int64_t p = l + (int64_t)lane * stride;
+    const bool t = p < h && pred(p);
+    const int c = __popcll((__ballot(t) >> sh) & gm);  // probes p_0 .. p_{c-1} true, p_c (if < h) false
+    if (c == 0) return l;
+    const int64_t pc = l + (int64_t)c * stride;
+    l = l + (int64_t)(c - 1) * stride + 1;
+    h = min(h, pc);
+  }
+  const int64_t p = l + lane;
+  const bool t = p < h && pred(p);
+  return l + __popcll((__ballot(t) >> sh) & gm);
+}
+
 // ---------------------------------------------------------------- 1. edge bitmap
 // blockIdx.y = window.  Points of window w in [lo, hi): tumbling multiples of size, sliding multiples of slide
 // (assignNextWindowStart, C/windowType/TumblingWindow.java:29-31, SlidingWindow.java:41-43), fixed band
@@ -99,12 +120,15 @@ __global__ void count_tcand_kernel(CTimeArgs a) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.n_cand) return;
   const int64_t g = a.step ? a.cand0 + k * a.step : a.cand[k];
+  // (a binary search per thread: lane groups searching together -- 8 or 64 lanes per candidate -- issued more loads
+  // than they saved latency, profiles/r06/ab/count_ingest/)
   int64_t l = a.start, h = a.n;
   while (l < h) {
     const int64_t m = (l + h) >> 1;
     if (a.ts[m] < g) l = m + 1; else h = m;
   }
-  const int64_t p = l;  // < n: the host enumerates candidates up to the batch's last (= max) ts
+  const int64_t p = l;
+  // p < n: the host enumerates candidates up to the batch's last (= max) ts
   const int64_t e = a.ts[p];
   const int64_t m = p > a.start ? a.ts[p - 1] : a.prev_max;
   // the pending edge is appended once crossed; a later grid point iff the running max before its first tuple
@@ -254,73 +278,59 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
   };
   typedef long long v2i64 __attribute__((ext_vector_type(2)));
   typedef int v2i32 __attribute__((ext_vector_type(2)));
-  // a step's tuples, its edge-bitmap word (lanes 0-7), slice base and packed time edges
-  auto ld = [&](int64_t s, int64_t* t, int64_t* v, bool* ok, uint32_t& bw, int64_t& sbv, uint32_t& tpv) {
-    const int64_t base = s * CSTEP;
-    const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
-    if (base + CSTEP <= a.n) {
-      const v2i64 ta = __builtin_nontemporal_load((const v2i64*)(a.ts + i0));
-      const v2i64 tb = __builtin_nontemporal_load((const v2i64*)(a.ts + i1));
-      t[0] = ta.x; t[1] = ta.y; t[2] = tb.x; t[3] = tb.y;
-      if constexpr (VT == VT_I32) {
-        const v2i32 va = __builtin_nontemporal_load((const v2i32*)((const int32_t*)a.val + i0));
-        const v2i32 vb = __builtin_nontemporal_load((const v2i32*)((const int32_t*)a.val + i1));
-        v[0] = va.x; v[1] = va.y; v[2] = vb.x; v[3] = vb.y;
-      } else {
-        const v2i64 va = __builtin_nontemporal_load((const v2i64*)((const int64_t*)a.val + i0));
-        const v2i64 vb = __builtin_nontemporal_load((const v2i64*)((const int64_t*)a.val + i1));
-        v[0] = va.x; v[1] = va.y; v[2] = vb.x; v[3] = vb.y;
-      }
-      ok[0] = ok[1] = ok[2] = ok[3] = true;
-    } else {  // ragged last step
-      const int64_t idx[4] = {i0, i0 + 1, i1, i1 + 1};
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        ok[j] = idx[j] < a.n;
-        t[j] = ok[j] ? a.ts[idx[j]] : JMIN;
-        if constexpr (VT == VT_I32) v[j] = ok[j] ? (int64_t)((const int32_t*)a.val)[idx[j]] : 0;
-        else v[j] = ok[j] ? ((const int64_t*)a.val)[idx[j]] : 0;
-      }
-    }
-    const int64_t wi = s * 8 + lane;
-    bw = lane < 8 && wi < a.nwords ? a.bits[wi] : 0u;
-    sbv = a.stepbase[s];
-    tpv = a.n_te > 0 ? a.steptp[s] : 0u;
+  using VV = typename std::conditional<VT == VT_I32, v2i32, v2i64>::type;
+  using VE = typename std::conditional<VT == VT_I32, int32_t, int64_t>::type;
+  // A full step's loads, kept as loaded (vectors, no conversion: a conversion at the load would wait for the data
+  // there) -- the step's edge-bitmap word (lanes 0-7), slice base and packed time edges first, then its tuples, so
+  // the scalars of the next step can be read while later steps' tuples are still in flight.  Two steps are in
+  // flight ahead of the one being combined (one was not enough: a wave waited a full HBM round trip per step).
+  struct CStep {
+    uint32_t bw, tp;
+    int64_t sb;
+    v2i64 ta, tb;
+    VV va, vb;
   };
-  int64_t nt[4], nv[4], nsb;
-  bool nok[4];
-  uint32_t nbw, ntp;
-  ld(s0, nt, nv, nok, nbw, nsb, ntp);
+  const int64_t nfull = a.n / CSTEP;        // steps with CSTEP tuples
+  const int64_t e1 = min(s1, nfull);        // the wave's full steps [s0, e1); a ragged last step after them
+  auto ld_full = [&](int64_t s, CStep& st) {  // s < nfull: every load unconditional, every value as loaded
+    const int64_t base = s * CSTEP;
+    st.bw = a.bits[min(s * 8 + lane, a.nwords - 1)];  // (lanes 0-7 hold the step's words; masked at use)
+    st.sb = a.stepbase[s];
+    st.tp = a.steptp[s];  // (meaningful when a.n_te > 0; masked at use)
+    const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
+    st.ta = __builtin_nontemporal_load((const v2i64*)(a.ts + i0));
+    st.tb = __builtin_nontemporal_load((const v2i64*)(a.ts + i1));
+    st.va = __builtin_nontemporal_load((const VV*)((const VE*)a.val + i0));
+    st.vb = __builtin_nontemporal_load((const VV*)((const VE*)a.val + i1));
+  };
+  auto unpack = [&](const CStep& st, int64_t* t, int64_t* v) {
+    t[0] = st.ta.x; t[1] = st.ta.y; t[2] = st.tb.x; t[3] = st.tb.y;
+    v[0] = (int64_t)st.va.x; v[1] = (int64_t)st.va.y; v[2] = (int64_t)st.vb.x; v[3] = (int64_t)st.vb.y;
+  };
   // in-order batches: the ts before the wave's first tuple (a count edge's slice start)
   int64_t prev_last = JMIN;
   if (a.check_sorted) prev_last = s0 > 0 ? a.ts[s0 * CSTEP - 1] : (a.shard ? JMIN : (int64_t)a.meta->prev_max);
-  for (int64_t s = s0; s < s1; s++) {
+  // one step: t/v/ok its tuples, bw_ its bitmap word (lanes 0-7), sb_ / tp_ its slice base and packed time edges
+  auto step = [&](int64_t s, const int64_t (&t)[4], const int64_t (&v)[4], const bool (&ok)[4], uint32_t bw_,
+                  int64_t sb_, uint32_t tp_) {
     const int64_t base = s * CSTEP;
     const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
-    int64_t t[4], v[4];
-    bool ok[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      t[j] = nt[j];
-      v[j] = nv[j];
-      ok[j] = nok[j];
-    }
-    const uint32_t bw = nbw, tp = __builtin_amdgcn_readfirstlane(ntp);
-    const int64_t sb = uni(nsb);
-    const bool more = s + 1 < s1;
-    if (more) ld(s + 1, nt, nv, nok, nbw, nsb, ntp);
+    const uint32_t bw = lane < 8 && s * 8 + lane < a.nwords ? bw_ : 0u;
+    const uint32_t tp = a.n_te > 0 ? __builtin_amdgcn_readfirstlane(tp_) : 0u;
+    const int64_t sb = uni(sb_);
     int64_t before_step = JMIN;  // ts of the tuple before this step (in-order batches)
     if (a.check_sorted) {
       before_step = prev_last;
       prev_last = (int64_t)__shfl((long long)t[3], 63);
-      // the time-edge search (count_tcand_kernel) assumes a nondecreasing batch
+      // the time-edge search (count_tcand_kernel) assumes a nondecreasing batch: every adjacent pair inside the step,
+      // and the pair across the step's start (the tuple before it: the previous step's last, or the one before the
+      // wave's range) -- so no step needs the next step's tuples
       const int64_t n0 = (int64_t)__shfl_down((long long)t[0], 1), n2 = (int64_t)__shfl_down((long long)t[2], 1);
       const int64_t l2 = (int64_t)__shfl((long long)t[2], 0);
-      const int64_t nx = more ? (int64_t)__shfl((long long)nt[0], 0) : (i1 + 2 < a.n ? a.ts[i1 + 2] : JMAX);
       const int64_t s1_ = lane < 63 ? n0 : l2;  // successor of i0 + 1
-      const int64_t s3 = lane < 63 ? n2 : nx;   // successor of i1 + 1
       const bool bad = (i0 + 1 < a.n && t[1] < t[0]) || (i0 + 2 < a.n && s1_ < t[1]) ||
-                       (i1 + 1 < a.n && t[3] < t[2]) || (i1 + 2 < a.n && s3 < t[3]);
+                       (i1 + 1 < a.n && t[3] < t[2]) || (lane < 63 && i1 + 2 < a.n && n2 < t[3]) ||
+                       (lane == 0 && base > 0 && base < a.n && t[0] < before_step);
       if (bad) atomicOr((unsigned long long*)&a.meta->err, 8ull);
     }
     // edge words of the step (wave-uniform) and its time edges
@@ -352,7 +362,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         if (t[j] < first_start) n_late++;
         else add(t[j], v[j]);
       }
-      continue;
+      return;
     }
     // time edges at in-step offsets <= o (le) or < o
     auto tcount = [&](int o, bool le) -> int64_t {
@@ -490,7 +500,7 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         if (t[j] < first_start) n_late++;
         else if (cell[j] == last) add(t[j], v[j]);
       }
-      continue;
+      return;
     }
     // many edges in the step: the last cell in registers, other tuples straight to their cell
     if (last != cur) {
@@ -513,6 +523,49 @@ __global__ __launch_bounds__(256) void count_ingest_kernel(CPushArgs a) {
         cell_add<VT, NEED>(a.cells, cell[j], 1, t[j], t[j], w, __longlong_as_double((long long)w), l, h);
       }
     }
+  };
+  // full steps, two in flight ahead of the one combined: buffers a_ / b_ take turns (no register copies: a copy of
+  // a buffer whose loads are in flight waits for them); the loads of step s + 2 are clamped to the wave's last full
+  // step (unconditional: nothing waits for them before their use)
+  if (s0 < e1) {
+    CStep a_, b_;
+    ld_full(s0, a_);
+    ld_full(min(s0 + 1, e1 - 1), b_);
+    const bool all_ok[4] = {true, true, true, true};
+    auto run = [&](int64_t s, CStep& buf, int64_t reload) {
+      int64_t t[4], v[4];
+      unpack(buf, t, v);
+      const uint32_t bw = buf.bw, tp = buf.tp;
+      const int64_t sb = buf.sb;
+      step(s, t, v, all_ok, bw, sb, tp);
+      ld_full(min(reload, e1 - 1), buf);
+    };
+    const int64_t npair = (e1 - s0) / 2;
+    for (int64_t k = 0; k < npair; k++) {
+      const int64_t s = s0 + 2 * k;
+      run(s, a_, s + 2);
+      run(s + 1, b_, s + 3);
+    }
+    if ((e1 - s0) & 1) run(e1 - 1, a_, e1 - 1);
+  }
+  if (e1 < s1) {  // the batch's ragged last step (s = nfull, fewer than CSTEP tuples)
+    const int64_t s = e1;
+    const int64_t base = s * CSTEP;
+    const int64_t i0 = base + 2 * lane, i1 = base + 128 + 2 * lane;
+    const int64_t idx[4] = {i0, i0 + 1, i1, i1 + 1};
+    int64_t t[4], v[4];
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      ok[j] = idx[j] < a.n;
+      t[j] = ok[j] ? a.ts[idx[j]] : JMIN;
+      if constexpr (VT == VT_I32) v[j] = ok[j] ? (int64_t)((const int32_t*)a.val)[idx[j]] : 0;
+      else v[j] = ok[j] ? ((const int64_t*)a.val)[idx[j]] : 0;
+    }
+    const int64_t wi = s * 8 + lane;
+    const uint32_t bw = lane < 8 && wi < a.nwords ? a.bits[wi] : 0u;
+    const uint32_t tp = a.n_te > 0 ? a.steptp[s] : 0u;
+    step(s, t, v, ok, bw, a.stepbase[s], tp);
   }
   if (cur >= 0) flush();
   const uint32_t nl = wred(n_late, [](uint32_t p, uint32_t q) { return p + q; });
@@ -681,15 +734,26 @@ __global__ void count_wm_find_kernel(CWmArgs a) {
 // LazyAggregateStore.aggregate start/end index (S/aggregationstore/LazyAggregateStore.java:83-90; with no time
 // windows minTs = MAX, maxTs = 0)
 __global__ void count_wm_range_kernel(CWmArgs a) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (blockIdx.x != 0) return;
+  const int lane = threadIdx.x;
   CMeta& m = *a.meta;
   const int64_t head = m.head, tail = m.tail, S = tail - head;
   auto rel = [&](int64_t i) { return i < head ? (int64_t)-1 : i - head; };
-  // cLast is not stored; cStart is nondecreasing, findSliceIndexByCount = last slice with cStart <= c
-  int64_t si = max(rel(last_le(a.sl.ts, head, tail, a.min_ts)), (int64_t)0);
-  si = min(si, rel(last_le(a.sl.cs, head, tail, a.min_count)));
-  int64_t ei = min(S - 1, rel(last_le(a.sl.ts, head, tail, a.max_ts)));
-  ei = max(ei, rel(last_le(a.sl.cs, head, tail, a.max_count)));
+  // cLast is not stored; cStart is nondecreasing, findSliceIndexByCount = last slice with cStart <= c.  The four
+  // searches are independent: lanes 0-3 run one each (one chain of dependent loads instead of four in a row)
+  int64_t r = 0;
+  if (lane < 4) {
+    const int64_t* key = (lane & 1) ? a.sl.cs : a.sl.ts;
+    const int64_t x = lane == 0 ? a.min_ts : lane == 1 ? a.min_count : lane == 2 ? a.max_ts : a.max_count;
+    r = rel(last_le(key, head, tail, x));
+  }
+  const int64_t r_ts_lo = (int64_t)__shfl((long long)r, 0), r_c_lo = (int64_t)__shfl((long long)r, 1);
+  const int64_t r_ts_hi = (int64_t)__shfl((long long)r, 2), r_c_hi = (int64_t)__shfl((long long)r, 3);
+  if (lane != 0) return;
+  int64_t si = max(r_ts_lo, (int64_t)0);
+  si = min(si, r_c_lo);
+  int64_t ei = min(S - 1, r_ts_hi);
+  ei = max(ei, r_c_hi);
   if (si < 0 && si <= ei) {
     m.range_err = 1;
     si = 0;
@@ -799,19 +863,28 @@ __global__ __launch_bounds__(256) void count_wm_agg_kernel(CWmArgs a) {
   // contained slices (AggregateWindowState.containsSlice, S/state/AggregateWindowState.java:25-35): count
   // measure ws <= cStart && we >= cLast, cStart >= ws a suffix and cLast = cStart + cnt <= we a prefix; time
   // measure ws <= tStart && we > tLast, both nondecreasing on an in-order stream's slices
-  int64_t l = r_lo, h = r_hi;
-  while (l < h) {
-    const int64_t mid = (l + h) >> 1;
-    if ((tmeas ? a.sl.ts[mid] : a.sl.cs[mid]) < ws) l = mid + 1; else h = mid;
+  int64_t lo, hi;
+  if (!tmeas) {
+    // count measure: cStart and cLast are nondecreasing on the count path's slices, so the window's G lanes search
+    // together, G probes per round (log_G instead of log_2 rounds of dependent loads)
+    lo = group_first_false<G>(r_lo, r_hi, lane, [&](int64_t i) { return a.sl.cs[i] < ws; });
+    hi = group_first_false<G>(lo, r_hi, lane,
+                              [&](int64_t i) { return a.sl.cs[i] + (int64_t)a.sl.cnt[i] <= we; });
+  } else {
+    int64_t l = r_lo, h = r_hi;
+    while (l < h) {
+      const int64_t mid = (l + h) >> 1;
+      if (a.sl.ts[mid] < ws) l = mid + 1; else h = mid;
+    }
+    lo = l;
+    l = lo;
+    h = r_hi;
+    while (l < h) {
+      const int64_t mid = (l + h) >> 1;
+      if (a.sl.tl[mid] < we) l = mid + 1; else h = mid;
+    }
+    hi = l;
   }
-  const int64_t lo = l;
-  l = lo;
-  h = r_hi;
-  while (l < h) {
-    const int64_t mid = (l + h) >> 1;
-    if (tmeas ? a.sl.tl[mid] < we : a.sl.cs[mid] + (int64_t)a.sl.cnt[mid] <= we) l = mid + 1; else h = mid;
-  }
-  const int64_t hi = l;
   uint64_t cnt = 0, sw = 0;
   double sf = 0.0;
   int64_t mn = ID_MIN, mx = ID_MAX;

@@ -48,6 +48,8 @@ def main():
                 _, gb = op._bufs()
                 gb.fill_(-0x5A5A5A5A5A5A5A5A)  # poison: overwritten by the all-gather before the commit may read it
                 torch.cuda.synchronize(dev)  # (the fill runs on torch's stream, the exchange on the op's own)
+            # (t and v are dropped at the next push: their memory goes back to torch's allocator while the op's
+            # stream may still read them -- the operator orders torch's stream after the chunk, so the reuse waits)
             op.processChunk(t.data_ptr(), v.data_ptr(), b - a, int(ts[0]))
             if backend != "nccl":
                 torch.cuda.synchronize(dev)
