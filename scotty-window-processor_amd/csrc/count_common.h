@@ -158,6 +158,7 @@ struct CWmArgs {
   const int64_t* w_end;
   const int32_t* w_meas;         // [nw] SCOTTY_MEASURE_* of each window
   int64_t min_ts, max_ts;        // LazyAggregateStore.aggregate arguments (time part)
+  int64_t ts_sorted_from;        // slices from here on have nondecreasing tStart / tLast (CEngine::ts_sorted_from)
   int64_t nw;
   int32_t need, vt, n_aggs, prefix;  // prefix: all aggregations invertible integer kinds -> prefix sums
   int32_t agg_kind[8];

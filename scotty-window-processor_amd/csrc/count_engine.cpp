@@ -232,6 +232,7 @@ int CEngine::time_edges(const int64_t* d_ts, int64_t n, CPushArgs& a, const Shar
     prev = std::max(prev, te);
   }
   const int64_t nf_all = (int64_t)first.size();
+  if (!started) ts_sorted_from = 1 + nf_all;
   if (!first_here) first.clear();
   // union grid from the pending edge up to the batch max: the chunk's candidates are the points in (prev, t_last]
   std::vector<int64_t> cand;
@@ -379,6 +380,7 @@ int CEngine::grow_slices(int64_t need_more) {
   scap = ncap;
   tail_ub = S;
   head_lb = 0;
+  ts_sorted_from = std::max<int64_t>(0, ts_sorted_from - head);
   return SCOTTY_OK;
 }
 
@@ -783,6 +785,7 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   a.max_count = max_c;
   a.min_ts = min_t;
   a.max_ts = max_t;
+  a.ts_sorted_from = ts_sorted_from;
   a.w_meas = d_meas;
   a.gc_before = jsub(jsub(wm, max_lateness), max_fixed);
   a.w_start = d_wstart;

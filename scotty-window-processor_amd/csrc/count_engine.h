@@ -92,6 +92,9 @@ class CEngine {
   int64_t* h_tmp = nullptr;  // pinned scratch (batch ends, edge count)
   uint64_t dropped_ = 0;
   int64_t tail_ub = 0, head_lb = 0;  // slice range bounds between synchronisations
+  // slices [ts_sorted_from, tail) have nondecreasing tStart and tLast: only the stream's first tuple puts slices out of
+  // order (its own slice, then the time edges its walk crosses below its timestamp, all at position 0)
+  int64_t ts_sorted_from = 0;
   // device
   CMeta* d_meta = nullptr;
   CMeta* h_meta = nullptr;  // pinned, host-mapped

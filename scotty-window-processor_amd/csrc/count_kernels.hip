@@ -870,6 +870,9 @@ __global__ __launch_bounds__(256) void count_wm_agg_kernel(CWmArgs a) {
     lo = group_first_false<G>(r_lo, r_hi, lane, [&](int64_t i) { return a.sl.cs[i] < ws; });
     hi = group_first_false<G>(lo, r_hi, lane,
                               [&](int64_t i) { return a.sl.cs[i] + (int64_t)a.sl.cnt[i] <= we; });
+  } else if (r_lo >= a.ts_sorted_from) {  // time measure over slices past the first tuple's: tStart / tLast sorted
+    lo = group_first_false<G>(r_lo, r_hi, lane, [&](int64_t i) { return a.sl.ts[i] < ws; });
+    hi = group_first_false<G>(lo, r_hi, lane, [&](int64_t i) { return a.sl.tl[i] < we; });
   } else {
     int64_t l = r_lo, h = r_hi;
     while (l < h) {
