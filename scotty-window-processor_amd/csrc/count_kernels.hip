@@ -105,13 +105,47 @@ __global__ __launch_bounds__(256) void count_mark_kernel(CPushArgs a) {
 }
 
 // first time edge with batch position >= x
-__device__ __forceinline__ int64_t te_lb(const CPushArgs& a, int64_t x) {
-  int64_t l = 0, h = a.n_te;
+// First index in [lo, hi) with key >= g (key nondecreasing), hi if none, searched from a guess p: a galloping search
+// outwards from p, then bisection inside the bracket -- O(log distance) dependent loads, 1-2 when the guess is close
+// (event times and edge positions of a batch are near-uniform; a bisection from scratch took log2(n))
+__device__ __forceinline__ int64_t lb_from(const int64_t* key, int64_t lo, int64_t hi, int64_t g, int64_t p) {
+  p = p < lo ? lo : (p > hi ? hi : p);
+  int64_t l, h;  // the answer lies in [l, h]
+  if (p < hi && key[p] < g) {
+    l = p + 1;
+    h = hi;
+    for (int64_t d = 1;; d <<= 1) {
+      const int64_t q = p + d;
+      if (q >= hi) break;
+      if (key[q] >= g) {
+        h = q;
+        break;
+      }
+      l = q + 1;
+    }
+  } else {
+    l = lo;
+    h = p;
+    for (int64_t d = 1;; d <<= 1) {
+      const int64_t q = p - d;
+      if (q < lo) break;
+      if (key[q] < g) {
+        l = q + 1;
+        break;
+      }
+      h = q;
+    }
+  }
   while (l < h) {
     const int64_t m = (l + h) >> 1;
-    if (a.te_pos[m] < x) l = m + 1; else h = m;
+    if (key[m] < g) l = m + 1; else h = m;
   }
   return l;
+}
+// time edges before batch position x; guess: edges spread evenly over the batch
+__device__ __forceinline__ int64_t te_lb(const CPushArgs& a, int64_t x) {
+  const int64_t guess = a.n > 0 ? (int64_t)((double)x / (double)a.n * (double)a.n_te) : 0;
+  return lb_from(a.te_pos, 0, a.n_te, x, guess);
 }
 
 // ---------------------------------------------------------------- 1b. time edges (time windows, in-order stream)
@@ -120,14 +154,14 @@ __global__ void count_tcand_kernel(CTimeArgs a) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= a.n_cand) return;
   const int64_t g = a.step ? a.cand0 + k * a.step : a.cand[k];
-  // (a binary search per thread: lane groups searching together -- 8 or 64 lanes per candidate -- issued more loads
-  // than they saved latency, profiles/r06/ab/count_ingest/)
-  int64_t l = a.start, h = a.n;
-  while (l < h) {
-    const int64_t m = (l + h) >> 1;
-    if (a.ts[m] < g) l = m + 1; else h = m;
-  }
-  const int64_t p = l;
+  // the first tuple >= g: a galloping search from the position the batch's first and last timestamps interpolate
+  // (lane groups searching together -- 8 or 64 lanes per candidate -- issued more loads than they saved latency,
+  // profiles/r06/ab/count_ingest/)
+  const int64_t t0 = a.ts[a.start], t1 = a.ts[a.n - 1];
+  double r = t1 > t0 ? ((double)g - (double)t0) / ((double)t1 - (double)t0) : 0.0;  // (no int64 wrap)
+  r = r > 0.0 ? (r < 1.0 ? r : 1.0) : 0.0;                                            // (NaN -> 0)
+  const int64_t guess = a.start + (int64_t)(r * (double)(a.n - 1 - a.start));
+  const int64_t p = lb_from(a.ts, a.start, a.n, g, guess);
   // p < n: the host enumerates candidates up to the batch's last (= max) ts
   const int64_t e = a.ts[p];
   const int64_t m = p > a.start ? a.ts[p - 1] : a.prev_max;
