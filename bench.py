@@ -1167,6 +1167,14 @@ def main():
     nroof = max(1, args.roof_steps)
     nsteps = args.steps + args.warmup + nroof
 
+    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c4s", "c4c", "c5", "c5t", "pcie"}
+    pcie = None
+    if world == 1 and not args.no_extra and "pcie" in legs:
+        # before everything else: once the headline's or C4's device buffers have come and gone, the leg's first pinned
+        # staging allocation makes its host-fed steps 17.7-19.4 ms instead of 14.4 (plain pinned copies stay at
+        # 57 GB/s; DESIGN.md §4, profiles/r06/ab/pcie_order/)
+        pcie = extra_pcie(pkg, sizes, 1 << 26, 5)
+        log("bench: PCIe-inclusive C2 done")
     res = {"metric": METRIC, "skipped_headline": True} if rank == 0 else None
     batches = op = None
     if not args.skip_headline:
@@ -1252,17 +1260,13 @@ def main():
                            **({"tune": dict(TUNE)} if TUNE else {})},
                 "roofline": roof,
             }
-    legs = set(x for x in args.only.split(",") if x) or {"c1", "c2s", "c3", "c4", "c4s", "c4c", "c5", "c5t", "pcie"}
     extra = {}
     if not args.no_extra:
         batches = op = None
         torch.cuda.empty_cache()
         if world == 1:
-            if "pcie" in legs:
-                # first: run after the C4 leg in the same process, the host-fed steps take 18-19 ms instead of 14.4
-                # (plain pinned copies stay at 57 GB/s there; DESIGN.md §4, profiles/r06/ab/pcie_order/)
-                extra["pcie_inclusive"] = extra_pcie(pkg, sizes, 1 << 26, 5)
-                log("bench: PCIe-inclusive C2 done")
+            if pcie is not None:
+                extra["pcie_inclusive"] = pcie
             if "c1" in legs:
                 extra["c1"] = extra_c1(pkg, dev, 1 << 26, 10)
                 log("bench: C1 done")
