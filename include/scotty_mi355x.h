@@ -151,6 +151,10 @@ int scotty_process_watermark_device(scotty_op* op, int64_t watermark_ts, scotty_
  *   2. the caller all-gathers the G records in rank order into one device buffer (RCCL / NCCL all_gather);
  *   3. scotty_shard_commit(op, gathered, G): every rank decides the same slice edges (StreamSlicer rule from
  *      the global first crossings, S/StreamSlicer.java:55-116) and folds every rank's partials.
+ * Without shard_async the push returns after the op's stream finished (the chunk's buffers are free again);
+ * with scotty_tune("shard_async", 1) it returns at once and, as for scotty_process_elements_device, the chunk's
+ * buffers must stay valid and unmodified until the op's stream has run the push (order the caller's stream after
+ * it with scotty_stream_order, or wait for the next watermark).
  * Watermarks then run unchanged (and identically) on every rank.  Context-free time windows only (the grid
  * path), or count windows with optional context-free time windows (the count path, with
  * scotty_shard_push_counted / scotty_shard_push_timed); other configurations return SCOTTY_ERR_UNSUPPORTED. */
