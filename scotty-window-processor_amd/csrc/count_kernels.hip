@@ -712,6 +712,26 @@ __global__ __launch_bounds__(256) void count_append_kernel(CPushArgs a) {
   }
 }
 
+// cells to identity, plus (block 0, thread 0) the batch's edge count and the first-push scalars: one launch for what were
+// three (count_nedges_kernel + count_cells_init_kernel + count_first_start_kernel, kept below for reference)
+__global__ void count_prep_kernel(CPushArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t last = a.nsteps - 1;
+    CMeta& m = *a.meta;
+    m.n_edges = a.stepbase[last] + a.stepc[last];
+    m.first_start = m.tail > m.head ? a.sl.ts[m.head] : (a.shard ? a.ts0 : a.ts[0]);
+    m.late_push = 0;
+  }
+  const CCells& c = a.cells;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.cell_cap; j += (int64_t)gridDim.x * blockDim.x) {
+    c.cnt[j] = 0;
+    c.tl[j] = JMIN;
+    c.tf[j] = JMAX;
+    c.p[0][j] = 0;
+    c.p[1][j] = (unsigned long long)ID_MIN;
+    c.p[2][j] = (unsigned long long)ID_MAX;
+  }
+}
 __global__ void count_nedges_kernel(CPushArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int64_t last = a.nsteps - 1;
@@ -876,6 +896,71 @@ __global__ __launch_bounds__(1024) void count_pre_bscan_kernel(CWmArgs a, unsign
   if (tid == 0 && n >= 0) {
     a.pre_cnt[n] = carry[0];
     a.pre_sum[n] = carry[1];
+  }
+}
+// the same exclusive prefix sums (and the range totals at index n) in one workgroup, 8 slices per thread per round:
+// one launch instead of three for the few thousand slices a watermark usually scans
+__global__ __launch_bounds__(1024) void count_pre_one_kernel(CWmArgs a) {
+  constexpr int PER = 8;
+  __shared__ unsigned long long wt[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t lo = a.meta->r_lo, n = a.meta->r_hi - lo;
+  unsigned long long cc = 0, cs = 0;  // running totals before the round
+  for (int64_t base = 0; base < n; base += 1024 * PER) {
+    unsigned long long vc[PER], vs[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int64_t i = base + (int64_t)tid * PER + j;
+      vc[j] = i < n ? a.sl.cnt[lo + i] : 0;
+      vs[j] = i < n ? a.sl.p[0][lo + i] : 0;
+    }
+    unsigned long long tc = 0, ts_ = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      tc += vc[j];
+      ts_ += vs[j];
+    }
+    unsigned long long ic = tc, is = ts_;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long uc = __shfl_up(ic, o), us = __shfl_up(is, o);
+      if (lane >= o) {
+        ic += uc;
+        is += us;
+      }
+    }
+    if (lane == 63) {
+      wt[0][wid] = ic;
+      wt[1][wid] = is;
+    }
+    __syncthreads();
+    unsigned long long bc = cc, bs = cs, totc = cc, tots = cs;
+    for (int w = 0; w < 16; w++) {
+      if (w < wid) {
+        bc += wt[0][w];
+        bs += wt[1][w];
+      }
+      totc += wt[0][w];
+      tots += wt[1][w];
+    }
+    unsigned long long rc = bc + ic - tc, rs = bs + is - ts_;  // exclusive prefix of this thread's first slice
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const int64_t i = base + (int64_t)tid * PER + j;
+      if (i < n) {
+        a.pre_cnt[i] = rc;
+        a.pre_sum[i] = rs;
+      }
+      rc += vc[j];
+      rs += vs[j];
+    }
+    cc = totc;
+    cs = tots;
+    __syncthreads();
+  }
+  if (tid == 0 && n >= 0) {
+    a.pre_cnt[n] = cc;
+    a.pre_sum[n] = cs;
   }
 }
 __global__ __launch_bounds__(1024) void count_pre_add_kernel(CWmArgs a, const unsigned long long* bsum) {
@@ -1144,14 +1229,13 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
   hipLaunchKernelGGL(ck::count_stepc_kernel, dim3((unsigned)((a.nsteps + 255) / 256)), dim3(256), 0, st, a);
   hipError_t e = launch_scan_i64(a.stepc, a.stepbase, a.nsteps, scan_tmp, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ck::count_nedges_kernel, dim3(1), dim3(64), 0, st, a);
-  hipLaunchKernelGGL(ck::count_cells_init_kernel, dim3((unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 4096)),
-                     dim3(256), 0, st, a.cells, a.cell_cap);
-  hipLaunchKernelGGL(ck::count_first_start_kernel, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(ck::count_prep_kernel, dim3((unsigned)std::min<int64_t>((a.cell_cap + 255) / 256, 4096)), dim3(256),
+                     0, st, a);
   if (a.vt == VT_I32) launch_ingest_cv<VT_I32>(a, st, ingest_start, ingest_end);
   else if (a.vt == VT_I64) launch_ingest_cv<VT_I64>(a, st, ingest_start, ingest_end);
   else launch_ingest_cv<VT_F64>(a, st, ingest_start, ingest_end);
-  // prefix max over the wave maxima
+  // prefix max over the wave maxima (a one-workgroup variant, count_premax_one_kernel, measured no faster: its
+  // 16-values-per-thread loads do not coalesce)
   const int64_t nb = (a.nwaves + 1023) / 1024;
   hipLaunchKernelGGL(ck::count_premax_block_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a.stepmax, a.steppre,
                      a.nwaves, premax_tmp);
@@ -1216,7 +1300,9 @@ hipError_t launch_count_wm_find(const CWmArgs& a, hipStream_t st) {
 hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st) {
   hipLaunchKernelGGL(ck::count_wm_range_kernel, dim3(1), dim3(64), 0, st, a);
   if (a.nw > 0) {
-    if (a.prefix) {
+    if (a.prefix && range_blocks <= 64) {  // (<= 2^16 slices in range: one workgroup)
+      hipLaunchKernelGGL(ck::count_pre_one_kernel, dim3(1), dim3(1024), 0, st, a);
+    } else if (a.prefix) {
       hipLaunchKernelGGL(ck::count_pre_block_kernel, dim3((unsigned)std::max<int64_t>(1, range_blocks)), dim3(1024), 0,
                          st, a, bsum);
       hipLaunchKernelGGL(ck::count_pre_bscan_kernel, dim3(1), dim3(1024), 0, st, a, bsum,
