@@ -242,7 +242,8 @@ int scotty_device_timing(scotty_op* op, int cls, double* total_ms, uint64_t* int
  * segmented-reduction count path; an out-of-order tuple that would move records then fails loudly -- without the
  * promise they run on the exact engine, which keeps the record sets), "ingest_blocks", "shard_cells" / "shard_cands" (cells /
  * edge candidates per rank record of the time-window exchange), "shard_count_cells" (count cells per rank record
- * of the count-window exchange), "shard_async" 1 (shard pushes return without a host synchronisation: the caller
+ * of the count-window exchange), "count_prefix_one" 0 (the count path's watermark prefix sums by three kernels
+ * instead of one workgroup; tests), "shard_async" 1 (shard pushes return without a host synchronisation: the caller
  * orders its collective's stream with scotty_stream_order -- same HIP runtime only, see there), "exact_prefix" n
  * (exact engine, non-keyed: the first event-exact piece of a batch the one-pass quiet path refused, in tuples;
  * 0 = max(batch / 32, 2^20); later pieces grow 4x; the split is invisible in the results), "quiet_band" 1 (exact

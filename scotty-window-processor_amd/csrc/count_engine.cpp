@@ -15,7 +15,8 @@ hipError_t launch_count_push(const CPushArgs& a, int64_t max_points_per_window, 
 hipError_t launch_count_wm_find(const CWmArgs& a, hipStream_t st);
 hipError_t launch_count_export(const CPushArgs& a, int64_t* rec, int64_t cap, hipStream_t st);
 hipError_t launch_count_shard_commit(const CShardArgs& a, int64_t max_edges, hipStream_t st);
-hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st);
+hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st,
+                               bool one_wg);
 hipError_t launch_count_gc(const CWmArgs& a, hipStream_t st);
 hipError_t launch_count_time_edges(const CTimeArgs& a, int64_t* scan_tmp, hipStream_t st);
 hipError_t launch_count_rows(const CRowSeg* segs, const int64_t* seg_off, int nseg, int64_t* w_start, int64_t* w_end,
@@ -805,7 +806,7 @@ int CEngine::watermark(int64_t wm, XResult& r, bool to_host) {
   // LazyAggregateStore.aggregate runs only with windows (S/WindowManager.java:73-75), then clearAfterWatermark(wm -
   // maxLateness) (:82-95) -- which the GC kernel skips when the aggregation's range check threw; the host learns
   // that at the one synchronisation below, with the result copies
-  if (nw > 0) CCHK(launch_count_wm_agg(a, (S_ub + 1023) / 1024 + 1, d_bsum, stream));
+  if (nw > 0) CCHK(launch_count_wm_agg(a, (S_ub + 1023) / 1024 + 1, d_bsum, stream, prefix_one));
   CCHK(launch_count_gc(a, stream));
   if (nw > 0) CCHK(launch_copy_to_host(d_meta, h_meta_dev, sizeof(CMeta), stream));
   r.n = nw;

@@ -27,6 +27,7 @@ class CEngine {
   int shard_commit(const int64_t* d_gathered, int world);
   int64_t shard_cap = 1 << 16;  // cells per rank record (scotty_tune "shard_count_cells")
   bool shard_async = false;     // scotty_tune "shard_async": shard_push returns without a host sync
+  bool prefix_one = true;       // scotty_tune "count_prefix_one" 0: the watermark's prefix sums always by three kernels
   int watermark(int64_t wm, XResult& r, bool to_host);
   int set_last_watermark(int64_t lw) {
     last_wm = lw;

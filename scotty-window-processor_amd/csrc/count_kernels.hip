@@ -1297,10 +1297,11 @@ hipError_t launch_count_wm_find(const CWmArgs& a, hipStream_t st) {
 }
 
 // range + (prefix sums) + per-window aggregation + GC; range_blocks = upper bound of (r_hi - r_lo + 1) / 1024
-hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st) {
+hipError_t launch_count_wm_agg(const CWmArgs& a, int64_t range_blocks, unsigned long long* bsum, hipStream_t st,
+                               bool one_wg) {
   hipLaunchKernelGGL(ck::count_wm_range_kernel, dim3(1), dim3(64), 0, st, a);
   if (a.nw > 0) {
-    if (a.prefix && range_blocks <= 64) {  // (<= 2^16 slices in range: one workgroup)
+    if (a.prefix && one_wg && range_blocks <= 64) {  // (<= 2^16 slices in range: one workgroup)
       hipLaunchKernelGGL(ck::count_pre_one_kernel, dim3(1), dim3(1024), 0, st, a);
     } else if (a.prefix) {
       hipLaunchKernelGGL(ck::count_pre_block_kernel, dim3((unsigned)std::max<int64_t>(1, range_blocks)), dim3(1024), 0,

@@ -93,6 +93,7 @@ struct scotty_op {
   bool cix_ready = false;         // the cell index on the device matches the current slice store (built at the end
                                   // of the last watermark, overlapping the host's result handling)
   bool shard_async = false;       // scotty_tune("shard_async", 1): shard pushes return without a host sync
+  bool c_prefix_one = true;       // scotty_tune("count_prefix_one", 0): count-path prefix sums by three kernels (tests)
   std::string err;
   bool failed = false;
 
@@ -1026,6 +1027,7 @@ static int decide_mode(scotty_op* op) {
     if (!rc && op->last_watermark != -1) rc = op->c->set_last_watermark(op->last_watermark);
     op->c->shard_cap = op->count_shard_cap;
     op->c->shard_async = op->shard_async;
+    op->c->prefix_one = op->c_prefix_one;
     if (rc) {
       op->failed = true;
       return fail(op, rc, e.empty() ? op->c->err : e);
@@ -1722,6 +1724,12 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     if (op->mode != 0) return SCOTTY_ERR_ARG;
     op->x_kg_off = value == 0;
     if (op->x) op->x->kg_off = op->x_kg_off;
+    return SCOTTY_OK;
+  }
+  if (std::strcmp(key, "count_prefix_one") == 0) {  // 0: the count watermark's prefix sums by three kernels (tests)
+    if (value < 0 || value > 1) return SCOTTY_ERR_ARG;
+    op->c_prefix_one = value != 0;
+    if (op->c) op->c->prefix_one = op->c_prefix_one;
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "shard_async") == 0) {  // shard pushes without a host sync (the caller orders its streams)

@@ -64,6 +64,22 @@ def test_count_path_matches_oracle(seed):
 
 
 @pytest.mark.parametrize("seed", range(6))
+def test_count_path_prefix_sum_kernels_agree(seed):
+    """The watermark's prefix sums of SUM / COUNT windows: one workgroup (the default up to 2^16 slices in range) and
+    the three-kernel scan (scotty_tune "count_prefix_one" 0) both match the oracle on the same stream."""
+    for one in (1, 0):
+        rng = np.random.default_rng(12500 + seed)
+        cfg = dict(windows=_count_windows(rng, [20, 200, 2000][seed % 3]), aggs=[SUM, COUNT],
+                   lateness=int(rng.choice([1, 10, 1000])))
+        n = int(rng.integers(20_000, 80_000))
+        ts, vals = _in_order_stream(rng, n, [0.3, 2, 25][seed % 3], int(rng.integers(0, 5000)), "i32")
+        gpu, ora = build_ops(cfg, "i32", tune={"count_path": 1, "count_prefix_one": one})
+        sched = interval_schedule(ts, int(rng.integers(2, 12)), lag=int(rng.integers(0, 50)),
+                                  pushes_per_interval=int(rng.integers(1, 4)))
+        run_schedule(gpu, ora, ts, vals, sched, value_type="i32")
+
+
+@pytest.mark.parametrize("seed", range(6))
 def test_count_path_out_of_order_never_silently_wrong(pkg, seed):
     """Out-of-order tuples older than their own count slice need LazySlice record moves (S/SliceManager.java:
     77-85): the count path must either match the oracle (the tuples landed in the open slice) or fail loudly."""
