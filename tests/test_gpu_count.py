@@ -63,6 +63,29 @@ def test_count_path_matches_oracle(seed):
     run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols)
 
 
+@pytest.mark.parametrize("vt", ["i32", "i64", "f64"])
+def test_count_path_push_sizes_around_the_step(vt):
+    """The count ingest's step pipeline at its boundaries: pushes of 1, 255, 256, 257, 511, 512, 513, 767, 768, 769,
+    4095, 4096, 4097 and 70000 tuples (a lone ragged step, one / two / three full steps with and without a ragged
+    one, odd and even numbers of full steps per wave), a watermark after every other push, against the oracle."""
+    rng = np.random.default_rng(12700 + ["i32", "i64", "f64"].index(vt))
+    sizes = [1, 255, 256, 257, 511, 512, 513, 767, 768, 769, 4095, 4096, 4097, 70000]
+    n = int(sum(sizes))
+    cfg = dict(windows=[Tumbling(Count, 97), Sliding(Count, 700, 300), Tumbling(Count, 5000)],
+               aggs=_aggs(np.random.default_rng(1), vt) if vt != "i32" else [SUM, COUNT, MIN, MAX], lateness=10)
+    ts, vals = _in_order_stream(rng, n, 2, 1000, vt)
+    sched, lo = [], 0
+    for i, m in enumerate(sizes):
+        sched.append(("push", lo, lo + m))
+        lo += m
+        if i % 2 == 1:
+            sched.append(("wm", int(ts[:lo].max()) - 3))
+    sched.append(("wm", int(ts.max())))
+    gpu, ora = build_ops(cfg, vt, tune={"count_path": 1})
+    f64_cols = [i for i, a in enumerate(cfg["aggs"]) if a == SUM_F64]
+    run_schedule(gpu, ora, ts, vals, sched, value_type=vt, f64_cols=f64_cols)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_count_path_prefix_sum_kernels_agree(seed):
     """The watermark's prefix sums of SUM / COUNT windows: one workgroup (the default up to 2^16 slices in range) and
