@@ -1293,6 +1293,9 @@ def main():
             if "c4s10" in args.only.split(","):  # A/B only: the replay sort's 10-bit digits (keyed_sort_digit10 1)
                 extra["c4s10"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_sort_digit10": 1})
                 log("bench: C4s (10-bit sort digits) done")
+            if "c4s8" in args.only.split(","):  # A/B only: 8-bit digits in every sort pass (keyed_sort_digit10 2)
+                extra["c4s8"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_sort_digit10": 2})
+                log("bench: C4s (8-bit last sort pass) done")
             if "c4s3" in args.only.split(","):  # A/B only: the lane-session kernel's 3-waves-per-SIMD build
                 extra["c4s3"] = extra_c4s(pkg, dev, C4_BATCH, 1 << 20, tune={"keyed_lane_session": 2})
                 log("bench: C4s (keyed sessions) done")

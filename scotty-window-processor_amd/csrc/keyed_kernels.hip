@@ -258,8 +258,9 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
                                                                       int64_t nblocks, Rec<REC>* out, PackP pk) {
   constexpr int TILE = SORT_THREADS * SI;
   constexpr int RADIX = 1 << B;
-  constexpr int PER = RADIX / SORT_THREADS;  // digits per thread in the tile scan
-  static_assert(PER >= 1 && PER * SORT_THREADS == RADIX, "digit count must be a multiple of the workgroup");
+  // digits per thread in the tile scan (a 4-bit last pass: the first 16 threads hold one digit each)
+  constexpr int PER = RADIX >= SORT_THREADS ? RADIX / SORT_THREADS : 1;
+  static_assert(RADIX < SORT_THREADS || PER * SORT_THREADS == RADIX, "digit count must be a multiple of the workgroup");
   __shared__ __attribute__((aligned(16))) unsigned char smem[REC * TILE + 4 * 6 * RADIX];
   void* stage = smem;                                                      // [TILE] records
   int32_t* wc = (int32_t*)(smem + sizeof(Rec<REC>) * TILE);               // [4][RADIX] per-wave counters
@@ -308,10 +309,11 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
 #pragma unroll
     for (int q = 0; q < PER; q++) {
       const int d = tid * PER + q;
-      c[q][0] = wc[d];
-      c[q][1] = wc[RADIX + d];
-      c[q][2] = wc[2 * RADIX + d];
-      c[q][3] = wc[3 * RADIX + d];
+      const bool dv = d < RADIX;
+      c[q][0] = dv ? wc[d] : 0;
+      c[q][1] = dv ? wc[RADIX + d] : 0;
+      c[q][2] = dv ? wc[2 * RADIX + d] : 0;
+      c[q][3] = dv ? wc[3 * RADIX + d] : 0;
       v[q] = c[q][0] + c[q][1] + c[q][2] + c[q][3];
       ex[q] = s;
       s += v[q];
@@ -326,9 +328,11 @@ __global__ __launch_bounds__(SORT_THREADS) void radix_scatter_kernel(const Rec<R
     __syncthreads();
     int32_t add = 0;
     for (int w = 0; w < wid; w++) add += tot[w];
+    // (the reads above precede these writes of wc: the barrier in the wave-sum exchange separates them)
 #pragma unroll
     for (int q = 0; q < PER; q++) {
       const int d = tid * PER + q;
+      if (d >= RADIX) continue;
       const int32_t st0 = inc - s + add + ex[q];
       tstart[d] = st0;
       wc[d] = st0;
@@ -758,34 +762,49 @@ hipError_t launch_slot(const uint32_t* keys, int64_t n, const unsigned long long
 
 int64_t sort_tile() { return k::SORT_TILE; }  // the smallest tile (sizes the histogram buffers)
 
-template <int REC, int SI, int B = k::RB>
-static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t* slot, int64_t n, int passes,
-                              void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp, void** result, hipStream_t st,
-                              k::PackP pk, bool hist0) {
+// one LSD pass: digit histogram per tile (or range_hist_kernel's, pass 0 with hist0), its scan, the stable scatter
+template <int REC, int SI, int B>
+static void sort_pass(int p, bool hist0, int shift, const void* src, void* dst, const int64_t* ts, const void* val,
+                      const uint32_t* slot, int64_t n, int32_t* hist, int32_t* scan_tmp, hipStream_t st, k::PackP pk,
+                      hipError_t& e) {
   using R = k::Rec<REC>;
   const int64_t nb = (n + k::SORT_THREADS * SI - 1) / (k::SORT_THREADS * SI);
   const unsigned hb = (unsigned)((nb + k::HIST_TILES - 1) / k::HIST_TILES);
   const unsigned sb = (unsigned)(8 * ((nb + 7) / 8));  // scatter: XCD-aware tile order (radix_scatter_kernel)
+  if (p == 0 && hist0) {
+    // the first digit's histogram is range_hist_kernel's
+  } else if (p == 0)
+    hipLaunchKernelGGL((k::radix_hist_kernel<REC, true, SI, B>), dim3(hb), dim3(k::SORT_THREADS), 0, st,
+                       (const R*)nullptr, ts, val, slot, n, shift, hist, nb, pk);
+  else
+    hipLaunchKernelGGL((k::radix_hist_kernel<REC, false, SI, B>), dim3(hb), dim3(k::SORT_THREADS), 0, st,
+                       (const R*)src, ts, val, slot, n, shift, hist, nb, pk);
+  e = launch_scan_i32(hist, hist, ((int64_t)1 << B) * nb, scan_tmp, st);
+  if (e != hipSuccess) return;
+  if (p == 0)
+    hipLaunchKernelGGL((k::radix_scatter_kernel<REC, true, SI, B>), dim3(sb), dim3(k::SORT_THREADS), 0, st,
+                       (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
+  else
+    hipLaunchKernelGGL((k::radix_scatter_kernel<REC, false, SI, B>), dim3(sb), dim3(k::SORT_THREADS), 0, st,
+                       (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
+}
+
+// narrow_last: the last pass sorts the top bits_last <= 4 key bits with 4-bit digits (16 digit runs per tile instead
+// of 256, half the ballots per record; keys of 17-20 bits: 8 + 8 + 4)
+template <int REC, int SI, int B = k::RB>
+static hipError_t sort_passes(const int64_t* ts, const void* val, const uint32_t* slot, int64_t n, int passes,
+                              void* bufA, void* bufB, int32_t* hist, int32_t* scan_tmp, void** result, hipStream_t st,
+                              k::PackP pk, bool hist0, bool narrow_last = false) {
   void* src = nullptr;
   void* dst = bufA;
   for (int p = 0; p < passes; p++) {
     const int shift = p * B + (REC == 8 ? pk.tb : 0);
-    if (p == 0 && hist0) {
-      // the first digit's histogram is range_hist_kernel's
-    } else if (p == 0)
-      hipLaunchKernelGGL((k::radix_hist_kernel<REC, true, SI, B>), dim3(hb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb, pk);
+    hipError_t e = hipSuccess;
+    if (narrow_last && p == passes - 1 && p > 0)
+      sort_pass<REC, SI, 4>(p, hist0, shift, src, dst, ts, val, slot, n, hist, scan_tmp, st, pk, e);
     else
-      hipLaunchKernelGGL((k::radix_hist_kernel<REC, false, SI, B>), dim3(hb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)src, ts, val, slot, n, shift, hist, nb, pk);
-    hipError_t e = launch_scan_i32(hist, hist, ((int64_t)1 << B) * nb, scan_tmp, st);
+      sort_pass<REC, SI, B>(p, hist0, shift, src, dst, ts, val, slot, n, hist, scan_tmp, st, pk, e);
     if (e != hipSuccess) return e;
-    if (p == 0)
-      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, true, SI, B>), dim3(sb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)nullptr, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
-    else
-      hipLaunchKernelGGL((k::radix_scatter_kernel<REC, false, SI, B>), dim3(sb), dim3(k::SORT_THREADS), 0, st,
-                         (const R*)src, ts, val, slot, n, shift, hist, nb, (R*)dst, pk);
     src = dst;
     dst = dst == bufA ? bufB : bufA;
   }
@@ -820,15 +839,20 @@ hipError_t launch_sort_by_slot(int rec, const int64_t* ts, const void* val, cons
   }
   int passes = (slot_bits + k::RB - 1) / k::RB;
   if (passes < 1) passes = 1;
+  // a last pass over at most 4 key bits takes 4-bit digits (digit10 == 2: 8-bit digits throughout, the A/B)
+  const bool narrow = digit10 != 2 && passes > 1 && slot_bits - k::RB * (passes - 1) <= 4;
   // (4096-record tiles for 16-byte records, SI = 16: histogram 291 -> 240 us but scatter 593 -> 803 us per 2^26
   // records -- the 70-KB stage halves the resident workgroups; profiles/r05/c4s_sort_by_key/)
   // packed 8-byte records: 2048-record tiles like the others (4096, SI = 16: histogram 350 -> 285 us but scatter
   // 700 -> 893 us per two passes over 2^26 records, profiles/r05/c4s_packed/)
   if (rec == 8)
-    return sort_passes<8, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0);
+    return sort_passes<8, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0,
+                                         narrow);
   if (rec == 16)
-    return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0);
-  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0);
+    return sort_passes<16, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0,
+                                          narrow);
+  return sort_passes<24, k::SORT_ITEMS>(ts, val, slot, n, passes, bufA, bufB, hist, scan_tmp, result, st, pk, hist0,
+                                        narrow);
 }
 
 // range[0] the largest key, range[1] ~ the smallest and range[2] the largest timestamp biased (ts ^ 1 << 63; with ts

@@ -1681,7 +1681,7 @@ int scotty_tune(scotty_op* op, const char* key, int64_t value) {
     return SCOTTY_OK;
   }
   if (std::strcmp(key, "keyed_sort_digit10") == 0) {  // keyed replay sort: 10-bit digits for 17-20-bit keys (A/B)
-    if (value < -1 || value > 1) return fail(op, SCOTTY_ERR_ARG, "keyed_sort_digit10 is -1, 0 or 1");
+    if (value < -1 || value > 2) return fail(op, SCOTTY_ERR_ARG, "keyed_sort_digit10 is -1, 0, 1 or 2");
     op->x_digit10 = (int)value;
     if (op->x) op->x->sort_digit10 = op->x_digit10;
     return SCOTTY_OK;
